@@ -1,0 +1,197 @@
+#!/usr/bin/env python3
+"""Benchmark: EL+ classification (DistEL hot path) on MI355X.
+
+One "step" = one full classification of the workload: el_init (S(X) = {X, ⊤})
++ el_saturate to the fixpoint, with the axiom indexes already resident in HBM.
+``value`` = derived axioms per second over all ranks (SURVEY.md §8(d):
+D = Σ|S(X)| − init facts + Σ|R(r)|).  Result copy-back to the host is timed
+separately (``copyback_ms``) and never part of ``value``.
+
+Multi-GPU (``torch.distributed.run``): weak scaling.  Rank i classifies its own
+disjoint copy of the workload (OntologyMultiplier ×N semantics, the G4 config);
+copies share no concepts, so there is no data-path collective — only the
+barrier and the max-over-ranks timing.
+
+Extra objects on the JSON line:
+  roofline      dominant kernel (largest Σ time in a profiled classification):
+                algorithmic bytes per launch ÷ average launch time (HIP events on
+                the engine's stream), against the 8 TB/s HBM peak
+  cpu_baseline  the CPU oracle (oracle/el_oracle.c, 1 thread, same Jacobi
+                algorithm) on the same workload; the Java/Redis reference cannot run
+                on this image (no JVM, no redis-server)
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+
+WORKLOAD_DESC = {
+    "g1": "G1 GO-like synthetic (20k classes, 8 roles, part_of transitive, 1 chain)",
+    "g2": "G2 NCI-like synthetic (70k classes, 60 roles, tree-like, no chains) — BASELINE configs[1]",
+    "g3": "G3 SNOMED-shaped synthetic (300k classes, 60 roles, 0.3N definitions, 2 chains + 3 transitive)",
+    "g5": "G5 role-heavy synthetic (100k classes, 200 roles, depth-20 chains, hub fillers)",
+}
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--workload", default="g2", choices=sorted(WORKLOAD_DESC))
+    ap.add_argument("--scale", type=float, default=1.0)
+    ap.add_argument("--no-cpu", action="store_true", help="skip the cpu_baseline leg")
+    ap.add_argument("--no-profile", action="store_true", help="skip the profiled roofline pass")
+    ap.add_argument("--verbose", action="store_true")
+    return ap.parse_args()
+
+
+def main():
+    args = parse()
+    import torch
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        backend = "nccl" if torch.cuda.is_available() else "gloo"
+        if backend == "nccl":
+            torch.cuda.set_device(local)
+        dist.init_process_group(backend=backend)
+    has_cuda = torch.cuda.is_available()
+
+    def barrier_sync():
+        if has_cuda:
+            torch.cuda.synchronize()
+        if dist is not None:
+            dist.barrier()
+        if has_cuda:
+            torch.cuda.synchronize()
+
+    from distel_amd import engine, generators
+
+    t0 = time.time()
+    ax = generators.workload(args.workload, args.scale)
+    gen_s = time.time() - t0
+
+    eng = engine.Engine(device=local if has_cuda else 0)
+    t0 = time.time()
+    eng.load(ax)  # host index build + upload: AxiomLoader's part, reported separately
+    load_s = time.time() - t0
+
+    st = None
+    for _ in range(args.warmup):
+        eng.init()
+        st = eng.saturate()
+    barrier_sync()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        eng.init()
+        st = eng.saturate()
+    barrier_sync()
+    elapsed = time.perf_counter() - t0
+    t_max = elapsed
+    derived_all = st["derived"] * world
+    if dist is not None:
+        dev = torch.device("cuda", local) if has_cuda else torch.device("cpu")
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        t_max = float(t.item())
+        d = torch.tensor([st["derived"]], dtype=torch.int64, device=dev)
+        dist.all_reduce(d, op=dist.ReduceOp.SUM)
+        derived_all = int(d.item())
+    ms_per_step = 1e3 * t_max / args.steps
+    value = derived_all * args.steps / t_max
+
+    # result copy-back (not part of value): S facts + links to host memory
+    t0 = time.perf_counter()
+    eng.facts()
+    eng.links()
+    copyback_ms = 1e3 * (time.perf_counter() - t0)
+    eng.close()
+
+    roofline = None
+    kernels = None
+    if rank == 0 and not args.no_profile:
+        # profiled classification: HIP events bracket every launch on the engine stream
+        peng = engine.Engine(device=local if has_cuda else 0, profile=True)
+        peng.load(ax)
+        peng.init()
+        pst = peng.saturate()
+        ks = peng.kernel_stats()
+        peng.close()
+        timed = [k for k in ks if k["launches"] and k["ms"] > 0]
+        dom = max(timed, key=lambda k: k["ms"])
+        per_launch_bytes = dom["bytes"] / dom["launches"]
+        avg_ms = dom["ms"] / dom["launches"]
+        achieved = per_launch_bytes / (avg_ms * 1e-3) / 1e9
+        roofline = {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                    "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": None,
+                    "kernel": dom["kernel"], "bytes_per_launch": int(per_launch_bytes),
+                    "avg_launch_us": round(avg_ms * 1e3, 3), "launches": dom["launches"],
+                    "profiled_ms": round(pst["ms"], 3)}
+        kernels = {k["kernel"]: {"launches": k["launches"], "ms": round(k["ms"], 4), "bytes": k["bytes"]}
+                   for k in ks if k["launches"]}
+
+    cpu = None
+    if rank == 0 and not args.no_cpu:
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import oracle  # cpu_baseline leg only: the CPU restatement, timed, never the product
+        t0 = time.perf_counter()
+        o = oracle.saturate(ax, 0)
+        cpu_s = time.perf_counter() - t0
+        ost = o.stats()
+        o.close()
+        cpu = {"value": round(ost["derived"] / cpu_s, 1), "unit": "axioms/s", "cores": 1, "kind": "port",
+               "sample": f"one full classification of {args.workload} (scale {args.scale}) by the CPU oracle "
+                         f"(semi-naive Jacobi, 1 thread): {cpu_s:.3f} s",
+               "classification_s": round(cpu_s, 4),
+               "parity_derived_equal": ost["derived"] == st["derived"]}
+
+    if rank == 0:
+        line = {
+            "metric": "derived_axioms_per_sec (EL+ classification, SURVEY.md §8(d))",
+            "value": round(value, 1),
+            "unit": "axioms/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_per_step, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u32",
+            "data": "synthetic",
+            "config": {"workload": WORKLOAD_DESC[args.workload] + (f" ×scale {args.scale}" if args.scale != 1 else ""),
+                       "concepts_per_rank": ax.n_concepts, "roles": ax.n_roles, "axioms": ax.counts(),
+                       "parallelism": f"{world} disjoint copies, one per GPU (OntologyMultiplier ×{world})"},
+            "classification_wall_s": round(ms_per_step / 1e3, 6),
+            "derived_axioms": derived_all,
+            "s_facts_per_rank": st["s_facts"],
+            "links_per_rank": st["links"],
+            "supersteps": st["supersteps"],
+            "load_s": round(load_s, 3),
+            "generate_s": round(gen_s, 3),
+            "copyback_ms": round(copyback_ms, 3),
+            "roofline": roofline,
+            "cpu_baseline": cpu,
+        }
+        if args.verbose and kernels:
+            line["kernels"] = kernels
+        print(json.dumps(line), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,1641 @@
+// el_gpu.hip — MI355X (gfx950) EL+ saturation engine behind the C-ABI of include/el_gpu.h.
+//
+// What the reference does: eight rule-type JVM processes run
+// Lua scripts against Redis shards and funnel every new subsumption into a
+// single result node, each iteration closed by an all-to-all "anything new?"
+// barrier (CommunicationHandler.java:49-84).  Here the whole state lives in HBM:
+//
+//   S(X)      dense bit rows, N × W uint32 words      (dedup: atomicOr, test: 1 word)
+//             + CSR of the facts by row X             (iteration of S(Y) for CR4)
+//             + append-only fact log                  (semi-naive Δ = log[wm, end))
+//   R(r)      link set {(X, pid)} as an open-addressing hash of 64-bit keys,
+//             pid = dense (role, filler) pair id (el_index.cpp), + predecessor
+//             CSR keyed by pid and successor CSR keyed by X, + link log
+//
+// One Jacobi superstep t (all rules, or one rule type for el_step):
+//   generation  k_expand_s (Δ S-facts), k_expand_l (Δ links), k_expand_a (Δ range
+//               activations) and k_jobs (wide fan-outs) read ONLY the state of
+//               step t-1 and append candidate facts that are not yet present;
+//   commit      k_commit_s / k_commit_l / k_commit_a dedup the candidates against
+//               the bit rows / hash sets and append the new ones to the logs;
+//   merge       per-row delta counts → hipcub exclusive scan → k_merge_ptr,
+//               k_scatter_old, k_scatter_new rebuild the three CSRs.
+// Generation never writes state, so a step can be re-run after growing a buffer,
+// and the delta of every step is exactly {candidates} \ S_{t-1}: the same sets
+// and the same algorithmic event counts as the CPU oracle (oracle/el_oracle.c).
+//
+// Everything is integer/bitset work: no MFMA.  The roofline is HBM bandwidth
+// (SURVEY.md §8(d)); kernels use wave-aggregated appends (one atomic per wave via
+// __ballot/popcount) and per-wave event-counter reduction.
+#include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
+
+#include <algorithm>
+#include <chrono>
+#include <cstdio>
+#include <cstring>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "el_gpu.h"
+#include "el_index.h"
+
+namespace {
+
+constexpr uint32_t NONE = 0xffffffffu;
+constexpr unsigned long long EMPTY_KEY = ~0ull;
+constexpr int BLOCK = 256;
+
+// sub-rule mask bits
+enum : uint32_t {
+  M_R1 = 1u << 0,    // CR1
+  M_R2 = 1u << 1,    // CR2
+  M_R3 = 1u << 2,    // CR3
+  M_R4Y = 1u << 3,   // CR4 half-1 (new A ∈ S(Y))
+  M_R4L = 1u << 4,   // CR4 half-2 (new link)
+  M_R5 = 1u << 5,    // CR5
+  M_R6 = 1u << 6,    // CR6
+  M_RBOT = 1u << 7,  // ⊥
+  M_RDOM = 1u << 8,  // domain
+  M_RRNG = 1u << 9,  // range
+  M_ALL = (1u << 10) - 1
+};
+
+// el_rule → sub-rules it owns (see el_gpu.h)
+const uint32_t kRuleMask[EL_NUM_RULE_TYPES] = {
+    M_R1, M_R2, M_R3 | M_RDOM | M_RRNG, M_R4Y, M_R4L, M_R5, M_R6, M_RBOT};
+
+enum : uint32_t { JOB_PRED_S = 0, JOB_PRED_L = 1, JOB_R4L = 2, JOB_R6A = 3 };
+
+struct ElError {
+  int code;
+  std::string msg;
+};
+
+#define HIPCHK(expr)                                                                  \
+  do {                                                                                \
+    hipError_t e_ = (expr);                                                           \
+    if (e_ != hipSuccess)                                                             \
+      throw ElError{e_ == hipErrorOutOfMemory ? EL_ENOMEM : EL_EHIP,                  \
+                    std::string(#expr) + ": " + hipGetErrorString(e_)};               \
+  } while (0)
+
+// ---------------------------------------------------------------- device views
+
+struct DIndex {
+  uint32_t N, R, P;
+  uint64_t W;  // uint32 words per bit row
+  const uint8_t* kind;
+  const uint32_t *told_ptr, *told_b;
+  const uint32_t *cidx_ptr, *cidx_c;
+  const uint32_t *conj_ptr, *conj_ops, *conj_b;
+  const uint32_t *exr_ptr, *exr_pid;
+  const uint32_t *exl_ptr, *exl_r, *exl_b;
+  const uint32_t *fp_ptr, *pair_role, *pair_y;
+  const uint32_t *psup_ptr, *psup_pid;
+  const uint32_t *chf_ptr, *chf_s, *chf_t;
+  const uint32_t *chs_ptr, *chs_p, *chs_t;
+  const uint32_t *dom_ptr, *dom_c;
+  const uint32_t *rng_ptr, *rng_c;
+  const uint8_t* role_has_exl;
+  uint32_t has_range;
+};
+
+struct DCounters {
+  unsigned long long ev[EL_NUM_KERNELS][EL_NUM_EVENTS];
+  uint32_t s_log, l_log, a_log, pad0;
+  uint32_t cand_s, cand_l, cand_a, jobs;
+};
+
+struct DState {
+  uint32_t* bits;
+  uint32_t *slog_x, *slog_a;
+  unsigned long long* lhash;
+  unsigned long long lmask;
+  uint32_t *llog_x, *llog_p;
+  unsigned long long* ahash;
+  unsigned long long amask;
+  uint32_t *alog_y, *alog_c;
+  uint8_t* has_act;
+  const uint32_t *s_ptr, *s_val;    // S rows (CSR, current)
+  const uint32_t *pr_ptr, *pr_val;  // predecessors per pid
+  const uint32_t *sc_ptr, *sc_val;  // successors per X
+  uint32_t *s_dcnt, *pr_dcnt, *sc_dcnt;
+  uint32_t *cs_x, *cs_a, cs_cap;
+  uint32_t *cl_x, *cl_p, cl_cap;
+  uint32_t *ca_y, *ca_c, ca_cap;
+  uint4* jobs;
+  uint32_t job_cap;
+  DCounters* ctr;
+};
+
+// ---------------------------------------------------------------- device helpers
+
+struct Ev {
+  uint32_t v[EL_NUM_EVENTS];
+  __device__ Ev() {
+#pragma unroll
+    for (int i = 0; i < EL_NUM_EVENTS; ++i) v[i] = 0;
+  }
+};
+
+__device__ __forceinline__ uint32_t lane_id() { return __lane_id(); }
+
+__device__ __forceinline__ unsigned long long wave_sum(uint32_t x) {
+  unsigned long long v = x;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  return v;
+}
+
+// Every lane of the wave must call this (it reduces over all 64 lanes).
+__device__ __forceinline__ void ev_flush(DCounters* c, int k, const Ev& e) {
+#pragma unroll
+  for (int i = 0; i < EL_NUM_EVENTS; ++i) {
+    unsigned long long s = wave_sum(e.v[i]);
+    if (lane_id() == 0 && s) atomicAdd(&c->ev[k][i], s);
+  }
+}
+
+// Wave-aggregated append: one atomic per wave; returns this lane's slot when pred.
+__device__ __forceinline__ uint32_t wave_append(uint32_t* counter, bool pred) {
+  unsigned long long m = __ballot(pred);
+  if (m == 0) return NONE;
+  int leader = __ffsll((long long)m) - 1;
+  uint32_t base = 0;
+  if ((int)lane_id() == leader) base = atomicAdd(counter, (uint32_t)__popcll(m));
+  base = __shfl(base, leader);
+  uint32_t rank = (uint32_t)__popcll(m & ((1ull << lane_id()) - 1ull));
+  return pred ? base + rank : NONE;
+}
+
+__device__ __forceinline__ bool test_bit(const uint32_t* bits, uint64_t W, uint32_t x, uint32_t b) {
+  return (bits[(uint64_t)x * W + (b >> 5)] >> (b & 31u)) & 1u;
+}
+
+__device__ __forceinline__ unsigned long long mix64(unsigned long long k) {
+  k ^= k >> 33;
+  k *= 0xff51afd7ed558ccdULL;
+  k ^= k >> 33;
+  k *= 0xc4ceb9fe1a85ec53ULL;
+  k ^= k >> 33;
+  return k;
+}
+
+__device__ __forceinline__ unsigned long long link_key(uint32_t pid, uint32_t x) {
+  return ((unsigned long long)pid << 32) | x;
+}
+
+__device__ __forceinline__ bool hash_contains(const unsigned long long* t, unsigned long long mask,
+                                              unsigned long long key) {
+  unsigned long long h = mix64(key) & mask;
+  while (true) {
+    unsigned long long k = t[h];
+    if (k == key) return true;
+    if (k == EMPTY_KEY) return false;
+    h = (h + 1) & mask;
+  }
+}
+
+// true when the key was not present and this thread inserted it
+__device__ __forceinline__ bool hash_insert(unsigned long long* t, unsigned long long mask,
+                                            unsigned long long key) {
+  unsigned long long h = mix64(key) & mask;
+  while (true) {
+    unsigned long long prev = atomicCAS(&t[h], EMPTY_KEY, key);
+    if (prev == EMPTY_KEY) return true;
+    if (prev == key) return false;
+    h = (h + 1) & mask;
+  }
+}
+
+// (role, filler) -> pid by a scan of the filler's pair range (sorted by role)
+__device__ __forceinline__ uint32_t pair_lookup(const DIndex& ix, uint32_t r, uint32_t y, Ev& ev) {
+  ev.v[EL_EV_ROW]++;
+  uint32_t b = ix.fp_ptr[y], e = ix.fp_ptr[y + 1];
+  for (uint32_t p = b; p < e; ++p) {
+    ev.v[EL_EV_ENT]++;
+    uint32_t rr = ix.pair_role[p];
+    if (rr == r) return p;
+    if (rr > r) return NONE;
+  }
+  return NONE;
+}
+
+__device__ __forceinline__ void emit_s(const DState& st, bool pred, uint32_t x, uint32_t a, Ev& ev) {
+  uint32_t slot = wave_append(&st.ctr->cand_s, pred);
+  if (pred) {
+    ev.v[EL_EV_EMIT]++;
+    if (slot < st.cs_cap) {
+      st.cs_x[slot] = x;
+      st.cs_a[slot] = a;
+    }
+  }
+}
+
+__device__ __forceinline__ void emit_l(const DState& st, bool pred, uint32_t x, uint32_t pid, Ev& ev) {
+  uint32_t slot = wave_append(&st.ctr->cand_l, pred);
+  if (pred) {
+    ev.v[EL_EV_EMIT]++;
+    if (slot < st.cl_cap) {
+      st.cl_x[slot] = x;
+      st.cl_p[slot] = pid;
+    }
+  }
+}
+
+__device__ __forceinline__ void emit_a(const DState& st, bool pred, uint32_t y, uint32_t c, Ev& ev) {
+  uint32_t slot = wave_append(&st.ctr->cand_a, pred);
+  if (pred) {
+    ev.v[EL_EV_EMIT]++;
+    if (slot < st.ca_cap) {
+      st.ca_y[slot] = y;
+      st.ca_c[slot] = c;
+    }
+  }
+}
+
+__device__ __forceinline__ void emit_job(const DState& st, bool pred, uint32_t type, uint32_t begin,
+                                         uint32_t len, uint32_t a, uint32_t b, Ev& ev) {
+  uint32_t slot = wave_append(&st.ctr->jobs, pred);
+  if (pred) {
+    ev.v[EL_EV_JOB]++;
+    if (slot < st.job_cap) st.jobs[slot] = make_uint4(begin, len | (type << 28), a, b);
+  }
+}
+
+// ---------------------------------------------------------------- kernels
+
+// S(X) = {X, ⊤} for classes and individuals, {X} for ⊤, ⊥ and datatypes
+// (AxiomLoader.java:1237-1245 classes, :1281-1289 individuals).
+__global__ void k_init(DIndex ix, DState st) {
+  Ev ev;
+  const uint32_t stride = gridDim.x * blockDim.x;
+  for (uint32_t x = blockIdx.x * blockDim.x + threadIdx.x; x < ix.N; x += stride) {
+    const bool two = x != EL_TOP && x != EL_BOTTOM && ix.kind[x] != EL_KIND_DATATYPE;
+    ev.v[EL_EV_ENT]++;
+    uint32_t* row = st.bits + (uint64_t)x * ix.W;
+    atomicOr(row + (x >> 5), 1u << (x & 31u));
+    ev.v[EL_EV_RMW]++;
+    if (two) {
+      atomicOr(row + (EL_TOP >> 5), 1u << (EL_TOP & 31u));
+      ev.v[EL_EV_RMW]++;
+    }
+    uint32_t s0 = wave_append(&st.ctr->s_log, true);
+    st.slog_x[s0] = x;
+    st.slog_a[s0] = x;
+    ev.v[EL_EV_EMIT]++;
+    uint32_t s1 = wave_append(&st.ctr->s_log, two);
+    if (two) {
+      st.slog_x[s1] = x;
+      st.slog_a[s1] = EL_TOP;
+      ev.v[EL_EV_EMIT]++;
+    }
+    st.s_dcnt[x] = two ? 2u : 1u;
+  }
+  ev_flush(st.ctr, EL_K_INIT, ev);
+}
+
+// Rules triggered by new S-facts (X, A) = log[begin, end).
+//  CR1  Type1_1AxiomProcessorBase.java:22-43      CR2  Type1_2AxiomProcessorBase.java:45-66
+//  CR3  Type2AxiomProcessorBase.java:45-75        CR4½ Type3_1AxiomProcessorBase.java:194-239
+//  ⊥    TypeBottomAxiomProcessorBase.java:62-123  range RolePairHandler.java:471-479 + K10
+__global__ void k_expand_s(DIndex ix, DState st, uint32_t begin, uint32_t end, uint32_t mask,
+                           uint32_t a_end) {
+  Ev ev;
+  const uint32_t stride = gridDim.x * blockDim.x;
+  for (uint32_t i = begin + blockIdx.x * blockDim.x + threadIdx.x; i < end; i += stride) {
+    const uint32_t X = st.slog_x[i], A = st.slog_a[i];
+    ev.v[EL_EV_TRIG]++;
+    if (mask & M_R1) {  // A ∈ S(X), A ⊑ B  =>  B ∈ S(X)
+      ev.v[EL_EV_ROW]++;
+      const uint32_t b1 = ix.told_ptr[A + 1];
+      for (uint32_t j = ix.told_ptr[A]; j < b1; ++j) {
+        const uint32_t B = ix.told_b[j];
+        ev.v[EL_EV_ENT]++;
+        ev.v[EL_EV_TEST]++;
+        emit_s(st, !test_bit(st.bits, ix.W, X, B), X, B, ev);
+      }
+    }
+    if (mask & M_R2) {  // A1..An ∈ S(X), ⊓Ai ⊑ B  =>  B ∈ S(X)
+      ev.v[EL_EV_ROW]++;
+      const uint32_t c1 = ix.cidx_ptr[A + 1];
+      for (uint32_t j = ix.cidx_ptr[A]; j < c1; ++j) {
+        const uint32_t c = ix.cidx_c[j];
+        ev.v[EL_EV_ENT]++;
+        ev.v[EL_EV_ROW]++;
+        const uint32_t o1 = ix.conj_ptr[c + 1];
+        bool ok = true;
+        for (uint32_t k = ix.conj_ptr[c]; k < o1; ++k) {
+          const uint32_t op = ix.conj_ops[k];
+          ev.v[EL_EV_ENT]++;
+          if (op == A) continue;
+          ev.v[EL_EV_TEST]++;
+          if (!test_bit(st.bits, ix.W, X, op)) {
+            ok = false;
+            break;
+          }
+        }
+        bool nw = false;
+        const uint32_t B = ix.conj_b[c];
+        if (ok) {
+          ev.v[EL_EV_ENT]++;
+          ev.v[EL_EV_TEST]++;
+          nw = !test_bit(st.bits, ix.W, X, B);
+        }
+        emit_s(st, nw, X, B, ev);
+      }
+    }
+    if (mask & M_R3) {  // A ∈ S(X), A ⊑ ∃r.B  =>  (X, B) ∈ R(r)
+      ev.v[EL_EV_ROW]++;
+      const uint32_t e1 = ix.exr_ptr[A + 1];
+      for (uint32_t j = ix.exr_ptr[A]; j < e1; ++j) {
+        const uint32_t pid = ix.exr_pid[j];
+        ev.v[EL_EV_ENT]++;
+        ev.v[EL_EV_HASH]++;
+        emit_l(st, !hash_contains(st.lhash, st.lmask, link_key(pid, X)), X, pid, ev);
+      }
+    }
+    if (mask & M_R4Y) {  // A ∈ S(Y=X) new, ∃r.A ⊑ B, (X', Y) ∈ R(r)  =>  B ∈ S(X')
+      ev.v[EL_EV_ROW]++;
+      const uint32_t e1 = ix.exl_ptr[A + 1];
+      for (uint32_t j = ix.exl_ptr[A]; j < e1; ++j) {
+        const uint32_t r = ix.exl_r[j], B = ix.exl_b[j];
+        ev.v[EL_EV_ENT] += 2;
+        const uint32_t pid = pair_lookup(ix, r, X, ev);
+        uint32_t pb = 0, pl = 0;
+        if (pid != NONE) {
+          ev.v[EL_EV_ROW]++;
+          pb = st.pr_ptr[pid];
+          pl = st.pr_ptr[pid + 1] - pb;
+        }
+        emit_job(st, pl > 0, JOB_PRED_S, pb, pl, 0, B, ev);
+      }
+    }
+    if ((mask & M_RBOT) && A == EL_BOTTOM) {  // ⊥ ∈ S(Y=X) new, (X', Y) ∈ R(*)  =>  ⊥ ∈ S(X')
+      ev.v[EL_EV_ROW]++;
+      const uint32_t p1 = ix.fp_ptr[X + 1];
+      for (uint32_t p = ix.fp_ptr[X]; p < p1; ++p) {
+        ev.v[EL_EV_ROW]++;
+        const uint32_t pb = st.pr_ptr[p], pl = st.pr_ptr[p + 1] - pb;
+        emit_job(st, pl > 0, JOB_PRED_S, pb, pl, 0, EL_BOTTOM, ev);
+      }
+    }
+    if ((mask & M_RRNG) && ix.has_range) {  // Y=A ∈ S(X) new, active range (Y, C)  =>  C ∈ S(X)
+      ev.v[EL_EV_ENT]++;
+      if (st.has_act[A]) {
+        for (uint32_t k = 0; k < a_end; ++k) {
+          ev.v[EL_EV_ENT] += 2;
+          const bool hit = st.alog_y[k] == A;
+          const uint32_t C = st.alog_c[k];
+          bool nw = false;
+          if (hit) {
+            ev.v[EL_EV_TEST]++;
+            nw = !test_bit(st.bits, ix.W, X, C);
+          }
+          emit_s(st, nw, X, C, ev);
+        }
+      }
+    }
+  }
+  ev_flush(st.ctr, EL_K_EXPAND_S, ev);
+}
+
+// Rules triggered by new links (X, pid = (r, Y)) = link log[begin, end).
+//  CR4½ Type3_2AxiomProcessorBase.java:67-96,182-224   CR5 Type4AxiomProcessorBase.java:38-76
+//  CR6  Type5AxiomProcessorBase.java:115-154           ⊥   RolePairHandler.java:358-372
+//  domain/range RolePairHandler.java:456-491
+__global__ void k_expand_l(DIndex ix, DState st, uint32_t begin, uint32_t end, uint32_t mask) {
+  Ev ev;
+  const uint32_t stride = gridDim.x * blockDim.x;
+  for (uint32_t i = begin + blockIdx.x * blockDim.x + threadIdx.x; i < end; i += stride) {
+    const uint32_t X = st.llog_x[i], pid = st.llog_p[i];
+    ev.v[EL_EV_TRIG]++;
+    const uint32_t r = ix.pair_role[pid], Y = ix.pair_y[pid];
+    ev.v[EL_EV_ENT] += 2;
+    if (mask & M_R4L) {  // (X, Y) ∈ R(r) new, A ∈ S(Y), ∃r.A ⊑ B  =>  B ∈ S(X)
+      ev.v[EL_EV_ENT]++;
+      const bool has = ix.role_has_exl[r] != 0;
+      uint32_t sb = 0, sl = 0;
+      if (has) {
+        ev.v[EL_EV_ROW]++;
+        sb = st.s_ptr[Y];
+        sl = st.s_ptr[Y + 1] - sb;
+      }
+      emit_job(st, has && sl > 0, JOB_R4L, sb, sl, X, r, ev);
+    }
+    if (mask & M_RBOT) {  // ⊥ ∈ S(Y)  =>  ⊥ ∈ S(X)
+      ev.v[EL_EV_TEST]++;
+      bool nw = false;
+      if (test_bit(st.bits, ix.W, Y, EL_BOTTOM)) {
+        ev.v[EL_EV_TEST]++;
+        nw = !test_bit(st.bits, ix.W, X, EL_BOTTOM);
+      }
+      emit_s(st, nw, X, EL_BOTTOM, ev);
+    }
+    if (mask & M_R5) {  // r ⊑ s  =>  (X, Y) ∈ R(s)
+      ev.v[EL_EV_ROW]++;
+      const uint32_t q1 = ix.psup_ptr[pid + 1];
+      for (uint32_t j = ix.psup_ptr[pid]; j < q1; ++j) {
+        const uint32_t q = ix.psup_pid[j];
+        ev.v[EL_EV_ENT]++;
+        ev.v[EL_EV_HASH]++;
+        emit_l(st, !hash_contains(st.lhash, st.lmask, link_key(q, X)), X, q, ev);
+      }
+    }
+    if (mask & M_R6) {  // r ∘ s ⊑ t
+      ev.v[EL_EV_ROW]++;
+      const bool first = ix.chf_ptr[r + 1] > ix.chf_ptr[r];
+      uint32_t sb = 0, sl = 0;
+      if (first) {  // r first: (Y, Z) ∈ R(s)  =>  (X, Z) ∈ R(t)
+        ev.v[EL_EV_ROW]++;
+        sb = st.sc_ptr[Y];
+        sl = st.sc_ptr[Y + 1] - sb;
+      }
+      emit_job(st, first && sl > 0, JOB_R6A, sb, sl, X, r, ev);
+      ev.v[EL_EV_ROW]++;
+      const uint32_t h1 = ix.chs_ptr[r + 1];
+      for (uint32_t j = ix.chs_ptr[r]; j < h1; ++j) {  // r second: (X', X) ∈ R(p)  =>  (X', Y) ∈ R(t)
+        const uint32_t p = ix.chs_p[j], t = ix.chs_t[j];
+        ev.v[EL_EV_ENT] += 2;
+        const uint32_t pq = pair_lookup(ix, p, X, ev);
+        uint32_t pb = 0, pl = 0, pt = NONE;
+        if (pq != NONE) {
+          ev.v[EL_EV_ROW]++;
+          pb = st.pr_ptr[pq];
+          pl = st.pr_ptr[pq + 1] - pb;
+          if (pl) pt = pair_lookup(ix, t, Y, ev);
+        }
+        emit_job(st, pl > 0, JOB_PRED_L, pb, pl, pt, 0, ev);
+      }
+    }
+    if (mask & M_RDOM) {  // domain(r) = D  =>  D ∈ S(X)   (X ≠ ⊤, not a datatype)
+      ev.v[EL_EV_ROW]++;
+      const uint32_t d0 = ix.dom_ptr[r], d1 = ix.dom_ptr[r + 1];
+      bool ok = false;
+      if (d1 > d0) {
+        ev.v[EL_EV_ENT]++;
+        ok = X != EL_TOP && ix.kind[X] != EL_KIND_DATATYPE;
+      }
+      for (uint32_t j = d0; j < d1; ++j) {
+        const uint32_t D = ix.dom_c[j];
+        ev.v[EL_EV_ENT]++;
+        bool nw = false;
+        if (ok) {
+          ev.v[EL_EV_TEST]++;
+          nw = !test_bit(st.bits, ix.W, X, D);
+        }
+        emit_s(st, nw, X, D, ev);
+      }
+    }
+    if (mask & M_RRNG) {  // range(r) = C  =>  activate Y ⊑ C  (Y ≠ ⊤, not a datatype; H1)
+      ev.v[EL_EV_ROW]++;
+      const uint32_t g0 = ix.rng_ptr[r], g1 = ix.rng_ptr[r + 1];
+      bool ok = false;
+      if (g1 > g0) {
+        ev.v[EL_EV_ENT]++;
+        ok = Y != EL_TOP && ix.kind[Y] != EL_KIND_DATATYPE;
+      }
+      for (uint32_t j = g0; j < g1; ++j) {
+        const uint32_t C = ix.rng_c[j];
+        ev.v[EL_EV_ENT]++;
+        bool nw = false;
+        if (ok) {
+          ev.v[EL_EV_HASH]++;
+          nw = !hash_contains(st.ahash, st.amask, link_key(C, Y));
+        }
+        emit_a(st, nw, Y, C, ev);
+      }
+    }
+  }
+  ev_flush(st.ctr, EL_K_EXPAND_L, ev);
+}
+
+// Wide fan-outs: one wave per job record, lanes stride over the list.
+//  JOB_PRED_S  preds(pid) × {B}         (CR4 half-1, ⊥)
+//  JOB_PRED_L  preds(pq)  × {pid_t}     (CR6, r second)
+//  JOB_R4L     S(Y) row   × ∃r.A ⊑ B    (CR4 half-2)
+//  JOB_R6A     succ(Y)    × chains of r (CR6, r first)
+__global__ void k_jobs(DIndex ix, DState st) {
+  Ev ev;
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t wid = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const uint32_t nwaves = (gridDim.x * blockDim.x) >> 6;
+  const uint32_t njobs = min(st.ctr->jobs, st.job_cap);
+  for (uint32_t j = wid; j < njobs; j += nwaves) {
+    const uint4 jb = st.jobs[j];
+    const uint32_t begin = jb.x, type = jb.y >> 28, len = jb.y & 0x0fffffffu, a = jb.z, b = jb.w;
+    if (lane == 0) ev.v[EL_EV_JOB]++;
+    if (type == JOB_PRED_S) {
+      for (uint32_t k = lane; k < len; k += 64) {
+        const uint32_t xp = st.pr_val[begin + k];
+        ev.v[EL_EV_ENT]++;
+        ev.v[EL_EV_TEST]++;
+        emit_s(st, !test_bit(st.bits, ix.W, xp, b), xp, b, ev);
+      }
+    } else if (type == JOB_PRED_L) {
+      for (uint32_t k = lane; k < len; k += 64) {
+        const uint32_t xp = st.pr_val[begin + k];
+        ev.v[EL_EV_ENT]++;
+        ev.v[EL_EV_HASH]++;
+        emit_l(st, !hash_contains(st.lhash, st.lmask, link_key(a, xp)), xp, a, ev);
+      }
+    } else if (type == JOB_R4L) {
+      const uint32_t X = a, r = b;
+      for (uint32_t k = lane; k < len; k += 64) {
+        const uint32_t A = st.s_val[begin + k];
+        ev.v[EL_EV_ENT]++;
+        ev.v[EL_EV_ROW]++;
+        const uint32_t e1 = ix.exl_ptr[A + 1];
+        for (uint32_t e = ix.exl_ptr[A]; e < e1; ++e) {
+          const uint32_t rr = ix.exl_r[e];
+          ev.v[EL_EV_ENT] += 2;
+          if (rr > r) break;
+          bool nw = false;
+          const uint32_t B = ix.exl_b[e];
+          if (rr == r) {
+            ev.v[EL_EV_TEST]++;
+            nw = !test_bit(st.bits, ix.W, X, B);
+          }
+          emit_s(st, nw, X, B, ev);
+        }
+      }
+    } else {  // JOB_R6A
+      const uint32_t X = a, r = b;
+      for (uint32_t k = lane; k < len; k += 64) {
+        const uint32_t q = st.sc_val[begin + k];
+        ev.v[EL_EV_ENT]++;
+        const uint32_t s2 = ix.pair_role[q], Z = ix.pair_y[q];
+        ev.v[EL_EV_ENT] += 2;
+        ev.v[EL_EV_ROW]++;
+        const uint32_t f1 = ix.chf_ptr[r + 1];
+        for (uint32_t f = ix.chf_ptr[r]; f < f1; ++f) {
+          const uint32_t s = ix.chf_s[f], t = ix.chf_t[f];
+          ev.v[EL_EV_ENT] += 2;
+          bool nw = false;
+          uint32_t pt = NONE;
+          if (s == s2) {
+            pt = pair_lookup(ix, t, Z, ev);
+            ev.v[EL_EV_HASH]++;
+            nw = !hash_contains(st.lhash, st.lmask, link_key(pt, X));
+          }
+          emit_l(st, nw, X, pt, ev);
+        }
+      }
+    }
+  }
+  ev_flush(st.ctr, EL_K_JOBS, ev);
+}
+
+// Range activations (Y, C) = act log[a_begin, a_end): every X with Y ∈ S(X) gets C
+// (ScriptsCollection.insertClassAssertions1 :45-62 copies result[Y] into result[C]).
+__global__ void k_expand_a(DIndex ix, DState st, uint32_t a_begin, uint32_t a_end) {
+  Ev ev;
+  const uint32_t stride = gridDim.x * blockDim.x;
+  const uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x;
+  if (tid == 0) ev.v[EL_EV_TRIG] += a_end - a_begin;
+  for (uint32_t x = tid; x < ix.N; x += stride) {
+    for (uint32_t k = a_begin; k < a_end; ++k) {
+      const uint32_t Y = st.alog_y[k], C = st.alog_c[k];
+      ev.v[EL_EV_TEST]++;
+      bool nw = false;
+      if (test_bit(st.bits, ix.W, x, Y)) {
+        ev.v[EL_EV_TEST]++;
+        nw = !test_bit(st.bits, ix.W, x, C);
+      }
+      emit_s(st, nw, x, C, ev);
+    }
+  }
+  ev_flush(st.ctr, EL_K_EXPAND_A, ev);
+}
+
+// Dedup S candidates against the bit rows; new facts go to the log (the versioned
+// ZADD of every Lua kernel, e.g. Type1_1AxiomProcessorBase.java:36-41).
+__global__ void k_commit_s(DIndex ix, DState st, uint32_t n) {
+  Ev ev;
+  const uint32_t stride = gridDim.x * blockDim.x;
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    const uint32_t x = st.cs_x[i], a = st.cs_a[i];
+    ev.v[EL_EV_TRIG]++;
+    ev.v[EL_EV_RMW]++;
+    const uint32_t m = 1u << (a & 31u);
+    const uint32_t old = atomicOr(st.bits + (uint64_t)x * ix.W + (a >> 5), m);
+    const bool nw = (old & m) == 0;
+    const uint32_t slot = wave_append(&st.ctr->s_log, nw);
+    if (nw) {
+      ev.v[EL_EV_EMIT]++;
+      st.slog_x[slot] = x;
+      st.slog_a[slot] = a;
+      atomicAdd(st.s_dcnt + x, 1u);
+    }
+  }
+  ev_flush(st.ctr, EL_K_COMMIT_S, ev);
+}
+
+// Dedup link candidates against the link set (checkAndInsertScript,
+// RolePairHandler.java:133-168); new links feed the predecessor/successor CSRs.
+__global__ void k_commit_l(DIndex ix, DState st, uint32_t n) {
+  Ev ev;
+  const uint32_t stride = gridDim.x * blockDim.x;
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    const uint32_t x = st.cl_x[i], p = st.cl_p[i];
+    ev.v[EL_EV_TRIG]++;
+    ev.v[EL_EV_HASH]++;
+    const bool nw = hash_insert(st.lhash, st.lmask, link_key(p, x));
+    const uint32_t slot = wave_append(&st.ctr->l_log, nw);
+    if (nw) {
+      ev.v[EL_EV_EMIT]++;
+      st.llog_x[slot] = x;
+      st.llog_p[slot] = p;
+      atomicAdd(st.pr_dcnt + p, 1u);
+      atomicAdd(st.sc_dcnt + x, 1u);
+    }
+  }
+  ev_flush(st.ctr, EL_K_COMMIT_L, ev);
+}
+
+__global__ void k_commit_a(DIndex ix, DState st, uint32_t n) {
+  Ev ev;
+  const uint32_t stride = gridDim.x * blockDim.x;
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    const uint32_t y = st.ca_y[i], c = st.ca_c[i];
+    ev.v[EL_EV_TRIG]++;
+    ev.v[EL_EV_HASH]++;
+    const bool nw = hash_insert(st.ahash, st.amask, link_key(c, y));
+    const uint32_t slot = wave_append(&st.ctr->a_log, nw);
+    if (nw) {
+      ev.v[EL_EV_EMIT]++;
+      st.alog_y[slot] = y;
+      st.alog_c[slot] = c;
+      st.has_act[y] = 1;
+    }
+  }
+  ev_flush(st.ctr, EL_K_COMMIT_A, ev);
+}
+
+// CSR merge: new_ptr[x] = ptr[x] + exclusive_scan(dcnt)[x]
+__global__ void k_merge_ptr(uint32_t* __restrict__ ptr2, const uint32_t* __restrict__ ptr,
+                            const uint32_t* __restrict__ dscan, uint32_t n1) {
+  const uint32_t stride = gridDim.x * blockDim.x;
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n1; i += stride)
+    ptr2[i] = ptr[i] + dscan[i];
+}
+
+// existing entry i of row x moves by the number of delta entries in rows < x
+__global__ void k_scatter_old(const uint32_t* __restrict__ row, const uint32_t* __restrict__ val,
+                              uint32_t* __restrict__ row2, uint32_t* __restrict__ val2,
+                              const uint32_t* __restrict__ dscan, uint32_t n_old) {
+  const uint32_t stride = gridDim.x * blockDim.x;
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n_old; i += stride) {
+    const uint32_t x = row[i];
+    const uint32_t j = i + dscan[x];
+    row2[j] = x;
+    val2[j] = val[i];
+  }
+}
+
+// delta entries fill the tail of their row; dcnt is consumed back to zero
+__global__ void k_scatter_new(const uint32_t* __restrict__ lx, const uint32_t* __restrict__ lv,
+                              uint32_t begin, uint32_t end, const uint32_t* __restrict__ ptr2,
+                              uint32_t* dcnt, uint32_t* __restrict__ row2, uint32_t* __restrict__ val2) {
+  const uint32_t stride = gridDim.x * blockDim.x;
+  for (uint32_t i = begin + blockIdx.x * blockDim.x + threadIdx.x; i < end; i += stride) {
+    const uint32_t x = lx[i];
+    const uint32_t pos = ptr2[x + 1] - atomicSub(dcnt + x, 1u);
+    row2[pos] = x;
+    val2[pos] = lv[i];
+  }
+}
+
+__global__ void k_rehash(unsigned long long* t, unsigned long long mask, const uint32_t* kx,
+                         const uint32_t* kp, uint32_t n) {
+  const uint32_t stride = gridDim.x * blockDim.x;
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
+    hash_insert(t, mask, link_key(kp[i], kx[i]));
+}
+
+// ---------------------------------------------------------------- host side
+
+template <class T>
+T* dalloc(size_t n) {
+  void* p = nullptr;
+  if (n == 0) n = 1;
+  HIPCHK(hipMalloc(&p, n * sizeof(T)));
+  return (T*)p;
+}
+template <class T>
+void dfree(T*& p) {
+  if (p) (void)hipFree(p);
+  p = nullptr;
+}
+template <class T>
+T* dupload(const std::vector<T>& v) {
+  T* p = dalloc<T>(v.size());
+  if (!v.empty()) HIPCHK(hipMemcpy(p, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice));
+  return p;
+}
+// grow a device array to cap elements keeping the first used ones
+template <class T>
+void dgrow(T*& p, size_t used, size_t cap) {
+  T* q = dalloc<T>(cap);
+  if (used) HIPCHK(hipMemcpy(q, p, used * sizeof(T), hipMemcpyDeviceToDevice));
+  dfree(p);
+  p = q;
+}
+
+uint32_t grid_for(uint64_t n, uint32_t cap = 8192) {
+  uint64_t g = (n + BLOCK - 1) / BLOCK;
+  if (g < 1) g = 1;
+  if (g > cap) g = cap;
+  return (uint32_t)g;
+}
+
+uint64_t next_pow2(uint64_t v) {
+  uint64_t p = 1;
+  while (p < v) p <<= 1;
+  return p;
+}
+
+// CSR with double buffers and per-row delta counts
+struct DevCsr {
+  uint32_t nrows = 0;
+  uint64_t cap = 0;
+  uint32_t *ptr = nullptr, *row = nullptr, *val = nullptr;
+  uint32_t *ptr2 = nullptr, *row2 = nullptr, *val2 = nullptr;
+  uint32_t *dcnt = nullptr, *dscan = nullptr;
+  void alloc(uint32_t n, uint64_t c) {
+    nrows = n;
+    cap = c;
+    ptr = dalloc<uint32_t>(n + 1);
+    ptr2 = dalloc<uint32_t>(n + 1);
+    dcnt = dalloc<uint32_t>(n + 1);
+    dscan = dalloc<uint32_t>(n + 1);
+    row = dalloc<uint32_t>(c);
+    val = dalloc<uint32_t>(c);
+    row2 = dalloc<uint32_t>(c);
+    val2 = dalloc<uint32_t>(c);
+  }
+  void grow(uint64_t used, uint64_t c) {
+    dgrow(row, used, c);
+    dgrow(val, used, c);
+    dfree(row2);
+    dfree(val2);
+    row2 = dalloc<uint32_t>(c);
+    val2 = dalloc<uint32_t>(c);
+    cap = c;
+  }
+  void reset(hipStream_t s) {
+    HIPCHK(hipMemsetAsync(ptr, 0, (nrows + 1) * sizeof(uint32_t), s));
+    HIPCHK(hipMemsetAsync(dcnt, 0, (nrows + 1) * sizeof(uint32_t), s));
+  }
+  void release() {
+    dfree(ptr);
+    dfree(row);
+    dfree(val);
+    dfree(ptr2);
+    dfree(row2);
+    dfree(val2);
+    dfree(dcnt);
+    dfree(dscan);
+  }
+};
+
+struct PendingEvent {
+  int kernel;
+  hipEvent_t a, b;
+};
+
+}  // namespace
+
+struct el_ctx {
+  int device = 0;
+  int profile = 0;
+  hipStream_t stream = nullptr;
+  std::string err;
+  bool loaded = false, inited = false;
+
+  el::HostIndex hx;
+  DIndex ix{};
+  std::vector<void*> index_bufs;
+
+  // state
+  uint32_t* bits = nullptr;
+  uint64_t W = 0;
+  uint32_t *slog_x = nullptr, *slog_a = nullptr;
+  uint64_t slog_cap = 0;
+  unsigned long long* lhash = nullptr;
+  uint64_t lhash_cap = 0;
+  uint32_t *llog_x = nullptr, *llog_p = nullptr;
+  uint64_t llog_cap = 0;
+  unsigned long long* ahash = nullptr;
+  uint64_t ahash_cap = 0;
+  uint32_t *alog_y = nullptr, *alog_c = nullptr;
+  uint64_t alog_cap = 0;
+  uint8_t* has_act = nullptr;
+  DevCsr S, PR, SC;
+  uint32_t *cs_x = nullptr, *cs_a = nullptr, *cl_x = nullptr, *cl_p = nullptr, *ca_y = nullptr,
+           *ca_c = nullptr;
+  uint64_t cs_cap = 0, cl_cap = 0, ca_cap = 0;
+  uint4* jobs = nullptr;
+  uint64_t job_cap = 0;
+  DCounters* ctr = nullptr;
+  unsigned long long* ev_backup = nullptr;
+  void* scan_tmp = nullptr;
+  size_t scan_tmp_bytes = 0;
+
+  // host mirrors
+  DCounters hc{};
+  uint64_t s_count = 0, l_count = 0, a_count = 0, s_init = 0;
+  uint64_t wm_s[EL_NUM_RULE_TYPES] = {}, wm_l[EL_NUM_RULE_TYPES] = {}, wm_a[EL_NUM_RULE_TYPES] = {};
+  el_stats last{};
+  std::vector<uint64_t> tr_s, tr_l, tr_a;
+  // host-side per-kernel accounting (merge kernels, launches, times)
+  uint64_t launches[EL_NUM_KERNELS] = {};
+  uint64_t host_ev[EL_NUM_KERNELS][EL_NUM_EVENTS] = {};
+  double kms[EL_NUM_KERNELS] = {};
+  std::vector<PendingEvent> pending;
+  std::vector<hipEvent_t> event_pool;
+
+  DState dstate() const {
+    DState s{};
+    s.bits = bits;
+    s.slog_x = slog_x;
+    s.slog_a = slog_a;
+    s.lhash = lhash;
+    s.lmask = lhash_cap - 1;
+    s.llog_x = llog_x;
+    s.llog_p = llog_p;
+    s.ahash = ahash;
+    s.amask = ahash_cap - 1;
+    s.alog_y = alog_y;
+    s.alog_c = alog_c;
+    s.has_act = has_act;
+    s.s_ptr = S.ptr;
+    s.s_val = S.val;
+    s.pr_ptr = PR.ptr;
+    s.pr_val = PR.val;
+    s.sc_ptr = SC.ptr;
+    s.sc_val = SC.val;
+    s.s_dcnt = S.dcnt;
+    s.pr_dcnt = PR.dcnt;
+    s.sc_dcnt = SC.dcnt;
+    s.cs_x = cs_x;
+    s.cs_a = cs_a;
+    s.cs_cap = (uint32_t)cs_cap;
+    s.cl_x = cl_x;
+    s.cl_p = cl_p;
+    s.cl_cap = (uint32_t)cl_cap;
+    s.ca_y = ca_y;
+    s.ca_c = ca_c;
+    s.ca_cap = (uint32_t)ca_cap;
+    s.jobs = jobs;
+    s.job_cap = (uint32_t)job_cap;
+    s.ctr = ctr;
+    return s;
+  }
+
+  hipEvent_t take_event() {
+    if (!event_pool.empty()) {
+      hipEvent_t e = event_pool.back();
+      event_pool.pop_back();
+      return e;
+    }
+    hipEvent_t e;
+    HIPCHK(hipEventCreate(&e));
+    return e;
+  }
+  // bracket one kernel launch with HIP events on the launch stream (profile mode)
+  template <class F>
+  void launch(int k, F&& f) {
+    launches[k]++;
+    if (!profile) {
+      f();
+      HIPCHK(hipGetLastError());
+      return;
+    }
+    PendingEvent pe{k, take_event(), take_event()};
+    HIPCHK(hipEventRecord(pe.a, stream));
+    f();
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipEventRecord(pe.b, stream));
+    pending.push_back(pe);
+  }
+  void sync() {
+    HIPCHK(hipStreamSynchronize(stream));
+    for (auto& pe : pending) {
+      float ms = 0.f;
+      HIPCHK(hipEventElapsedTime(&ms, pe.a, pe.b));
+      kms[pe.kernel] += ms;
+      event_pool.push_back(pe.a);
+      event_pool.push_back(pe.b);
+    }
+    pending.clear();
+  }
+  void read_counters() { HIPCHK(hipMemcpy(&hc, ctr, sizeof(DCounters), hipMemcpyDeviceToHost)); }
+
+  void free_state();
+  void free_index();
+  void alloc_state();
+  void reset_state();
+  void ensure_capacity();
+  void merge(DevCsr& c, const uint32_t* lx, const uint32_t* lv, uint64_t old_n, uint64_t begin,
+             uint64_t end);
+  void rehash_links(uint64_t cap);
+  void rehash_acts(uint64_t cap);
+  bool superstep(uint32_t mask, uint64_t sb, uint64_t se, uint64_t lb, uint64_t le, uint64_t ab,
+                 uint64_t ae);
+  void fill_stats(el_stats* st, double ms);
+};
+
+void el_ctx::free_index() {
+  for (void* p : index_bufs) (void)hipFree(p);
+  index_bufs.clear();
+}
+
+void el_ctx::free_state() {
+  dfree(bits);
+  dfree(slog_x);
+  dfree(slog_a);
+  dfree(lhash);
+  dfree(llog_x);
+  dfree(llog_p);
+  dfree(ahash);
+  dfree(alog_y);
+  dfree(alog_c);
+  dfree(has_act);
+  S.release();
+  PR.release();
+  SC.release();
+  dfree(cs_x);
+  dfree(cs_a);
+  dfree(cl_x);
+  dfree(cl_p);
+  dfree(ca_y);
+  dfree(ca_c);
+  dfree(jobs);
+  dfree(ctr);
+  dfree(ev_backup);
+  if (scan_tmp) (void)hipFree(scan_tmp);
+  scan_tmp = nullptr;
+}
+
+void el_ctx::alloc_state() {
+  const uint64_t N = hx.N, P = hx.P;
+  W = (N + 31) / 32;
+  bits = dalloc<uint32_t>(N * W);
+  slog_cap = std::max<uint64_t>(1u << 20, 8 * N);
+  slog_x = dalloc<uint32_t>(slog_cap);
+  slog_a = dalloc<uint32_t>(slog_cap);
+  llog_cap = std::max<uint64_t>(1u << 20, 4 * N);
+  llog_x = dalloc<uint32_t>(llog_cap);
+  llog_p = dalloc<uint32_t>(llog_cap);
+  lhash_cap = next_pow2(2 * llog_cap);
+  lhash = dalloc<unsigned long long>(lhash_cap);
+  alog_cap = 1u << 12;
+  alog_y = dalloc<uint32_t>(alog_cap);
+  alog_c = dalloc<uint32_t>(alog_cap);
+  ahash_cap = next_pow2(2 * alog_cap);
+  ahash = dalloc<unsigned long long>(ahash_cap);
+  has_act = dalloc<uint8_t>(N);
+  S.alloc((uint32_t)N, slog_cap);
+  PR.alloc((uint32_t)P, llog_cap);
+  SC.alloc((uint32_t)N, llog_cap);
+  cs_cap = std::max<uint64_t>(1u << 20, 4 * N);
+  cl_cap = cs_cap;
+  ca_cap = 1u << 12;
+  cs_x = dalloc<uint32_t>(cs_cap);
+  cs_a = dalloc<uint32_t>(cs_cap);
+  cl_x = dalloc<uint32_t>(cl_cap);
+  cl_p = dalloc<uint32_t>(cl_cap);
+  ca_y = dalloc<uint32_t>(ca_cap);
+  ca_c = dalloc<uint32_t>(ca_cap);
+  job_cap = std::max<uint64_t>(1u << 20, 2 * N);
+  jobs = dalloc<uint4>(job_cap);
+  ctr = dalloc<DCounters>(1);
+  ev_backup = dalloc<unsigned long long>(EL_NUM_KERNELS * EL_NUM_EVENTS);
+  size_t b1 = 0;
+  uint32_t maxrows = (uint32_t)std::max<uint64_t>(N, P) + 1;
+  HIPCHK(hipcub::DeviceScan::ExclusiveSum(nullptr, b1, (uint32_t*)nullptr, (uint32_t*)nullptr,
+                                          maxrows, stream));
+  scan_tmp_bytes = b1;
+  HIPCHK(hipMalloc(&scan_tmp, b1 ? b1 : 1));
+}
+
+void el_ctx::reset_state() {
+  HIPCHK(hipMemsetAsync(bits, 0, hx.N * W * sizeof(uint32_t), stream));
+  HIPCHK(hipMemsetAsync(lhash, 0xff, lhash_cap * sizeof(unsigned long long), stream));
+  HIPCHK(hipMemsetAsync(ahash, 0xff, ahash_cap * sizeof(unsigned long long), stream));
+  HIPCHK(hipMemsetAsync(has_act, 0, hx.N, stream));
+  S.reset(stream);
+  PR.reset(stream);
+  SC.reset(stream);
+  HIPCHK(hipMemsetAsync(ctr, 0, sizeof(DCounters), stream));
+  s_count = l_count = a_count = s_init = 0;
+  for (int r = 0; r < EL_NUM_RULE_TYPES; ++r) wm_s[r] = wm_l[r] = wm_a[r] = 0;
+  memset(launches, 0, sizeof launches);
+  memset(host_ev, 0, sizeof host_ev);
+  memset(kms, 0, sizeof kms);
+  tr_s.clear();
+  tr_l.clear();
+  tr_a.clear();
+}
+
+void el_ctx::rehash_links(uint64_t cap) {
+  dfree(lhash);
+  lhash_cap = cap;
+  lhash = dalloc<unsigned long long>(cap);
+  HIPCHK(hipMemsetAsync(lhash, 0xff, cap * sizeof(unsigned long long), stream));
+  if (l_count)
+    launch(EL_K_REHASH, [&] {
+      hipLaunchKernelGGL(k_rehash, dim3(grid_for(l_count)), dim3(BLOCK), 0, stream, lhash, cap - 1,
+                         llog_x, llog_p, (uint32_t)l_count);
+    });
+}
+
+void el_ctx::rehash_acts(uint64_t cap) {
+  dfree(ahash);
+  ahash_cap = cap;
+  ahash = dalloc<unsigned long long>(cap);
+  HIPCHK(hipMemsetAsync(ahash, 0xff, cap * sizeof(unsigned long long), stream));
+  if (a_count)
+    launch(EL_K_REHASH, [&] {
+      hipLaunchKernelGGL(k_rehash, dim3(grid_for(a_count)), dim3(BLOCK), 0, stream, ahash, cap - 1,
+                         alog_y, alog_c, (uint32_t)a_count);
+    });
+}
+
+// Rebuild CSR c from its current contents (old_n entries) plus log[begin, end).
+// Row keys of the delta come from lx, values from lv.
+void el_ctx::merge(DevCsr& c, const uint32_t* lx, const uint32_t* lv, uint64_t old_n, uint64_t begin,
+                   uint64_t end) {
+  const uint32_t n1 = c.nrows + 1;
+  const uint64_t nn = end - begin;
+  size_t tb = scan_tmp_bytes;
+  launch(EL_K_SCAN, [&] {
+    HIPCHK(hipcub::DeviceScan::ExclusiveSum(scan_tmp, tb, c.dcnt, c.dscan, n1, stream));
+  });
+  host_ev[EL_K_SCAN][EL_EV_ENT] += 2ull * n1;  // read dcnt, write dscan
+  launch(EL_K_MERGE_PTR, [&] {
+    hipLaunchKernelGGL(k_merge_ptr, dim3(grid_for(n1)), dim3(BLOCK), 0, stream, c.ptr2, c.ptr,
+                       c.dscan, n1);
+  });
+  host_ev[EL_K_MERGE_PTR][EL_EV_ENT] += 3ull * n1;  // read ptr, dscan; write ptr2
+  if (old_n) {
+    launch(EL_K_SCATTER_OLD, [&] {
+      hipLaunchKernelGGL(k_scatter_old, dim3(grid_for(old_n)), dim3(BLOCK), 0, stream, c.row,
+                         c.val, c.row2, c.val2, c.dscan, (uint32_t)old_n);
+    });
+    host_ev[EL_K_SCATTER_OLD][EL_EV_TRIG] += old_n;  // read (row, val)
+    host_ev[EL_K_SCATTER_OLD][EL_EV_ENT] += old_n;   // read dscan[row]
+    host_ev[EL_K_SCATTER_OLD][EL_EV_EMIT] += old_n;  // write (row2, val2)
+  }
+  if (nn) {
+    launch(EL_K_SCATTER_NEW, [&] {
+      hipLaunchKernelGGL(k_scatter_new, dim3(grid_for(nn)), dim3(BLOCK), 0, stream, lx, lv,
+                         (uint32_t)begin, (uint32_t)end, c.ptr2, c.dcnt, c.row2, c.val2);
+    });
+    host_ev[EL_K_SCATTER_NEW][EL_EV_TRIG] += nn;  // read log pair
+    host_ev[EL_K_SCATTER_NEW][EL_EV_ENT] += nn;   // read ptr2[x+1]
+    host_ev[EL_K_SCATTER_NEW][EL_EV_RMW] += nn;   // atomicSub dcnt
+    host_ev[EL_K_SCATTER_NEW][EL_EV_EMIT] += nn;  // write (row2, val2)
+  }
+  std::swap(c.ptr, c.ptr2);
+  std::swap(c.row, c.row2);
+  std::swap(c.val, c.val2);
+}
+
+// One Jacobi superstep over the given trigger ranges.  Returns true if anything new.
+bool el_ctx::superstep(uint32_t mask, uint64_t sb, uint64_t se, uint64_t lb, uint64_t le,
+                       uint64_t ab, uint64_t ae) {
+  const bool any_trig = se > sb || le > lb || ((mask & M_RRNG) && ae > ab);
+  if (!any_trig) return false;
+  // ---- generation (read-only on the state; re-run after growing a buffer)
+  HIPCHK(hipMemcpyAsync(ev_backup, ctr->ev, sizeof(hc.ev), hipMemcpyDeviceToDevice, stream));
+  uint64_t saved_launch[EL_NUM_KERNELS];
+  memcpy(saved_launch, launches, sizeof launches);
+  for (;;) {
+    HIPCHK(hipMemsetAsync(&ctr->cand_s, 0, 4 * sizeof(uint32_t), stream));
+    DState st = dstate();
+    if (se > sb)
+      launch(EL_K_EXPAND_S, [&] {
+        hipLaunchKernelGGL(k_expand_s, dim3(grid_for(se - sb)), dim3(BLOCK), 0, stream, ix, st,
+                           (uint32_t)sb, (uint32_t)se, mask, (uint32_t)a_count);
+      });
+    if (le > lb)
+      launch(EL_K_EXPAND_L, [&] {
+        hipLaunchKernelGGL(k_expand_l, dim3(grid_for(le - lb)), dim3(BLOCK), 0, stream, ix, st,
+                           (uint32_t)lb, (uint32_t)le, mask);
+      });
+    if ((mask & M_RRNG) && ae > ab)
+      launch(EL_K_EXPAND_A, [&] {
+        hipLaunchKernelGGL(k_expand_a, dim3(grid_for(hx.N)), dim3(BLOCK), 0, stream, ix, st,
+                           (uint32_t)ab, (uint32_t)ae);
+      });
+    launch(EL_K_JOBS, [&] {
+      hipLaunchKernelGGL(k_jobs, dim3(2048), dim3(BLOCK), 0, stream, ix, st);
+    });
+    sync();
+    read_counters();
+    bool redo = false;
+    if (hc.jobs > job_cap) {
+      job_cap = next_pow2((uint64_t)hc.jobs + hc.jobs / 4);
+      dfree(jobs);
+      jobs = dalloc<uint4>(job_cap);
+      redo = true;
+    }
+    if (hc.cand_s > cs_cap) {
+      cs_cap = next_pow2((uint64_t)hc.cand_s + hc.cand_s / 4);
+      dfree(cs_x);
+      dfree(cs_a);
+      cs_x = dalloc<uint32_t>(cs_cap);
+      cs_a = dalloc<uint32_t>(cs_cap);
+      redo = true;
+    }
+    if (hc.cand_l > cl_cap) {
+      cl_cap = next_pow2((uint64_t)hc.cand_l + hc.cand_l / 4);
+      dfree(cl_x);
+      dfree(cl_p);
+      cl_x = dalloc<uint32_t>(cl_cap);
+      cl_p = dalloc<uint32_t>(cl_cap);
+      redo = true;
+    }
+    if (hc.cand_a > ca_cap) {
+      ca_cap = next_pow2((uint64_t)hc.cand_a + hc.cand_a / 4);
+      dfree(ca_y);
+      dfree(ca_c);
+      ca_y = dalloc<uint32_t>(ca_cap);
+      ca_c = dalloc<uint32_t>(ca_cap);
+      redo = true;
+    }
+    if (!redo) break;
+    // restore counters: the retried generation must count exactly once
+    HIPCHK(hipMemcpyAsync(ctr->ev, ev_backup, sizeof(hc.ev), hipMemcpyDeviceToDevice, stream));
+    memcpy(launches, saved_launch, sizeof launches);
+  }
+  const uint64_t cand_s = hc.cand_s, cand_l = hc.cand_l, cand_a = hc.cand_a;
+  if (cand_s + cand_l + cand_a == 0) return false;
+
+  // ---- capacities for the commit (new facts <= candidates)
+  if (s_count + cand_s > slog_cap) {
+    uint64_t c = next_pow2(s_count + cand_s + (s_count + cand_s) / 2);
+    dgrow(slog_x, s_count, c);
+    dgrow(slog_a, s_count, c);
+    slog_cap = c;
+  }
+  if (s_count + cand_s > S.cap) S.grow(s_count, slog_cap);
+  if (l_count + cand_l > llog_cap) {
+    uint64_t c = next_pow2(l_count + cand_l + (l_count + cand_l) / 2);
+    dgrow(llog_x, l_count, c);
+    dgrow(llog_p, l_count, c);
+    llog_cap = c;
+  }
+  if (l_count + cand_l > PR.cap) PR.grow(l_count, llog_cap);
+  if (l_count + cand_l > SC.cap) SC.grow(l_count, llog_cap);
+  if (2 * (l_count + cand_l) > lhash_cap) rehash_links(next_pow2(4 * (l_count + cand_l)));
+  if (a_count + cand_a > alog_cap) {
+    uint64_t c = next_pow2(a_count + cand_a + 64);
+    dgrow(alog_y, a_count, c);
+    dgrow(alog_c, a_count, c);
+    alog_cap = c;
+  }
+  if (2 * (a_count + cand_a) > ahash_cap) rehash_acts(next_pow2(4 * (a_count + cand_a)));
+
+  // ---- commit
+  DState st = dstate();
+  if (cand_s)
+    launch(EL_K_COMMIT_S, [&] {
+      hipLaunchKernelGGL(k_commit_s, dim3(grid_for(cand_s)), dim3(BLOCK), 0, stream, ix, st,
+                         (uint32_t)cand_s);
+    });
+  if (cand_l)
+    launch(EL_K_COMMIT_L, [&] {
+      hipLaunchKernelGGL(k_commit_l, dim3(grid_for(cand_l)), dim3(BLOCK), 0, stream, ix, st,
+                         (uint32_t)cand_l);
+    });
+  if (cand_a)
+    launch(EL_K_COMMIT_A, [&] {
+      hipLaunchKernelGGL(k_commit_a, dim3(grid_for(cand_a)), dim3(BLOCK), 0, stream, ix, st,
+                         (uint32_t)cand_a);
+    });
+  sync();
+  read_counters();
+  const uint64_t s_new = hc.s_log, l_new = hc.l_log, a_new = hc.a_log;
+  // ---- merge deltas into the CSRs
+  if (s_new > s_count) merge(S, slog_x, slog_a, s_count, s_count, s_new);
+  if (l_new > l_count) {
+    if (hx.P) merge(PR, llog_p, llog_x, l_count, l_count, l_new);
+    merge(SC, llog_x, llog_p, l_count, l_count, l_new);
+  }
+  const bool changed = s_new > s_count || l_new > l_count || a_new > a_count;
+  s_count = s_new;
+  l_count = l_new;
+  a_count = a_new;
+  return changed;
+}
+
+void el_ctx::fill_stats(el_stats* out, double ms) {
+  el_stats st{};
+  st.supersteps = (uint32_t)tr_s.size();
+  st.s_facts = s_count;
+  st.s_init = s_init;
+  st.links = l_count;
+  st.derived = s_count - s_init + l_count;
+  st.activations = a_count;
+  uint64_t bytes = 0;
+  static const uint64_t width[EL_NUM_EVENTS] = {8, 8, 4, 4, 8, 8, 16, 8};
+  for (int k = 0; k < EL_NUM_KERNELS; ++k)
+    for (int e = 0; e < EL_NUM_EVENTS; ++e) bytes += (hc.ev[k][e] + host_ev[k][e]) * width[e];
+  st.bytes = bytes;
+  st.ms = ms;
+  last = st;
+  if (out) *out = st;
+}
+
+// ---------------------------------------------------------------- C ABI
+
+namespace {
+
+int fail(el_ctx* c, int code, const std::string& m) {
+  if (c) c->err = m;
+  return code;
+}
+
+template <class F>
+int guarded(el_ctx* c, F&& f) {
+  if (!c) return EL_EINVAL;
+  try {
+    HIPCHK(hipSetDevice(c->device));
+    return f();
+  } catch (const ElError& e) {
+    return fail(c, e.code, e.msg);
+  } catch (const std::bad_alloc&) {
+    return fail(c, EL_ENOMEM, "host allocation failed");
+  } catch (const std::exception& e) {
+    return fail(c, EL_EHIP, e.what());
+  }
+}
+
+}  // namespace
+
+extern "C" {
+
+int el_abi_version(void) { return EL_ABI_VERSION; }
+
+int el_device_count(int* n) {
+  if (!n) return EL_EINVAL;
+  *n = 0;
+  hipError_t e = hipGetDeviceCount(n);
+  if (e != hipSuccess) {
+    *n = 0;
+    return EL_EHIP;
+  }
+  return EL_OK;
+}
+
+int el_create(el_ctx** out, const el_config* cfg) {
+  if (!out) return EL_EINVAL;
+  *out = nullptr;
+  el_ctx* c = new (std::nothrow) el_ctx();
+  if (!c) return EL_ENOMEM;
+  if (cfg) {
+    if (cfg->flags != 0) {
+      delete c;
+      return EL_EINVAL;
+    }
+    c->device = cfg->device;
+    c->profile = cfg->profile;
+  }
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) {
+    delete c;
+    return EL_EHIP;
+  }
+  if (c->device < 0 || c->device >= n) {
+    delete c;
+    return EL_EINVAL;
+  }
+  int rc = guarded(c, [&] {
+    HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+    return EL_OK;
+  });
+  if (rc != EL_OK) {
+    delete c;
+    return rc;
+  }
+  *out = c;
+  return EL_OK;
+}
+
+int el_load(el_ctx* c, const el_axioms* ax) {
+  if (!c || !ax) return EL_EINVAL;
+  return guarded(c, [&] {
+    el::HostIndex hx;
+    std::string e = el::build_index(*ax, hx);
+    if (!e.empty()) return fail(c, EL_EINVAL, e);
+    HIPCHK(hipStreamSynchronize(c->stream));
+    c->free_state();
+    c->free_index();
+    c->hx = std::move(hx);
+    const el::HostIndex& h = c->hx;
+    auto up32 = [&](const std::vector<uint32_t>& v) {
+      uint32_t* p = dupload(v);
+      c->index_bufs.push_back(p);
+      return (const uint32_t*)p;
+    };
+    auto up8 = [&](const std::vector<uint8_t>& v) {
+      uint8_t* p = dupload(v);
+      c->index_bufs.push_back(p);
+      return (const uint8_t*)p;
+    };
+    DIndex& d = c->ix;
+    d.N = h.N;
+    d.R = h.R;
+    d.P = h.P;
+    d.W = (h.N + 31) / 32;
+    d.kind = up8(h.kind);
+    d.told_ptr = up32(h.told.ptr);
+    d.told_b = up32(h.told.a);
+    d.cidx_ptr = up32(h.cidx.ptr);
+    d.cidx_c = up32(h.cidx.a);
+    d.conj_ptr = up32(h.conj.ptr);
+    d.conj_ops = up32(h.conj.a);
+    d.conj_b = up32(h.conj_b);
+    d.exr_ptr = up32(h.exr.ptr);
+    d.exr_pid = up32(h.exr.a);
+    d.exl_ptr = up32(h.exl.ptr);
+    d.exl_r = up32(h.exl.a);
+    d.exl_b = up32(h.exl.b);
+    d.fp_ptr = up32(h.fp_ptr);
+    d.pair_role = up32(h.pair_role);
+    d.pair_y = up32(h.pair_y);
+    d.psup_ptr = up32(h.psup.ptr);
+    d.psup_pid = up32(h.psup.a);
+    d.chf_ptr = up32(h.chf.ptr);
+    d.chf_s = up32(h.chf.a);
+    d.chf_t = up32(h.chf.b);
+    d.chs_ptr = up32(h.chs.ptr);
+    d.chs_p = up32(h.chs.a);
+    d.chs_t = up32(h.chs.b);
+    d.dom_ptr = up32(h.dom.ptr);
+    d.dom_c = up32(h.dom.a);
+    d.rng_ptr = up32(h.rng.ptr);
+    d.rng_c = up32(h.rng.a);
+    d.role_has_exl = up8(h.role_has_exl);
+    d.has_range = h.rng.a.empty() ? 0u : 1u;
+    c->alloc_state();
+    c->loaded = true;
+    c->inited = false;
+    return EL_OK;
+  });
+}
+
+int el_init(el_ctx* c) {
+  if (!c) return EL_EINVAL;
+  if (!c->loaded) return fail(c, EL_ESTATE, "el_init before el_load");
+  return guarded(c, [&] {
+    c->reset_state();
+    DState st = c->dstate();
+    c->launch(EL_K_INIT, [&] {
+      hipLaunchKernelGGL(k_init, dim3(grid_for(c->hx.N)), dim3(BLOCK), 0, c->stream, c->ix, st);
+    });
+    c->sync();
+    c->read_counters();
+    c->s_count = c->hc.s_log;
+    c->s_init = c->s_count;
+    c->merge(c->S, c->slog_x, c->slog_a, 0, 0, c->s_count);
+    c->sync();
+    c->inited = true;
+    c->fill_stats(nullptr, 0.0);
+    return EL_OK;
+  });
+}
+
+int el_step(el_ctx* c, el_rule rule, int* changed) {
+  if (!c || !changed || (int)rule < 0 || (int)rule >= EL_NUM_RULE_TYPES) return EL_EINVAL;
+  if (!c->inited) return fail(c, EL_ESTATE, "el_step before el_init");
+  return guarded(c, [&] {
+    const int r = (int)rule;
+    const uint64_t se = c->s_count, le = c->l_count, ae = c->a_count;
+    bool ch = c->superstep(kRuleMask[r], c->wm_s[r], se, c->wm_l[r], le, c->wm_a[r], ae);
+    c->wm_s[r] = se;
+    c->wm_l[r] = le;
+    c->wm_a[r] = ae;
+    *changed = ch ? 1 : 0;
+    c->fill_stats(nullptr, 0.0);
+    return EL_OK;
+  });
+}
+
+int el_saturate(el_ctx* c, el_stats* stats) {
+  if (!c) return EL_EINVAL;
+  if (!c->inited) return fail(c, EL_ESTATE, "el_saturate before el_init");
+  return guarded(c, [&] {
+    auto t0 = std::chrono::steady_clock::now();
+    // all rule types share one frontier: start at the oldest watermark
+    uint64_t sb = c->s_count, lb = c->l_count, ab = c->a_count;
+    for (int r = 0; r < EL_NUM_RULE_TYPES; ++r) {
+      sb = std::min(sb, c->wm_s[r]);
+      lb = std::min(lb, c->wm_l[r]);
+      ab = std::min(ab, c->wm_a[r]);
+    }
+    c->tr_s.clear();
+    c->tr_l.clear();
+    c->tr_a.clear();
+    for (;;) {
+      const uint64_t se = c->s_count, le = c->l_count, ae = c->a_count;
+      if (se == sb && le == lb && ae == ab) break;
+      c->tr_s.push_back(se - sb);
+      c->tr_l.push_back(le - lb);
+      c->tr_a.push_back(ae - ab);
+      c->superstep(M_ALL, sb, se, lb, le, ab, ae);
+      sb = se;
+      lb = le;
+      ab = ae;
+    }
+    for (int r = 0; r < EL_NUM_RULE_TYPES; ++r) {
+      c->wm_s[r] = c->s_count;
+      c->wm_l[r] = c->l_count;
+      c->wm_a[r] = c->a_count;
+    }
+    c->sync();
+    c->read_counters();
+    double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    c->fill_stats(stats, ms);
+    return EL_OK;
+  });
+}
+
+int el_get_stats(el_ctx* c, el_stats* stats) {
+  if (!c || !stats) return EL_EINVAL;
+  *stats = c->last;
+  return EL_OK;
+}
+
+int el_kernel_stats(el_ctx* c, el_kernel_stat* out, int n) {
+  if (!c || !out || n < EL_NUM_KERNELS) return EL_EINVAL;
+  return guarded(c, [&] {
+    c->sync();
+    c->read_counters();
+    static const uint64_t width[EL_NUM_EVENTS] = {8, 8, 4, 4, 8, 8, 16, 8};
+    for (int k = 0; k < EL_NUM_KERNELS; ++k) {
+      el_kernel_stat s{};
+      s.launches = c->launches[k];
+      for (int e = 0; e < EL_NUM_EVENTS; ++e) {
+        s.events[e] = c->hc.ev[k][e] + c->host_ev[k][e];
+        s.bytes += s.events[e] * width[e];
+      }
+      s.ms = c->kms[k];
+      out[k] = s;
+    }
+    return EL_OK;
+  });
+}
+
+int el_superstep_trace(el_ctx* c, uint64_t* ds, uint64_t* dl, uint64_t* da, size_t cap, size_t* n) {
+  if (!c || !n) return EL_EINVAL;
+  *n = c->tr_s.size();
+  if (cap < *n) return EL_ERANGE;
+  for (size_t i = 0; i < *n; ++i) {
+    if (ds) ds[i] = c->tr_s[i];
+    if (dl) dl[i] = c->tr_l[i];
+    if (da) da[i] = c->tr_a[i];
+  }
+  return EL_OK;
+}
+
+int el_get_subsumers(el_ctx* c, uint32_t x, uint32_t* out, size_t cap, size_t* n) {
+  if (!c || !n) return EL_EINVAL;
+  if (!c->inited) return fail(c, EL_ESTATE, "no state");
+  if (x >= c->hx.N) return fail(c, EL_EINVAL, "concept id out of range");
+  return guarded(c, [&] {
+    c->sync();
+    uint32_t p[2];
+    HIPCHK(hipMemcpy(p, c->S.ptr + x, 2 * sizeof(uint32_t), hipMemcpyDeviceToHost));
+    *n = p[1] - p[0];
+    if (cap < *n) return EL_ERANGE;
+    if (*n) {
+      HIPCHK(hipMemcpy(out, c->S.val + p[0], *n * sizeof(uint32_t), hipMemcpyDeviceToHost));
+      std::sort(out, out + *n);
+    }
+    return EL_OK;
+  });
+}
+
+int el_copy_facts(el_ctx* c, uint32_t* x, uint32_t* a, size_t cap, size_t* n) {
+  if (!c || !n) return EL_EINVAL;
+  if (!c->inited) return fail(c, EL_ESTATE, "no state");
+  return guarded(c, [&] {
+    c->sync();
+    *n = c->s_count;
+    if (cap < *n) return EL_ERANGE;
+    if (!*n) return EL_OK;
+    std::vector<uint32_t> ptr(c->hx.N + 1);
+    HIPCHK(hipMemcpy(ptr.data(), c->S.ptr, ptr.size() * 4, hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(a, c->S.val, *n * 4, hipMemcpyDeviceToHost));
+    for (uint32_t r = 0; r < c->hx.N; ++r) {
+      for (uint32_t j = ptr[r]; j < ptr[r + 1]; ++j) x[j] = r;
+      std::sort(a + ptr[r], a + ptr[r + 1]);
+    }
+    return EL_OK;
+  });
+}
+
+int el_copy_links(el_ctx* c, uint32_t* x, uint32_t* r, uint32_t* y, size_t cap, size_t* n) {
+  if (!c || !n) return EL_EINVAL;
+  if (!c->inited) return fail(c, EL_ESTATE, "no state");
+  return guarded(c, [&] {
+    c->sync();
+    *n = c->l_count;
+    if (cap < *n) return EL_ERANGE;
+    if (!*n) return EL_OK;
+    std::vector<uint32_t> px(*n), pp(*n);
+    HIPCHK(hipMemcpy(px.data(), c->llog_x, *n * 4, hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(pp.data(), c->llog_p, *n * 4, hipMemcpyDeviceToHost));
+    std::vector<uint64_t> ord(*n);
+    for (size_t i = 0; i < *n; ++i) ord[i] = ((uint64_t)px[i] << 32) | pp[i];
+    std::sort(ord.begin(), ord.end());
+    for (size_t i = 0; i < *n; ++i) {
+      uint32_t xx = (uint32_t)(ord[i] >> 32), p = (uint32_t)ord[i];
+      x[i] = xx;
+      r[i] = c->hx.pair_role[p];
+      y[i] = c->hx.pair_y[p];
+    }
+    return EL_OK;
+  });
+}
+
+int el_export_result(el_ctx* c, int layout, el_sink sink, void* user) {
+  if (!c || !sink || (layout != EL_LAYOUT_X_TO_B && layout != EL_LAYOUT_B_TO_X)) return EL_EINVAL;
+  if (!c->inited) return fail(c, EL_ESTATE, "no state");
+  return guarded(c, [&] {
+    c->sync();
+    const uint32_t N = c->hx.N;
+    std::vector<uint32_t> ptr(N + 1), val(c->s_count);
+    HIPCHK(hipMemcpy(ptr.data(), c->S.ptr, ptr.size() * 4, hipMemcpyDeviceToHost));
+    if (!val.empty())
+      HIPCHK(hipMemcpy(val.data(), c->S.val, val.size() * 4, hipMemcpyDeviceToHost));
+    // result node rows: classes and individuals only (⊥ and datatypes have no key)
+    auto exported = [&](uint32_t x) {
+      return x != EL_BOTTOM && c->hx.kind[x] != EL_KIND_DATATYPE;
+    };
+    std::vector<uint32_t> ks, vs;
+    const size_t batch = 1 << 16;
+    auto flush = [&]() -> int {
+      if (ks.empty()) return 0;
+      int rc = sink(user, ks.data(), vs.data(), ks.size());
+      ks.clear();
+      vs.clear();
+      return rc;
+    };
+    if (layout == EL_LAYOUT_X_TO_B) {
+      for (uint32_t x = 0; x < N; ++x) {
+        if (!exported(x)) continue;
+        std::sort(val.begin() + ptr[x], val.begin() + ptr[x + 1]);
+        for (uint32_t j = ptr[x]; j < ptr[x + 1]; ++j) {
+          ks.push_back(x);
+          vs.push_back(val[j]);
+          if (ks.size() >= batch && flush()) return fail(c, EL_EINVAL, "sink aborted");
+        }
+      }
+    } else {
+      std::vector<uint32_t> cnt(N + 1, 0);
+      for (uint32_t x = 0; x < N; ++x)
+        if (exported(x))
+          for (uint32_t j = ptr[x]; j < ptr[x + 1]; ++j) cnt[val[j] + 1]++;
+      for (uint32_t b = 0; b < N; ++b) cnt[b + 1] += cnt[b];
+      std::vector<uint32_t> mem(cnt[N]);
+      std::vector<uint32_t> cur(cnt.begin(), cnt.end() - 1);
+      for (uint32_t x = 0; x < N; ++x)
+        if (exported(x))
+          for (uint32_t j = ptr[x]; j < ptr[x + 1]; ++j) mem[cur[val[j]]++] = x;
+      for (uint32_t b = 0; b < N; ++b)
+        for (uint32_t j = cnt[b]; j < cnt[b + 1]; ++j) {
+          ks.push_back(b);
+          vs.push_back(mem[j]);
+          if (ks.size() >= batch && flush()) return fail(c, EL_EINVAL, "sink aborted");
+        }
+    }
+    if (flush()) return fail(c, EL_EINVAL, "sink aborted");
+    return EL_OK;
+  });
+}
+
+const char* el_last_error(el_ctx* c) { return c ? c->err.c_str() : "null context"; }
+
+void el_destroy(el_ctx* c) {
+  if (!c) return;
+  (void)hipSetDevice(c->device);
+  if (c->stream) (void)hipStreamSynchronize(c->stream);
+  for (auto& pe : c->pending) {
+    (void)hipEventDestroy(pe.a);
+    (void)hipEventDestroy(pe.b);
+  }
+  for (auto e : c->event_pool) (void)hipEventDestroy(e);
+  c->free_state();
+  c->free_index();
+  if (c->stream) (void)hipStreamDestroy(c->stream);
+  delete c;
+}
+
+}  // extern "C"

@@ -1,0 +1,217 @@
+// el_index.cpp — canonical CSR axiom indexes (see el_index.h).
+//
+// Pair universe.  Links (X, Y) ∈ R(r) only ever point at a filler Y that some
+// CR3 axiom A ⊑ ∃r0.Y names (RolePairHandler.insertRolePair is only reached from
+// CR3, CR5 and CR6: Type2AxiomProcessorBase.java:58-65, Type4…:58-66,
+// Type5…:135-143), and the role of such a link is reachable from r0 through
+// r ⊑ s (CR5) and through the second position of a chain p ∘ s ⊑ t (CR6 emits
+// (X, Z) ∈ R(t) from (Y, Z) ∈ R(s)).  So every possible link target (r, Y) is
+// known before saturation; each gets a dense pair id (pid), sorted by (Y, r).
+#include "el_index.h"
+
+#include <algorithm>
+#include <array>
+#include <cstdio>
+#include <numeric>
+#include <utility>
+
+namespace el {
+
+namespace {
+
+// Build a CSR from (key, a[, b]) triples: rows sorted by (a, b), duplicates removed.
+Csr make_csr(uint32_t rows, std::vector<std::array<uint32_t, 3>>& t, bool two) {
+  std::sort(t.begin(), t.end());
+  t.erase(std::unique(t.begin(), t.end()), t.end());
+  Csr c;
+  c.ptr.assign(rows + 1, 0);
+  for (auto& e : t) c.ptr[e[0] + 1]++;
+  for (uint32_t i = 0; i < rows; ++i) c.ptr[i + 1] += c.ptr[i];
+  c.a.resize(t.size());
+  if (two) c.b.resize(t.size());
+  for (size_t i = 0; i < t.size(); ++i) {
+    c.a[i] = t[i][1];
+    if (two) c.b[i] = t[i][2];
+  }
+  return c;
+}
+
+}  // namespace
+
+std::string build_index(const el_axioms& ax, HostIndex& o) {
+  char msg[256];
+  const uint32_t N = ax.n_concepts, R = ax.n_roles;
+  if (N < 2) return "n_concepts must be >= 2 (⊥ = 0 and ⊤ = 1 are reserved)";
+  o.N = N;
+  o.R = R;
+  o.kind.assign(N, EL_KIND_CLASS);
+  if (ax.concept_kind) {
+    for (uint32_t i = 0; i < N; ++i) {
+      uint8_t k = ax.concept_kind[i];
+      if (k != EL_KIND_CLASS && k != EL_KIND_INDIVIDUAL && k != EL_KIND_DATATYPE) {
+        snprintf(msg, sizeof msg, "concept %u has unknown kind %u", i, (unsigned)k);
+        return msg;
+      }
+      o.kind[i] = k;
+    }
+  }
+  o.kind[EL_BOTTOM] = EL_KIND_CLASS;
+  o.kind[EL_TOP] = EL_KIND_CLASS;
+
+  auto bad_c = [&](uint32_t v) { return v >= N; };
+  auto bad_r = [&](uint32_t v) { return v >= R; };
+#define CHECK(cond, what, i)                                               \
+  if (cond) {                                                              \
+    snprintf(msg, sizeof msg, "%s: id out of range in axiom %u", what, i); \
+    return msg;                                                            \
+  }
+
+  // CR1 told subsumers
+  {
+    std::vector<std::array<uint32_t, 3>> t;
+    t.reserve(ax.n_sub);
+    for (uint32_t i = 0; i < ax.n_sub; ++i) {
+      CHECK(bad_c(ax.sub_a[i]) || bad_c(ax.sub_b[i]), "sub", i);
+      if (ax.sub_a[i] != ax.sub_b[i]) t.push_back({ax.sub_a[i], ax.sub_b[i], 0});
+    }
+    o.told = make_csr(N, t, false);
+  }
+  // CR2 conjunctions: operands sorted/unique per conjunction, conj ids in input order
+  {
+    o.conj.ptr.assign(ax.n_conj + 1, 0);
+    o.conj_b.resize(ax.n_conj);
+    std::vector<std::array<uint32_t, 3>> ci;
+    for (uint32_t c = 0; c < ax.n_conj; ++c) {
+      uint32_t b0 = ax.conj_ptr[c], b1 = ax.conj_ptr[c + 1];
+      if (b1 < b0 || b1 == b0) {
+        snprintf(msg, sizeof msg, "conj %u: empty or malformed operand list", c);
+        return msg;
+      }
+      std::vector<uint32_t> ops(ax.conj_ops + b0, ax.conj_ops + b1);
+      for (uint32_t v : ops) CHECK(bad_c(v), "conj operand", c);
+      CHECK(bad_c(ax.conj_b[c]), "conj rhs", c);
+      std::sort(ops.begin(), ops.end());
+      ops.erase(std::unique(ops.begin(), ops.end()), ops.end());
+      for (uint32_t v : ops) {
+        o.conj.a.push_back(v);
+        ci.push_back({v, c, 0});
+      }
+      o.conj.ptr[c + 1] = (uint32_t)o.conj.a.size();
+      o.conj_b[c] = ax.conj_b[c];
+    }
+    o.cidx = make_csr(N, ci, false);
+  }
+  // role graph: edges r -> s (r ⊑ s) and s -> t (p ∘ s ⊑ t)
+  std::vector<std::vector<uint32_t>> sup_edges(R), reach_edges(R);
+  for (uint32_t i = 0; i < ax.n_subrole; ++i) {
+    CHECK(bad_r(ax.sr_r[i]) || bad_r(ax.sr_s[i]), "subrole", i);
+    sup_edges[ax.sr_r[i]].push_back(ax.sr_s[i]);
+    reach_edges[ax.sr_r[i]].push_back(ax.sr_s[i]);
+  }
+  for (uint32_t i = 0; i < ax.n_chain; ++i) {
+    CHECK(bad_r(ax.ch_r[i]) || bad_r(ax.ch_s[i]) || bad_r(ax.ch_t[i]), "chain", i);
+    reach_edges[ax.ch_s[i]].push_back(ax.ch_t[i]);
+  }
+  auto closure = [&](const std::vector<std::vector<uint32_t>>& g, uint32_t r0, bool refl) {
+    std::vector<uint8_t> seen(R, 0);
+    std::vector<uint32_t> st{r0}, out;
+    seen[r0] = 1;
+    while (!st.empty()) {
+      uint32_t r = st.back();
+      st.pop_back();
+      for (uint32_t s : g[r])
+        if (!seen[s]) {
+          seen[s] = 1;
+          st.push_back(s);
+        }
+    }
+    for (uint32_t r = 0; r < R; ++r)
+      if (seen[r] && (refl || r != r0)) out.push_back(r);
+    return out;
+  };
+  std::vector<std::vector<uint32_t>> supers(R), reach(R);
+  for (uint32_t r = 0; r < R; ++r) {
+    supers[r] = closure(sup_edges, r, false);  // strict supers+(r), r itself excluded
+    reach[r] = closure(reach_edges, r, true);  // reach*(r), r included
+  }
+
+  // pair universe
+  std::vector<std::pair<uint32_t, uint32_t>> pairs;  // (Y, r)
+  for (uint32_t i = 0; i < ax.n_ex_rhs; ++i) {
+    CHECK(bad_c(ax.exr_a[i]) || bad_r(ax.exr_r[i]) || bad_c(ax.exr_b[i]), "ex_rhs", i);
+    for (uint32_t t : reach[ax.exr_r[i]]) pairs.push_back({ax.exr_b[i], t});
+  }
+  std::sort(pairs.begin(), pairs.end());
+  pairs.erase(std::unique(pairs.begin(), pairs.end()), pairs.end());
+  o.P = (uint32_t)pairs.size();
+  o.pair_role.resize(o.P);
+  o.pair_y.resize(o.P);
+  o.fp_ptr.assign(N + 1, 0);
+  for (uint32_t p = 0; p < o.P; ++p) {
+    o.pair_y[p] = pairs[p].first;
+    o.pair_role[p] = pairs[p].second;
+    o.fp_ptr[pairs[p].first + 1]++;
+  }
+  for (uint32_t y = 0; y < N; ++y) o.fp_ptr[y + 1] += o.fp_ptr[y];
+  auto pid_of = [&](uint32_t r, uint32_t y) -> uint32_t {
+    auto b = pairs.begin() + o.fp_ptr[y], e = pairs.begin() + o.fp_ptr[y + 1];
+    auto it = std::lower_bound(b, e, std::make_pair(y, r));
+    return (it != e && it->second == r) ? (uint32_t)(it - pairs.begin()) : 0xffffffffu;
+  };
+  {
+    std::vector<std::array<uint32_t, 3>> t;
+    for (uint32_t i = 0; i < ax.n_ex_rhs; ++i)
+      t.push_back({ax.exr_a[i], pid_of(ax.exr_r[i], ax.exr_b[i]), 0});
+    o.exr = make_csr(N, t, false);
+  }
+  // CR4 LHS existentials
+  {
+    std::vector<std::array<uint32_t, 3>> t;
+    o.role_has_exl.assign(R, 0);
+    for (uint32_t i = 0; i < ax.n_ex_lhs; ++i) {
+      CHECK(bad_r(ax.exl_r[i]) || bad_c(ax.exl_a[i]) || bad_c(ax.exl_b[i]), "ex_lhs", i);
+      t.push_back({ax.exl_a[i], ax.exl_r[i], ax.exl_b[i]});
+      o.role_has_exl[ax.exl_r[i]] = 1;
+    }
+    o.exl = make_csr(N, t, true);
+  }
+  // CR5 per pair: pids of (s, Y) for every strict super-role s of r
+  {
+    std::vector<std::array<uint32_t, 3>> t;
+    for (uint32_t p = 0; p < o.P; ++p)
+      for (uint32_t s : supers[o.pair_role[p]]) {
+        uint32_t q = pid_of(s, o.pair_y[p]);
+        if (q == 0xffffffffu) return "internal: super-role pair missing from pair universe";
+        t.push_back({p, q, 0});
+      }
+    o.psup = make_csr(o.P, t, false);
+  }
+  // CR6 chain indexes
+  {
+    std::vector<std::array<uint32_t, 3>> f, s;
+    for (uint32_t i = 0; i < ax.n_chain; ++i) {
+      f.push_back({ax.ch_r[i], ax.ch_s[i], ax.ch_t[i]});
+      s.push_back({ax.ch_s[i], ax.ch_r[i], ax.ch_t[i]});
+    }
+    o.chf = make_csr(R, f, true);
+    o.chs = make_csr(R, s, true);
+  }
+  // domain / range
+  {
+    std::vector<std::array<uint32_t, 3>> d, g;
+    for (uint32_t i = 0; i < ax.n_domain; ++i) {
+      CHECK(bad_r(ax.dom_r[i]) || bad_c(ax.dom_c[i]), "domain", i);
+      d.push_back({ax.dom_r[i], ax.dom_c[i], 0});
+    }
+    for (uint32_t i = 0; i < ax.n_range; ++i) {
+      CHECK(bad_r(ax.rng_r[i]) || bad_c(ax.rng_c[i]), "range", i);
+      g.push_back({ax.rng_r[i], ax.rng_c[i], 0});
+    }
+    o.dom = make_csr(R, d, false);
+    o.rng = make_csr(R, g, false);
+  }
+#undef CHECK
+  return "";
+}
+
+}  // namespace el

@@ -1,0 +1,50 @@
+// el_index.h — host-side construction of the device-resident axiom indexes.
+//
+// The reference keeps every axiom type in its own Redis shard keyed by the
+// packed-ID string of the premise (AxiomLoader.java:654-1132).  Here the same
+// information becomes read-only CSR arrays in HBM, one per rule family, in a
+// canonical order (every row sorted ascending, duplicates dropped) so the GPU
+// kernels and the CPU oracle count identical algorithmic events.
+#pragma once
+#include <cstdint>
+#include <string>
+#include <vector>
+
+#include "el_gpu.h"
+
+namespace el {
+
+struct Csr {
+  std::vector<uint32_t> ptr;   // rows + 1
+  std::vector<uint32_t> a;     // first value column
+  std::vector<uint32_t> b;     // optional second value column (empty if unused)
+};
+
+struct HostIndex {
+  uint32_t N = 0;   // concepts
+  uint32_t R = 0;   // roles
+  uint32_t P = 0;   // (role, filler) pairs = link targets
+  std::vector<uint8_t> kind;          // EntityType digit per concept
+
+  Csr told;       // A -> B                      CR1  (told(A), B != A)
+  Csr cidx;       // A -> conj id c              CR2  conjunct index (AxiomLoader.java:931-941, DB3)
+  Csr conj;       // c -> operands (sorted)      CR2
+  std::vector<uint32_t> conj_b;     // c -> B
+  Csr exr;        // A -> pid                    CR3  (A ⊑ ∃r.B)
+  Csr exl;        // A -> (r, B) sorted (r,B)    CR4  (∃r.A ⊑ B)
+  std::vector<uint32_t> fp_ptr;     // Y -> pid range (pairs sorted by (Y, r))
+  std::vector<uint32_t> pair_role;  // pid -> r
+  std::vector<uint32_t> pair_y;     // pid -> Y
+  Csr psup;       // pid -> pids of (s, Y), s ∈ supers+(r)       CR5
+  Csr chf;        // r -> (s, t) for r ∘ s ⊑ t                    CR6 (r first)
+  Csr chs;        // s -> (p, t) for p ∘ s ⊑ t                    CR6 (s second)
+  Csr dom;        // r -> D
+  Csr rng;        // r -> C
+  std::vector<uint8_t> role_has_exl;  // r -> any ∃r.A ⊑ B
+};
+
+// Validates ids and builds the canonical indexes.  Returns "" on success or an
+// error message (the reference throws on unknown concepts, AxiomLoader.java:1343-1354).
+std::string build_index(const el_axioms& ax, HostIndex& out);
+
+}  // namespace el

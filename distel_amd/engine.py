@@ -1,0 +1,316 @@
+"""ctypes binding of the C-ABI (include/el_gpu.h) — the only way Python reaches the GPU.
+
+There is deliberately no CPU fallback: if ``libel_gpu.so`` is missing or no HIP
+device is visible, every call raises ``ElError``.  (The CPU oracle under
+``oracle/`` is test infrastructure and is never imported from here.)
+"""
+from __future__ import annotations
+
+import ctypes as C
+import enum
+import os
+from typing import Dict, Iterator, List, Optional, Tuple
+
+import numpy as np
+
+from .ir import Axioms
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "lib", "libel_gpu.so")
+
+EL_OK, EL_EINVAL, EL_ENOMEM, EL_EHIP, EL_ESTATE, EL_ERANGE = 0, -1, -2, -3, -4, -5
+LAYOUT_X_TO_B, LAYOUT_B_TO_X = 0, 1
+
+KERNEL_NAMES = ["k_expand_s", "k_expand_l", "k_jobs", "k_expand_a", "k_commit_s", "k_commit_l", "k_commit_a",
+                "hipcub_scan", "k_merge_ptr", "k_scatter_old", "k_scatter_new", "k_init", "k_rehash"]
+EVENT_NAMES = ["trig", "row", "ent", "test", "hash", "emit", "job", "rmw"]
+EVENT_BYTES = [8, 8, 4, 4, 8, 8, 16, 8]
+NUM_KERNELS = len(KERNEL_NAMES)
+NUM_EVENTS = len(EVENT_NAMES)
+
+
+class AxiomDistributionType(enum.IntEnum):
+    """Rule types = ``kc/init/AxiomDistributionType.java:9-31`` (ordinal order)."""
+    CR_TYPE1_1 = 0
+    CR_TYPE1_2 = 1
+    CR_TYPE2 = 2
+    CR_TYPE3_1 = 3
+    CR_TYPE3_2 = 4
+    CR_TYPE4 = 5
+    CR_TYPE5 = 6
+    CR_TYPE_BOTTOM = 7
+
+
+class ElError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"el error {code}: {msg}")
+        self.code = code
+
+
+_u32p = C.POINTER(C.c_uint32)
+_u8p = C.POINTER(C.c_uint8)
+
+
+class _ElAxioms(C.Structure):
+    _fields_ = [
+        ("n_concepts", C.c_uint32), ("n_roles", C.c_uint32), ("concept_kind", _u8p),
+        ("n_sub", C.c_uint32), ("sub_a", _u32p), ("sub_b", _u32p),
+        ("n_conj", C.c_uint32), ("conj_ptr", _u32p), ("conj_ops", _u32p), ("conj_b", _u32p),
+        ("n_ex_rhs", C.c_uint32), ("exr_a", _u32p), ("exr_r", _u32p), ("exr_b", _u32p),
+        ("n_ex_lhs", C.c_uint32), ("exl_r", _u32p), ("exl_a", _u32p), ("exl_b", _u32p),
+        ("n_subrole", C.c_uint32), ("sr_r", _u32p), ("sr_s", _u32p),
+        ("n_chain", C.c_uint32), ("ch_r", _u32p), ("ch_s", _u32p), ("ch_t", _u32p),
+        ("n_domain", C.c_uint32), ("dom_r", _u32p), ("dom_c", _u32p),
+        ("n_range", C.c_uint32), ("rng_r", _u32p), ("rng_c", _u32p),
+    ]
+
+
+class _ElConfig(C.Structure):
+    _fields_ = [("device", C.c_int), ("profile", C.c_int), ("flags", C.c_uint32)]
+
+
+class _ElStats(C.Structure):
+    _fields_ = [("supersteps", C.c_uint32), ("s_facts", C.c_uint64), ("s_init", C.c_uint64),
+                ("links", C.c_uint64), ("derived", C.c_uint64), ("activations", C.c_uint64),
+                ("bytes", C.c_uint64), ("ms", C.c_double)]
+
+
+class _ElKernelStat(C.Structure):
+    _fields_ = [("launches", C.c_uint64), ("events", C.c_uint64 * NUM_EVENTS), ("bytes", C.c_uint64),
+                ("ms", C.c_double)]
+
+
+_SINK = C.CFUNCTYPE(C.c_int, C.c_void_p, _u32p, _u32p, C.c_size_t)
+
+EXPORTED_SYMBOLS = [
+    "el_abi_version", "el_device_count", "el_create", "el_load", "el_init", "el_step", "el_saturate",
+    "el_get_stats", "el_kernel_stats", "el_superstep_trace", "el_get_subsumers", "el_copy_facts",
+    "el_copy_links", "el_export_result", "el_last_error", "el_destroy",
+]
+
+_lib: Optional[C.CDLL] = None
+
+
+def load_library(path: Optional[str] = None) -> C.CDLL:
+    """Load libel_gpu.so (built by ``__graft_entry__.build()``); raise if absent."""
+    global _lib
+    if _lib is not None and path is None:
+        return _lib
+    p = path or os.environ.get("EL_GPU_LIB", LIB_PATH)
+    if not os.path.exists(p):
+        raise ElError(EL_EHIP, f"HIP extension not built: {p} missing (run __graft_entry__.build())")
+    lib = C.CDLL(p)
+    P = C.c_void_p
+    lib.el_abi_version.restype = C.c_int
+    lib.el_device_count.argtypes = [C.POINTER(C.c_int)]
+    lib.el_create.argtypes = [C.POINTER(P), C.POINTER(_ElConfig)]
+    lib.el_load.argtypes = [P, C.POINTER(_ElAxioms)]
+    lib.el_init.argtypes = [P]
+    lib.el_step.argtypes = [P, C.c_int, C.POINTER(C.c_int)]
+    lib.el_saturate.argtypes = [P, C.POINTER(_ElStats)]
+    lib.el_get_stats.argtypes = [P, C.POINTER(_ElStats)]
+    lib.el_kernel_stats.argtypes = [P, C.POINTER(_ElKernelStat), C.c_int]
+    lib.el_superstep_trace.argtypes = [P, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64), C.POINTER(C.c_uint64),
+                                       C.c_size_t, C.POINTER(C.c_size_t)]
+    lib.el_get_subsumers.argtypes = [P, C.c_uint32, _u32p, C.c_size_t, C.POINTER(C.c_size_t)]
+    lib.el_copy_facts.argtypes = [P, _u32p, _u32p, C.c_size_t, C.POINTER(C.c_size_t)]
+    lib.el_copy_links.argtypes = [P, _u32p, _u32p, _u32p, C.c_size_t, C.POINTER(C.c_size_t)]
+    lib.el_export_result.argtypes = [P, C.c_int, _SINK, C.c_void_p]
+    lib.el_last_error.argtypes = [P]
+    lib.el_last_error.restype = C.c_char_p
+    lib.el_destroy.argtypes = [P]
+    lib.el_destroy.restype = None
+    if path is None:
+        _lib = lib
+    return lib
+
+
+def device_count() -> int:
+    lib = load_library()
+    n = C.c_int(0)
+    lib.el_device_count(C.byref(n))
+    return int(n.value)
+
+
+def _ptr(a: np.ndarray, t=_u32p):
+    return a.ctypes.data_as(t) if a.size else None
+
+
+class AxiomsView:
+    """Keeps the numpy columns alive while the C struct points at them."""
+
+    def __init__(self, ax: Axioms):
+        ax.validate()
+        col = lambda a, j: np.ascontiguousarray(a[:, j], dtype=np.uint32)
+        self._keep = []
+
+        def k(a):
+            a = np.ascontiguousarray(a, dtype=np.uint32)
+            self._keep.append(a)
+            return _ptr(a)
+        kind = np.ascontiguousarray(ax.kind, dtype=np.uint8)
+        self._keep.append(kind)
+        s = _ElAxioms()
+        s.n_concepts, s.n_roles, s.concept_kind = ax.n_concepts, ax.n_roles, _ptr(kind, _u8p)
+        s.n_sub, s.sub_a, s.sub_b = len(ax.sub), k(col(ax.sub, 0)), k(col(ax.sub, 1))
+        s.n_conj, s.conj_ptr, s.conj_ops, s.conj_b = ax.n_conj, k(ax.conj_ptr), k(ax.conj_ops), k(ax.conj_b)
+        s.n_ex_rhs, s.exr_a, s.exr_r, s.exr_b = (len(ax.ex_rhs), k(col(ax.ex_rhs, 0)), k(col(ax.ex_rhs, 1)),
+                                                 k(col(ax.ex_rhs, 2)))
+        s.n_ex_lhs, s.exl_r, s.exl_a, s.exl_b = (len(ax.ex_lhs), k(col(ax.ex_lhs, 0)), k(col(ax.ex_lhs, 1)),
+                                                 k(col(ax.ex_lhs, 2)))
+        s.n_subrole, s.sr_r, s.sr_s = len(ax.subrole), k(col(ax.subrole, 0)), k(col(ax.subrole, 1))
+        s.n_chain, s.ch_r, s.ch_s, s.ch_t = (len(ax.chain), k(col(ax.chain, 0)), k(col(ax.chain, 1)),
+                                             k(col(ax.chain, 2)))
+        s.n_domain, s.dom_r, s.dom_c = len(ax.domain), k(col(ax.domain, 0)), k(col(ax.domain, 1))
+        s.n_range, s.rng_r, s.rng_c = len(ax.range), k(col(ax.range, 0)), k(col(ax.range, 1))
+        self.struct = s
+
+
+class Stats(dict):
+    @staticmethod
+    def from_c(s: _ElStats) -> "Stats":
+        return Stats(supersteps=s.supersteps, s_facts=s.s_facts, s_init=s.s_init, links=s.links, derived=s.derived,
+                     activations=s.activations, bytes=s.bytes, ms=s.ms)
+
+
+class Engine:
+    """One GPU saturation context (one DistEL rule cluster), on one device."""
+
+    def __init__(self, device: int = 0, profile: bool = False):
+        self._lib = load_library()
+        self._ctx = C.c_void_p()
+        cfg = _ElConfig(device, 1 if profile else 0, 0)
+        rc = self._lib.el_create(C.byref(self._ctx), C.byref(cfg))
+        if rc != EL_OK:
+            raise ElError(rc, f"el_create(device={device}) failed: no usable HIP device")
+        self.ax: Optional[Axioms] = None
+
+    def _check(self, rc: int, what: str) -> None:
+        if rc != EL_OK:
+            msg = self._lib.el_last_error(self._ctx)
+            raise ElError(rc, f"{what}: {msg.decode() if msg else ''}")
+
+    def close(self) -> None:
+        if self._ctx:
+            self._lib.el_destroy(self._ctx)
+            self._ctx = C.c_void_p()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # ------------------------------------------------------------ lifecycle
+    def load(self, ax: Axioms) -> None:
+        view = AxiomsView(ax)
+        self._check(self._lib.el_load(self._ctx, C.byref(view.struct)), "el_load")
+        self.ax = ax
+
+    def init(self) -> None:
+        self._check(self._lib.el_init(self._ctx), "el_init")
+
+    def step(self, rule: int) -> bool:
+        ch = C.c_int(0)
+        self._check(self._lib.el_step(self._ctx, int(rule), C.byref(ch)), "el_step")
+        return bool(ch.value)
+
+    def saturate(self) -> Stats:
+        s = _ElStats()
+        self._check(self._lib.el_saturate(self._ctx, C.byref(s)), "el_saturate")
+        return Stats.from_c(s)
+
+    def stats(self) -> Stats:
+        s = _ElStats()
+        self._check(self._lib.el_get_stats(self._ctx, C.byref(s)), "el_get_stats")
+        return Stats.from_c(s)
+
+    def kernel_stats(self) -> List[Dict]:
+        arr = (_ElKernelStat * NUM_KERNELS)()
+        self._check(self._lib.el_kernel_stats(self._ctx, arr, NUM_KERNELS), "el_kernel_stats")
+        out = []
+        for k in range(NUM_KERNELS):
+            s = arr[k]
+            out.append(dict(kernel=KERNEL_NAMES[k], launches=int(s.launches), bytes=int(s.bytes), ms=float(s.ms),
+                            events={EVENT_NAMES[e]: int(s.events[e]) for e in range(NUM_EVENTS)}))
+        return out
+
+    def events(self) -> np.ndarray:
+        """(kernels, events) uint64 matrix of algorithmic event counts."""
+        ks = self.kernel_stats()
+        return np.array([[k["events"][e] for e in EVENT_NAMES] for k in ks], dtype=np.uint64)
+
+    def trace(self) -> Tuple[np.ndarray, np.ndarray, np.ndarray]:
+        n = C.c_size_t(0)
+        rc = self._lib.el_superstep_trace(self._ctx, None, None, None, 0, C.byref(n))
+        if rc not in (EL_OK, EL_ERANGE):
+            self._check(rc, "el_superstep_trace")
+        m = n.value
+        a, b, c = (np.zeros(m, dtype=np.uint64) for _ in range(3))
+        p = lambda x: x.ctypes.data_as(C.POINTER(C.c_uint64))
+        self._check(self._lib.el_superstep_trace(self._ctx, p(a), p(b), p(c), m, C.byref(n)), "el_superstep_trace")
+        return a, b, c
+
+    # ------------------------------------------------------------ results
+    def subsumers(self, x: int) -> np.ndarray:
+        n = C.c_size_t(0)
+        rc = self._lib.el_get_subsumers(self._ctx, int(x), None, 0, C.byref(n))
+        if rc not in (EL_OK, EL_ERANGE):
+            self._check(rc, "el_get_subsumers")
+        out = np.zeros(n.value, dtype=np.uint32)
+        self._check(self._lib.el_get_subsumers(self._ctx, int(x), _ptr(out), out.size, C.byref(n)),
+                    "el_get_subsumers")
+        return out
+
+    def facts(self) -> Tuple[np.ndarray, np.ndarray]:
+        """All (x, a) with a ∈ S(x), sorted by (x, a)."""
+        n = C.c_size_t(0)
+        rc = self._lib.el_copy_facts(self._ctx, None, None, 0, C.byref(n))
+        if rc not in (EL_OK, EL_ERANGE):
+            self._check(rc, "el_copy_facts")
+        x = np.zeros(n.value, dtype=np.uint32)
+        a = np.zeros(n.value, dtype=np.uint32)
+        self._check(self._lib.el_copy_facts(self._ctx, _ptr(x), _ptr(a), x.size, C.byref(n)), "el_copy_facts")
+        return x, a
+
+    def links(self) -> Tuple[np.ndarray, np.ndarray, np.ndarray]:
+        """All (x, r, y) with (x, y) ∈ R(r), sorted by (x, r, y)."""
+        n = C.c_size_t(0)
+        rc = self._lib.el_copy_links(self._ctx, None, None, None, 0, C.byref(n))
+        if rc not in (EL_OK, EL_ERANGE):
+            self._check(rc, "el_copy_links")
+        x, r, y = (np.zeros(n.value, dtype=np.uint32) for _ in range(3))
+        self._check(self._lib.el_copy_links(self._ctx, _ptr(x), _ptr(r), _ptr(y), x.size, C.byref(n)),
+                    "el_copy_links")
+        order = np.lexsort((y, r, x))
+        return x[order], r[order], y[order]
+
+    def export_result(self, layout: int = LAYOUT_X_TO_B) -> Tuple[np.ndarray, np.ndarray]:
+        """Stream the result node through the C sink; returns (keys, values)."""
+        ks: List[np.ndarray] = []
+        vs: List[np.ndarray] = []
+
+        def sink(_user, k, v, n):
+            ks.append(np.ctypeslib.as_array(k, shape=(n,)).copy())
+            vs.append(np.ctypeslib.as_array(v, shape=(n,)).copy())
+            return 0
+        cb = _SINK(sink)
+        self._check(self._lib.el_export_result(self._ctx, int(layout), cb, None), "el_export_result")
+        if not ks:
+            return np.zeros(0, np.uint32), np.zeros(0, np.uint32)
+        return np.concatenate(ks), np.concatenate(vs)
+
+
+def classify(ax: Axioms, device: int = 0, profile: bool = False) -> Tuple[Engine, Stats]:
+    """Load + init + saturate in one call (ELClassifier.classify() over all rule types)."""
+    eng = Engine(device=device, profile=profile)
+    eng.load(ax)
+    eng.init()
+    st = eng.saturate()
+    return eng, st

@@ -1,0 +1,365 @@
+"""Normalized EL+ axiom IR — the input boundary of the engine.
+
+DistEL's AxiomLoader (``kc/init/AxiomLoader.java:126-207``) parses a normalized
+OWL ontology, types every axiom into one rule family
+(``categorizeAxiomsIntoTypes`` :495-577) and writes one Redis key layout per
+family (``insertType{11,12,2,31,4,5}Axioms`` :654-1132).  This module holds the
+same typed content as dense integer arrays, one group per rule crosswalk row
+(SURVEY.md §0), which is exactly what ``el_load`` (include/el_gpu.h) copies to
+the device.
+
+Id conventions (``kc/misc/Constants.java:30-31``, ``kc/init/EntityType.java:9-12``):
+
+* concept id 0 is owl:Nothing (⊥), concept id 1 is owl:Thing (⊤);
+* classes, individuals and datatypes share the concept id space, ``kind`` holds
+  the EntityType digit (0 class, 1 individual, 3 datatype);
+* roles have their own dense id space.
+
+The text form (``.elax``) is a line format a human can write for known-answer
+tests::
+
+    elax 1
+    concept A                # declares a class (implicit on first use)
+    individual a
+    datatype xsd:string
+    role r
+    sub A B                  # A ⊑ B                CR_TYPE1_1
+    conj B A1 A2 ...         # A1 ⊓ … ⊓ An ⊑ B      CR_TYPE1_2
+    some_rhs A r B           # A ⊑ ∃r.B             CR_TYPE2
+    some_lhs r A B           # ∃r.A ⊑ B             CR_TYPE3_1
+    subrole r s              # r ⊑ s                CR_TYPE4
+    chain r s t              # r ∘ s ⊑ t            CR_TYPE5
+    transitive r             # r ∘ r ⊑ r
+    domain r D
+    range r C
+    assert_class a C         # {a} ⊑ C   (ClassAssertion)
+    assert_role r a b        # {a} ⊑ ∃r.{b}  (ObjectPropertyAssertion, AxiomLoader.java:764-765)
+"""
+from __future__ import annotations
+
+import dataclasses
+import hashlib
+import io
+from typing import Dict, Iterable, List, Optional, Sequence, Tuple
+
+import numpy as np
+
+BOTTOM = 0
+TOP = 1
+BOTTOM_NAME = "owl:Nothing"
+TOP_NAME = "owl:Thing"
+
+KIND_CLASS = 0
+KIND_INDIVIDUAL = 1
+KIND_ROLE = 2
+KIND_DATATYPE = 3
+
+U32 = np.uint32
+
+
+def _arr(x, cols: int) -> np.ndarray:
+    a = np.asarray(x, dtype=np.int64)
+    if a.size == 0:
+        return np.zeros((0, cols), dtype=U32)
+    a = a.reshape(-1, cols)
+    if (a < 0).any() or (a > 0xFFFFFFFF).any():
+        raise ValueError("ids must fit uint32")
+    return np.ascontiguousarray(a.astype(U32))
+
+
+@dataclasses.dataclass
+class Axioms:
+    """Typed normalized axioms over dense ids (see module docstring)."""
+
+    n_concepts: int
+    n_roles: int
+    kind: np.ndarray                       # uint8[n_concepts]
+    sub: np.ndarray                        # (n, 2)  A ⊑ B
+    conj_ptr: np.ndarray                   # uint32[n_conj + 1]
+    conj_ops: np.ndarray                   # uint32[conj_ptr[-1]]
+    conj_b: np.ndarray                     # uint32[n_conj]
+    ex_rhs: np.ndarray                     # (n, 3)  (A, r, B): A ⊑ ∃r.B
+    ex_lhs: np.ndarray                     # (n, 3)  (r, A, B): ∃r.A ⊑ B
+    subrole: np.ndarray                    # (n, 2)  r ⊑ s
+    chain: np.ndarray                      # (n, 3)  r ∘ s ⊑ t
+    domain: np.ndarray                     # (n, 2)  (r, D)
+    range: np.ndarray                      # (n, 2)  (r, C)
+    concept_names: Optional[List[str]] = None
+    role_names: Optional[List[str]] = None
+
+    # ------------------------------------------------------------ construction
+    @staticmethod
+    def build(n_concepts: int, n_roles: int, kind=None, sub=(), conj: Sequence[Tuple[Sequence[int], int]] = (),
+              ex_rhs=(), ex_lhs=(), subrole=(), chain=(), domain=(), range=(),
+              concept_names=None, role_names=None) -> "Axioms":
+        if n_concepts < 2:
+            raise ValueError("n_concepts must be >= 2 (⊥ and ⊤ are reserved)")
+        k = np.zeros(n_concepts, dtype=np.uint8) if kind is None else np.asarray(kind, dtype=np.uint8).copy()
+        if k.shape != (n_concepts,):
+            raise ValueError("kind must have n_concepts entries")
+        ptr = [0]
+        ops: List[int] = []
+        rhs: List[int] = []
+        for operands, b in conj:
+            operands = list(operands)
+            if not operands:
+                raise ValueError("empty conjunction")
+            ops.extend(operands)
+            ptr.append(len(ops))
+            rhs.append(b)
+        return Axioms(
+            n_concepts=int(n_concepts), n_roles=int(n_roles), kind=k,
+            sub=_arr(sub, 2),
+            conj_ptr=np.asarray(ptr, dtype=U32), conj_ops=np.asarray(ops, dtype=U32),
+            conj_b=np.asarray(rhs, dtype=U32),
+            ex_rhs=_arr(ex_rhs, 3), ex_lhs=_arr(ex_lhs, 3), subrole=_arr(subrole, 2),
+            chain=_arr(chain, 3), domain=_arr(domain, 2), range=_arr(range, 2),
+            concept_names=concept_names, role_names=role_names)
+
+    @property
+    def n_conj(self) -> int:
+        return int(len(self.conj_b))
+
+    def counts(self) -> Dict[str, int]:
+        """Per-rule-type axiom counts (OntologyStats.printOntologyStats analogue)."""
+        return {"CR_TYPE1_1": len(self.sub), "CR_TYPE1_2": self.n_conj, "CR_TYPE2": len(self.ex_rhs),
+                "CR_TYPE3_1": len(self.ex_lhs), "CR_TYPE4": len(self.subrole), "CR_TYPE5": len(self.chain),
+                "domain": len(self.domain), "range": len(self.range)}
+
+    def validate(self) -> None:
+        n, r = self.n_concepts, self.n_roles
+
+        def chk(a, lim, what):
+            if a.size and int(a.max()) >= lim:
+                raise ValueError(f"{what}: id out of range")
+        chk(self.sub, n, "sub")
+        chk(self.conj_ops, n, "conj")
+        chk(self.conj_b, n, "conj")
+        chk(self.ex_rhs[:, [0, 2]], n, "some_rhs")
+        chk(self.ex_rhs[:, 1], r, "some_rhs role")
+        chk(self.ex_lhs[:, [1, 2]], n, "some_lhs")
+        chk(self.ex_lhs[:, 0], r, "some_lhs role")
+        chk(self.subrole, r, "subrole")
+        chk(self.chain, r, "chain")
+        chk(self.domain[:, 0], r, "domain")
+        chk(self.domain[:, 1], n, "domain")
+        chk(self.range[:, 0], r, "range")
+        chk(self.range[:, 1], n, "range")
+        if not set(np.unique(self.kind).tolist()) <= {KIND_CLASS, KIND_INDIVIDUAL, KIND_DATATYPE}:
+            raise ValueError("unknown concept kind")
+
+    def digest(self) -> str:
+        """SHA-256 over the typed arrays (fixture / generator pinning)."""
+        h = hashlib.sha256()
+        h.update(np.asarray([self.n_concepts, self.n_roles], dtype=np.uint64).tobytes())
+        for a in (self.kind, self.sub, self.conj_ptr, self.conj_ops, self.conj_b, self.ex_rhs, self.ex_lhs,
+                  self.subrole, self.chain, self.domain, self.range):
+            h.update(np.ascontiguousarray(a).tobytes())
+        return h.hexdigest()
+
+    def concept_name(self, i: int) -> str:
+        if self.concept_names is not None:
+            return self.concept_names[i]
+        return {BOTTOM: BOTTOM_NAME, TOP: TOP_NAME}.get(i, f"C{i}")
+
+    def role_name(self, i: int) -> str:
+        return self.role_names[i] if self.role_names is not None else f"r{i}"
+
+    # ------------------------------------------------------------ text form
+    def to_text(self) -> str:
+        out = io.StringIO()
+        out.write("elax 1\n")
+        kinds = {KIND_CLASS: "concept", KIND_INDIVIDUAL: "individual", KIND_DATATYPE: "datatype"}
+        for i in range(2, self.n_concepts):
+            out.write(f"{kinds[int(self.kind[i])]} {self.concept_name(i)}\n")
+        for r in range(self.n_roles):
+            out.write(f"role {self.role_name(r)}\n")
+        c, rn = self.concept_name, self.role_name
+        for a, b in self.sub:
+            out.write(f"sub {c(a)} {c(b)}\n")
+        for i in range(self.n_conj):
+            ops = " ".join(c(o) for o in self.conj_ops[self.conj_ptr[i]:self.conj_ptr[i + 1]])
+            out.write(f"conj {c(self.conj_b[i])} {ops}\n")
+        for a, r, b in self.ex_rhs:
+            out.write(f"some_rhs {c(a)} {rn(r)} {c(b)}\n")
+        for r, a, b in self.ex_lhs:
+            out.write(f"some_lhs {rn(r)} {c(a)} {c(b)}\n")
+        for r, s in self.subrole:
+            out.write(f"subrole {rn(r)} {rn(s)}\n")
+        for r, s, t in self.chain:
+            out.write(f"chain {rn(r)} {rn(s)} {rn(t)}\n")
+        for r, d in self.domain:
+            out.write(f"domain {rn(r)} {c(d)}\n")
+        for r, d in self.range:
+            out.write(f"range {rn(r)} {c(d)}\n")
+        return out.getvalue()
+
+
+class _Builder:
+    def __init__(self):
+        self.concepts: Dict[str, int] = {BOTTOM_NAME: BOTTOM, TOP_NAME: TOP}
+        self.cnames: List[str] = [BOTTOM_NAME, TOP_NAME]
+        self.kinds: List[int] = [KIND_CLASS, KIND_CLASS]
+        self.roles: Dict[str, int] = {}
+        self.rnames: List[str] = []
+        self.sub: List[Tuple[int, int]] = []
+        self.conj: List[Tuple[List[int], int]] = []
+        self.ex_rhs: List[Tuple[int, int, int]] = []
+        self.ex_lhs: List[Tuple[int, int, int]] = []
+        self.subrole: List[Tuple[int, int]] = []
+        self.chain: List[Tuple[int, int, int]] = []
+        self.domain: List[Tuple[int, int]] = []
+        self.range: List[Tuple[int, int]] = []
+
+    def c(self, name: str, kind: int = KIND_CLASS, declare: bool = False) -> int:
+        i = self.concepts.get(name)
+        if i is None:
+            i = len(self.cnames)
+            self.concepts[name] = i
+            self.cnames.append(name)
+            self.kinds.append(kind)
+        elif declare and i > TOP:
+            self.kinds[i] = kind
+        return i
+
+    def r(self, name: str) -> int:
+        i = self.roles.get(name)
+        if i is None:
+            i = len(self.rnames)
+            self.roles[name] = i
+            self.rnames.append(name)
+        return i
+
+    def axioms(self) -> Axioms:
+        return Axioms.build(len(self.cnames), len(self.rnames), kind=self.kinds, sub=self.sub, conj=self.conj,
+                            ex_rhs=self.ex_rhs, ex_lhs=self.ex_lhs, subrole=self.subrole, chain=self.chain,
+                            domain=self.domain, range=self.range, concept_names=list(self.cnames),
+                            role_names=list(self.rnames))
+
+
+def parse_text(text: str) -> Axioms:
+    """Parse the ``.elax`` line format (see module docstring)."""
+    b = _Builder()
+    arity = {"concept": 1, "individual": 1, "datatype": 1, "role": 1, "sub": 2, "some_rhs": 3, "some_lhs": 3,
+             "subrole": 2, "chain": 3, "transitive": 1, "domain": 2, "range": 2, "assert_class": 2,
+             "assert_role": 3}
+    for ln, raw in enumerate(text.splitlines(), 1):
+        line = raw.split("#", 1)[0].strip()
+        if not line:
+            continue
+        tok = line.split()
+        op, args = tok[0], tok[1:]
+        if op == "elax":
+            if args != ["1"]:
+                raise ValueError(f"line {ln}: unsupported elax version {args}")
+            continue
+        if op == "conj":
+            if len(args) < 2:
+                raise ValueError(f"line {ln}: conj needs a rhs and at least one operand")
+            b.conj.append(([b.c(x) for x in args[1:]], b.c(args[0])))
+            continue
+        if op not in arity:
+            raise ValueError(f"line {ln}: unknown directive {op!r}")
+        if len(args) != arity[op]:
+            raise ValueError(f"line {ln}: {op} takes {arity[op]} arguments")
+        if op == "concept":
+            b.c(args[0], KIND_CLASS, True)
+        elif op == "individual":
+            b.c(args[0], KIND_INDIVIDUAL, True)
+        elif op == "datatype":
+            b.c(args[0], KIND_DATATYPE, True)
+        elif op == "role":
+            b.r(args[0])
+        elif op == "sub":
+            b.sub.append((b.c(args[0]), b.c(args[1])))
+        elif op == "some_rhs":
+            b.ex_rhs.append((b.c(args[0]), b.r(args[1]), b.c(args[2])))
+        elif op == "some_lhs":
+            b.ex_lhs.append((b.r(args[0]), b.c(args[1]), b.c(args[2])))
+        elif op == "subrole":
+            b.subrole.append((b.r(args[0]), b.r(args[1])))
+        elif op == "chain":
+            b.chain.append((b.r(args[0]), b.r(args[1]), b.r(args[2])))
+        elif op == "transitive":
+            r = b.r(args[0])
+            b.chain.append((r, r, r))
+        elif op == "domain":
+            b.domain.append((b.r(args[0]), b.c(args[1])))
+        elif op == "range":
+            b.range.append((b.r(args[0]), b.c(args[1])))
+        elif op == "assert_class":
+            b.sub.append((b.c(args[0], KIND_INDIVIDUAL), b.c(args[1])))
+        elif op == "assert_role":
+            b.ex_rhs.append((b.c(args[1], KIND_INDIVIDUAL), b.r(args[0]), b.c(args[2], KIND_INDIVIDUAL)))
+    return b.axioms()
+
+
+def load(path: str) -> Axioms:
+    with open(path, "r", encoding="utf-8") as f:
+        return parse_text(f.read())
+
+
+def save(ax: Axioms, path: str) -> None:
+    with open(path, "w", encoding="utf-8") as f:
+        f.write(ax.to_text())
+
+
+def replicate(ax: Axioms, copies: int) -> Axioms:
+    """``copies`` disjoint copies of an ontology (OntologyMultiplier semantics,
+    ``kc/samples/OntologyMultiplier.java:44-83``: every class and property gets a
+    suffix ``_i``; ⊤ and ⊥ stay shared).  Copy i keeps its concepts contiguous:
+    ids 2.. of copy i are ``2 + i * (n - 2) + (old - 2)``."""
+    if copies < 1:
+        raise ValueError("copies >= 1")
+    n, r = ax.n_concepts, ax.n_roles
+    m = n - 2
+
+    def cmap(a: np.ndarray, i: int) -> np.ndarray:
+        a = a.astype(np.int64)
+        return np.where(a < 2, a, a + i * m).astype(U32)
+
+    def rmap(a: np.ndarray, i: int) -> np.ndarray:
+        return (a.astype(np.int64) + i * r).astype(U32)
+
+    parts = {k: [] for k in ("sub", "ex_rhs", "ex_lhs", "subrole", "chain", "domain", "range", "ops", "b")}
+    ptr = [0]
+    for i in range(copies):
+        parts["sub"].append(cmap(ax.sub, i))
+        e = ax.ex_rhs.copy()
+        e[:, [0, 2]] = cmap(ax.ex_rhs[:, [0, 2]], i)
+        e[:, 1] = rmap(ax.ex_rhs[:, 1], i)
+        parts["ex_rhs"].append(e)
+        e = ax.ex_lhs.copy()
+        e[:, [1, 2]] = cmap(ax.ex_lhs[:, [1, 2]], i)
+        e[:, 0] = rmap(ax.ex_lhs[:, 0], i)
+        parts["ex_lhs"].append(e)
+        parts["subrole"].append(rmap(ax.subrole, i))
+        parts["chain"].append(rmap(ax.chain, i))
+        for key in ("domain", "range"):
+            e = getattr(ax, key).copy()
+            e[:, 0] = rmap(e[:, 0], i)
+            e[:, 1] = cmap(e[:, 1], i)
+            parts[key].append(e)
+        parts["ops"].append(cmap(ax.conj_ops, i))
+        parts["b"].append(cmap(ax.conj_b, i))
+        ptr.extend((ax.conj_ptr[1:].astype(np.int64) + ptr[-1]).tolist())
+    kind = np.concatenate([ax.kind[:2]] + [ax.kind[2:]] * copies)
+    names = None
+    if ax.concept_names is not None:
+        names = ax.concept_names[:2] + [f"{nm}_{i}" for i in range(copies) for nm in ax.concept_names[2:]]
+    rnames = None
+    if ax.role_names is not None:
+        rnames = [f"{nm}_{i}" for i in range(copies) for nm in ax.role_names]
+    cat = lambda k, cols: np.ascontiguousarray(np.concatenate(parts[k]).reshape(-1, cols).astype(U32))
+    return Axioms(n_concepts=2 + copies * m, n_roles=copies * r, kind=kind.astype(np.uint8),
+                  sub=cat("sub", 2), conj_ptr=np.asarray(ptr, dtype=U32),
+                  conj_ops=np.concatenate(parts["ops"]).astype(U32), conj_b=np.concatenate(parts["b"]).astype(U32),
+                  ex_rhs=cat("ex_rhs", 3), ex_lhs=cat("ex_lhs", 3), subrole=cat("subrole", 2),
+                  chain=cat("chain", 3), domain=cat("domain", 2), range=cat("range", 2),
+                  concept_names=names, role_names=rnames)
+
+
+def copy_slice(ax: Axioms, copies: int, index: int) -> Tuple[int, int]:
+    """Concept-id range [lo, hi) owned by copy ``index`` of ``replicate(ax, copies)``."""
+    m = ax.n_concepts - 2
+    return 2 + index * m, 2 + (index + 1) * m

@@ -1,0 +1,226 @@
+/*
+ * el_gpu.h — C-ABI of the MI355X-native EL+ saturation engine (distel_amd).
+ *
+ * Drop-in boundary for DistEL's hot path:
+ *
+ *   reference interface                                  replaced by
+ *   ---------------------------------------------------  ---------------------------
+ *   AxiomLoader typed KV layout (AxiomLoader.java:597-   el_load()   (typed uint32 arrays,
+ *     1132, ids from mapConceptToID :1155-1341)                       one per rule crosswalk row)
+ *   S(X)={X,T} init (AxiomLoader.java:1237-1245,         el_init()
+ *     individuals :1281-1289)
+ *   AxiomProcessor.processOneWorkChunk(...) -> boolean   el_step(ctx, rule, &changed)
+ *     (base/AxiomProcessor.java:14-21), dispatched by
+ *     ELClassifier.classify() switch (ELClassifier.java:74-111)
+ *   whole classify-all.sh run + CommunicationHandler     el_saturate()
+ *     termination (CommunicationHandler.java:49-84)
+ *   result node DB0 B->{X} / ResultRearranger DB1         el_export_result(), el_get_subsumers()
+ *     X->{B} (ResultRearranger.java:57-105)
+ *   AxiomCounter totals (AxiomCounter.java:168-216)      el_stats
+ *
+ * Conventions
+ *   - Concept ids are dense uint32 in [0, n_concepts).  0 = owl:Nothing (BOTTOM_ID,
+ *     Constants.java:30), 1 = owl:Thing (TOP_ID, Constants.java:31).  Classes,
+ *     individuals and datatypes share this space; concept_kind[] carries the
+ *     EntityType digit (EntityType.java:9-12: 0 class, 1 individual, 3 datatype).
+ *   - Role ids are dense uint32 in [0, n_roles) (their own space).
+ *   - Every function returns 0 (EL_OK) or a negative EL_E* code; no C++ exception
+ *     crosses the ABI.  el_last_error() gives the message for the last failure.
+ *   - Input arrays are COPIED; the caller keeps ownership.
+ *   - A context is single-threaded (like one DistEL rule process); independent
+ *     contexts are thread-safe.  Multi-GPU = one context per rank (config.device).
+ *   - There is no CPU fallback: every compute entry point runs HIP kernels on
+ *     gfx950 and fails with EL_EHIP when no device is present.
+ */
+#ifndef EL_GPU_H
+#define EL_GPU_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define EL_ABI_VERSION 1
+
+/* return codes */
+#define EL_OK        0
+#define EL_EINVAL   -1   /* bad argument / malformed axioms (AxiomLoader.java:1343-1354 throws) */
+#define EL_ENOMEM   -2   /* device or host allocation failed */
+#define EL_EHIP     -3   /* HIP runtime error (no device, launch failure, ...) */
+#define EL_ESTATE   -4   /* call out of order (e.g. el_step before el_init) */
+#define EL_ERANGE   -5   /* caller buffer too small; *n holds the size needed */
+
+/* concept kinds = EntityType digits (EntityType.java:9-12) */
+#define EL_KIND_CLASS      0
+#define EL_KIND_INDIVIDUAL 1
+#define EL_KIND_DATATYPE   3
+
+#define EL_BOTTOM 0u
+#define EL_TOP    1u
+
+/* Per-rule-type entry points = AxiomDistributionType (init/AxiomDistributionType.java:9-31).
+ * Each maps to the completion rules it owns in this engine:
+ *   CR_TYPE1_1  CR1  A ⊑ B
+ *   CR_TYPE1_2  CR2  A1 ⊓ … ⊓ An ⊑ B
+ *   CR_TYPE2    CR3  A ⊑ ∃r.B, plus domain/range class assertions
+ *               (RolePairHandler.insertClassAssertions :456-491 runs in the T2 process)
+ *   CR_TYPE3_1  CR4 half-1: new A ∈ S(Y), ∃r.A ⊑ B, (X,Y) ∈ R(r)  => B ∈ S(X)
+ *   CR_TYPE3_2  CR4 half-2: new (X,Y) ∈ R(r), A ∈ S(Y), ∃r.A ⊑ B  => B ∈ S(X)
+ *   CR_TYPE4    CR5  r ⊑ s
+ *   CR_TYPE5    CR6  r ∘ s ⊑ t
+ *   CR_TYPE_BOTTOM  ⊥ ∈ S(Y), (X,Y) ∈ R(r) => ⊥ ∈ S(X)               */
+typedef enum el_rule {
+  EL_CR_TYPE1_1 = 0,
+  EL_CR_TYPE1_2 = 1,
+  EL_CR_TYPE2 = 2,
+  EL_CR_TYPE3_1 = 3,
+  EL_CR_TYPE3_2 = 4,
+  EL_CR_TYPE4 = 5,
+  EL_CR_TYPE5 = 6,
+  EL_CR_TYPE_BOTTOM = 7,
+  EL_NUM_RULE_TYPES = 8
+} el_rule;
+
+/* Normalized axioms, one typed array group per rule crosswalk row.
+ * All pointers may be NULL when the matching count is 0. */
+typedef struct el_axioms {
+  uint32_t n_concepts;            /* >= 2 (⊥, ⊤) */
+  uint32_t n_roles;
+  const uint8_t* concept_kind;    /* n_concepts entries, or NULL = all classes */
+
+  /* CR1  A ⊑ B                                   (insertType11Axioms :959-1049) */
+  uint32_t n_sub;
+  const uint32_t* sub_a;
+  const uint32_t* sub_b;
+
+  /* CR2  A1 ⊓ … ⊓ An ⊑ B, operands as CSR      (insertType12Axioms :900-957) */
+  uint32_t n_conj;
+  const uint32_t* conj_ptr;       /* n_conj + 1 offsets into conj_ops */
+  const uint32_t* conj_ops;
+  const uint32_t* conj_b;
+
+  /* CR3  A ⊑ ∃r.B (incl. property assertions)   (insertType2Axioms :747-841) */
+  uint32_t n_ex_rhs;
+  const uint32_t* exr_a;
+  const uint32_t* exr_r;
+  const uint32_t* exr_b;
+
+  /* CR4  ∃r.A ⊑ B                                (insertType31Axioms :654-729) */
+  uint32_t n_ex_lhs;
+  const uint32_t* exl_r;
+  const uint32_t* exl_a;
+  const uint32_t* exl_b;
+
+  /* CR5  r ⊑ s                                   (insertType4Axioms :1051-1082) */
+  uint32_t n_subrole;
+  const uint32_t* sr_r;
+  const uint32_t* sr_s;
+
+  /* CR6  r ∘ s ⊑ t  (binary chains only, :1109) (insertType5Axioms :1084-1132) */
+  uint32_t n_chain;
+  const uint32_t* ch_r;
+  const uint32_t* ch_s;
+  const uint32_t* ch_t;
+
+  /* domain(r) = D, range(r) = C                (insertPropertyDomainRangeAxioms :843-898) */
+  uint32_t n_domain;
+  const uint32_t* dom_r;
+  const uint32_t* dom_c;
+  uint32_t n_range;
+  const uint32_t* rng_r;
+  const uint32_t* rng_c;
+} el_axioms;
+
+typedef struct el_config {
+  int device;            /* HIP device ordinal (one context per GPU / rank) */
+  int profile;           /* 1 = record per-kernel HIP-event times (el_kernel_stats) */
+  uint32_t flags;        /* reserved, must be 0 */
+} el_config;
+
+/* Kernel ids for el_kernel_stats: one row per __global__ kernel (names match
+ * the rocprofv3 kernel trace), plus the hipcub scan used by the CSR merges. */
+typedef enum el_kernel {
+  EL_K_EXPAND_S = 0,     /* k_expand_s:  ΔS-triggered CR1, CR2, CR3, CR4 half-1, ⊥ (Y side), range */
+  EL_K_EXPAND_L = 1,     /* k_expand_l:  Δlink-triggered CR4 half-2, CR5, CR6, ⊥, domain/range */
+  EL_K_JOBS = 2,         /* k_jobs:      fan-out over predecessor / S-row / successor lists */
+  EL_K_EXPAND_A = 3,     /* k_expand_a:  range activations, column sweep of S */
+  EL_K_COMMIT_S = 4,     /* k_commit_s:  bit-row atomicOr dedup + ΔS append */
+  EL_K_COMMIT_L = 5,     /* k_commit_l:  link hash-set dedup + Δlink append */
+  EL_K_COMMIT_A = 6,     /* k_commit_a:  activation set dedup */
+  EL_K_SCAN = 7,         /* hipcub exclusive scan of per-row delta counts */
+  EL_K_MERGE_PTR = 8,    /* k_merge_ptr: new row offsets */
+  EL_K_SCATTER_OLD = 9,  /* k_scatter_old: move existing CSR entries */
+  EL_K_SCATTER_NEW = 10, /* k_scatter_new: place delta entries */
+  EL_K_INIT = 11,        /* k_init:      S(X) = {X, ⊤} */
+  EL_K_REHASH = 12,      /* k_rehash:    link / activation set growth */
+  EL_NUM_KERNELS = 13
+} el_kernel;
+
+/* Algorithmic event counters; identical in the CPU oracle. */
+typedef enum el_event {
+  EL_EV_TRIG = 0,   /* trigger facts read             8 B */
+  EL_EV_ROW = 1,    /* index / CSR row lookups        8 B (ptr pair) */
+  EL_EV_ENT = 2,    /* 4-byte index entries read      4 B */
+  EL_EV_TEST = 3,   /* bit-word tests                 4 B */
+  EL_EV_HASH = 4,   /* link / activation set probes   8 B (nominal, one per lookup) */
+  EL_EV_EMIT = 5,   /* candidates / facts written     8 B */
+  EL_EV_JOB = 6,    /* fan-out job records written or read 16 B */
+  EL_EV_RMW = 7,    /* bit-word read-modify-writes    8 B */
+  EL_NUM_EVENTS = 8
+} el_event;
+
+typedef struct el_kernel_stat {
+  uint64_t launches;
+  uint64_t events[EL_NUM_EVENTS];
+  uint64_t bytes;        /* algorithmic bytes = Σ events × width above */
+  double ms;             /* Σ HIP-event time (only with config.profile = 1) */
+} el_kernel_stat;
+
+typedef struct el_stats {
+  uint32_t supersteps;         /* Jacobi supersteps until the delta was empty */
+  uint64_t s_facts;            /* Σ_X |S(X)| over all concepts (incl. init) */
+  uint64_t s_init;             /* init facts (S(X) = {X, ⊤}) */
+  uint64_t links;              /* Σ_r |R(r)| */
+  uint64_t derived;            /* s_facts - s_init + links   */
+  uint64_t activations;        /* range activations (Y, C) */
+  uint64_t bytes;              /* Σ algorithmic bytes over all kernels */
+  double ms;                   /* wall ms of the call (device synchronised) */
+} el_stats;
+
+typedef struct el_ctx el_ctx;
+
+/* batch sink for el_export_result: n (key, value) pairs */
+typedef int (*el_sink)(void* user, const uint32_t* keys, const uint32_t* vals, size_t n);
+
+#define EL_LAYOUT_X_TO_B 0   /* rearranged view X -> {B}   (ResultRearranger DB1) */
+#define EL_LAYOUT_B_TO_X 1   /* result node DB0 B -> {X}   (AxiomLoader.java:1237-1245) */
+
+int el_abi_version(void);
+int el_device_count(int* n);
+
+int el_create(el_ctx** ctx, const el_config* cfg);
+int el_load(el_ctx* ctx, const el_axioms* ax);
+int el_init(el_ctx* ctx);
+int el_step(el_ctx* ctx, el_rule rule, int* changed);
+int el_saturate(el_ctx* ctx, el_stats* stats);
+int el_get_stats(el_ctx* ctx, el_stats* stats);
+int el_kernel_stats(el_ctx* ctx, el_kernel_stat* out, int n);
+/* per-superstep delta sizes of the last el_saturate (|ΔS|, |Δlink|, |Δact|) */
+int el_superstep_trace(el_ctx* ctx, uint64_t* ds, uint64_t* dl, uint64_t* da, size_t cap, size_t* n);
+
+int el_get_subsumers(el_ctx* ctx, uint32_t x, uint32_t* out, size_t cap, size_t* n);
+/* all S facts (x[i], a[i]) meaning a ∈ S(x), grouped by x (rows in id order) */
+int el_copy_facts(el_ctx* ctx, uint32_t* x, uint32_t* a, size_t cap, size_t* n);
+/* all links (x[i], r[i], y[i]) meaning (x, y) ∈ R(r) */
+int el_copy_links(el_ctx* ctx, uint32_t* x, uint32_t* r, uint32_t* y, size_t cap, size_t* n);
+int el_export_result(el_ctx* ctx, int layout, el_sink sink, void* user);
+
+const char* el_last_error(el_ctx* ctx);
+void el_destroy(el_ctx* ctx);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* EL_GPU_H */
