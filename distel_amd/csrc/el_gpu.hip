@@ -46,6 +46,7 @@ namespace {
 constexpr uint32_t NONE = 0xffffffffu;
 constexpr unsigned long long EMPTY_KEY = ~0ull;
 constexpr int BLOCK = 256;
+static_assert(BLOCK <= 512, "commit kernels stage one block round in LDS");
 
 // sub-rule mask bits
 enum : uint32_t {
@@ -223,28 +224,85 @@ __device__ __forceinline__ uint32_t pair_lookup(const DIndex& ix, uint32_t r, ui
   return NONE;
 }
 
-__device__ __forceinline__ void emit_s(const DState& st, bool pred, uint32_t x, uint32_t a, Ev& ev) {
-  uint32_t slot = wave_append(&st.ctr->cand_s, pred);
+// Block-level staging of appended records in LDS.  A single global append counter
+// saturates at ~88 atomics/us (MI355X_MICROARCH.md, row "dequeue"), so candidates are
+// reserved with an LDS atomic per wave and published with ONE global atomic per block
+// flush (>= QS_CAP/2 records).  A full LDS queue spills straight to global memory.
+constexpr uint32_t QS_CAP = 1024;  // S candidates (x, a)
+constexpr uint32_t QL_CAP = 1024;  // link candidates (x, pid)
+constexpr uint32_t QJ_CAP = 256;   // fan-out jobs
+
+struct BlockQ {
+  uint4 jb[QJ_CAP];
+  uint32_t sx[QS_CAP], sa[QS_CAP];
+  uint32_t lx[QL_CAP], lp[QL_CAP];
+  uint32_t ns, nl, nj, bs, bl, bj;
+};
+
+__device__ __forceinline__ void q_init(BlockQ& q) {
+  if (threadIdx.x == 0) q.ns = q.nl = q.nj = 0;
+  __syncthreads();
+}
+
+// LDS slot for each predicated lane (one LDS atomic per wave)
+__device__ __forceinline__ uint32_t lds_reserve(uint32_t* qn, bool pred) {
+  unsigned long long m = __ballot(pred);
+  if (m == 0) return NONE;
+  int leader = __ffsll((long long)m) - 1;
+  uint32_t off = 0;
+  if ((int)lane_id() == leader) off = atomicAdd(qn, (uint32_t)__popcll(m));
+  off = __shfl(off, leader);
+  return pred ? off + (uint32_t)__popcll(m & ((1ull << lane_id()) - 1ull)) : NONE;
+}
+
+__device__ __forceinline__ void emit_s(const DState& st, BlockQ& q, bool pred, uint32_t x, uint32_t a, Ev& ev) {
+  const uint32_t off = lds_reserve(&q.ns, pred);
+  const bool spill = pred && off >= QS_CAP;
   if (pred) {
     ev.v[EL_EV_EMIT]++;
-    if (slot < st.cs_cap) {
-      st.cs_x[slot] = x;
-      st.cs_a[slot] = a;
+    if (!spill) {
+      q.sx[off] = x;
+      q.sa[off] = a;
     }
+  }
+  const uint32_t slot = wave_append(&st.ctr->cand_s, spill);
+  if (spill && slot < st.cs_cap) {
+    st.cs_x[slot] = x;
+    st.cs_a[slot] = a;
   }
 }
 
-__device__ __forceinline__ void emit_l(const DState& st, bool pred, uint32_t x, uint32_t pid, Ev& ev) {
-  uint32_t slot = wave_append(&st.ctr->cand_l, pred);
+__device__ __forceinline__ void emit_l(const DState& st, BlockQ& q, bool pred, uint32_t x, uint32_t pid, Ev& ev) {
+  const uint32_t off = lds_reserve(&q.nl, pred);
+  const bool spill = pred && off >= QL_CAP;
   if (pred) {
     ev.v[EL_EV_EMIT]++;
-    if (slot < st.cl_cap) {
-      st.cl_x[slot] = x;
-      st.cl_p[slot] = pid;
+    if (!spill) {
+      q.lx[off] = x;
+      q.lp[off] = pid;
     }
+  }
+  const uint32_t slot = wave_append(&st.ctr->cand_l, spill);
+  if (spill && slot < st.cl_cap) {
+    st.cl_x[slot] = x;
+    st.cl_p[slot] = pid;
   }
 }
 
+__device__ __forceinline__ void emit_job(const DState& st, BlockQ& q, bool pred, uint32_t type, uint32_t begin,
+                                         uint32_t len, uint32_t a, uint32_t b, Ev& ev) {
+  const uint32_t off = lds_reserve(&q.nj, pred);
+  const bool spill = pred && off >= QJ_CAP;
+  const uint4 rec = make_uint4(begin, len | (type << 28), a, b);
+  if (pred) {
+    ev.v[EL_EV_JOB]++;
+    if (!spill) q.jb[off] = rec;
+  }
+  const uint32_t slot = wave_append(&st.ctr->jobs, spill);
+  if (spill && slot < st.job_cap) st.jobs[slot] = rec;
+}
+
+// activations are rare: plain wave-aggregated global append
 __device__ __forceinline__ void emit_a(const DState& st, bool pred, uint32_t y, uint32_t c, Ev& ev) {
   uint32_t slot = wave_append(&st.ctr->cand_a, pred);
   if (pred) {
@@ -256,13 +314,44 @@ __device__ __forceinline__ void emit_a(const DState& st, bool pred, uint32_t y, 
   }
 }
 
-__device__ __forceinline__ void emit_job(const DState& st, bool pred, uint32_t type, uint32_t begin,
-                                         uint32_t len, uint32_t a, uint32_t b, Ev& ev) {
-  uint32_t slot = wave_append(&st.ctr->jobs, pred);
-  if (pred) {
-    ev.v[EL_EV_JOB]++;
-    if (slot < st.job_cap) st.jobs[slot] = make_uint4(begin, len | (type << 28), a, b);
+// Publish the block's staged records: one global atomic per non-empty queue.
+// Every thread of the block must call this (it contains barriers).
+__device__ void q_flush(BlockQ& q, const DState& st) {
+  __syncthreads();
+  const uint32_t ns = min(q.ns, QS_CAP), nl = min(q.nl, QL_CAP), nj = min(q.nj, QJ_CAP);
+  if (threadIdx.x == 0) {
+    q.bs = ns ? atomicAdd(&st.ctr->cand_s, ns) : 0u;
+    q.bl = nl ? atomicAdd(&st.ctr->cand_l, nl) : 0u;
+    q.bj = nj ? atomicAdd(&st.ctr->jobs, nj) : 0u;
   }
+  __syncthreads();
+  for (uint32_t k = threadIdx.x; k < ns; k += blockDim.x) {
+    const uint32_t slot = q.bs + k;
+    if (slot < st.cs_cap) {
+      st.cs_x[slot] = q.sx[k];
+      st.cs_a[slot] = q.sa[k];
+    }
+  }
+  for (uint32_t k = threadIdx.x; k < nl; k += blockDim.x) {
+    const uint32_t slot = q.bl + k;
+    if (slot < st.cl_cap) {
+      st.cl_x[slot] = q.lx[k];
+      st.cl_p[slot] = q.lp[k];
+    }
+  }
+  for (uint32_t k = threadIdx.x; k < nj; k += blockDim.x) {
+    const uint32_t slot = q.bj + k;
+    if (slot < st.job_cap) st.jobs[slot] = q.jb[k];
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) q.ns = q.nl = q.nj = 0;
+  __syncthreads();
+}
+
+// Called by every thread after each block-uniform loop round.
+__device__ __forceinline__ void q_maybe_flush(BlockQ& q, const DState& st) {
+  __syncthreads();
+  if (q.ns > QS_CAP / 2 || q.nl > QL_CAP / 2 || q.nj > QJ_CAP / 2) q_flush(q, st);
 }
 
 // ---------------------------------------------------------------- kernels
@@ -303,102 +392,108 @@ __global__ void k_init(DIndex ix, DState st) {
 //  ⊥    TypeBottomAxiomProcessorBase.java:62-123  range RolePairHandler.java:471-479 + K10
 __global__ void k_expand_s(DIndex ix, DState st, uint32_t begin, uint32_t end, uint32_t mask,
                            uint32_t a_end) {
+  __shared__ BlockQ q;
+  q_init(q);
   Ev ev;
-  const uint32_t stride = gridDim.x * blockDim.x;
-  for (uint32_t i = begin + blockIdx.x * blockDim.x + threadIdx.x; i < end; i += stride) {
-    const uint32_t X = st.slog_x[i], A = st.slog_a[i];
-    ev.v[EL_EV_TRIG]++;
-    if (mask & M_R1) {  // A ∈ S(X), A ⊑ B  =>  B ∈ S(X)
-      ev.v[EL_EV_ROW]++;
-      const uint32_t b1 = ix.told_ptr[A + 1];
-      for (uint32_t j = ix.told_ptr[A]; j < b1; ++j) {
-        const uint32_t B = ix.told_b[j];
-        ev.v[EL_EV_ENT]++;
-        ev.v[EL_EV_TEST]++;
-        emit_s(st, !test_bit(st.bits, ix.W, X, B), X, B, ev);
-      }
-    }
-    if (mask & M_R2) {  // A1..An ∈ S(X), ⊓Ai ⊑ B  =>  B ∈ S(X)
-      ev.v[EL_EV_ROW]++;
-      const uint32_t c1 = ix.cidx_ptr[A + 1];
-      for (uint32_t j = ix.cidx_ptr[A]; j < c1; ++j) {
-        const uint32_t c = ix.cidx_c[j];
-        ev.v[EL_EV_ENT]++;
+  for (uint32_t base = begin + blockIdx.x * blockDim.x; base < end; base += gridDim.x * blockDim.x) {
+    const uint32_t i = base + threadIdx.x;
+    if (i < end) {
+      const uint32_t X = st.slog_x[i], A = st.slog_a[i];
+      ev.v[EL_EV_TRIG]++;
+      if (mask & M_R1) {  // A ∈ S(X), A ⊑ B  =>  B ∈ S(X)
         ev.v[EL_EV_ROW]++;
-        const uint32_t o1 = ix.conj_ptr[c + 1];
-        bool ok = true;
-        for (uint32_t k = ix.conj_ptr[c]; k < o1; ++k) {
-          const uint32_t op = ix.conj_ops[k];
-          ev.v[EL_EV_ENT]++;
-          if (op == A) continue;
-          ev.v[EL_EV_TEST]++;
-          if (!test_bit(st.bits, ix.W, X, op)) {
-            ok = false;
-            break;
-          }
-        }
-        bool nw = false;
-        const uint32_t B = ix.conj_b[c];
-        if (ok) {
+        const uint32_t b1 = ix.told_ptr[A + 1];
+        for (uint32_t j = ix.told_ptr[A]; j < b1; ++j) {
+          const uint32_t B = ix.told_b[j];
           ev.v[EL_EV_ENT]++;
           ev.v[EL_EV_TEST]++;
-          nw = !test_bit(st.bits, ix.W, X, B);
+          emit_s(st, q, !test_bit(st.bits, ix.W, X, B), X, B, ev);
         }
-        emit_s(st, nw, X, B, ev);
       }
-    }
-    if (mask & M_R3) {  // A ∈ S(X), A ⊑ ∃r.B  =>  (X, B) ∈ R(r)
-      ev.v[EL_EV_ROW]++;
-      const uint32_t e1 = ix.exr_ptr[A + 1];
-      for (uint32_t j = ix.exr_ptr[A]; j < e1; ++j) {
-        const uint32_t pid = ix.exr_pid[j];
-        ev.v[EL_EV_ENT]++;
-        ev.v[EL_EV_HASH]++;
-        emit_l(st, !hash_contains(st.lhash, st.lmask, link_key(pid, X)), X, pid, ev);
-      }
-    }
-    if (mask & M_R4Y) {  // A ∈ S(Y=X) new, ∃r.A ⊑ B, (X', Y) ∈ R(r)  =>  B ∈ S(X')
-      ev.v[EL_EV_ROW]++;
-      const uint32_t e1 = ix.exl_ptr[A + 1];
-      for (uint32_t j = ix.exl_ptr[A]; j < e1; ++j) {
-        const uint32_t r = ix.exl_r[j], B = ix.exl_b[j];
-        ev.v[EL_EV_ENT] += 2;
-        const uint32_t pid = pair_lookup(ix, r, X, ev);
-        uint32_t pb = 0, pl = 0;
-        if (pid != NONE) {
+      if (mask & M_R2) {  // A1..An ∈ S(X), ⊓Ai ⊑ B  =>  B ∈ S(X)
+        ev.v[EL_EV_ROW]++;
+        const uint32_t c1 = ix.cidx_ptr[A + 1];
+        for (uint32_t j = ix.cidx_ptr[A]; j < c1; ++j) {
+          const uint32_t c = ix.cidx_c[j];
+          ev.v[EL_EV_ENT]++;
           ev.v[EL_EV_ROW]++;
-          pb = st.pr_ptr[pid];
-          pl = st.pr_ptr[pid + 1] - pb;
-        }
-        emit_job(st, pl > 0, JOB_PRED_S, pb, pl, 0, B, ev);
-      }
-    }
-    if ((mask & M_RBOT) && A == EL_BOTTOM) {  // ⊥ ∈ S(Y=X) new, (X', Y) ∈ R(*)  =>  ⊥ ∈ S(X')
-      ev.v[EL_EV_ROW]++;
-      const uint32_t p1 = ix.fp_ptr[X + 1];
-      for (uint32_t p = ix.fp_ptr[X]; p < p1; ++p) {
-        ev.v[EL_EV_ROW]++;
-        const uint32_t pb = st.pr_ptr[p], pl = st.pr_ptr[p + 1] - pb;
-        emit_job(st, pl > 0, JOB_PRED_S, pb, pl, 0, EL_BOTTOM, ev);
-      }
-    }
-    if ((mask & M_RRNG) && ix.has_range) {  // Y=A ∈ S(X) new, active range (Y, C)  =>  C ∈ S(X)
-      ev.v[EL_EV_ENT]++;
-      if (st.has_act[A]) {
-        for (uint32_t k = 0; k < a_end; ++k) {
-          ev.v[EL_EV_ENT] += 2;
-          const bool hit = st.alog_y[k] == A;
-          const uint32_t C = st.alog_c[k];
-          bool nw = false;
-          if (hit) {
+          const uint32_t o1 = ix.conj_ptr[c + 1];
+          bool ok = true;
+          for (uint32_t k = ix.conj_ptr[c]; k < o1; ++k) {
+            const uint32_t op = ix.conj_ops[k];
+            ev.v[EL_EV_ENT]++;
+            if (op == A) continue;
             ev.v[EL_EV_TEST]++;
-            nw = !test_bit(st.bits, ix.W, X, C);
+            if (!test_bit(st.bits, ix.W, X, op)) {
+              ok = false;
+              break;
+            }
           }
-          emit_s(st, nw, X, C, ev);
+          bool nw = false;
+          const uint32_t B = ix.conj_b[c];
+          if (ok) {
+            ev.v[EL_EV_ENT]++;
+            ev.v[EL_EV_TEST]++;
+            nw = !test_bit(st.bits, ix.W, X, B);
+          }
+          emit_s(st, q, nw, X, B, ev);
+        }
+      }
+      if (mask & M_R3) {  // A ∈ S(X), A ⊑ ∃r.B  =>  (X, B) ∈ R(r)
+        ev.v[EL_EV_ROW]++;
+        const uint32_t e1 = ix.exr_ptr[A + 1];
+        for (uint32_t j = ix.exr_ptr[A]; j < e1; ++j) {
+          const uint32_t pid = ix.exr_pid[j];
+          ev.v[EL_EV_ENT]++;
+          ev.v[EL_EV_HASH]++;
+          emit_l(st, q, !hash_contains(st.lhash, st.lmask, link_key(pid, X)), X, pid, ev);
+        }
+      }
+      if (mask & M_R4Y) {  // A ∈ S(Y=X) new, ∃r.A ⊑ B, (X', Y) ∈ R(r)  =>  B ∈ S(X')
+        ev.v[EL_EV_ROW]++;
+        const uint32_t e1 = ix.exl_ptr[A + 1];
+        for (uint32_t j = ix.exl_ptr[A]; j < e1; ++j) {
+          const uint32_t r = ix.exl_r[j], B = ix.exl_b[j];
+          ev.v[EL_EV_ENT] += 2;
+          const uint32_t pid = pair_lookup(ix, r, X, ev);
+          uint32_t pb = 0, pl = 0;
+          if (pid != NONE) {
+            ev.v[EL_EV_ROW]++;
+            pb = st.pr_ptr[pid];
+            pl = st.pr_ptr[pid + 1] - pb;
+          }
+          emit_job(st, q, pl > 0, JOB_PRED_S, pb, pl, 0, B, ev);
+        }
+      }
+      if ((mask & M_RBOT) && A == EL_BOTTOM) {  // ⊥ ∈ S(Y=X) new, (X', Y) ∈ R(*)  =>  ⊥ ∈ S(X')
+        ev.v[EL_EV_ROW]++;
+        const uint32_t p1 = ix.fp_ptr[X + 1];
+        for (uint32_t p = ix.fp_ptr[X]; p < p1; ++p) {
+          ev.v[EL_EV_ROW]++;
+          const uint32_t pb = st.pr_ptr[p], pl = st.pr_ptr[p + 1] - pb;
+          emit_job(st, q, pl > 0, JOB_PRED_S, pb, pl, 0, EL_BOTTOM, ev);
+        }
+      }
+      if ((mask & M_RRNG) && ix.has_range) {  // Y=A ∈ S(X) new, active range (Y, C)  =>  C ∈ S(X)
+        ev.v[EL_EV_ENT]++;
+        if (st.has_act[A]) {
+          for (uint32_t k = 0; k < a_end; ++k) {
+            ev.v[EL_EV_ENT] += 2;
+            const bool hit = st.alog_y[k] == A;
+            const uint32_t C = st.alog_c[k];
+            bool nw = false;
+            if (hit) {
+              ev.v[EL_EV_TEST]++;
+              nw = !test_bit(st.bits, ix.W, X, C);
+            }
+            emit_s(st, q, nw, X, C, ev);
+          }
         }
       }
     }
+    q_maybe_flush(q, st);
   }
+  q_flush(q, st);
   ev_flush(st.ctr, EL_K_EXPAND_S, ev);
 }
 
@@ -407,108 +502,114 @@ __global__ void k_expand_s(DIndex ix, DState st, uint32_t begin, uint32_t end, u
 //  CR6  Type5AxiomProcessorBase.java:115-154           ⊥   RolePairHandler.java:358-372
 //  domain/range RolePairHandler.java:456-491
 __global__ void k_expand_l(DIndex ix, DState st, uint32_t begin, uint32_t end, uint32_t mask) {
+  __shared__ BlockQ q;
+  q_init(q);
   Ev ev;
-  const uint32_t stride = gridDim.x * blockDim.x;
-  for (uint32_t i = begin + blockIdx.x * blockDim.x + threadIdx.x; i < end; i += stride) {
-    const uint32_t X = st.llog_x[i], pid = st.llog_p[i];
-    ev.v[EL_EV_TRIG]++;
-    const uint32_t r = ix.pair_role[pid], Y = ix.pair_y[pid];
-    ev.v[EL_EV_ENT] += 2;
-    if (mask & M_R4L) {  // (X, Y) ∈ R(r) new, A ∈ S(Y), ∃r.A ⊑ B  =>  B ∈ S(X)
-      ev.v[EL_EV_ENT]++;
-      const bool has = ix.role_has_exl[r] != 0;
-      uint32_t sb = 0, sl = 0;
-      if (has) {
-        ev.v[EL_EV_ROW]++;
-        sb = st.s_ptr[Y];
-        sl = st.s_ptr[Y + 1] - sb;
-      }
-      emit_job(st, has && sl > 0, JOB_R4L, sb, sl, X, r, ev);
-    }
-    if (mask & M_RBOT) {  // ⊥ ∈ S(Y)  =>  ⊥ ∈ S(X)
-      ev.v[EL_EV_TEST]++;
-      bool nw = false;
-      if (test_bit(st.bits, ix.W, Y, EL_BOTTOM)) {
-        ev.v[EL_EV_TEST]++;
-        nw = !test_bit(st.bits, ix.W, X, EL_BOTTOM);
-      }
-      emit_s(st, nw, X, EL_BOTTOM, ev);
-    }
-    if (mask & M_R5) {  // r ⊑ s  =>  (X, Y) ∈ R(s)
-      ev.v[EL_EV_ROW]++;
-      const uint32_t q1 = ix.psup_ptr[pid + 1];
-      for (uint32_t j = ix.psup_ptr[pid]; j < q1; ++j) {
-        const uint32_t q = ix.psup_pid[j];
+  for (uint32_t base = begin + blockIdx.x * blockDim.x; base < end; base += gridDim.x * blockDim.x) {
+    const uint32_t i = base + threadIdx.x;
+    if (i < end) {
+      const uint32_t X = st.llog_x[i], pid = st.llog_p[i];
+      ev.v[EL_EV_TRIG]++;
+      const uint32_t r = ix.pair_role[pid], Y = ix.pair_y[pid];
+      ev.v[EL_EV_ENT] += 2;
+      if (mask & M_R4L) {  // (X, Y) ∈ R(r) new, A ∈ S(Y), ∃r.A ⊑ B  =>  B ∈ S(X)
         ev.v[EL_EV_ENT]++;
-        ev.v[EL_EV_HASH]++;
-        emit_l(st, !hash_contains(st.lhash, st.lmask, link_key(q, X)), X, q, ev);
-      }
-    }
-    if (mask & M_R6) {  // r ∘ s ⊑ t
-      ev.v[EL_EV_ROW]++;
-      const bool first = ix.chf_ptr[r + 1] > ix.chf_ptr[r];
-      uint32_t sb = 0, sl = 0;
-      if (first) {  // r first: (Y, Z) ∈ R(s)  =>  (X, Z) ∈ R(t)
-        ev.v[EL_EV_ROW]++;
-        sb = st.sc_ptr[Y];
-        sl = st.sc_ptr[Y + 1] - sb;
-      }
-      emit_job(st, first && sl > 0, JOB_R6A, sb, sl, X, r, ev);
-      ev.v[EL_EV_ROW]++;
-      const uint32_t h1 = ix.chs_ptr[r + 1];
-      for (uint32_t j = ix.chs_ptr[r]; j < h1; ++j) {  // r second: (X', X) ∈ R(p)  =>  (X', Y) ∈ R(t)
-        const uint32_t p = ix.chs_p[j], t = ix.chs_t[j];
-        ev.v[EL_EV_ENT] += 2;
-        const uint32_t pq = pair_lookup(ix, p, X, ev);
-        uint32_t pb = 0, pl = 0, pt = NONE;
-        if (pq != NONE) {
+        const bool has = ix.role_has_exl[r] != 0;
+        uint32_t sb = 0, sl = 0;
+        if (has) {
           ev.v[EL_EV_ROW]++;
-          pb = st.pr_ptr[pq];
-          pl = st.pr_ptr[pq + 1] - pb;
-          if (pl) pt = pair_lookup(ix, t, Y, ev);
+          sb = st.s_ptr[Y];
+          sl = st.s_ptr[Y + 1] - sb;
         }
-        emit_job(st, pl > 0, JOB_PRED_L, pb, pl, pt, 0, ev);
+        emit_job(st, q, has && sl > 0, JOB_R4L, sb, sl, X, r, ev);
       }
-    }
-    if (mask & M_RDOM) {  // domain(r) = D  =>  D ∈ S(X)   (X ≠ ⊤, not a datatype)
-      ev.v[EL_EV_ROW]++;
-      const uint32_t d0 = ix.dom_ptr[r], d1 = ix.dom_ptr[r + 1];
-      bool ok = false;
-      if (d1 > d0) {
-        ev.v[EL_EV_ENT]++;
-        ok = X != EL_TOP && ix.kind[X] != EL_KIND_DATATYPE;
-      }
-      for (uint32_t j = d0; j < d1; ++j) {
-        const uint32_t D = ix.dom_c[j];
-        ev.v[EL_EV_ENT]++;
+      if (mask & M_RBOT) {  // ⊥ ∈ S(Y)  =>  ⊥ ∈ S(X)
+        ev.v[EL_EV_TEST]++;
         bool nw = false;
-        if (ok) {
+        if (test_bit(st.bits, ix.W, Y, EL_BOTTOM)) {
           ev.v[EL_EV_TEST]++;
-          nw = !test_bit(st.bits, ix.W, X, D);
+          nw = !test_bit(st.bits, ix.W, X, EL_BOTTOM);
         }
-        emit_s(st, nw, X, D, ev);
+        emit_s(st, q, nw, X, EL_BOTTOM, ev);
       }
-    }
-    if (mask & M_RRNG) {  // range(r) = C  =>  activate Y ⊑ C  (Y ≠ ⊤, not a datatype; H1)
-      ev.v[EL_EV_ROW]++;
-      const uint32_t g0 = ix.rng_ptr[r], g1 = ix.rng_ptr[r + 1];
-      bool ok = false;
-      if (g1 > g0) {
-        ev.v[EL_EV_ENT]++;
-        ok = Y != EL_TOP && ix.kind[Y] != EL_KIND_DATATYPE;
-      }
-      for (uint32_t j = g0; j < g1; ++j) {
-        const uint32_t C = ix.rng_c[j];
-        ev.v[EL_EV_ENT]++;
-        bool nw = false;
-        if (ok) {
+      if (mask & M_R5) {  // r ⊑ s  =>  (X, Y) ∈ R(s)
+        ev.v[EL_EV_ROW]++;
+        const uint32_t q1 = ix.psup_ptr[pid + 1];
+        for (uint32_t j = ix.psup_ptr[pid]; j < q1; ++j) {
+          const uint32_t sp = ix.psup_pid[j];
+          ev.v[EL_EV_ENT]++;
           ev.v[EL_EV_HASH]++;
-          nw = !hash_contains(st.ahash, st.amask, link_key(C, Y));
+          emit_l(st, q, !hash_contains(st.lhash, st.lmask, link_key(sp, X)), X, sp, ev);
         }
-        emit_a(st, nw, Y, C, ev);
+      }
+      if (mask & M_R6) {  // r ∘ s ⊑ t
+        ev.v[EL_EV_ROW]++;
+        const bool first = ix.chf_ptr[r + 1] > ix.chf_ptr[r];
+        uint32_t sb = 0, sl = 0;
+        if (first) {  // r first: (Y, Z) ∈ R(s)  =>  (X, Z) ∈ R(t)
+          ev.v[EL_EV_ROW]++;
+          sb = st.sc_ptr[Y];
+          sl = st.sc_ptr[Y + 1] - sb;
+        }
+        emit_job(st, q, first && sl > 0, JOB_R6A, sb, sl, X, r, ev);
+        ev.v[EL_EV_ROW]++;
+        const uint32_t h1 = ix.chs_ptr[r + 1];
+        for (uint32_t j = ix.chs_ptr[r]; j < h1; ++j) {  // r second: (X', X) ∈ R(p)  =>  (X', Y) ∈ R(t)
+          const uint32_t p = ix.chs_p[j], t = ix.chs_t[j];
+          ev.v[EL_EV_ENT] += 2;
+          const uint32_t pq = pair_lookup(ix, p, X, ev);
+          uint32_t pb = 0, pl = 0, pt = NONE;
+          if (pq != NONE) {
+            ev.v[EL_EV_ROW]++;
+            pb = st.pr_ptr[pq];
+            pl = st.pr_ptr[pq + 1] - pb;
+            if (pl) pt = pair_lookup(ix, t, Y, ev);
+          }
+          emit_job(st, q, pl > 0, JOB_PRED_L, pb, pl, pt, 0, ev);
+        }
+      }
+      if (mask & M_RDOM) {  // domain(r) = D  =>  D ∈ S(X)   (X ≠ ⊤, not a datatype)
+        ev.v[EL_EV_ROW]++;
+        const uint32_t d0 = ix.dom_ptr[r], d1 = ix.dom_ptr[r + 1];
+        bool ok = false;
+        if (d1 > d0) {
+          ev.v[EL_EV_ENT]++;
+          ok = X != EL_TOP && ix.kind[X] != EL_KIND_DATATYPE;
+        }
+        for (uint32_t j = d0; j < d1; ++j) {
+          const uint32_t D = ix.dom_c[j];
+          ev.v[EL_EV_ENT]++;
+          bool nw = false;
+          if (ok) {
+            ev.v[EL_EV_TEST]++;
+            nw = !test_bit(st.bits, ix.W, X, D);
+          }
+          emit_s(st, q, nw, X, D, ev);
+        }
+      }
+      if (mask & M_RRNG) {  // range(r) = C  =>  activate Y ⊑ C  (Y ≠ ⊤, not a datatype; H1)
+        ev.v[EL_EV_ROW]++;
+        const uint32_t g0 = ix.rng_ptr[r], g1 = ix.rng_ptr[r + 1];
+        bool ok = false;
+        if (g1 > g0) {
+          ev.v[EL_EV_ENT]++;
+          ok = Y != EL_TOP && ix.kind[Y] != EL_KIND_DATATYPE;
+        }
+        for (uint32_t j = g0; j < g1; ++j) {
+          const uint32_t C = ix.rng_c[j];
+          ev.v[EL_EV_ENT]++;
+          bool nw = false;
+          if (ok) {
+            ev.v[EL_EV_HASH]++;
+            nw = !hash_contains(st.ahash, st.amask, link_key(C, Y));
+          }
+          emit_a(st, nw, Y, C, ev);
+        }
       }
     }
+    q_maybe_flush(q, st);
   }
+  q_flush(q, st);
   ev_flush(st.ctr, EL_K_EXPAND_L, ev);
 }
 
@@ -518,116 +619,154 @@ __global__ void k_expand_l(DIndex ix, DState st, uint32_t begin, uint32_t end, u
 //  JOB_R4L     S(Y) row   × ∃r.A ⊑ B    (CR4 half-2)
 //  JOB_R6A     succ(Y)    × chains of r (CR6, r first)
 __global__ void k_jobs(DIndex ix, DState st) {
+  __shared__ BlockQ q;
+  q_init(q);
   Ev ev;
   const uint32_t lane = threadIdx.x & 63u;
-  const uint32_t wid = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-  const uint32_t nwaves = (gridDim.x * blockDim.x) >> 6;
+  const uint32_t wpb = blockDim.x >> 6;
+  const uint32_t nwaves = gridDim.x * wpb;
   const uint32_t njobs = min(st.ctr->jobs, st.job_cap);
-  for (uint32_t j = wid; j < njobs; j += nwaves) {
-    const uint4 jb = st.jobs[j];
-    const uint32_t begin = jb.x, type = jb.y >> 28, len = jb.y & 0x0fffffffu, a = jb.z, b = jb.w;
-    if (lane == 0) ev.v[EL_EV_JOB]++;
-    if (type == JOB_PRED_S) {
-      for (uint32_t k = lane; k < len; k += 64) {
-        const uint32_t xp = st.pr_val[begin + k];
-        ev.v[EL_EV_ENT]++;
-        ev.v[EL_EV_TEST]++;
-        emit_s(st, !test_bit(st.bits, ix.W, xp, b), xp, b, ev);
-      }
-    } else if (type == JOB_PRED_L) {
-      for (uint32_t k = lane; k < len; k += 64) {
-        const uint32_t xp = st.pr_val[begin + k];
-        ev.v[EL_EV_ENT]++;
-        ev.v[EL_EV_HASH]++;
-        emit_l(st, !hash_contains(st.lhash, st.lmask, link_key(a, xp)), xp, a, ev);
-      }
-    } else if (type == JOB_R4L) {
-      const uint32_t X = a, r = b;
-      for (uint32_t k = lane; k < len; k += 64) {
-        const uint32_t A = st.s_val[begin + k];
-        ev.v[EL_EV_ENT]++;
-        ev.v[EL_EV_ROW]++;
-        const uint32_t e1 = ix.exl_ptr[A + 1];
-        for (uint32_t e = ix.exl_ptr[A]; e < e1; ++e) {
-          const uint32_t rr = ix.exl_r[e];
-          ev.v[EL_EV_ENT] += 2;
-          if (rr > r) break;
-          bool nw = false;
-          const uint32_t B = ix.exl_b[e];
-          if (rr == r) {
-            ev.v[EL_EV_TEST]++;
-            nw = !test_bit(st.bits, ix.W, X, B);
-          }
-          emit_s(st, nw, X, B, ev);
+  for (uint32_t base = blockIdx.x * wpb; base < njobs; base += nwaves) {
+    const uint32_t j = base + (threadIdx.x >> 6);
+    if (j < njobs) {
+      const uint4 jb = st.jobs[j];
+      const uint32_t begin = jb.x, type = jb.y >> 28, len = jb.y & 0x0fffffffu, a = jb.z, b = jb.w;
+      if (lane == 0) ev.v[EL_EV_JOB]++;
+      if (type == JOB_PRED_S) {
+        for (uint32_t k = lane; k < len; k += 64) {
+          const uint32_t xp = st.pr_val[begin + k];
+          ev.v[EL_EV_ENT]++;
+          ev.v[EL_EV_TEST]++;
+          emit_s(st, q, !test_bit(st.bits, ix.W, xp, b), xp, b, ev);
         }
-      }
-    } else {  // JOB_R6A
-      const uint32_t X = a, r = b;
-      for (uint32_t k = lane; k < len; k += 64) {
-        const uint32_t q = st.sc_val[begin + k];
-        ev.v[EL_EV_ENT]++;
-        const uint32_t s2 = ix.pair_role[q], Z = ix.pair_y[q];
-        ev.v[EL_EV_ENT] += 2;
-        ev.v[EL_EV_ROW]++;
-        const uint32_t f1 = ix.chf_ptr[r + 1];
-        for (uint32_t f = ix.chf_ptr[r]; f < f1; ++f) {
-          const uint32_t s = ix.chf_s[f], t = ix.chf_t[f];
-          ev.v[EL_EV_ENT] += 2;
-          bool nw = false;
-          uint32_t pt = NONE;
-          if (s == s2) {
-            pt = pair_lookup(ix, t, Z, ev);
-            ev.v[EL_EV_HASH]++;
-            nw = !hash_contains(st.lhash, st.lmask, link_key(pt, X));
+      } else if (type == JOB_PRED_L) {
+        for (uint32_t k = lane; k < len; k += 64) {
+          const uint32_t xp = st.pr_val[begin + k];
+          ev.v[EL_EV_ENT]++;
+          ev.v[EL_EV_HASH]++;
+          emit_l(st, q, !hash_contains(st.lhash, st.lmask, link_key(a, xp)), xp, a, ev);
+        }
+      } else if (type == JOB_R4L) {
+        const uint32_t X = a, r = b;
+        for (uint32_t k = lane; k < len; k += 64) {
+          const uint32_t A = st.s_val[begin + k];
+          ev.v[EL_EV_ENT]++;
+          ev.v[EL_EV_ROW]++;
+          const uint32_t e1 = ix.exl_ptr[A + 1];
+          for (uint32_t e = ix.exl_ptr[A]; e < e1; ++e) {
+            const uint32_t rr = ix.exl_r[e];
+            ev.v[EL_EV_ENT] += 2;
+            if (rr > r) break;
+            bool nw = false;
+            const uint32_t B = ix.exl_b[e];
+            if (rr == r) {
+              ev.v[EL_EV_TEST]++;
+              nw = !test_bit(st.bits, ix.W, X, B);
+            }
+            emit_s(st, q, nw, X, B, ev);
           }
-          emit_l(st, nw, X, pt, ev);
+        }
+      } else {  // JOB_R6A
+        const uint32_t X = a, r = b;
+        for (uint32_t k = lane; k < len; k += 64) {
+          const uint32_t sq = st.sc_val[begin + k];
+          ev.v[EL_EV_ENT]++;
+          const uint32_t s2 = ix.pair_role[sq], Z = ix.pair_y[sq];
+          ev.v[EL_EV_ENT] += 2;
+          ev.v[EL_EV_ROW]++;
+          const uint32_t f1 = ix.chf_ptr[r + 1];
+          for (uint32_t f = ix.chf_ptr[r]; f < f1; ++f) {
+            const uint32_t s = ix.chf_s[f], t = ix.chf_t[f];
+            ev.v[EL_EV_ENT] += 2;
+            bool nw = false;
+            uint32_t pt = NONE;
+            if (s == s2) {
+              pt = pair_lookup(ix, t, Z, ev);
+              ev.v[EL_EV_HASH]++;
+              nw = !hash_contains(st.lhash, st.lmask, link_key(pt, X));
+            }
+            emit_l(st, q, nw, X, pt, ev);
+          }
         }
       }
     }
+    q_maybe_flush(q, st);
   }
+  q_flush(q, st);
   ev_flush(st.ctr, EL_K_JOBS, ev);
 }
 
 // Range activations (Y, C) = act log[a_begin, a_end): every X with Y ∈ S(X) gets C
 // (ScriptsCollection.insertClassAssertions1 :45-62 copies result[Y] into result[C]).
 __global__ void k_expand_a(DIndex ix, DState st, uint32_t a_begin, uint32_t a_end) {
+  __shared__ BlockQ q;
+  q_init(q);
   Ev ev;
-  const uint32_t stride = gridDim.x * blockDim.x;
   const uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x;
   if (tid == 0) ev.v[EL_EV_TRIG] += a_end - a_begin;
-  for (uint32_t x = tid; x < ix.N; x += stride) {
-    for (uint32_t k = a_begin; k < a_end; ++k) {
-      const uint32_t Y = st.alog_y[k], C = st.alog_c[k];
-      ev.v[EL_EV_TEST]++;
-      bool nw = false;
-      if (test_bit(st.bits, ix.W, x, Y)) {
+  for (uint32_t base = blockIdx.x * blockDim.x; base < ix.N; base += gridDim.x * blockDim.x) {
+    const uint32_t x = base + threadIdx.x;
+    if (x < ix.N) {
+      for (uint32_t k = a_begin; k < a_end; ++k) {
+        const uint32_t Y = st.alog_y[k], C = st.alog_c[k];
         ev.v[EL_EV_TEST]++;
-        nw = !test_bit(st.bits, ix.W, x, C);
+        bool nw = false;
+        if (test_bit(st.bits, ix.W, x, Y)) {
+          ev.v[EL_EV_TEST]++;
+          nw = !test_bit(st.bits, ix.W, x, C);
+        }
+        emit_s(st, q, nw, x, C, ev);
       }
-      emit_s(st, nw, x, C, ev);
     }
+    q_maybe_flush(q, st);
   }
+  q_flush(q, st);
   ev_flush(st.ctr, EL_K_EXPAND_A, ev);
 }
 
 // Dedup S candidates against the bit rows; new facts go to the log (the versioned
 // ZADD of every Lua kernel, e.g. Type1_1AxiomProcessorBase.java:36-41).
 __global__ void k_commit_s(DIndex ix, DState st, uint32_t n) {
+  __shared__ uint32_t lx[QS_CAP], la[QS_CAP];
+  __shared__ uint32_t ln, lbase;
+  if (threadIdx.x == 0) ln = 0;
+  __syncthreads();
   Ev ev;
-  const uint32_t stride = gridDim.x * blockDim.x;
-  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
-    const uint32_t x = st.cs_x[i], a = st.cs_a[i];
-    ev.v[EL_EV_TRIG]++;
-    ev.v[EL_EV_RMW]++;
-    const uint32_t m = 1u << (a & 31u);
-    const uint32_t old = atomicOr(st.bits + (uint64_t)x * ix.W + (a >> 5), m);
-    const bool nw = (old & m) == 0;
-    const uint32_t slot = wave_append(&st.ctr->s_log, nw);
+  for (uint32_t base = blockIdx.x * blockDim.x; base < n; base += gridDim.x * blockDim.x) {
+    const uint32_t i = base + threadIdx.x;
+    bool nw = false;
+    uint32_t x = 0, a = 0;
+    if (i < n) {
+      x = st.cs_x[i];
+      a = st.cs_a[i];
+      ev.v[EL_EV_TRIG]++;
+      ev.v[EL_EV_RMW]++;
+      const uint32_t m = 1u << (a & 31u);
+      const uint32_t old = atomicOr(st.bits + (uint64_t)x * ix.W + (a >> 5), m);
+      nw = (old & m) == 0;
+      if (nw) {
+        ev.v[EL_EV_EMIT]++;
+        atomicAdd(st.s_dcnt + x, 1u);
+      }
+    }
+    // one LDS slot per new fact; blockDim <= QS_CAP/2 so a round never overflows
+    const uint32_t off = lds_reserve(&ln, nw);
     if (nw) {
-      ev.v[EL_EV_EMIT]++;
-      st.slog_x[slot] = x;
-      st.slog_a[slot] = a;
-      atomicAdd(st.s_dcnt + x, 1u);
+      lx[off] = x;
+      la[off] = a;
+    }
+    __syncthreads();
+    if (ln > QS_CAP / 2 || base + gridDim.x * blockDim.x >= n) {
+      const uint32_t cnt = ln;
+      if (threadIdx.x == 0) lbase = cnt ? atomicAdd(&st.ctr->s_log, cnt) : 0u;
+      __syncthreads();
+      for (uint32_t k = threadIdx.x; k < cnt; k += blockDim.x) {
+        st.slog_x[lbase + k] = lx[k];
+        st.slog_a[lbase + k] = la[k];
+      }
+      __syncthreads();
+      if (threadIdx.x == 0) ln = 0;
+      __syncthreads();
     }
   }
   ev_flush(st.ctr, EL_K_COMMIT_S, ev);
@@ -636,20 +775,44 @@ __global__ void k_commit_s(DIndex ix, DState st, uint32_t n) {
 // Dedup link candidates against the link set (checkAndInsertScript,
 // RolePairHandler.java:133-168); new links feed the predecessor/successor CSRs.
 __global__ void k_commit_l(DIndex ix, DState st, uint32_t n) {
+  __shared__ uint32_t lx[QL_CAP], lp[QL_CAP];
+  __shared__ uint32_t ln, lbase;
+  if (threadIdx.x == 0) ln = 0;
+  __syncthreads();
   Ev ev;
-  const uint32_t stride = gridDim.x * blockDim.x;
-  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
-    const uint32_t x = st.cl_x[i], p = st.cl_p[i];
-    ev.v[EL_EV_TRIG]++;
-    ev.v[EL_EV_HASH]++;
-    const bool nw = hash_insert(st.lhash, st.lmask, link_key(p, x));
-    const uint32_t slot = wave_append(&st.ctr->l_log, nw);
+  for (uint32_t base = blockIdx.x * blockDim.x; base < n; base += gridDim.x * blockDim.x) {
+    const uint32_t i = base + threadIdx.x;
+    bool nw = false;
+    uint32_t x = 0, p = 0;
+    if (i < n) {
+      x = st.cl_x[i];
+      p = st.cl_p[i];
+      ev.v[EL_EV_TRIG]++;
+      ev.v[EL_EV_HASH]++;
+      nw = hash_insert(st.lhash, st.lmask, link_key(p, x));
+      if (nw) {
+        ev.v[EL_EV_EMIT]++;
+        atomicAdd(st.pr_dcnt + p, 1u);
+        atomicAdd(st.sc_dcnt + x, 1u);
+      }
+    }
+    const uint32_t off = lds_reserve(&ln, nw);
     if (nw) {
-      ev.v[EL_EV_EMIT]++;
-      st.llog_x[slot] = x;
-      st.llog_p[slot] = p;
-      atomicAdd(st.pr_dcnt + p, 1u);
-      atomicAdd(st.sc_dcnt + x, 1u);
+      lx[off] = x;
+      lp[off] = p;
+    }
+    __syncthreads();
+    if (ln > QL_CAP / 2 || base + gridDim.x * blockDim.x >= n) {
+      const uint32_t cnt = ln;
+      if (threadIdx.x == 0) lbase = cnt ? atomicAdd(&st.ctr->l_log, cnt) : 0u;
+      __syncthreads();
+      for (uint32_t k = threadIdx.x; k < cnt; k += blockDim.x) {
+        st.llog_x[lbase + k] = lx[k];
+        st.llog_p[lbase + k] = lp[k];
+      }
+      __syncthreads();
+      if (threadIdx.x == 0) ln = 0;
+      __syncthreads();
     }
   }
   ev_flush(st.ctr, EL_K_COMMIT_L, ev);

@@ -1,0 +1,68 @@
+"""The C-ABI library loads and exports every symbol include/el_gpu.h declares (no compute:
+there is no GPU here); without a device every entry point fails loudly (EL_EHIP)."""
+import ctypes
+import os
+import re
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "el_gpu.h")
+
+
+def _declared():
+    text = open(HEADER).read()
+    return sorted(set(re.findall(r"^\s*(?:int|void|const char\*)\s+(el_\w+)\s*\(", text, re.M)))
+
+
+@pytest.fixture(scope="module")
+def lib():
+    import __graft_entry__ as g
+    g.build_lib()
+    from distel_amd import engine
+    return engine.load_library()
+
+
+def test_header_declares_expected(lib):
+    from distel_amd import engine
+    assert _declared() == sorted(engine.EXPORTED_SYMBOLS)
+
+
+def test_exports_every_symbol(lib):
+    out = subprocess.run(["nm", "-D", "--defined-only", os.path.join(ROOT, "distel_amd", "lib", "libel_gpu.so")],
+                         capture_output=True, text=True, check=True).stdout
+    exported = set(re.findall(r" T (el_\w+)$", out, re.M))
+    for sym in _declared():
+        assert sym in exported, sym
+        assert getattr(lib, sym) is not None
+
+
+def test_abi_version(lib):
+    assert lib.el_abi_version() == 1
+
+
+def test_no_device_fails_loudly(lib):
+    from distel_amd import engine
+    if engine.device_count() > 0:
+        pytest.skip("a HIP device is visible")
+    with pytest.raises(engine.ElError) as e:
+        engine.Engine(device=0)
+    assert e.value.code == engine.EL_EHIP
+
+
+def test_null_arguments(lib):
+    assert lib.el_create(None, None) == -1
+    assert lib.el_init(None) == -1
+    assert lib.el_saturate(None, None) == -1
+    lib.el_destroy(None)
+
+
+def test_no_oracle_in_product():
+    """The product package never imports or links the CPU oracle."""
+    for dirpath, _, files in os.walk(os.path.join(ROOT, "distel_amd")):
+        for f in files:
+            if f.endswith((".py", ".hip", ".cpp", ".h")):
+                src = open(os.path.join(dirpath, f), encoding="utf-8").read()
+                for bad in ('#include "el_oracle', "libel_oracle", "import oracle", "from oracle"):
+                    assert bad not in src, (f, bad)

@@ -1,0 +1,101 @@
+"""CPU oracle checks (no GPU): the oracle is pinned by the hand-derived KATs, by the
+pure-Python restatement and by naive-vs-semi-naive agreement on random ontologies."""
+import os
+import random
+
+import numpy as np
+import pytest
+
+import kat
+import naive
+from distel_amd import generators
+
+
+@pytest.mark.parametrize("path", kat.kat_files(), ids=lambda p: os.path.basename(p))
+@pytest.mark.parametrize("mode", [0, 1])
+def test_kat_oracle(path, mode, oracle_lib):
+    ax, exp = kat.load_kat(path)
+    o = oracle_lib.saturate(ax, mode)
+    S, R = kat.to_sets(*o.facts(), *o.links())
+    kat.check(exp, S, R)
+
+
+@pytest.mark.parametrize("path", kat.kat_files(), ids=lambda p: os.path.basename(p))
+def test_kat_python_naive(path):
+    ax, exp = kat.load_kat(path)
+    S, R = naive.saturate(ax)
+    kat.check(exp, S, R)
+
+
+def _same(a, b):
+    return all(np.array_equal(x, y) for x, y in zip(a.facts() + a.links(), b.facts() + b.links()))
+
+
+def test_seminaive_equals_naive_1000_seeds(oracle_lib):
+    for seed in range(1000):
+        ax = generators.random_small(seed, n=6 + seed % 34, n_roles=1 + seed % 4)
+        assert _same(oracle_lib.saturate(ax, 0), oracle_lib.saturate(ax, 1)), seed
+
+
+def test_oracle_equals_python_naive(oracle_lib):
+    for seed in range(120):
+        ax = generators.random_small(5000 + seed, n=8 + seed % 20, n_roles=1 + seed % 3)
+        o = oracle_lib.saturate(ax, 0)
+        S0, R0 = kat.to_sets(*o.facts(), *o.links())
+        S, R = naive.saturate(ax)
+        assert S0 == S and R0 == R, seed
+
+
+def test_step_schedule_reaches_fixpoint(oracle_lib):
+    rnd = random.Random(3)
+    for seed in range(60):
+        ax = generators.random_small(2000 + seed, n=25, n_roles=3)
+        o = oracle_lib.Oracle(ax, 0)
+        o.init()
+        idle, calls = set(), 0
+        while len(idle) < 8 and calls < 20000:
+            r = rnd.randrange(8)
+            idle = set() if o.step(r) else idle | {r}
+            calls += 1
+        assert _same(o, oracle_lib.saturate(ax, 0)), seed
+
+
+def test_trace_sums(oracle_lib):
+    ax = generators.workload("g1", scale=0.05)
+    o = oracle_lib.saturate(ax, 0)
+    ds, dl, da = o.trace()
+    st = o.stats()
+    assert int(ds.sum()) == st["s_facts"] and int(dl.sum()) == st["links"]
+    assert ds[0] == st["s_init"] and dl[0] == 0
+
+
+def test_generators_deterministic():
+    a = generators.workload("g1", scale=0.2)
+    b = generators.workload("g1", scale=0.2)
+    assert a.digest() == b.digest()
+    assert generators.random_small(1).digest() == generators.random_small(1).digest()
+
+
+GOLDEN_DIGESTS = os.path.join(kat.GOLDEN, "closure_digests.txt")
+
+
+def _closure_digest(o):
+    import hashlib
+    h = hashlib.sha256()
+    for a in o.facts() + o.links():
+        h.update(np.ascontiguousarray(a).tobytes())
+    return h.hexdigest()
+
+
+def test_closure_digests(oracle_lib):
+    """Closures of seeded generator outputs, pinned by SHA-256 (tests/golden/closure_digests.txt,
+    written by tests/golden/make_digests.py)."""
+    want = {}
+    for line in open(GOLDEN_DIGESTS):
+        if line.strip() and not line.startswith("#"):
+            name, scale, inp, clo = line.split()
+            want[(name, float(scale))] = (inp, clo)
+    for (name, scale), (inp, clo) in want.items():
+        ax = generators.workload(name, scale)
+        assert ax.digest() == inp, name
+        assert _closure_digest(oracle_lib.saturate(ax, 0)) == clo, name
