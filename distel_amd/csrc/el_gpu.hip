@@ -60,14 +60,16 @@ enum : uint32_t {
   M_RBOT = 1u << 7,  // ⊥
   M_RDOM = 1u << 8,  // domain
   M_RRNG = 1u << 9,  // range
-  M_ALL = (1u << 10) - 1
+  M_R4P = 1u << 10,  // CR4: new propagations × existing predecessors (per-rule stepping)
+  M_R4D = 1u << 11,  // CR4: fused mode — a new propagation fans out to predecessors at once
+  M_ALL = M_R1 | M_R2 | M_R3 | M_R4Y | M_R4L | M_R5 | M_R6 | M_RBOT | M_RDOM | M_RRNG | M_R4D
 };
 
 // el_rule → sub-rules it owns (see el_gpu.h)
 const uint32_t kRuleMask[EL_NUM_RULE_TYPES] = {
-    M_R1, M_R2, M_R3 | M_RDOM | M_RRNG, M_R4Y, M_R4L, M_R5, M_R6, M_RBOT};
+    M_R1, M_R2, M_R3 | M_RDOM | M_RRNG, M_R4Y, M_R4L | M_R4P, M_R5, M_R6, M_RBOT};
 
-enum : uint32_t { JOB_PRED_S = 0, JOB_PRED_L = 1, JOB_R4L = 2, JOB_R6A = 3 };
+enum : uint32_t { JOB_PRED_S = 0, JOB_PRED_L = 1, JOB_R6A = 3 };
 
 struct ElError {
   int code;
@@ -105,8 +107,9 @@ struct DIndex {
 
 struct DCounters {
   unsigned long long ev[EL_NUM_KERNELS][EL_NUM_EVENTS];
-  uint32_t s_log, l_log, a_log, pad0;
+  uint32_t s_log, l_log, a_log, p_log;
   uint32_t cand_s, cand_l, cand_a, jobs;
+  uint32_t cand_p, pad1, pad2, pad3;
 };
 
 struct DState {
@@ -119,6 +122,12 @@ struct DState {
   unsigned long long amask;
   uint32_t *alog_y, *alog_c;
   uint8_t* has_act;
+  unsigned long long* phash;  // CR4 propagations (pid, B)
+  unsigned long long pmask;
+  uint32_t *plog_p, *plog_b;
+  const uint32_t *pp_ptr, *pp_val;  // propagations per pid (CSR, current)
+  uint32_t* pp_dcnt;
+  uint32_t *cp_p, *cp_b, cp_cap;
   const uint32_t *s_ptr, *s_val;    // S rows (CSR, current)
   const uint32_t *pr_ptr, *pr_val;  // predecessors per pid
   const uint32_t *sc_ptr, *sc_val;  // successors per X
@@ -314,6 +323,18 @@ __device__ __forceinline__ void emit_a(const DState& st, bool pred, uint32_t y, 
   }
 }
 
+// CR4 propagations: a few per S-fact at most, plain wave-aggregated global append
+__device__ __forceinline__ void emit_p(const DState& st, bool pred, uint32_t pid, uint32_t b, Ev& ev) {
+  uint32_t slot = wave_append(&st.ctr->cand_p, pred);
+  if (pred) {
+    ev.v[EL_EV_EMIT]++;
+    if (slot < st.cp_cap) {
+      st.cp_p[slot] = pid;
+      st.cp_b[slot] = b;
+    }
+  }
+}
+
 // Publish the block's staged records: one global atomic per non-empty queue.
 // Every thread of the block must call this (it contains barriers).
 __device__ void q_flush(BlockQ& q, const DState& st) {
@@ -449,19 +470,25 @@ __global__ void k_expand_s(DIndex ix, DState st, uint32_t begin, uint32_t end, u
           emit_l(st, q, !hash_contains(st.lhash, st.lmask, link_key(pid, X)), X, pid, ev);
         }
       }
-      if (mask & M_R4Y) {  // A ∈ S(Y=X) new, ∃r.A ⊑ B, (X', Y) ∈ R(r)  =>  B ∈ S(X')
-        ev.v[EL_EV_ROW]++;
+      if (mask & M_R4Y) {  // A ∈ S(Y=X) new, ∃r.A ⊑ B  =>  propagation ((r, Y), B)
+        ev.v[EL_EV_ROW]++;   // (Type3_1AxiomProcessorBase.java:208-234 writes "Yr" -> B)
         const uint32_t e1 = ix.exl_ptr[A + 1];
         for (uint32_t j = ix.exl_ptr[A]; j < e1; ++j) {
           const uint32_t r = ix.exl_r[j], B = ix.exl_b[j];
           ev.v[EL_EV_ENT] += 2;
           const uint32_t pid = pair_lookup(ix, r, X, ev);
+          bool fresh = false;
           uint32_t pb = 0, pl = 0;
           if (pid != NONE) {
-            ev.v[EL_EV_ROW]++;
-            pb = st.pr_ptr[pid];
-            pl = st.pr_ptr[pid + 1] - pb;
+            ev.v[EL_EV_HASH]++;
+            fresh = !hash_contains(st.phash, st.pmask, link_key(pid, B));
+            if (fresh && (mask & M_R4D)) {  // fused mode: B reaches today's predecessors now
+              ev.v[EL_EV_ROW]++;
+              pb = st.pr_ptr[pid];
+              pl = st.pr_ptr[pid + 1] - pb;
+            }
           }
+          emit_p(st, fresh, pid, B, ev);
           emit_job(st, q, pl > 0, JOB_PRED_S, pb, pl, 0, B, ev);
         }
       }
@@ -512,16 +539,15 @@ __global__ void k_expand_l(DIndex ix, DState st, uint32_t begin, uint32_t end, u
       ev.v[EL_EV_TRIG]++;
       const uint32_t r = ix.pair_role[pid], Y = ix.pair_y[pid];
       ev.v[EL_EV_ENT] += 2;
-      if (mask & M_R4L) {  // (X, Y) ∈ R(r) new, A ∈ S(Y), ∃r.A ⊑ B  =>  B ∈ S(X)
-        ev.v[EL_EV_ENT]++;
-        const bool has = ix.role_has_exl[r] != 0;
-        uint32_t sb = 0, sl = 0;
-        if (has) {
-          ev.v[EL_EV_ROW]++;
-          sb = st.s_ptr[Y];
-          sl = st.s_ptr[Y + 1] - sb;
+      if (mask & M_R4L) {  // (X, Y) ∈ R(r) new, propagation ((r, Y), B)  =>  B ∈ S(X)
+        ev.v[EL_EV_ROW]++;   // (Type3_2AxiomProcessorBase.java:67-96, part 2: all B × ΔX)
+        const uint32_t g1 = st.pp_ptr[pid + 1];
+        for (uint32_t j = st.pp_ptr[pid]; j < g1; ++j) {
+          const uint32_t B = st.pp_val[j];
+          ev.v[EL_EV_ENT]++;
+          ev.v[EL_EV_TEST]++;
+          emit_s(st, q, !test_bit(st.bits, ix.W, X, B), X, B, ev);
         }
-        emit_job(st, q, has && sl > 0, JOB_R4L, sb, sl, X, r, ev);
       }
       if (mask & M_RBOT) {  // ⊥ ∈ S(Y)  =>  ⊥ ∈ S(X)
         ev.v[EL_EV_TEST]++;
@@ -616,7 +642,6 @@ __global__ void k_expand_l(DIndex ix, DState st, uint32_t begin, uint32_t end, u
 // Wide fan-outs: one wave per job record, lanes stride over the list.
 //  JOB_PRED_S  preds(pid) × {B}         (CR4 half-1, ⊥)
 //  JOB_PRED_L  preds(pq)  × {pid_t}     (CR6, r second)
-//  JOB_R4L     S(Y) row   × ∃r.A ⊑ B    (CR4 half-2)
 //  JOB_R6A     succ(Y)    × chains of r (CR6, r first)
 __global__ void k_jobs(DIndex ix, DState st) {
   __shared__ BlockQ q;
@@ -645,26 +670,6 @@ __global__ void k_jobs(DIndex ix, DState st) {
           ev.v[EL_EV_ENT]++;
           ev.v[EL_EV_HASH]++;
           emit_l(st, q, !hash_contains(st.lhash, st.lmask, link_key(a, xp)), xp, a, ev);
-        }
-      } else if (type == JOB_R4L) {
-        const uint32_t X = a, r = b;
-        for (uint32_t k = lane; k < len; k += 64) {
-          const uint32_t A = st.s_val[begin + k];
-          ev.v[EL_EV_ENT]++;
-          ev.v[EL_EV_ROW]++;
-          const uint32_t e1 = ix.exl_ptr[A + 1];
-          for (uint32_t e = ix.exl_ptr[A]; e < e1; ++e) {
-            const uint32_t rr = ix.exl_r[e];
-            ev.v[EL_EV_ENT] += 2;
-            if (rr > r) break;
-            bool nw = false;
-            const uint32_t B = ix.exl_b[e];
-            if (rr == r) {
-              ev.v[EL_EV_TEST]++;
-              nw = !test_bit(st.bits, ix.W, X, B);
-            }
-            emit_s(st, q, nw, X, B, ev);
-          }
         }
       } else {  // JOB_R6A
         const uint32_t X = a, r = b;
@@ -837,6 +842,48 @@ __global__ void k_commit_a(DIndex ix, DState st, uint32_t n) {
   ev_flush(st.ctr, EL_K_COMMIT_A, ev);
 }
 
+// New CR4 propagations ((r, Y), B) = prop log[begin, end) × existing predecessors of (r, Y)
+// (per-rule stepping: Type3_2AxiomProcessor part 1, ΔB × all X).  In fused saturation the
+// fan-out happens when the propagation is generated (M_R4D), so this kernel is idle there.
+__global__ void k_expand_p(DIndex ix, DState st, uint32_t begin, uint32_t end) {
+  __shared__ BlockQ q;
+  q_init(q);
+  Ev ev;
+  for (uint32_t base = begin + blockIdx.x * blockDim.x; base < end; base += gridDim.x * blockDim.x) {
+    const uint32_t i = base + threadIdx.x;
+    if (i < end) {
+      const uint32_t pid = st.plog_p[i], B = st.plog_b[i];
+      ev.v[EL_EV_TRIG]++;
+      ev.v[EL_EV_ROW]++;
+      const uint32_t pb = st.pr_ptr[pid], pl = st.pr_ptr[pid + 1] - pb;
+      emit_job(st, q, pl > 0, JOB_PRED_S, pb, pl, 0, B, ev);
+    }
+    q_maybe_flush(q, st);
+  }
+  q_flush(q, st);
+  ev_flush(st.ctr, EL_K_EXPAND_P, ev);
+}
+
+// Dedup propagation candidates (checkAndInsertScript, Type3_1AxiomProcessorBase.java:88-121)
+__global__ void k_commit_p(DIndex ix, DState st, uint32_t n) {
+  Ev ev;
+  const uint32_t stride = gridDim.x * blockDim.x;
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    const uint32_t pid = st.cp_p[i], b = st.cp_b[i];
+    ev.v[EL_EV_TRIG]++;
+    ev.v[EL_EV_HASH]++;
+    const bool nw = hash_insert(st.phash, st.pmask, link_key(pid, b));
+    const uint32_t slot = wave_append(&st.ctr->p_log, nw);
+    if (nw) {
+      ev.v[EL_EV_EMIT]++;
+      st.plog_p[slot] = pid;
+      st.plog_b[slot] = b;
+      atomicAdd(st.pp_dcnt + pid, 1u);
+    }
+  }
+  ev_flush(st.ctr, EL_K_COMMIT_P, ev);
+}
+
 // CSR merge: new_ptr[x] = ptr[x] + exclusive_scan(dcnt)[x]
 __global__ void k_merge_ptr(uint32_t* __restrict__ ptr2, const uint32_t* __restrict__ ptr,
                             const uint32_t* __restrict__ dscan, uint32_t n1) {
@@ -996,7 +1043,13 @@ struct el_ctx {
   uint32_t *alog_y = nullptr, *alog_c = nullptr;
   uint64_t alog_cap = 0;
   uint8_t* has_act = nullptr;
-  DevCsr S, PR, SC;
+  unsigned long long* phash = nullptr;
+  uint64_t phash_cap = 0;
+  uint32_t *plog_p = nullptr, *plog_b = nullptr;
+  uint64_t plog_cap = 0;
+  uint32_t *cp_p = nullptr, *cp_b = nullptr;
+  uint64_t cp_cap = 0;
+  DevCsr S, PR, SC, PP;
   uint32_t *cs_x = nullptr, *cs_a = nullptr, *cl_x = nullptr, *cl_p = nullptr, *ca_y = nullptr,
            *ca_c = nullptr;
   uint64_t cs_cap = 0, cl_cap = 0, ca_cap = 0;
@@ -1009,8 +1062,9 @@ struct el_ctx {
 
   // host mirrors
   DCounters hc{};
-  uint64_t s_count = 0, l_count = 0, a_count = 0, s_init = 0;
-  uint64_t wm_s[EL_NUM_RULE_TYPES] = {}, wm_l[EL_NUM_RULE_TYPES] = {}, wm_a[EL_NUM_RULE_TYPES] = {};
+  uint64_t s_count = 0, l_count = 0, a_count = 0, p_count = 0, s_init = 0;
+  uint64_t wm_s[EL_NUM_RULE_TYPES] = {}, wm_l[EL_NUM_RULE_TYPES] = {}, wm_a[EL_NUM_RULE_TYPES] = {},
+           wm_p[EL_NUM_RULE_TYPES] = {};
   el_stats last{};
   std::vector<uint64_t> tr_s, tr_l, tr_a;
   // host-side per-kernel accounting (merge kernels, launches, times)
@@ -1034,6 +1088,16 @@ struct el_ctx {
     s.alog_y = alog_y;
     s.alog_c = alog_c;
     s.has_act = has_act;
+    s.phash = phash;
+    s.pmask = phash_cap - 1;
+    s.plog_p = plog_p;
+    s.plog_b = plog_b;
+    s.pp_ptr = PP.ptr;
+    s.pp_val = PP.val;
+    s.pp_dcnt = PP.dcnt;
+    s.cp_p = cp_p;
+    s.cp_b = cp_b;
+    s.cp_cap = (uint32_t)cp_cap;
     s.s_ptr = S.ptr;
     s.s_val = S.val;
     s.pr_ptr = PR.ptr;
@@ -1106,8 +1170,9 @@ struct el_ctx {
              uint64_t end);
   void rehash_links(uint64_t cap);
   void rehash_acts(uint64_t cap);
+  void rehash_props(uint64_t cap);
   bool superstep(uint32_t mask, uint64_t sb, uint64_t se, uint64_t lb, uint64_t le, uint64_t ab,
-                 uint64_t ae);
+                 uint64_t ae, uint64_t pb, uint64_t pe);
   void fill_stats(el_stats* st, double ms);
 };
 
@@ -1127,9 +1192,15 @@ void el_ctx::free_state() {
   dfree(alog_y);
   dfree(alog_c);
   dfree(has_act);
+  dfree(phash);
+  dfree(plog_p);
+  dfree(plog_b);
+  dfree(cp_p);
+  dfree(cp_b);
   S.release();
   PR.release();
   SC.release();
+  PP.release();
   dfree(cs_x);
   dfree(cs_a);
   dfree(cl_x);
@@ -1161,6 +1232,15 @@ void el_ctx::alloc_state() {
   ahash_cap = next_pow2(2 * alog_cap);
   ahash = dalloc<unsigned long long>(ahash_cap);
   has_act = dalloc<uint8_t>(N);
+  plog_cap = std::max<uint64_t>(1u << 16, P);
+  plog_p = dalloc<uint32_t>(plog_cap);
+  plog_b = dalloc<uint32_t>(plog_cap);
+  phash_cap = next_pow2(2 * plog_cap);
+  phash = dalloc<unsigned long long>(phash_cap);
+  cp_cap = plog_cap;
+  cp_p = dalloc<uint32_t>(cp_cap);
+  cp_b = dalloc<uint32_t>(cp_cap);
+  PP.alloc((uint32_t)P, plog_cap);
   S.alloc((uint32_t)N, slog_cap);
   PR.alloc((uint32_t)P, llog_cap);
   SC.alloc((uint32_t)N, llog_cap);
@@ -1190,12 +1270,14 @@ void el_ctx::reset_state() {
   HIPCHK(hipMemsetAsync(lhash, 0xff, lhash_cap * sizeof(unsigned long long), stream));
   HIPCHK(hipMemsetAsync(ahash, 0xff, ahash_cap * sizeof(unsigned long long), stream));
   HIPCHK(hipMemsetAsync(has_act, 0, hx.N, stream));
+  HIPCHK(hipMemsetAsync(phash, 0xff, phash_cap * sizeof(unsigned long long), stream));
+  PP.reset(stream);
   S.reset(stream);
   PR.reset(stream);
   SC.reset(stream);
   HIPCHK(hipMemsetAsync(ctr, 0, sizeof(DCounters), stream));
-  s_count = l_count = a_count = s_init = 0;
-  for (int r = 0; r < EL_NUM_RULE_TYPES; ++r) wm_s[r] = wm_l[r] = wm_a[r] = 0;
+  s_count = l_count = a_count = p_count = s_init = 0;
+  for (int r = 0; r < EL_NUM_RULE_TYPES; ++r) wm_s[r] = wm_l[r] = wm_a[r] = wm_p[r] = 0;
   memset(launches, 0, sizeof launches);
   memset(host_ev, 0, sizeof host_ev);
   memset(kms, 0, sizeof kms);
@@ -1225,6 +1307,18 @@ void el_ctx::rehash_acts(uint64_t cap) {
     launch(EL_K_REHASH, [&] {
       hipLaunchKernelGGL(k_rehash, dim3(grid_for(a_count)), dim3(BLOCK), 0, stream, ahash, cap - 1,
                          alog_y, alog_c, (uint32_t)a_count);
+    });
+}
+
+void el_ctx::rehash_props(uint64_t cap) {
+  dfree(phash);
+  phash_cap = cap;
+  phash = dalloc<unsigned long long>(cap);
+  HIPCHK(hipMemsetAsync(phash, 0xff, cap * sizeof(unsigned long long), stream));
+  if (p_count)
+    launch(EL_K_REHASH, [&] {
+      hipLaunchKernelGGL(k_rehash, dim3(grid_for(p_count)), dim3(BLOCK), 0, stream, phash, cap - 1,
+                         plog_b, plog_p, (uint32_t)p_count);
     });
 }
 
@@ -1270,15 +1364,16 @@ void el_ctx::merge(DevCsr& c, const uint32_t* lx, const uint32_t* lv, uint64_t o
 
 // One Jacobi superstep over the given trigger ranges.  Returns true if anything new.
 bool el_ctx::superstep(uint32_t mask, uint64_t sb, uint64_t se, uint64_t lb, uint64_t le,
-                       uint64_t ab, uint64_t ae) {
-  const bool any_trig = se > sb || le > lb || ((mask & M_RRNG) && ae > ab);
-  if (!any_trig) return false;
+                       uint64_t ab, uint64_t ae, uint64_t pb, uint64_t pe) {
+  const bool do_a = (mask & M_RRNG) && ae > ab;
+  const bool do_p = (mask & M_R4P) && pe > pb;
+  if (!(se > sb || le > lb || do_a || do_p)) return false;
   // ---- generation (read-only on the state; re-run after growing a buffer)
   HIPCHK(hipMemcpyAsync(ev_backup, ctr->ev, sizeof(hc.ev), hipMemcpyDeviceToDevice, stream));
   uint64_t saved_launch[EL_NUM_KERNELS];
   memcpy(saved_launch, launches, sizeof launches);
   for (;;) {
-    HIPCHK(hipMemsetAsync(&ctr->cand_s, 0, 4 * sizeof(uint32_t), stream));
+    HIPCHK(hipMemsetAsync(&ctr->cand_s, 0, 8 * sizeof(uint32_t), stream));
     DState st = dstate();
     if (se > sb)
       launch(EL_K_EXPAND_S, [&] {
@@ -1290,10 +1385,15 @@ bool el_ctx::superstep(uint32_t mask, uint64_t sb, uint64_t se, uint64_t lb, uin
         hipLaunchKernelGGL(k_expand_l, dim3(grid_for(le - lb)), dim3(BLOCK), 0, stream, ix, st,
                            (uint32_t)lb, (uint32_t)le, mask);
       });
-    if ((mask & M_RRNG) && ae > ab)
+    if (do_a)
       launch(EL_K_EXPAND_A, [&] {
         hipLaunchKernelGGL(k_expand_a, dim3(grid_for(hx.N)), dim3(BLOCK), 0, stream, ix, st,
                            (uint32_t)ab, (uint32_t)ae);
+      });
+    if (do_p)
+      launch(EL_K_EXPAND_P, [&] {
+        hipLaunchKernelGGL(k_expand_p, dim3(grid_for(pe - pb)), dim3(BLOCK), 0, stream, ix, st,
+                           (uint32_t)pb, (uint32_t)pe);
       });
     launch(EL_K_JOBS, [&] {
       hipLaunchKernelGGL(k_jobs, dim3(2048), dim3(BLOCK), 0, stream, ix, st);
@@ -1301,68 +1401,52 @@ bool el_ctx::superstep(uint32_t mask, uint64_t sb, uint64_t se, uint64_t lb, uin
     sync();
     read_counters();
     bool redo = false;
+    auto regrow2 = [&](uint32_t need, uint64_t& cap, uint32_t*& a, uint32_t*& b) {
+      if (need <= cap) return;
+      cap = next_pow2((uint64_t)need + need / 4);
+      dfree(a);
+      dfree(b);
+      a = dalloc<uint32_t>(cap);
+      b = dalloc<uint32_t>(cap);
+      redo = true;
+    };
     if (hc.jobs > job_cap) {
       job_cap = next_pow2((uint64_t)hc.jobs + hc.jobs / 4);
       dfree(jobs);
       jobs = dalloc<uint4>(job_cap);
       redo = true;
     }
-    if (hc.cand_s > cs_cap) {
-      cs_cap = next_pow2((uint64_t)hc.cand_s + hc.cand_s / 4);
-      dfree(cs_x);
-      dfree(cs_a);
-      cs_x = dalloc<uint32_t>(cs_cap);
-      cs_a = dalloc<uint32_t>(cs_cap);
-      redo = true;
-    }
-    if (hc.cand_l > cl_cap) {
-      cl_cap = next_pow2((uint64_t)hc.cand_l + hc.cand_l / 4);
-      dfree(cl_x);
-      dfree(cl_p);
-      cl_x = dalloc<uint32_t>(cl_cap);
-      cl_p = dalloc<uint32_t>(cl_cap);
-      redo = true;
-    }
-    if (hc.cand_a > ca_cap) {
-      ca_cap = next_pow2((uint64_t)hc.cand_a + hc.cand_a / 4);
-      dfree(ca_y);
-      dfree(ca_c);
-      ca_y = dalloc<uint32_t>(ca_cap);
-      ca_c = dalloc<uint32_t>(ca_cap);
-      redo = true;
-    }
+    regrow2(hc.cand_s, cs_cap, cs_x, cs_a);
+    regrow2(hc.cand_l, cl_cap, cl_x, cl_p);
+    regrow2(hc.cand_a, ca_cap, ca_y, ca_c);
+    regrow2(hc.cand_p, cp_cap, cp_p, cp_b);
     if (!redo) break;
     // restore counters: the retried generation must count exactly once
     HIPCHK(hipMemcpyAsync(ctr->ev, ev_backup, sizeof(hc.ev), hipMemcpyDeviceToDevice, stream));
     memcpy(launches, saved_launch, sizeof launches);
   }
-  const uint64_t cand_s = hc.cand_s, cand_l = hc.cand_l, cand_a = hc.cand_a;
-  if (cand_s + cand_l + cand_a == 0) return false;
+  const uint64_t cand_s = hc.cand_s, cand_l = hc.cand_l, cand_a = hc.cand_a, cand_p = hc.cand_p;
+  if (cand_s + cand_l + cand_a + cand_p == 0) return false;
 
   // ---- capacities for the commit (new facts <= candidates)
-  if (s_count + cand_s > slog_cap) {
-    uint64_t c = next_pow2(s_count + cand_s + (s_count + cand_s) / 2);
-    dgrow(slog_x, s_count, c);
-    dgrow(slog_a, s_count, c);
-    slog_cap = c;
-  }
+  auto grow_log = [&](uint64_t used, uint64_t add, uint64_t& cap, uint32_t*& a, uint32_t*& b) {
+    if (used + add <= cap) return;
+    uint64_t c = next_pow2(used + add + (used + add) / 2);
+    dgrow(a, used, c);
+    dgrow(b, used, c);
+    cap = c;
+  };
+  grow_log(s_count, cand_s, slog_cap, slog_x, slog_a);
   if (s_count + cand_s > S.cap) S.grow(s_count, slog_cap);
-  if (l_count + cand_l > llog_cap) {
-    uint64_t c = next_pow2(l_count + cand_l + (l_count + cand_l) / 2);
-    dgrow(llog_x, l_count, c);
-    dgrow(llog_p, l_count, c);
-    llog_cap = c;
-  }
+  grow_log(l_count, cand_l, llog_cap, llog_x, llog_p);
   if (l_count + cand_l > PR.cap) PR.grow(l_count, llog_cap);
   if (l_count + cand_l > SC.cap) SC.grow(l_count, llog_cap);
   if (2 * (l_count + cand_l) > lhash_cap) rehash_links(next_pow2(4 * (l_count + cand_l)));
-  if (a_count + cand_a > alog_cap) {
-    uint64_t c = next_pow2(a_count + cand_a + 64);
-    dgrow(alog_y, a_count, c);
-    dgrow(alog_c, a_count, c);
-    alog_cap = c;
-  }
+  grow_log(a_count, cand_a + 64, alog_cap, alog_y, alog_c);
   if (2 * (a_count + cand_a) > ahash_cap) rehash_acts(next_pow2(4 * (a_count + cand_a)));
+  grow_log(p_count, cand_p, plog_cap, plog_p, plog_b);
+  if (p_count + cand_p > PP.cap) PP.grow(p_count, plog_cap);
+  if (2 * (p_count + cand_p) > phash_cap) rehash_props(next_pow2(4 * (p_count + cand_p)));
 
   // ---- commit
   DState st = dstate();
@@ -1381,19 +1465,26 @@ bool el_ctx::superstep(uint32_t mask, uint64_t sb, uint64_t se, uint64_t lb, uin
       hipLaunchKernelGGL(k_commit_a, dim3(grid_for(cand_a)), dim3(BLOCK), 0, stream, ix, st,
                          (uint32_t)cand_a);
     });
+  if (cand_p)
+    launch(EL_K_COMMIT_P, [&] {
+      hipLaunchKernelGGL(k_commit_p, dim3(grid_for(cand_p)), dim3(BLOCK), 0, stream, ix, st,
+                         (uint32_t)cand_p);
+    });
   sync();
   read_counters();
-  const uint64_t s_new = hc.s_log, l_new = hc.l_log, a_new = hc.a_log;
+  const uint64_t s_new = hc.s_log, l_new = hc.l_log, a_new = hc.a_log, p_new = hc.p_log;
   // ---- merge deltas into the CSRs
   if (s_new > s_count) merge(S, slog_x, slog_a, s_count, s_count, s_new);
   if (l_new > l_count) {
     if (hx.P) merge(PR, llog_p, llog_x, l_count, l_count, l_new);
     merge(SC, llog_x, llog_p, l_count, l_count, l_new);
   }
-  const bool changed = s_new > s_count || l_new > l_count || a_new > a_count;
+  if (p_new > p_count) merge(PP, plog_p, plog_b, p_count, p_count, p_new);
+  const bool changed = s_new > s_count || l_new > l_count || a_new > a_count || p_new > p_count;
   s_count = s_new;
   l_count = l_new;
   a_count = a_new;
+  p_count = p_new;
   return changed;
 }
 
@@ -1405,6 +1496,7 @@ void el_ctx::fill_stats(el_stats* out, double ms) {
   st.links = l_count;
   st.derived = s_count - s_init + l_count;
   st.activations = a_count;
+  st.propagations = p_count;
   uint64_t bytes = 0;
   static const uint64_t width[EL_NUM_EVENTS] = {8, 8, 4, 4, 8, 8, 16, 8};
   for (int k = 0; k < EL_NUM_KERNELS; ++k)
@@ -1579,11 +1671,12 @@ int el_step(el_ctx* c, el_rule rule, int* changed) {
   if (!c->inited) return fail(c, EL_ESTATE, "el_step before el_init");
   return guarded(c, [&] {
     const int r = (int)rule;
-    const uint64_t se = c->s_count, le = c->l_count, ae = c->a_count;
-    bool ch = c->superstep(kRuleMask[r], c->wm_s[r], se, c->wm_l[r], le, c->wm_a[r], ae);
+    const uint64_t se = c->s_count, le = c->l_count, ae = c->a_count, pe = c->p_count;
+    bool ch = c->superstep(kRuleMask[r], c->wm_s[r], se, c->wm_l[r], le, c->wm_a[r], ae, c->wm_p[r], pe);
     c->wm_s[r] = se;
     c->wm_l[r] = le;
     c->wm_a[r] = ae;
+    c->wm_p[r] = pe;
     *changed = ch ? 1 : 0;
     c->fill_stats(nullptr, 0.0);
     return EL_OK;
@@ -1596,30 +1689,36 @@ int el_saturate(el_ctx* c, el_stats* stats) {
   return guarded(c, [&] {
     auto t0 = std::chrono::steady_clock::now();
     // all rule types share one frontier: start at the oldest watermark
-    uint64_t sb = c->s_count, lb = c->l_count, ab = c->a_count;
+    uint64_t sb = c->s_count, lb = c->l_count, ab = c->a_count, pb = c->p_count;
     for (int r = 0; r < EL_NUM_RULE_TYPES; ++r) {
       sb = std::min(sb, c->wm_s[r]);
       lb = std::min(lb, c->wm_l[r]);
       ab = std::min(ab, c->wm_a[r]);
     }
+    // propagations left by per-rule stepping that CR_TYPE3_2 has not fanned out yet; every
+    // propagation generated by a fused superstep fans out immediately (M_R4D)
+    pb = std::min(pb, c->wm_p[EL_CR_TYPE3_2]);
+    uint64_t pe = c->p_count;
     c->tr_s.clear();
     c->tr_l.clear();
     c->tr_a.clear();
     for (;;) {
       const uint64_t se = c->s_count, le = c->l_count, ae = c->a_count;
-      if (se == sb && le == lb && ae == ab) break;
+      if (se == sb && le == lb && ae == ab && pb == pe) break;
       c->tr_s.push_back(se - sb);
       c->tr_l.push_back(le - lb);
       c->tr_a.push_back(ae - ab);
-      c->superstep(M_ALL, sb, se, lb, le, ab, ae);
+      c->superstep(pb < pe ? (M_ALL | M_R4P) : M_ALL, sb, se, lb, le, ab, ae, pb, pe);
       sb = se;
       lb = le;
       ab = ae;
+      pb = pe = c->p_count;
     }
     for (int r = 0; r < EL_NUM_RULE_TYPES; ++r) {
       c->wm_s[r] = c->s_count;
       c->wm_l[r] = c->l_count;
       c->wm_a[r] = c->a_count;
+      c->wm_p[r] = c->p_count;
     }
     c->sync();
     c->read_counters();

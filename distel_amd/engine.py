@@ -22,7 +22,8 @@ EL_OK, EL_EINVAL, EL_ENOMEM, EL_EHIP, EL_ESTATE, EL_ERANGE = 0, -1, -2, -3, -4, 
 LAYOUT_X_TO_B, LAYOUT_B_TO_X = 0, 1
 
 KERNEL_NAMES = ["k_expand_s", "k_expand_l", "k_jobs", "k_expand_a", "k_commit_s", "k_commit_l", "k_commit_a",
-                "hipcub_scan", "k_merge_ptr", "k_scatter_old", "k_scatter_new", "k_init", "k_rehash"]
+                "hipcub_scan", "k_merge_ptr", "k_scatter_old", "k_scatter_new", "k_init", "k_rehash",
+                "k_expand_p", "k_commit_p"]
 EVENT_NAMES = ["trig", "row", "ent", "test", "hash", "emit", "job", "rmw"]
 EVENT_BYTES = [8, 8, 4, 4, 8, 8, 16, 8]
 NUM_KERNELS = len(KERNEL_NAMES)
@@ -72,7 +73,7 @@ class _ElConfig(C.Structure):
 class _ElStats(C.Structure):
     _fields_ = [("supersteps", C.c_uint32), ("s_facts", C.c_uint64), ("s_init", C.c_uint64),
                 ("links", C.c_uint64), ("derived", C.c_uint64), ("activations", C.c_uint64),
-                ("bytes", C.c_uint64), ("ms", C.c_double)]
+                ("propagations", C.c_uint64), ("bytes", C.c_uint64), ("ms", C.c_double)]
 
 
 class _ElKernelStat(C.Structure):
@@ -170,7 +171,7 @@ class Stats(dict):
     @staticmethod
     def from_c(s: _ElStats) -> "Stats":
         return Stats(supersteps=s.supersteps, s_facts=s.s_facts, s_init=s.s_init, links=s.links, derived=s.derived,
-                     activations=s.activations, bytes=s.bytes, ms=s.ms)
+                     activations=s.activations, propagations=s.propagations, bytes=s.bytes, ms=s.ms)
 
 
 class Engine:

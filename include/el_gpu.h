@@ -144,7 +144,7 @@ typedef struct el_config {
 typedef enum el_kernel {
   EL_K_EXPAND_S = 0,     /* k_expand_s:  ΔS-triggered CR1, CR2, CR3, CR4 half-1, ⊥ (Y side), range */
   EL_K_EXPAND_L = 1,     /* k_expand_l:  Δlink-triggered CR4 half-2, CR5, CR6, ⊥, domain/range */
-  EL_K_JOBS = 2,         /* k_jobs:      fan-out over predecessor / S-row / successor lists */
+  EL_K_JOBS = 2,         /* k_jobs:      fan-out over predecessor / successor lists */
   EL_K_EXPAND_A = 3,     /* k_expand_a:  range activations, column sweep of S */
   EL_K_COMMIT_S = 4,     /* k_commit_s:  bit-row atomicOr dedup + ΔS append */
   EL_K_COMMIT_L = 5,     /* k_commit_l:  link hash-set dedup + Δlink append */
@@ -154,8 +154,10 @@ typedef enum el_kernel {
   EL_K_SCATTER_OLD = 9,  /* k_scatter_old: move existing CSR entries */
   EL_K_SCATTER_NEW = 10, /* k_scatter_new: place delta entries */
   EL_K_INIT = 11,        /* k_init:      S(X) = {X, ⊤} */
-  EL_K_REHASH = 12,      /* k_rehash:    link / activation set growth */
-  EL_NUM_KERNELS = 13
+  EL_K_REHASH = 12,      /* k_rehash:    link / activation / propagation set growth */
+  EL_K_EXPAND_P = 13,    /* k_expand_p:  new CR4 propagations × predecessors (per-rule stepping) */
+  EL_K_COMMIT_P = 14,    /* k_commit_p:  CR4 propagation set dedup ("Yr" -> B, T3_2 DB0) */
+  EL_NUM_KERNELS = 15
 } el_kernel;
 
 /* Algorithmic event counters; identical in the CPU oracle. */
@@ -185,6 +187,7 @@ typedef struct el_stats {
   uint64_t links;              /* Σ_r |R(r)| */
   uint64_t derived;            /* s_facts - s_init + links   */
   uint64_t activations;        /* range activations (Y, C) */
+  uint64_t propagations;       /* CR4 propagations ((r, Y), B): B for every X with (X, Y) ∈ R(r) */
   uint64_t bytes;              /* Σ algorithmic bytes over all kernels */
   double ms;                   /* wall ms of the call (device synchronised) */
 } el_stats;

@@ -45,10 +45,15 @@
 enum {
   M_R1 = 1u << 0, M_R2 = 1u << 1, M_R3 = 1u << 2, M_R4Y = 1u << 3, M_R4L = 1u << 4,
   M_R5 = 1u << 5, M_R6 = 1u << 6, M_RBOT = 1u << 7, M_RDOM = 1u << 8, M_RRNG = 1u << 9,
-  M_ALL = (1u << 10) - 1
+  M_R4P = 1u << 10, /* new propagations × existing predecessors (per-rule stepping) */
+  M_R4D = 1u << 11, /* fused mode: a new propagation fans out to predecessors at once */
+  M_ALL = M_R1 | M_R2 | M_R3 | M_R4Y | M_R4L | M_R5 | M_R6 | M_RBOT | M_RDOM | M_RRNG | M_R4D
 };
+/* el_rule -> sub-rules; CR4 is factored through propagations ((r, Y), B) exactly as the
+ * reference splits it: T3_1 writes "Yr" -> B (Type3_1AxiomProcessorBase.java:208-234),
+ * T3_2 joins them with R(r) (Type3_2AxiomProcessorBase.java:67-96, parts 1 and 2). */
 static const uint32_t rule_mask[EL_NUM_RULE_TYPES] = {
-    M_R1, M_R2, M_R3 | M_RDOM | M_RRNG, M_R4Y, M_R4L, M_R5, M_R6, M_RBOT};
+    M_R1, M_R2, M_R3 | M_RDOM | M_RRNG, M_R4Y, M_R4L | M_R4P, M_R5, M_R6, M_RBOT};
 
 /* ------------------------------------------------------------------ small containers */
 
@@ -200,8 +205,11 @@ struct elo_ctx {
   hset acts;
   vec alog_y, alog_c;
   uint8_t* has_act;
+  hset props; /* CR4 propagations (pid, B) */
+  vec plog_p, plog_b;
+  vec* prow; /* propagations per pid */
   uint64_t s_init;
-  uint64_t wm_s[EL_NUM_RULE_TYPES], wm_l[EL_NUM_RULE_TYPES], wm_a[EL_NUM_RULE_TYPES];
+  uint64_t wm_s[EL_NUM_RULE_TYPES], wm_l[EL_NUM_RULE_TYPES], wm_a[EL_NUM_RULE_TYPES], wm_p[EL_NUM_RULE_TYPES];
   uint64_t ev[EL_NUM_KERNELS][EL_NUM_EVENTS];
   vec tr_s, tr_l, tr_a; /* low 32 bits suffice for tests */
   uint32_t supersteps;
@@ -504,6 +512,8 @@ int elo_create(elo_ctx** out, const el_axioms* ax, int mode) {
   c->pred = (vec*)calloc(c->P ? c->P : 1, sizeof(vec));
   c->succ = (vec*)calloc(c->N, sizeof(vec));
   c->has_act = (uint8_t*)calloc(c->N, 1);
+  c->prow = (vec*)calloc(c->P ? c->P : 1, sizeof(vec));
+  hs_init(&c->props, 1024);
   hs_init(&c->links, 1024);
   hs_init(&c->acts, 64);
   if (mode == 1) {
@@ -522,12 +532,13 @@ int elo_create(elo_ctx** out, const el_axioms* ax, int mode) {
 /* ------------------------------------------------------------------ semi-naive engine */
 
 typedef struct {
-  vec sx, sa, lx, lp, ay, ac;
+  vec sx, sa, lx, lp, ay, ac, pp, pb;
   vec jt, jb, jl, ja, jbb; /* job records */
 } cands;
 
 static void cands_free(cands* k) {
   free(k->sx.v), free(k->sa.v), free(k->lx.v), free(k->lp.v), free(k->ay.v), free(k->ac.v);
+  free(k->pp.v), free(k->pb.v);
   free(k->jt.v), free(k->jb.v), free(k->jl.v), free(k->ja.v), free(k->jbb.v);
 }
 
@@ -551,7 +562,7 @@ static void emit_job(elo_ctx* c, cands* k, int kern, uint32_t type, uint32_t b, 
   vpush(&k->jbb, bb);
 }
 
-enum { JOB_PRED_S = 0, JOB_PRED_L = 1, JOB_R4L = 2, JOB_R6A = 3 };
+enum { JOB_PRED_S = 0, JOB_PRED_L = 1, JOB_R6A = 3 };
 
 /* scan of the filler's pair range (sorted by role): one row lookup + entries read */
 static uint32_t pair_lookup(elo_ctx* c, int kern, uint32_t r, uint32_t y) {
@@ -617,15 +628,23 @@ static void expand_s(elo_ctx* c, cands* k, uint32_t mask, uint64_t b, uint64_t e
         if (!hs_has(&c->links, lkey(pid, X))) emit_l(c, k, K, X, pid);
       }
     }
-    if (mask & M_R4Y) {
+    if (mask & M_R4Y) { /* A ∈ S(Y=X) new, ∃r.A ⊑ B => propagation ((r, Y), B) */
       EV(K, EL_EV_ROW);
       for (j = c->exl.ptr[A]; j < c->exl.ptr[A + 1]; ++j) {
         uint32_t r = c->exl.a[j], B = c->exl.b[j], pid;
         EVN(K, EL_EV_ENT, 2);
         pid = pair_lookup(c, K, r, X);
         if (pid != NONE) {
-          EV(K, EL_EV_ROW);
-          if (c->pred[pid].n) emit_job(c, k, K, JOB_PRED_S, pid, (uint32_t)c->pred[pid].n, 0, B);
+          EV(K, EL_EV_HASH);
+          if (!hs_has(&c->props, lkey(pid, B))) {
+            EV(K, EL_EV_EMIT);
+            vpush(&k->pp, pid);
+            vpush(&k->pb, B);
+            if (mask & M_R4D) {
+              EV(K, EL_EV_ROW);
+              if (c->pred[pid].n) emit_job(c, k, K, JOB_PRED_S, pid, (uint32_t)c->pred[pid].n, 0, B);
+            }
+          }
         }
       }
     }
@@ -663,11 +682,14 @@ static void expand_l(elo_ctx* c, cands* k, uint32_t mask, uint64_t b, uint64_t e
     uint32_t r = c->pair_role[pid], Y = c->pair_y[pid];
     EV(K, EL_EV_TRIG);
     EVN(K, EL_EV_ENT, 2);
-    if (mask & M_R4L) {
-      EV(K, EL_EV_ENT);
-      if (c->role_has_exl[r]) {
-        EV(K, EL_EV_ROW);
-        if (c->srow[Y].n) emit_job(c, k, K, JOB_R4L, Y, (uint32_t)c->srow[Y].n, X, r);
+    if (mask & M_R4L) { /* (X, Y) ∈ R(r) new, propagation ((r, Y), B) => B ∈ S(X) */
+      size_t q;
+      EV(K, EL_EV_ROW);
+      for (q = 0; q < c->prow[pid].n; ++q) {
+        uint32_t B = c->prow[pid].v[q];
+        EV(K, EL_EV_ENT);
+        EV(K, EL_EV_TEST);
+        if (!bit(c, X, B)) emit_s(c, k, K, X, B);
       }
     }
     if (mask & M_RBOT) {
@@ -766,23 +788,6 @@ static void run_jobs(elo_ctx* c, cands* k) {
         EV(K, EL_EV_HASH);
         if (!hs_has(&c->links, lkey(a, xp))) emit_l(c, k, K, xp, a);
       }
-    } else if (type == JOB_R4L) {
-      uint32_t X = a, r = b;
-      for (q = 0; q < len; ++q) {
-        uint32_t A = c->srow[owner].v[q];
-        EV(K, EL_EV_ENT);
-        EV(K, EL_EV_ROW);
-        for (e = c->exl.ptr[A]; e < c->exl.ptr[A + 1]; ++e) {
-          uint32_t rr = c->exl.a[e];
-          EVN(K, EL_EV_ENT, 2);
-          if (rr > r) break;
-          if (rr == r) {
-            uint32_t B = c->exl.b[e];
-            EV(K, EL_EV_TEST);
-            if (!bit(c, X, B)) emit_s(c, k, K, X, B);
-          }
-        }
-      }
     } else { /* JOB_R6A */
       uint32_t X = a, r = b;
       for (q = 0; q < len; ++q) {
@@ -820,6 +825,17 @@ static void expand_a(elo_ctx* c, cands* k, uint64_t ab, uint64_t ae) {
     }
 }
 
+static void expand_p(elo_ctx* c, cands* k, uint64_t pb, uint64_t pe) {
+  const int K = EL_K_EXPAND_P;
+  uint64_t i;
+  for (i = pb; i < pe; ++i) {
+    uint32_t pid = c->plog_p.v[i], B = c->plog_b.v[i];
+    EV(K, EL_EV_TRIG);
+    EV(K, EL_EV_ROW);
+    if (c->pred[pid].n) emit_job(c, k, K, JOB_PRED_S, pid, (uint32_t)c->pred[pid].n, 0, B);
+  }
+}
+
 /* analytic events of one CSR merge (same formula as the GPU host side) */
 static void merge_events(elo_ctx* c, uint64_t nrows, uint64_t old_n, uint64_t nn) {
   uint64_t n1 = nrows + 1;
@@ -839,18 +855,20 @@ static void merge_events(elo_ctx* c, uint64_t nrows, uint64_t old_n, uint64_t nn
 }
 
 static int superstep(elo_ctx* c, uint32_t mask, uint64_t sb, uint64_t se, uint64_t lb, uint64_t le,
-                     uint64_t ab, uint64_t ae) {
+                     uint64_t ab, uint64_t ae, uint64_t pb, uint64_t pe) {
   cands k;
   size_t i;
-  uint64_t s0 = c->slog_x.n, l0 = c->llog_x.n, a0 = c->alog_y.n;
-  if (!(se > sb || le > lb || ((mask & M_RRNG) && ae > ab))) return 0;
+  uint64_t s0 = c->slog_x.n, l0 = c->llog_x.n, a0 = c->alog_y.n, p0 = c->plog_p.n;
+  int do_a = (mask & M_RRNG) && ae > ab, do_p = (mask & M_R4P) && pe > pb;
+  if (!(se > sb || le > lb || do_a || do_p)) return 0;
   memset(&k, 0, sizeof k);
   /* generation: reads only the state of the previous step */
   expand_s(c, &k, mask, sb, se, a0);
   expand_l(c, &k, mask, lb, le);
-  if ((mask & M_RRNG) && ae > ab) expand_a(c, &k, ab, ae);
+  if (do_a) expand_a(c, &k, ab, ae);
+  if (do_p) expand_p(c, &k, pb, pe);
   run_jobs(c, &k);
-  if (k.sx.n + k.lx.n + k.ay.n == 0) {
+  if (k.sx.n + k.lx.n + k.ay.n + k.pp.n == 0) {
     cands_free(&k);
     return 0;
   }
@@ -889,13 +907,25 @@ static int superstep(elo_ctx* c, uint32_t mask, uint64_t sb, uint64_t se, uint64
       c->has_act[y] = 1;
     }
   }
+  for (i = 0; i < k.pp.n; ++i) {
+    uint32_t pid = k.pp.v[i], b = k.pb.v[i];
+    EV(EL_K_COMMIT_P, EL_EV_TRIG);
+    EV(EL_K_COMMIT_P, EL_EV_HASH);
+    if (hs_add(&c->props, lkey(pid, b))) {
+      EV(EL_K_COMMIT_P, EL_EV_EMIT);
+      vpush(&c->plog_p, pid);
+      vpush(&c->plog_b, b);
+      vpush(&c->prow[pid], b);
+    }
+  }
   cands_free(&k);
   if (c->slog_x.n > s0) merge_events(c, c->N, s0, c->slog_x.n - s0);
   if (c->llog_x.n > l0) {
     if (c->P) merge_events(c, c->P, l0, c->llog_x.n - l0);
     merge_events(c, c->N, l0, c->llog_x.n - l0);
   }
-  return c->slog_x.n > s0 || c->llog_x.n > l0 || c->alog_y.n > a0;
+  if (c->plog_p.n > p0) merge_events(c, c->P, p0, c->plog_p.n - p0);
+  return c->slog_x.n > s0 || c->llog_x.n > l0 || c->alog_y.n > a0 || c->plog_p.n > p0;
 }
 
 /* ------------------------------------------------------------------ naive engine */
@@ -997,18 +1027,20 @@ int elo_init(elo_ctx* c) {
 }
 
 int elo_step(elo_ctx* c, int rule, int* changed) {
-  uint64_t se, le, ae;
+  uint64_t se, le, ae, pe;
   if (!c || !changed || rule < 0 || rule >= EL_NUM_RULE_TYPES || c->mode != 0) return EL_EINVAL;
-  se = c->slog_x.n, le = c->llog_x.n, ae = c->alog_y.n;
-  *changed = superstep(c, rule_mask[rule], c->wm_s[rule], se, c->wm_l[rule], le, c->wm_a[rule], ae);
+  se = c->slog_x.n, le = c->llog_x.n, ae = c->alog_y.n, pe = c->plog_p.n;
+  *changed = superstep(c, rule_mask[rule], c->wm_s[rule], se, c->wm_l[rule], le, c->wm_a[rule], ae,
+                       c->wm_p[rule], pe);
   c->wm_s[rule] = se;
   c->wm_l[rule] = le;
   c->wm_a[rule] = ae;
+  c->wm_p[rule] = pe;
   return EL_OK;
 }
 
 int elo_saturate(elo_ctx* c) {
-  uint64_t sb, lb, ab;
+  uint64_t sb, lb, ab, pb, pe;
   int r;
   if (!c) return EL_EINVAL;
   if (c->mode == 1) return naive_saturate(c);
@@ -1018,22 +1050,27 @@ int elo_saturate(elo_ctx* c) {
     if (c->wm_l[r] < lb) lb = c->wm_l[r];
     if (c->wm_a[r] < ab) ab = c->wm_a[r];
   }
+  /* propagations from per-rule stepping not yet fanned out by CR_TYPE3_2 */
+  pb = c->wm_p[EL_CR_TYPE3_2] < c->plog_p.n ? c->wm_p[EL_CR_TYPE3_2] : c->plog_p.n;
+  pe = c->plog_p.n;
   c->tr_s.n = c->tr_l.n = c->tr_a.n = 0;
   c->supersteps = 0;
   for (;;) {
     uint64_t se = c->slog_x.n, le = c->llog_x.n, ae = c->alog_y.n;
-    if (se == sb && le == lb && ae == ab) break;
+    if (se == sb && le == lb && ae == ab && pb == pe) break;
     vpush(&c->tr_s, (uint32_t)(se - sb));
     vpush(&c->tr_l, (uint32_t)(le - lb));
     vpush(&c->tr_a, (uint32_t)(ae - ab));
     c->supersteps++;
-    superstep(c, M_ALL, sb, se, lb, le, ab, ae);
+    superstep(c, pb < pe ? (M_ALL | M_R4P) : M_ALL, sb, se, lb, le, ab, ae, pb, pe);
     sb = se, lb = le, ab = ae;
+    pb = pe = c->plog_p.n;
   }
   for (r = 0; r < EL_NUM_RULE_TYPES; ++r) {
     c->wm_s[r] = c->slog_x.n;
     c->wm_l[r] = c->llog_x.n;
     c->wm_a[r] = c->alog_y.n;
+    c->wm_p[r] = c->plog_p.n;
   }
   return EL_OK;
 }
@@ -1164,6 +1201,9 @@ void elo_destroy(elo_ctx* c) {
     for (i = 0; i < c->N; ++i) free(c->succ[i].v);
   if (c->pred)
     for (i = 0; i < c->P; ++i) free(c->pred[i].v);
+  if (c->prow)
+    for (i = 0; i < c->P; ++i) free(c->prow[i].v);
+  free(c->prow), free(c->props.t), free(c->plog_p.v), free(c->plog_b.v);
   free(c->srow), free(c->succ), free(c->pred), free(c->has_act);
   free(c->slog_x.v), free(c->slog_a.v), free(c->llog_x.v), free(c->llog_p.v);
   free(c->alog_y.v), free(c->alog_c.v), free(c->tr_s.v), free(c->tr_l.v), free(c->tr_a.v);
