@@ -58,30 +58,15 @@ def main():
     args = parse()
     import torch
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    dist = None
-    if world > 1:
-        import torch.distributed as dist
-        backend = "nccl" if torch.cuda.is_available() else "gloo"
-        if backend == "nccl":
-            torch.cuda.set_device(local)
-        dist.init_process_group(backend=backend)
-    has_cuda = torch.cuda.is_available()
-
-    def barrier_sync():
-        if has_cuda:
-            torch.cuda.synchronize()
-        if dist is not None:
-            dist.barrier()
-        if has_cuda:
-            torch.cuda.synchronize()
-
+    from distel_amd import dist as D
     from distel_amd import engine, generators
 
+    rk = D.init_from_env()
+    world, rank, local = rk.world, rk.rank, rk.local
+    has_cuda = torch.cuda.is_available()
+
     t0 = time.time()
-    ax = generators.workload(args.workload, args.scale)
+    ax = generators.workload(args.workload, args.scale)   # this rank's copy (×world disjoint copies)
     gen_s = time.time() - t0
 
     eng = engine.Engine(device=local if has_cuda else 0)
@@ -89,27 +74,11 @@ def main():
     eng.load(ax)  # host index build + upload: AxiomLoader's part, reported separately
     load_s = time.time() - t0
 
-    st = None
-    for _ in range(args.warmup):
+    def classify():
         eng.init()
-        st = eng.saturate()
-    barrier_sync()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        eng.init()
-        st = eng.saturate()
-    barrier_sync()
-    elapsed = time.perf_counter() - t0
-    t_max = elapsed
-    derived_all = st["derived"] * world
-    if dist is not None:
-        dev = torch.device("cuda", local) if has_cuda else torch.device("cpu")
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        t_max = float(t.item())
-        d = torch.tensor([st["derived"]], dtype=torch.int64, device=dev)
-        dist.all_reduce(d, op=dist.ReduceOp.SUM)
-        derived_all = int(d.item())
+        return eng.saturate()
+
+    t_max, derived_all, st = D.run_weak(rk, classify, args.steps, args.warmup)
     ms_per_step = 1e3 * t_max / args.steps
     value = derived_all * args.steps / t_max
 
@@ -189,8 +158,7 @@ def main():
         if args.verbose and kernels:
             line["kernels"] = kernels
         print(json.dumps(line), flush=True)
-    if dist is not None:
-        dist.destroy_process_group()
+    D.shutdown(rk)
 
 
 if __name__ == "__main__":

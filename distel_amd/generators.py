@@ -38,25 +38,35 @@ def _levels(m: int, depth: int, growth: float) -> np.ndarray:
     return np.minimum(b, m)
 
 
-def _taxonomy(rng: np.random.Generator, m: int, depth: int, mean_parents: float, growth: float = 1.45):
-    """Return (child, parent, level) arrays over local class indices 0..m-1."""
+def _taxonomy(rng: np.random.Generator, m: int, depth: int, mean_parents: float, growth: float = 1.45,
+              window: int = 6):
+    """Return (child, parent, level, bounds) over local class indices 0..m-1.
+
+    Every class below level 0 has a first parent on the previous level at the same
+    relative position (plus jitter), so subtrees stay local; extra parents (Poisson)
+    come from one to three levels up, near the first parent's relative position.
+    This keeps ancestor sets realistic (tens, not thousands)."""
     b = _levels(m, depth, growth)
     level = np.searchsorted(b, np.arange(m), side="right") - 1
-    ch, pa = [], []
     idx = np.arange(m)
     mask = level > 0
     kids = idx[mask]
     lv = level[mask]
-    lo, hi = b[lv - 1], b[lv]
-    first = lo + (rng.random(kids.size) * (hi - lo)).astype(np.int64)
-    ch.append(kids)
-    pa.append(first)
+    rel = (kids - b[lv]) / np.maximum(b[lv + 1] - b[lv], 1)      # relative position in own level
+
+    def pick(lvl, jitter):
+        lo, hi = b[lvl], b[lvl + 1]
+        pos = lo + np.floor(rel_sel * (hi - lo)).astype(np.int64) + jitter
+        return np.clip(pos, lo, hi - 1)
+    rel_sel = rel
+    first = pick(lv - 1, np.zeros(kids.size, dtype=np.int64))  # a proper tree spine
+    ch, pa = [kids], [first]
     extra = rng.poisson(max(mean_parents - 1.0, 0.0), kids.size)
     rep = np.repeat(np.arange(kids.size), extra)
     if rep.size:
-        lo2 = b[np.maximum(lv[rep] - 3, 0)]
-        hi2 = b[lv[rep]]
-        par = lo2 + (rng.random(rep.size) * (hi2 - lo2)).astype(np.int64)
+        tl = np.maximum(lv[rep] - 1, 0)   # a sibling of the first parent: diamonds re-converge
+        rel_sel = rel[rep]
+        par = pick(tl, rng.integers(-2, 3, rep.size))
         ch.append(kids[rep])
         pa.append(par)
     c = np.concatenate(ch)
@@ -74,12 +84,18 @@ def _zipf_roles(rng: np.random.Generator, n: int, roles: Sequence[int], s: float
 
 
 def _general_filler(rng: np.random.Generator, a_local: np.ndarray, level: np.ndarray, b: np.ndarray,
-                    lift: int = 1) -> np.ndarray:
-    """A filler strictly above A: a random class on a level in [0, level(A) - lift]."""
+                    lift: int = 1, span: int = 4, local: bool = False) -> np.ndarray:
+    """A filler above A: a class on a level in [level(A) - lift - span + 1, level(A) - lift]
+    (clamped at 0) — more general than A, but not arbitrarily general.  ``local`` keeps the
+    filler near A's relative position (definitions name related concepts)."""
     la = level[a_local]
     top = np.maximum(la - lift, 0)
-    lv = (rng.random(a_local.size) * (top + 1)).astype(np.int64)
+    lv = np.maximum(top - rng.integers(0, span, a_local.size), 0)
     lo, hi = b[lv], b[lv + 1]
+    if local:
+        rel = (a_local - b[la]) / np.maximum(b[la + 1] - b[la], 1)
+        pos = lo + np.floor(rel * (hi - lo)).astype(np.int64) + rng.integers(-3, 4, a_local.size)
+        return np.clip(pos, lo, hi - 1)
     return lo + (rng.random(a_local.size) * (hi - lo)).astype(np.int64)
 
 
@@ -131,7 +147,7 @@ def shaped(seed: int, n: int, n_roles: int, depth: int, mean_parents: float, ex_
         dr = rng.choice(n_roles, size=nd, p=w / w.sum())
     else:
         dr = _zipf_roles(rng, nd, list(range(n_roles)), zipf_s)
-    dc = _general_filler(rng, da, level, b, lift + 1)
+    dc = _general_filler(rng, da, level, b, lift + 1, local=True)
     F = base + m + np.arange(nd)
     ex_rhs.append(np.stack([da + base, dr, dc + base], 1))
     ex_lhs = np.stack([dr, dc + base, F], 1)
@@ -171,12 +187,12 @@ def g2_nci(seed: int = 0x4C1, n: int = 70_000) -> Axioms:
 
 
 def g3_snomed(seed: int = 0x5C7, n: int = 300_000) -> Axioms:
-    """G3 "SNOMED-shaped": 60 roles (Zipf 1.1), mean 1.7 parents, depth ≤ 30, 0.8·N
+    """G3 "SNOMED-shaped": 60 roles (Zipf 1.1), mean 1.7 parents, depth 24, 0.8·N
     existentials, 0.3·N full definitions, 10 r ⊑ s, 2 chains + 3 transitive roles."""
     sub = [(10 + i, 50 + i) for i in range(10)]
-    return shaped(seed, n, n_roles=60, depth=30, mean_parents=1.7, ex_frac=0.8, def_frac=0.3, zipf_s=1.1,
+    return shaped(seed, n, n_roles=60, depth=24, mean_parents=1.7, ex_frac=0.8, def_frac=0.3, zipf_s=1.1,
                   transitive=[57, 58, 59], subroles=sub, chains=[(20, 57, 20), (21, 58, 21)], lift=2,
-                  growth=1.25)
+                  growth=1.4)
 
 
 def g4_snomed_x(copies: int = 8, seed: int = 0x5C7, n: int = 300_000) -> Axioms:

@@ -186,3 +186,18 @@ def test_bad_input_rejected():
     with pytest.raises(engine.ElError):
         eng.init()  # state error: nothing loaded
     eng.close()
+
+
+def test_classifier_rule_types_equals_fused(oracle_mod):
+    from distel_amd.classifier import ELClassifier
+    ax = generators.workload("g1", scale=0.05)
+    with ELClassifier(ax) as a:
+        a.classify("rule-types")
+        fa = a.engine.facts()
+        la = a.engine.links()
+    with ELClassifier(ax) as b:
+        b.classify("fused")
+        fb = b.engine.facts()
+        lb = b.engine.links()
+    for u, v in zip(fa + la, fb + lb):
+        assert np.array_equal(u, v)

@@ -1,0 +1,58 @@
+"""Result-node output format (CPU: fed by the oracle's facts)."""
+import os
+
+import numpy as np
+
+import kat
+from distel_amd import ir, result
+
+
+def test_packed_ids():
+    # Constants.java:30-31: ⊤ = TOP_ID 1, ⊥ = BOTTOM_ID 0; EntityType digit last
+    assert result.packed_id(1, 0) == "0110"
+    assert result.packed_id(0, 0) == "0100"
+    assert result.packed_id(12345, 2) == "05123452"
+    assert result.unpack_ids("0110" + "05123452" + "0231") == ["0110", "05123452", "0231"]
+
+
+def test_distel_numbering_order():
+    ax = ir.parse_text("individual a\nconcept B\nrole r\ndatatype d\nconcept C\nsub B C\n")
+    ids, rids = result.distel_numbering(ax)
+    names = ax.concept_names
+    num = {names[i]: int(ids[i]) for i in range(ax.n_concepts)}
+    # classes first (from 2), then individuals, then roles, then datatypes
+    assert num["owl:Thing"] == 1 and num["owl:Nothing"] == 0
+    assert num["B"] == 2 and num["C"] == 3 and num["a"] == 4
+    assert rids.tolist() == [5] and num["d"] == 6
+
+
+def test_result_node_layouts(oracle_lib):
+    ax, _ = kat.load_kat(os.path.join(kat.GOLDEN, "kat_individuals.elax"))
+    o = oracle_lib.saturate(ax, 0)
+    fx, fa = o.facts()
+    rn = result.ResultNode(ax, fx, fa, distel_compat=True)
+    db0, db1 = rn.db0(), rn.db1()
+    cid = {n: i for i, n in enumerate(ax.concept_names)}
+    # ⊤ ∈ S(X) for every class and individual: result[⊤] holds all of them
+    assert set(db0[1].tolist()) == {i for i in range(1, ax.n_concepts)}
+    # H7: ⊥ ⊑ a for individuals (result[a] ∋ ⊥)
+    assert 0 in db0[cid["a"]].tolist() and 0 in db0[cid["b"]].tolist()
+    # flip consistency
+    pairs0 = {(int(x), b) for b, xs in db0.items() for x in xs}
+    pairs1 = {(x, int(b)) for x, bs in db1.items() for b in bs}
+    assert pairs0 == pairs1
+    lines = list(rn.saxiom_lines(use_names=True))
+    assert "a|H" in lines and "a|owl:Thing" in lines
+    assert rn.axiom_counter(1)["total_subclass_axioms"] == len(lines)
+    rn2 = result.ResultNode(ax, fx, fa, distel_compat=False)
+    assert len(list(rn2.saxiom_lines())) == len(lines) - 2
+
+
+def test_write_saxioms(tmp_path, oracle_lib):
+    ax, _ = kat.load_kat(os.path.join(kat.GOLDEN, "kat_cr1_chain.elax"))
+    o = oracle_lib.saturate(ax, 0)
+    rn = result.ResultNode(ax, *o.facts())
+    p = tmp_path / "final-saxioms-distel.txt"
+    n = rn.write_saxioms(str(p))
+    text = p.read_text().splitlines()
+    assert n == len(text) and "0120|0150" in text  # A (id 2) ⊑ D (id 5)
