@@ -102,11 +102,16 @@ struct DIndex {
   const uint32_t *dom_ptr, *dom_c;
   const uint32_t *rng_ptr, *rng_c;
   const uint8_t* role_has_exl;
+  const uint4* meta;  // per concept A: {told_ptr, cidx_ptr, exr_ptr, exl_ptr}[A] — one 32 B span for A, A+1
   uint32_t has_range;
 };
 
+// Event counters live in their own array, EV_SLOTS copies per (kernel, event) so the
+// per-block flushes of a launch spread over 16 addresses (host sums the slots).
+constexpr int EV_SLOTS = 16;
+constexpr size_t EV_WORDS = (size_t)EL_NUM_KERNELS * EL_NUM_EVENTS * EV_SLOTS;
+
 struct DCounters {
-  unsigned long long ev[EL_NUM_KERNELS][EL_NUM_EVENTS];
   uint32_t s_log, l_log, a_log, p_log;
   uint32_t cand_s, cand_l, cand_a, jobs;
   uint32_t cand_p, pad1, pad2, pad3;
@@ -126,18 +131,19 @@ struct DState {
   unsigned long long pmask;
   uint32_t *plog_p, *plog_b;
   const uint32_t *pp_ptr, *pp_val;  // propagations per pid (CSR, current)
-  uint32_t* pp_dcnt;
   uint32_t *cp_p, *cp_b, cp_cap;
   const uint32_t *s_ptr, *s_val;    // S rows (CSR, current)
   const uint32_t *pr_ptr, *pr_val;  // predecessors per pid
   const uint32_t *sc_ptr, *sc_val;  // successors per X
-  uint32_t *s_dcnt, *pr_dcnt, *sc_dcnt;
+  uint32_t* dcnt;  // all CSR delta counts, one array: [S rows | PR | SC | PP]
+  uint32_t off_s, off_pr, off_sc, off_pp;
   uint32_t *cs_x, *cs_a, cs_cap;
   uint32_t *cl_x, *cl_p, cl_cap;
   uint32_t *ca_y, *ca_c, ca_cap;
   uint4* jobs;
   uint32_t job_cap;
   DCounters* ctr;
+  unsigned long long* ev;  // [kernel][event][EV_SLOTS]
 };
 
 // ---------------------------------------------------------------- device helpers
@@ -159,13 +165,21 @@ __device__ __forceinline__ unsigned long long wave_sum(uint32_t x) {
   return v;
 }
 
-// Every lane of the wave must call this (it reduces over all 64 lanes).
-__device__ __forceinline__ void ev_flush(DCounters* c, int k, const Ev& e) {
+// Block-level reduction of the event counters: one LDS atomic per wave, then one global
+// atomic per (event, block) into a sharded slot.  Every thread of the block must call it.
+__device__ __forceinline__ void ev_flush(unsigned long long* evg, int k, const Ev& e) {
+  __shared__ unsigned long long sev[EL_NUM_EVENTS];
+  if (threadIdx.x < EL_NUM_EVENTS) sev[threadIdx.x] = 0;
+  __syncthreads();
 #pragma unroll
   for (int i = 0; i < EL_NUM_EVENTS; ++i) {
     unsigned long long s = wave_sum(e.v[i]);
-    if (lane_id() == 0 && s) atomicAdd(&c->ev[k][i], s);
+    if (lane_id() == 0 && s) atomicAdd(&sev[i], s);
   }
+  __syncthreads();
+  if (threadIdx.x < EL_NUM_EVENTS && sev[threadIdx.x])
+    atomicAdd(&evg[((size_t)k * EL_NUM_EVENTS + threadIdx.x) * EV_SLOTS + (blockIdx.x % EV_SLOTS)],
+              sev[threadIdx.x]);
 }
 
 // Wave-aggregated append: one atomic per wave; returns this lane's slot when pred.
@@ -178,6 +192,38 @@ __device__ __forceinline__ uint32_t wave_append(uint32_t* counter, bool pred) {
   base = __shfl(base, leader);
   uint32_t rank = (uint32_t)__popcll(m & ((1ull << lane_id()) - 1ull));
   return pred ? base + rank : NONE;
+}
+
+// Keyed counter update: lanes of a wave that hit the same counter (a hub row) share one
+// atomic.  Up to two distinct keys per wave are aggregated, the rest go one by one.  Only
+// used where hub rows exist (predecessor lists keyed by pid): for mostly-distinct keys the
+// rounds are pure overhead.
+// Returns, per lane, the value an individual atomic on that lane would have returned
+// in some serialisation (old + rank for add, old - rank for sub).
+__device__ __forceinline__ uint32_t wave_keyed_atomic(uint32_t* base, uint32_t key, bool pred, bool sub) {
+  unsigned long long pending = __ballot(pred);
+  const uint32_t lane = lane_id();
+  uint32_t result = 0;
+#pragma unroll
+  for (int round = 0; round < 2; ++round) {
+    if (pending == 0) return result;
+    const int leader = __ffsll((long long)pending) - 1;
+    const uint32_t lkey = __shfl(key, leader);
+    const unsigned long long same = __ballot(pred && key == lkey) & pending;
+    uint32_t old = 0;
+    if ((int)lane == leader) {
+      const uint32_t k = (uint32_t)__popcll(same);
+      old = sub ? atomicSub(base + lkey, k) : atomicAdd(base + lkey, k);
+    }
+    old = __shfl(old, leader);
+    if ((same >> lane) & 1ull) {
+      const uint32_t rank = (uint32_t)__popcll(same & ((1ull << lane) - 1ull));
+      result = sub ? old - rank : old + rank;
+    }
+    pending &= ~same;
+  }
+  if ((pending >> lane) & 1ull) result = sub ? atomicSub(base + key, 1u) : atomicAdd(base + key, 1u);
+  return result;
 }
 
 __device__ __forceinline__ bool test_bit(const uint32_t* bits, uint64_t W, uint32_t x, uint32_t b) {
@@ -298,8 +344,8 @@ __device__ __forceinline__ void emit_l(const DState& st, BlockQ& q, bool pred, u
   }
 }
 
-__device__ __forceinline__ void emit_job(const DState& st, BlockQ& q, bool pred, uint32_t type, uint32_t begin,
-                                         uint32_t len, uint32_t a, uint32_t b, Ev& ev) {
+__device__ __forceinline__ void emit_job1(const DState& st, BlockQ& q, bool pred, uint32_t type, uint32_t begin,
+                                          uint32_t len, uint32_t a, uint32_t b, Ev& ev) {
   const uint32_t off = lds_reserve(&q.nj, pred);
   const bool spill = pred && off >= QJ_CAP;
   const uint4 rec = make_uint4(begin, len | (type << 28), a, b);
@@ -309,6 +355,20 @@ __device__ __forceinline__ void emit_job(const DState& st, BlockQ& q, bool pred,
   }
   const uint32_t slot = wave_append(&st.ctr->jobs, spill);
   if (spill && slot < st.job_cap) st.jobs[slot] = rec;
+}
+
+// A fan-out list of len items becomes ceil(len / JOB_CHUNK) job records, so one hub
+// (a filler with 10^4 predecessors) is spread over many waves instead of serialising one.
+constexpr uint32_t JOB_CHUNK = 256;
+__device__ __forceinline__ void emit_job(const DState& st, BlockQ& q, bool pred, uint32_t type, uint32_t begin,
+                                         uint32_t len, uint32_t a, uint32_t b, Ev& ev) {
+  const uint32_t n = pred ? (len + JOB_CHUNK - 1) / JOB_CHUNK : 0u;
+  for (uint32_t c = 0; __ballot(c < n) != 0; ++c) {
+    const bool pc = c < n;
+    const uint32_t cb = begin + c * JOB_CHUNK;
+    const uint32_t cl = pc ? min(JOB_CHUNK, len - c * JOB_CHUNK) : 0u;
+    emit_job1(st, q, pc, type, cb, cl, a, b, ev);
+  }
 }
 
 // activations are rare: plain wave-aggregated global append
@@ -402,9 +462,8 @@ __global__ void k_init(DIndex ix, DState st) {
       st.slog_a[s1] = EL_TOP;
       ev.v[EL_EV_EMIT]++;
     }
-    st.s_dcnt[x] = two ? 2u : 1u;
   }
-  ev_flush(st.ctr, EL_K_INIT, ev);
+  ev_flush(st.ev, EL_K_INIT, ev);
 }
 
 // Rules triggered by new S-facts (X, A) = log[begin, end).
@@ -421,10 +480,10 @@ __global__ void k_expand_s(DIndex ix, DState st, uint32_t begin, uint32_t end, u
     if (i < end) {
       const uint32_t X = st.slog_x[i], A = st.slog_a[i];
       ev.v[EL_EV_TRIG]++;
+      const uint4 m0 = ix.meta[A], m1 = ix.meta[A + 1];  // the four CSR rows of A at once
       if (mask & M_R1) {  // A ∈ S(X), A ⊑ B  =>  B ∈ S(X)
         ev.v[EL_EV_ROW]++;
-        const uint32_t b1 = ix.told_ptr[A + 1];
-        for (uint32_t j = ix.told_ptr[A]; j < b1; ++j) {
+        for (uint32_t j = m0.x; j < m1.x; ++j) {
           const uint32_t B = ix.told_b[j];
           ev.v[EL_EV_ENT]++;
           ev.v[EL_EV_TEST]++;
@@ -433,8 +492,7 @@ __global__ void k_expand_s(DIndex ix, DState st, uint32_t begin, uint32_t end, u
       }
       if (mask & M_R2) {  // A1..An ∈ S(X), ⊓Ai ⊑ B  =>  B ∈ S(X)
         ev.v[EL_EV_ROW]++;
-        const uint32_t c1 = ix.cidx_ptr[A + 1];
-        for (uint32_t j = ix.cidx_ptr[A]; j < c1; ++j) {
+        for (uint32_t j = m0.y; j < m1.y; ++j) {
           const uint32_t c = ix.cidx_c[j];
           ev.v[EL_EV_ENT]++;
           ev.v[EL_EV_ROW]++;
@@ -462,8 +520,7 @@ __global__ void k_expand_s(DIndex ix, DState st, uint32_t begin, uint32_t end, u
       }
       if (mask & M_R3) {  // A ∈ S(X), A ⊑ ∃r.B  =>  (X, B) ∈ R(r)
         ev.v[EL_EV_ROW]++;
-        const uint32_t e1 = ix.exr_ptr[A + 1];
-        for (uint32_t j = ix.exr_ptr[A]; j < e1; ++j) {
+        for (uint32_t j = m0.z; j < m1.z; ++j) {
           const uint32_t pid = ix.exr_pid[j];
           ev.v[EL_EV_ENT]++;
           ev.v[EL_EV_HASH]++;
@@ -472,8 +529,7 @@ __global__ void k_expand_s(DIndex ix, DState st, uint32_t begin, uint32_t end, u
       }
       if (mask & M_R4Y) {  // A ∈ S(Y=X) new, ∃r.A ⊑ B  =>  propagation ((r, Y), B)
         ev.v[EL_EV_ROW]++;   // (Type3_1AxiomProcessorBase.java:208-234 writes "Yr" -> B)
-        const uint32_t e1 = ix.exl_ptr[A + 1];
-        for (uint32_t j = ix.exl_ptr[A]; j < e1; ++j) {
+        for (uint32_t j = m0.w; j < m1.w; ++j) {
           const uint32_t r = ix.exl_r[j], B = ix.exl_b[j];
           ev.v[EL_EV_ENT] += 2;
           const uint32_t pid = pair_lookup(ix, r, X, ev);
@@ -521,7 +577,7 @@ __global__ void k_expand_s(DIndex ix, DState st, uint32_t begin, uint32_t end, u
     q_maybe_flush(q, st);
   }
   q_flush(q, st);
-  ev_flush(st.ctr, EL_K_EXPAND_S, ev);
+  ev_flush(st.ev, EL_K_EXPAND_S, ev);
 }
 
 // Rules triggered by new links (X, pid = (r, Y)) = link log[begin, end).
@@ -636,7 +692,7 @@ __global__ void k_expand_l(DIndex ix, DState st, uint32_t begin, uint32_t end, u
     q_maybe_flush(q, st);
   }
   q_flush(q, st);
-  ev_flush(st.ctr, EL_K_EXPAND_L, ev);
+  ev_flush(st.ev, EL_K_EXPAND_L, ev);
 }
 
 // Wide fan-outs: one wave per job record, lanes stride over the list.
@@ -698,7 +754,7 @@ __global__ void k_jobs(DIndex ix, DState st) {
     q_maybe_flush(q, st);
   }
   q_flush(q, st);
-  ev_flush(st.ctr, EL_K_JOBS, ev);
+  ev_flush(st.ev, EL_K_JOBS, ev);
 }
 
 // Range activations (Y, C) = act log[a_begin, a_end): every X with Y ∈ S(X) gets C
@@ -726,7 +782,7 @@ __global__ void k_expand_a(DIndex ix, DState st, uint32_t a_begin, uint32_t a_en
     q_maybe_flush(q, st);
   }
   q_flush(q, st);
-  ev_flush(st.ctr, EL_K_EXPAND_A, ev);
+  ev_flush(st.ev, EL_K_EXPAND_A, ev);
 }
 
 // Dedup S candidates against the bit rows; new facts go to the log (the versioned
@@ -749,10 +805,7 @@ __global__ void k_commit_s(DIndex ix, DState st, uint32_t n) {
       const uint32_t m = 1u << (a & 31u);
       const uint32_t old = atomicOr(st.bits + (uint64_t)x * ix.W + (a >> 5), m);
       nw = (old & m) == 0;
-      if (nw) {
-        ev.v[EL_EV_EMIT]++;
-        atomicAdd(st.s_dcnt + x, 1u);
-      }
+      if (nw) ev.v[EL_EV_EMIT]++;
     }
     // one LDS slot per new fact; blockDim <= QS_CAP/2 so a round never overflows
     const uint32_t off = lds_reserve(&ln, nw);
@@ -774,7 +827,7 @@ __global__ void k_commit_s(DIndex ix, DState st, uint32_t n) {
       __syncthreads();
     }
   }
-  ev_flush(st.ctr, EL_K_COMMIT_S, ev);
+  ev_flush(st.ev, EL_K_COMMIT_S, ev);
 }
 
 // Dedup link candidates against the link set (checkAndInsertScript,
@@ -797,10 +850,10 @@ __global__ void k_commit_l(DIndex ix, DState st, uint32_t n) {
       nw = hash_insert(st.lhash, st.lmask, link_key(p, x));
       if (nw) {
         ev.v[EL_EV_EMIT]++;
-        atomicAdd(st.pr_dcnt + p, 1u);
-        atomicAdd(st.sc_dcnt + x, 1u);
+        atomicAdd(st.dcnt + st.off_sc + x, 1u);
       }
     }
+    wave_keyed_atomic(st.dcnt, st.off_pr + p, nw, false);  // hub pids: many new preds per step
     const uint32_t off = lds_reserve(&ln, nw);
     if (nw) {
       lx[off] = x;
@@ -820,7 +873,7 @@ __global__ void k_commit_l(DIndex ix, DState st, uint32_t n) {
       __syncthreads();
     }
   }
-  ev_flush(st.ctr, EL_K_COMMIT_L, ev);
+  ev_flush(st.ev, EL_K_COMMIT_L, ev);
 }
 
 __global__ void k_commit_a(DIndex ix, DState st, uint32_t n) {
@@ -839,7 +892,7 @@ __global__ void k_commit_a(DIndex ix, DState st, uint32_t n) {
       st.has_act[y] = 1;
     }
   }
-  ev_flush(st.ctr, EL_K_COMMIT_A, ev);
+  ev_flush(st.ev, EL_K_COMMIT_A, ev);
 }
 
 // New CR4 propagations ((r, Y), B) = prop log[begin, end) × existing predecessors of (r, Y)
@@ -861,7 +914,7 @@ __global__ void k_expand_p(DIndex ix, DState st, uint32_t begin, uint32_t end) {
     q_maybe_flush(q, st);
   }
   q_flush(q, st);
-  ev_flush(st.ctr, EL_K_EXPAND_P, ev);
+  ev_flush(st.ev, EL_K_EXPAND_P, ev);
 }
 
 // Dedup propagation candidates (checkAndInsertScript, Type3_1AxiomProcessorBase.java:88-121)
@@ -878,44 +931,86 @@ __global__ void k_commit_p(DIndex ix, DState st, uint32_t n) {
       ev.v[EL_EV_EMIT]++;
       st.plog_p[slot] = pid;
       st.plog_b[slot] = b;
-      atomicAdd(st.pp_dcnt + pid, 1u);
+      atomicAdd(st.dcnt + st.off_pp + pid, 1u);
     }
   }
-  ev_flush(st.ctr, EL_K_COMMIT_P, ev);
+  ev_flush(st.ev, EL_K_COMMIT_P, ev);
 }
 
-// CSR merge: new_ptr[x] = ptr[x] + exclusive_scan(dcnt)[x]
-__global__ void k_merge_ptr(uint32_t* __restrict__ ptr2, const uint32_t* __restrict__ ptr,
-                            const uint32_t* __restrict__ dscan, uint32_t n1) {
-  const uint32_t stride = gridDim.x * blockDim.x;
-  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n1; i += stride)
-    ptr2[i] = ptr[i] + dscan[i];
+// CSR merges of one superstep, all CSRs at once (segments: S, PR, SC, PP).  The delta
+// counts of every CSR sit in one array, scanned once; segment k's offsets are
+// dscan[off_k + x] - dscan[off_k].
+struct MergeSeg {
+  const uint32_t *ptr, *row, *val;
+  uint32_t *ptr2, *row2, *val2;
+  const uint32_t *lx, *lv;  // delta: row key / value arrays of the log
+  uint32_t off;             // segment offset in dcnt / dscan
+  uint32_t n1;              // rows + 1
+  uint32_t n_old;           // existing entries
+  uint32_t begin, end;      // delta range in the log
+  uint32_t keyed;           // hub rows possible: aggregate same-row counter updates per wave
+};
+struct MergeArgs {
+  MergeSeg seg[4];
+  uint32_t nseg;
+  uint32_t max_rows, max_old, max_new;
+};
+
+// blockIdx.y selects the segment (uniform per block: its descriptor is loaded once);
+// blockIdx.x grid-strides over that segment.
+__global__ void k_merge_ptr(MergeArgs m, const uint32_t* __restrict__ dscan) {
+  const MergeSeg g = m.seg[blockIdx.y];
+  const uint32_t stride = gridDim.x * blockDim.x, base = dscan[g.off];
+  for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < g.n1; j += stride)
+    g.ptr2[j] = g.ptr[j] + dscan[g.off + j] - base;
 }
 
-// existing entry i of row x moves by the number of delta entries in rows < x
-__global__ void k_scatter_old(const uint32_t* __restrict__ row, const uint32_t* __restrict__ val,
-                              uint32_t* __restrict__ row2, uint32_t* __restrict__ val2,
-                              const uint32_t* __restrict__ dscan, uint32_t n_old) {
-  const uint32_t stride = gridDim.x * blockDim.x;
-  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n_old; i += stride) {
-    const uint32_t x = row[i];
-    const uint32_t j = i + dscan[x];
-    row2[j] = x;
-    val2[j] = val[i];
+// existing entry j of row x moves by the number of delta entries in rows < x
+__global__ void k_scatter_old(MergeArgs m, const uint32_t* __restrict__ dscan) {
+  const MergeSeg g = m.seg[blockIdx.y];
+  const uint32_t stride = gridDim.x * blockDim.x, base = dscan[g.off];
+  const uint32_t* __restrict__ ds = dscan + g.off;
+  for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < g.n_old; j += stride) {
+    const uint32_t x = g.row[j];
+    const uint32_t d = j + ds[x] - base;
+    g.row2[d] = x;
+    g.val2[d] = g.val[j];
   }
 }
 
-// delta entries fill the tail of their row; dcnt is consumed back to zero
-__global__ void k_scatter_new(const uint32_t* __restrict__ lx, const uint32_t* __restrict__ lv,
-                              uint32_t begin, uint32_t end, const uint32_t* __restrict__ ptr2,
-                              uint32_t* dcnt, uint32_t* __restrict__ row2, uint32_t* __restrict__ val2) {
-  const uint32_t stride = gridDim.x * blockDim.x;
-  for (uint32_t i = begin + blockIdx.x * blockDim.x + threadIdx.x; i < end; i += stride) {
-    const uint32_t x = lx[i];
-    const uint32_t pos = ptr2[x + 1] - atomicSub(dcnt + x, 1u);
-    row2[pos] = x;
-    val2[pos] = lv[i];
+// delta entries fill the tail of their row; the counts are consumed back to zero
+__global__ void k_scatter_new(MergeArgs m, uint32_t* dcnt) {
+  const MergeSeg g = m.seg[blockIdx.y];
+  const uint32_t stride = gridDim.x * blockDim.x, n = g.end - g.begin;
+  for (uint32_t base = blockIdx.x * blockDim.x; base < n; base += stride) {
+    const uint32_t i = base + threadIdx.x;
+    const bool on = i < n;
+    const uint32_t x = on ? g.lx[g.begin + i] : 0u;
+    uint32_t old;
+    if (g.keyed) {
+      old = wave_keyed_atomic(dcnt + g.off, x, on, true);
+    } else {
+      old = on ? atomicSub(dcnt + g.off + x, 1u) : 0u;
+    }
+    if (on) {
+      const uint32_t pos = g.ptr2[x + 1] - old;
+      g.row2[pos] = x;
+      g.val2[pos] = g.lv[g.begin + i];
+    }
   }
+}
+
+// per-row counts of log[begin, end) (lazy S-row CSR build for export)
+__global__ void k_count_rows(uint32_t* dcnt, const uint32_t* lx, uint32_t begin, uint32_t end) {
+  const uint32_t stride = gridDim.x * blockDim.x;
+  for (uint32_t i = begin + blockIdx.x * blockDim.x + threadIdx.x; i < end; i += stride)
+    atomicAdd(dcnt + lx[i], 1u);
+}
+
+__global__ void k_pack_keys(unsigned long long* out, const uint32_t* hi, const uint32_t* lo, uint32_t n) {
+  const uint32_t stride = gridDim.x * blockDim.x;
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
+    out[i] = ((unsigned long long)hi[i] << 32) | lo[i];
 }
 
 __global__ void k_rehash(unsigned long long* t, unsigned long long mask, const uint32_t* kx,
@@ -954,7 +1049,9 @@ void dgrow(T*& p, size_t used, size_t cap) {
   p = q;
 }
 
-uint32_t grid_for(uint64_t n, uint32_t cap = 8192) {
+// Grid-stride kernels: at most 1024 blocks (4 per CU) — enough to fill the chip and few
+// enough that the per-block flush atomics of a launch stay cheap.
+uint32_t grid_for(uint64_t n, uint32_t cap = 1024) {
   uint64_t g = (n + BLOCK - 1) / BLOCK;
   if (g < 1) g = 1;
   if (g > cap) g = cap;
@@ -974,13 +1071,13 @@ struct DevCsr {
   uint32_t *ptr = nullptr, *row = nullptr, *val = nullptr;
   uint32_t *ptr2 = nullptr, *row2 = nullptr, *val2 = nullptr;
   uint32_t *dcnt = nullptr, *dscan = nullptr;
-  void alloc(uint32_t n, uint64_t c) {
+  void alloc(uint32_t n, uint64_t c, uint32_t* dcnt_view, uint32_t* dscan_view) {
     nrows = n;
     cap = c;
     ptr = dalloc<uint32_t>(n + 1);
     ptr2 = dalloc<uint32_t>(n + 1);
-    dcnt = dalloc<uint32_t>(n + 1);
-    dscan = dalloc<uint32_t>(n + 1);
+    dcnt = dcnt_view;
+    dscan = dscan_view;
     row = dalloc<uint32_t>(c);
     val = dalloc<uint32_t>(c);
     row2 = dalloc<uint32_t>(c);
@@ -995,10 +1092,7 @@ struct DevCsr {
     val2 = dalloc<uint32_t>(c);
     cap = c;
   }
-  void reset(hipStream_t s) {
-    HIPCHK(hipMemsetAsync(ptr, 0, (nrows + 1) * sizeof(uint32_t), s));
-    HIPCHK(hipMemsetAsync(dcnt, 0, (nrows + 1) * sizeof(uint32_t), s));
-  }
+  void reset(hipStream_t s) { HIPCHK(hipMemsetAsync(ptr, 0, (nrows + 1) * sizeof(uint32_t), s)); }
   void release() {
     dfree(ptr);
     dfree(row);
@@ -1006,8 +1100,7 @@ struct DevCsr {
     dfree(ptr2);
     dfree(row2);
     dfree(val2);
-    dfree(dcnt);
-    dfree(dscan);
+    dcnt = dscan = nullptr;
   }
 };
 
@@ -1050,13 +1143,20 @@ struct el_ctx {
   uint32_t *cp_p = nullptr, *cp_b = nullptr;
   uint64_t cp_cap = 0;
   DevCsr S, PR, SC, PP;
+  uint32_t *dcnt_all = nullptr, *dscan_all = nullptr;
+  uint64_t dcnt_total = 0;
+  uint64_t s_csr_count = 0;   // S-row CSR is built lazily (only export reads it)
+  bool need_pred = true;      // predecessor CSR has readers (CR4, ⊥, CR6)
+  bool need_succ = true;      // successor CSR has readers (CR6)
   uint32_t *cs_x = nullptr, *cs_a = nullptr, *cl_x = nullptr, *cl_p = nullptr, *ca_y = nullptr,
            *ca_c = nullptr;
   uint64_t cs_cap = 0, cl_cap = 0, ca_cap = 0;
   uint4* jobs = nullptr;
   uint64_t job_cap = 0;
   DCounters* ctr = nullptr;
+  unsigned long long* ev = nullptr;
   unsigned long long* ev_backup = nullptr;
+  unsigned long long hev[EL_NUM_KERNELS][EL_NUM_EVENTS] = {};
   void* scan_tmp = nullptr;
   size_t scan_tmp_bytes = 0;
 
@@ -1094,7 +1194,6 @@ struct el_ctx {
     s.plog_b = plog_b;
     s.pp_ptr = PP.ptr;
     s.pp_val = PP.val;
-    s.pp_dcnt = PP.dcnt;
     s.cp_p = cp_p;
     s.cp_b = cp_b;
     s.cp_cap = (uint32_t)cp_cap;
@@ -1104,9 +1203,11 @@ struct el_ctx {
     s.pr_val = PR.val;
     s.sc_ptr = SC.ptr;
     s.sc_val = SC.val;
-    s.s_dcnt = S.dcnt;
-    s.pr_dcnt = PR.dcnt;
-    s.sc_dcnt = SC.dcnt;
+    s.dcnt = dcnt_all;
+    s.off_s = (uint32_t)(S.dcnt - dcnt_all);
+    s.off_pr = (uint32_t)(PR.dcnt - dcnt_all);
+    s.off_sc = (uint32_t)(SC.dcnt - dcnt_all);
+    s.off_pp = (uint32_t)(PP.dcnt - dcnt_all);
     s.cs_x = cs_x;
     s.cs_a = cs_a;
     s.cs_cap = (uint32_t)cs_cap;
@@ -1119,6 +1220,7 @@ struct el_ctx {
     s.jobs = jobs;
     s.job_cap = (uint32_t)job_cap;
     s.ctr = ctr;
+    s.ev = ev;
     return s;
   }
 
@@ -1160,14 +1262,29 @@ struct el_ctx {
     pending.clear();
   }
   void read_counters() { HIPCHK(hipMemcpy(&hc, ctr, sizeof(DCounters), hipMemcpyDeviceToHost)); }
+  void read_events() {
+    std::vector<unsigned long long> h(EV_WORDS);
+    HIPCHK(hipMemcpy(h.data(), ev, EV_WORDS * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+    for (int k = 0; k < EL_NUM_KERNELS; ++k)
+      for (int e = 0; e < EL_NUM_EVENTS; ++e) {
+        unsigned long long t = 0;
+        for (int q = 0; q < EV_SLOTS; ++q) t += h[((size_t)k * EL_NUM_EVENTS + e) * EV_SLOTS + q];
+        hev[k][e] = t;
+      }
+  }
 
   void free_state();
   void free_index();
   void alloc_state();
   void reset_state();
   void ensure_capacity();
-  void merge(DevCsr& c, const uint32_t* lx, const uint32_t* lv, uint64_t old_n, uint64_t begin,
-             uint64_t end);
+  struct MergeReq {
+    DevCsr* c;
+    const uint32_t *lx, *lv;
+    uint64_t old_n, begin, end;
+  };
+  void merge_all(const std::vector<MergeReq>& reqs, bool account = true);
+  void ensure_s_csr();
   void rehash_links(uint64_t cap);
   void rehash_acts(uint64_t cap);
   void rehash_props(uint64_t cap);
@@ -1201,6 +1318,8 @@ void el_ctx::free_state() {
   PR.release();
   SC.release();
   PP.release();
+  dfree(dcnt_all);
+  dfree(dscan_all);
   dfree(cs_x);
   dfree(cs_a);
   dfree(cl_x);
@@ -1209,6 +1328,7 @@ void el_ctx::free_state() {
   dfree(ca_c);
   dfree(jobs);
   dfree(ctr);
+  dfree(ev);
   dfree(ev_backup);
   if (scan_tmp) (void)hipFree(scan_tmp);
   scan_tmp = nullptr;
@@ -1240,10 +1360,17 @@ void el_ctx::alloc_state() {
   cp_cap = plog_cap;
   cp_p = dalloc<uint32_t>(cp_cap);
   cp_b = dalloc<uint32_t>(cp_cap);
-  PP.alloc((uint32_t)P, plog_cap);
-  S.alloc((uint32_t)N, slog_cap);
-  PR.alloc((uint32_t)P, llog_cap);
-  SC.alloc((uint32_t)N, llog_cap);
+  dcnt_total = 2 * (N + 1) + 2 * (P + 1);
+  dcnt_all = dalloc<uint32_t>(dcnt_total);
+  dscan_all = dalloc<uint32_t>(dcnt_total);
+  uint64_t o = 0;
+  S.alloc((uint32_t)N, slog_cap, dcnt_all + o, dscan_all + o);
+  o += N + 1;
+  PR.alloc((uint32_t)P, llog_cap, dcnt_all + o, dscan_all + o);
+  o += P + 1;
+  SC.alloc((uint32_t)N, llog_cap, dcnt_all + o, dscan_all + o);
+  o += N + 1;
+  PP.alloc((uint32_t)P, plog_cap, dcnt_all + o, dscan_all + o);
   cs_cap = std::max<uint64_t>(1u << 20, 4 * N);
   cl_cap = cs_cap;
   ca_cap = 1u << 12;
@@ -1256,11 +1383,11 @@ void el_ctx::alloc_state() {
   job_cap = std::max<uint64_t>(1u << 20, 2 * N);
   jobs = dalloc<uint4>(job_cap);
   ctr = dalloc<DCounters>(1);
-  ev_backup = dalloc<unsigned long long>(EL_NUM_KERNELS * EL_NUM_EVENTS);
+  ev = dalloc<unsigned long long>(EV_WORDS);
+  ev_backup = dalloc<unsigned long long>(EV_WORDS);
   size_t b1 = 0;
-  uint32_t maxrows = (uint32_t)std::max<uint64_t>(N, P) + 1;
   HIPCHK(hipcub::DeviceScan::ExclusiveSum(nullptr, b1, (uint32_t*)nullptr, (uint32_t*)nullptr,
-                                          maxrows, stream));
+                                          (uint32_t)dcnt_total, stream));
   scan_tmp_bytes = b1;
   HIPCHK(hipMalloc(&scan_tmp, b1 ? b1 : 1));
 }
@@ -1272,11 +1399,13 @@ void el_ctx::reset_state() {
   HIPCHK(hipMemsetAsync(has_act, 0, hx.N, stream));
   HIPCHK(hipMemsetAsync(phash, 0xff, phash_cap * sizeof(unsigned long long), stream));
   PP.reset(stream);
+  HIPCHK(hipMemsetAsync(dcnt_all, 0, dcnt_total * sizeof(uint32_t), stream));
   S.reset(stream);
   PR.reset(stream);
   SC.reset(stream);
   HIPCHK(hipMemsetAsync(ctr, 0, sizeof(DCounters), stream));
-  s_count = l_count = a_count = p_count = s_init = 0;
+  HIPCHK(hipMemsetAsync(ev, 0, EV_WORDS * sizeof(unsigned long long), stream));
+  s_count = l_count = a_count = p_count = s_init = s_csr_count = 0;
   for (int r = 0; r < EL_NUM_RULE_TYPES; ++r) wm_s[r] = wm_l[r] = wm_a[r] = wm_p[r] = 0;
   memset(launches, 0, sizeof launches);
   memset(host_ev, 0, sizeof host_ev);
@@ -1322,44 +1451,78 @@ void el_ctx::rehash_props(uint64_t cap) {
     });
 }
 
-// Rebuild CSR c from its current contents (old_n entries) plus log[begin, end).
-// Row keys of the delta come from lx, values from lv.
-void el_ctx::merge(DevCsr& c, const uint32_t* lx, const uint32_t* lv, uint64_t old_n, uint64_t begin,
-                   uint64_t end) {
-  const uint32_t n1 = c.nrows + 1;
-  const uint64_t nn = end - begin;
+// Rebuild every CSR with new entries: one scan over all delta counts, then one launch
+// each of k_merge_ptr / k_scatter_old / k_scatter_new over all merged segments.
+void el_ctx::merge_all(const std::vector<MergeReq>& reqs, bool account) {
+  if (reqs.empty()) return;
+  uint64_t saved_ev[EL_NUM_KERNELS][EL_NUM_EVENTS];
+  if (!account) memcpy(saved_ev, host_ev, sizeof host_ev);
+  MergeArgs m{};
+  m.nseg = (uint32_t)reqs.size();
+  for (uint32_t k = 0; k < m.nseg; ++k) {
+    const MergeReq& r = reqs[k];
+    MergeSeg& g = m.seg[k];
+    g.ptr = r.c->ptr;
+    g.row = r.c->row;
+    g.val = r.c->val;
+    g.ptr2 = r.c->ptr2;
+    g.row2 = r.c->row2;
+    g.val2 = r.c->val2;
+    g.lx = r.lx;
+    g.lv = r.lv;
+    g.off = (uint32_t)(r.c->dcnt - dcnt_all);
+    g.n1 = r.c->nrows + 1;
+    g.n_old = (uint32_t)r.old_n;
+    g.begin = (uint32_t)r.begin;
+    g.end = (uint32_t)r.end;
+    g.keyed = r.c == &PR ? 1u : 0u;
+    m.max_rows = std::max(m.max_rows, g.n1);
+    m.max_old = std::max(m.max_old, g.n_old);
+    m.max_new = std::max(m.max_new, g.end - g.begin);
+    host_ev[EL_K_MERGE_PTR][EL_EV_ENT] += 3ull * g.n1;            // read ptr, dscan; write ptr2
+    host_ev[EL_K_SCATTER_OLD][EL_EV_TRIG] += g.n_old;             // read (row, val)
+    host_ev[EL_K_SCATTER_OLD][EL_EV_ENT] += g.n_old;              // read dscan[row]
+    host_ev[EL_K_SCATTER_OLD][EL_EV_EMIT] += g.n_old;             // write (row2, val2)
+    host_ev[EL_K_SCATTER_NEW][EL_EV_TRIG] += g.end - g.begin;     // read log pair
+    host_ev[EL_K_SCATTER_NEW][EL_EV_ENT] += g.end - g.begin;      // read ptr2[x + 1]
+    host_ev[EL_K_SCATTER_NEW][EL_EV_RMW] += g.end - g.begin;      // consume the delta count
+    host_ev[EL_K_SCATTER_NEW][EL_EV_EMIT] += g.end - g.begin;     // write (row2, val2)
+  }
   size_t tb = scan_tmp_bytes;
   launch(EL_K_SCAN, [&] {
-    HIPCHK(hipcub::DeviceScan::ExclusiveSum(scan_tmp, tb, c.dcnt, c.dscan, n1, stream));
+    HIPCHK(hipcub::DeviceScan::ExclusiveSum(scan_tmp, tb, dcnt_all, dscan_all, (uint32_t)dcnt_total, stream));
   });
-  host_ev[EL_K_SCAN][EL_EV_ENT] += 2ull * n1;  // read dcnt, write dscan
+  host_ev[EL_K_SCAN][EL_EV_ENT] += 2ull * dcnt_total;  // read dcnt, write dscan
   launch(EL_K_MERGE_PTR, [&] {
-    hipLaunchKernelGGL(k_merge_ptr, dim3(grid_for(n1)), dim3(BLOCK), 0, stream, c.ptr2, c.ptr,
-                       c.dscan, n1);
+    hipLaunchKernelGGL(k_merge_ptr, dim3(grid_for(m.max_rows, 512), m.nseg), dim3(BLOCK), 0, stream, m, dscan_all);
   });
-  host_ev[EL_K_MERGE_PTR][EL_EV_ENT] += 3ull * n1;  // read ptr, dscan; write ptr2
-  if (old_n) {
+  if (m.max_old)
     launch(EL_K_SCATTER_OLD, [&] {
-      hipLaunchKernelGGL(k_scatter_old, dim3(grid_for(old_n)), dim3(BLOCK), 0, stream, c.row,
-                         c.val, c.row2, c.val2, c.dscan, (uint32_t)old_n);
+      hipLaunchKernelGGL(k_scatter_old, dim3(grid_for(m.max_old, 512), m.nseg), dim3(BLOCK), 0, stream, m,
+                         dscan_all);
     });
-    host_ev[EL_K_SCATTER_OLD][EL_EV_TRIG] += old_n;  // read (row, val)
-    host_ev[EL_K_SCATTER_OLD][EL_EV_ENT] += old_n;   // read dscan[row]
-    host_ev[EL_K_SCATTER_OLD][EL_EV_EMIT] += old_n;  // write (row2, val2)
-  }
-  if (nn) {
+  if (m.max_new)
     launch(EL_K_SCATTER_NEW, [&] {
-      hipLaunchKernelGGL(k_scatter_new, dim3(grid_for(nn)), dim3(BLOCK), 0, stream, lx, lv,
-                         (uint32_t)begin, (uint32_t)end, c.ptr2, c.dcnt, c.row2, c.val2);
+      hipLaunchKernelGGL(k_scatter_new, dim3(grid_for(m.max_new, 512), m.nseg), dim3(BLOCK), 0, stream, m,
+                         dcnt_all);
     });
-    host_ev[EL_K_SCATTER_NEW][EL_EV_TRIG] += nn;  // read log pair
-    host_ev[EL_K_SCATTER_NEW][EL_EV_ENT] += nn;   // read ptr2[x+1]
-    host_ev[EL_K_SCATTER_NEW][EL_EV_RMW] += nn;   // atomicSub dcnt
-    host_ev[EL_K_SCATTER_NEW][EL_EV_EMIT] += nn;  // write (row2, val2)
+  for (const MergeReq& r : reqs) {
+    std::swap(r.c->ptr, r.c->ptr2);
+    std::swap(r.c->row, r.c->row2);
+    std::swap(r.c->val, r.c->val2);
   }
-  std::swap(c.ptr, c.ptr2);
-  std::swap(c.row, c.row2);
-  std::swap(c.val, c.val2);
+  if (!account) memcpy(host_ev, saved_ev, sizeof host_ev);
+}
+
+// Bring the S-row CSR up to date with the fact log (export path, not counted as saturation).
+void el_ctx::ensure_s_csr() {
+  if (s_csr_count == s_count) return;
+  hipLaunchKernelGGL(k_count_rows, dim3(grid_for(s_count - s_csr_count)), dim3(BLOCK), 0, stream, S.dcnt,
+                     slog_x, (uint32_t)s_csr_count, (uint32_t)s_count);
+  HIPCHK(hipGetLastError());
+  merge_all({{&S, slog_x, slog_a, s_csr_count, s_csr_count, s_count}}, false);
+  s_csr_count = s_count;
+  sync();
 }
 
 // One Jacobi superstep over the given trigger ranges.  Returns true if anything new.
@@ -1369,7 +1532,7 @@ bool el_ctx::superstep(uint32_t mask, uint64_t sb, uint64_t se, uint64_t lb, uin
   const bool do_p = (mask & M_R4P) && pe > pb;
   if (!(se > sb || le > lb || do_a || do_p)) return false;
   // ---- generation (read-only on the state; re-run after growing a buffer)
-  HIPCHK(hipMemcpyAsync(ev_backup, ctr->ev, sizeof(hc.ev), hipMemcpyDeviceToDevice, stream));
+  HIPCHK(hipMemcpyAsync(ev_backup, ev, EV_WORDS * sizeof(unsigned long long), hipMemcpyDeviceToDevice, stream));
   uint64_t saved_launch[EL_NUM_KERNELS];
   memcpy(saved_launch, launches, sizeof launches);
   for (;;) {
@@ -1396,7 +1559,7 @@ bool el_ctx::superstep(uint32_t mask, uint64_t sb, uint64_t se, uint64_t lb, uin
                            (uint32_t)pb, (uint32_t)pe);
       });
     launch(EL_K_JOBS, [&] {
-      hipLaunchKernelGGL(k_jobs, dim3(2048), dim3(BLOCK), 0, stream, ix, st);
+      hipLaunchKernelGGL(k_jobs, dim3(1024), dim3(BLOCK), 0, stream, ix, st);
     });
     sync();
     read_counters();
@@ -1422,7 +1585,7 @@ bool el_ctx::superstep(uint32_t mask, uint64_t sb, uint64_t se, uint64_t lb, uin
     regrow2(hc.cand_p, cp_cap, cp_p, cp_b);
     if (!redo) break;
     // restore counters: the retried generation must count exactly once
-    HIPCHK(hipMemcpyAsync(ctr->ev, ev_backup, sizeof(hc.ev), hipMemcpyDeviceToDevice, stream));
+    HIPCHK(hipMemcpyAsync(ev, ev_backup, EV_WORDS * sizeof(unsigned long long), hipMemcpyDeviceToDevice, stream));
     memcpy(launches, saved_launch, sizeof launches);
   }
   const uint64_t cand_s = hc.cand_s, cand_l = hc.cand_l, cand_a = hc.cand_a, cand_p = hc.cand_p;
@@ -1474,12 +1637,14 @@ bool el_ctx::superstep(uint32_t mask, uint64_t sb, uint64_t se, uint64_t lb, uin
   read_counters();
   const uint64_t s_new = hc.s_log, l_new = hc.l_log, a_new = hc.a_log, p_new = hc.p_log;
   // ---- merge deltas into the CSRs
-  if (s_new > s_count) merge(S, slog_x, slog_a, s_count, s_count, s_new);
+  // (the S-row CSR is not read during saturation: built lazily for export)
+  std::vector<MergeReq> reqs;
   if (l_new > l_count) {
-    if (hx.P) merge(PR, llog_p, llog_x, l_count, l_count, l_new);
-    merge(SC, llog_x, llog_p, l_count, l_count, l_new);
+    if (hx.P && need_pred) reqs.push_back({&PR, llog_p, llog_x, l_count, l_count, l_new});
+    if (need_succ) reqs.push_back({&SC, llog_x, llog_p, l_count, l_count, l_new});
   }
-  if (p_new > p_count) merge(PP, plog_p, plog_b, p_count, p_count, p_new);
+  if (p_new > p_count) reqs.push_back({&PP, plog_p, plog_b, p_count, p_count, p_new});
+  merge_all(reqs);
   const bool changed = s_new > s_count || l_new > l_count || a_new > a_count || p_new > p_count;
   s_count = s_new;
   l_count = l_new;
@@ -1489,6 +1654,7 @@ bool el_ctx::superstep(uint32_t mask, uint64_t sb, uint64_t se, uint64_t lb, uin
 }
 
 void el_ctx::fill_stats(el_stats* out, double ms) {
+  read_events();
   el_stats st{};
   st.supersteps = (uint32_t)tr_s.size();
   st.s_facts = s_count;
@@ -1500,7 +1666,7 @@ void el_ctx::fill_stats(el_stats* out, double ms) {
   uint64_t bytes = 0;
   static const uint64_t width[EL_NUM_EVENTS] = {8, 8, 4, 4, 8, 8, 16, 8};
   for (int k = 0; k < EL_NUM_KERNELS; ++k)
-    for (int e = 0; e < EL_NUM_EVENTS; ++e) bytes += (hc.ev[k][e] + host_ev[k][e]) * width[e];
+    for (int e = 0; e < EL_NUM_EVENTS; ++e) bytes += (hev[k][e] + host_ev[k][e]) * width[e];
   st.bytes = bytes;
   st.ms = ms;
   last = st;
@@ -1637,7 +1803,30 @@ int el_load(el_ctx* c, const el_axioms* ax) {
     d.rng_ptr = up32(h.rng.ptr);
     d.rng_c = up32(h.rng.a);
     d.role_has_exl = up8(h.role_has_exl);
+    {
+      std::vector<uint32_t> meta(4 * (size_t)(h.N + 1));
+      for (uint32_t a = 0; a <= h.N; ++a) {
+        meta[4 * a + 0] = h.told.ptr[a];
+        meta[4 * a + 1] = h.cidx.ptr[a];
+        meta[4 * a + 2] = h.exr.ptr[a];
+        meta[4 * a + 3] = h.exl.ptr[a];
+      }
+      d.meta = (const uint4*)up32(meta);
+    }
     d.has_range = h.rng.a.empty() ? 0u : 1u;
+    {
+      // ⊥ derivable only if some axiom mentions it (as a conclusion or a CR3 filler)
+      bool bot = false;
+      auto has0 = [](const uint32_t* v, uint32_t n) {
+        for (uint32_t i = 0; i < n; ++i)
+          if (v[i] == EL_BOTTOM) return true;
+        return false;
+      };
+      bot = has0(ax->sub_b, ax->n_sub) || has0(ax->conj_b, ax->n_conj) || has0(ax->exr_b, ax->n_ex_rhs) ||
+            has0(ax->exl_b, ax->n_ex_lhs) || has0(ax->dom_c, ax->n_domain) || has0(ax->rng_c, ax->n_range);
+      c->need_succ = !h.chf.a.empty();
+      c->need_pred = !h.exl.a.empty() || c->need_succ || bot;
+    }
     c->alloc_state();
     c->loaded = true;
     c->inited = false;
@@ -1658,8 +1847,7 @@ int el_init(el_ctx* c) {
     c->read_counters();
     c->s_count = c->hc.s_log;
     c->s_init = c->s_count;
-    c->merge(c->S, c->slog_x, c->slog_a, 0, 0, c->s_count);
-    c->sync();
+    c->s_csr_count = 0;
     c->inited = true;
     c->fill_stats(nullptr, 0.0);
     return EL_OK;
@@ -1739,12 +1927,13 @@ int el_kernel_stats(el_ctx* c, el_kernel_stat* out, int n) {
   return guarded(c, [&] {
     c->sync();
     c->read_counters();
+    c->read_events();
     static const uint64_t width[EL_NUM_EVENTS] = {8, 8, 4, 4, 8, 8, 16, 8};
     for (int k = 0; k < EL_NUM_KERNELS; ++k) {
       el_kernel_stat s{};
       s.launches = c->launches[k];
       for (int e = 0; e < EL_NUM_EVENTS; ++e) {
-        s.events[e] = c->hc.ev[k][e] + c->host_ev[k][e];
+        s.events[e] = c->hev[k][e] + c->host_ev[k][e];
         s.bytes += s.events[e] * width[e];
       }
       s.ms = c->kms[k];
@@ -1772,6 +1961,7 @@ int el_get_subsumers(el_ctx* c, uint32_t x, uint32_t* out, size_t cap, size_t* n
   if (x >= c->hx.N) return fail(c, EL_EINVAL, "concept id out of range");
   return guarded(c, [&] {
     c->sync();
+    c->ensure_s_csr();
     uint32_t p[2];
     HIPCHK(hipMemcpy(p, c->S.ptr + x, 2 * sizeof(uint32_t), hipMemcpyDeviceToHost));
     *n = p[1] - p[0];
@@ -1784,6 +1974,28 @@ int el_get_subsumers(el_ctx* c, uint32_t x, uint32_t* out, size_t cap, size_t* n
   });
 }
 
+// Copy the S CSR to the host with every row sorted (device segmented radix sort).
+static void copy_sorted_rows(el_ctx* c, std::vector<uint32_t>& ptr, uint32_t* vals) {
+  c->ensure_s_csr();
+  const uint32_t N = c->hx.N;
+  const uint64_t n = c->s_count;
+  ptr.resize(N + 1);
+  HIPCHK(hipMemcpy(ptr.data(), c->S.ptr, ptr.size() * 4, hipMemcpyDeviceToHost));
+  if (!n) return;
+  uint32_t* sorted = dalloc<uint32_t>(n);
+  size_t tb = 0;
+  HIPCHK(hipcub::DeviceSegmentedRadixSort::SortKeys(nullptr, tb, c->S.val, sorted, (int)n, (int)N,
+                                                    c->S.ptr, c->S.ptr + 1, 0, 32, c->stream));
+  void* tmp = nullptr;
+  HIPCHK(hipMalloc(&tmp, tb ? tb : 1));
+  HIPCHK(hipcub::DeviceSegmentedRadixSort::SortKeys(tmp, tb, c->S.val, sorted, (int)n, (int)N, c->S.ptr,
+                                                    c->S.ptr + 1, 0, 32, c->stream));
+  HIPCHK(hipStreamSynchronize(c->stream));
+  HIPCHK(hipMemcpy(vals, sorted, n * 4, hipMemcpyDeviceToHost));
+  (void)hipFree(tmp);
+  dfree(sorted);
+}
+
 int el_copy_facts(el_ctx* c, uint32_t* x, uint32_t* a, size_t cap, size_t* n) {
   if (!c || !n) return EL_EINVAL;
   if (!c->inited) return fail(c, EL_ESTATE, "no state");
@@ -1792,17 +2004,16 @@ int el_copy_facts(el_ctx* c, uint32_t* x, uint32_t* a, size_t cap, size_t* n) {
     *n = c->s_count;
     if (cap < *n) return EL_ERANGE;
     if (!*n) return EL_OK;
-    std::vector<uint32_t> ptr(c->hx.N + 1);
-    HIPCHK(hipMemcpy(ptr.data(), c->S.ptr, ptr.size() * 4, hipMemcpyDeviceToHost));
-    HIPCHK(hipMemcpy(a, c->S.val, *n * 4, hipMemcpyDeviceToHost));
-    for (uint32_t r = 0; r < c->hx.N; ++r) {
+    std::vector<uint32_t> ptr;
+    copy_sorted_rows(c, ptr, a);
+    for (uint32_t r = 0; r < c->hx.N; ++r)
       for (uint32_t j = ptr[r]; j < ptr[r + 1]; ++j) x[j] = r;
-      std::sort(a + ptr[r], a + ptr[r + 1]);
-    }
     return EL_OK;
   });
 }
 
+// Links sorted by (x, r, y): device radix sort of 64-bit (x, pid) keys, then each x's
+// short run is reordered from pid order ((y, r)) to (r, y) on the host.
 int el_copy_links(el_ctx* c, uint32_t* x, uint32_t* r, uint32_t* y, size_t cap, size_t* n) {
   if (!c || !n) return EL_EINVAL;
   if (!c->inited) return fail(c, EL_ESTATE, "no state");
@@ -1811,17 +2022,42 @@ int el_copy_links(el_ctx* c, uint32_t* x, uint32_t* r, uint32_t* y, size_t cap, 
     *n = c->l_count;
     if (cap < *n) return EL_ERANGE;
     if (!*n) return EL_OK;
-    std::vector<uint32_t> px(*n), pp(*n);
-    HIPCHK(hipMemcpy(px.data(), c->llog_x, *n * 4, hipMemcpyDeviceToHost));
-    HIPCHK(hipMemcpy(pp.data(), c->llog_p, *n * 4, hipMemcpyDeviceToHost));
-    std::vector<uint64_t> ord(*n);
-    for (size_t i = 0; i < *n; ++i) ord[i] = ((uint64_t)px[i] << 32) | pp[i];
-    std::sort(ord.begin(), ord.end());
-    for (size_t i = 0; i < *n; ++i) {
-      uint32_t xx = (uint32_t)(ord[i] >> 32), p = (uint32_t)ord[i];
-      x[i] = xx;
-      r[i] = c->hx.pair_role[p];
-      y[i] = c->hx.pair_y[p];
+    const uint64_t m = *n;
+    unsigned long long* keys = dalloc<unsigned long long>(m);
+    unsigned long long* out = dalloc<unsigned long long>(m);
+    // pack on the device: key = x << 32 | pid
+    hipLaunchKernelGGL(k_pack_keys, dim3(grid_for(m)), dim3(BLOCK), 0, c->stream, keys, c->llog_x, c->llog_p,
+                       (uint32_t)m);
+    HIPCHK(hipGetLastError());
+    size_t tb = 0;
+    HIPCHK(hipcub::DeviceRadixSort::SortKeys(nullptr, tb, keys, out, (int)m, 0, 64, c->stream));
+    void* tmp = nullptr;
+    HIPCHK(hipMalloc(&tmp, tb ? tb : 1));
+    HIPCHK(hipcub::DeviceRadixSort::SortKeys(tmp, tb, keys, out, (int)m, 0, 64, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    std::vector<unsigned long long> hs(m);
+    HIPCHK(hipMemcpy(hs.data(), out, m * 8, hipMemcpyDeviceToHost));
+    (void)hipFree(tmp);
+    dfree(keys);
+    dfree(out);
+    uint64_t s0 = 0;
+    while (s0 < m) {
+      uint64_t e = s0;
+      const uint32_t xx = (uint32_t)(hs[s0] >> 32);
+      while (e < m && (uint32_t)(hs[e] >> 32) == xx) ++e;
+      // pids are ordered by (y, r); order this x's run by (r, y)
+      std::sort(hs.begin() + s0, hs.begin() + e, [&](unsigned long long u, unsigned long long v) {
+        const uint32_t pu = (uint32_t)u, pv = (uint32_t)v;
+        const uint32_t ru = c->hx.pair_role[pu], rv = c->hx.pair_role[pv];
+        return ru != rv ? ru < rv : c->hx.pair_y[pu] < c->hx.pair_y[pv];
+      });
+      for (uint64_t k = s0; k < e; ++k) {
+        const uint32_t p = (uint32_t)hs[k];
+        x[k] = xx;
+        r[k] = c->hx.pair_role[p];
+        y[k] = c->hx.pair_y[p];
+      }
+      s0 = e;
     }
     return EL_OK;
   });
@@ -1833,10 +2069,8 @@ int el_export_result(el_ctx* c, int layout, el_sink sink, void* user) {
   return guarded(c, [&] {
     c->sync();
     const uint32_t N = c->hx.N;
-    std::vector<uint32_t> ptr(N + 1), val(c->s_count);
-    HIPCHK(hipMemcpy(ptr.data(), c->S.ptr, ptr.size() * 4, hipMemcpyDeviceToHost));
-    if (!val.empty())
-      HIPCHK(hipMemcpy(val.data(), c->S.val, val.size() * 4, hipMemcpyDeviceToHost));
+    std::vector<uint32_t> ptr, val(c->s_count);
+    copy_sorted_rows(c, ptr, val.data());
     // result node rows: classes and individuals only (⊥ and datatypes have no key)
     auto exported = [&](uint32_t x) {
       return x != EL_BOTTOM && c->hx.kind[x] != EL_KIND_DATATYPE;
@@ -1853,7 +2087,6 @@ int el_export_result(el_ctx* c, int layout, el_sink sink, void* user) {
     if (layout == EL_LAYOUT_X_TO_B) {
       for (uint32_t x = 0; x < N; ++x) {
         if (!exported(x)) continue;
-        std::sort(val.begin() + ptr[x], val.begin() + ptr[x + 1]);
         for (uint32_t j = ptr[x]; j < ptr[x + 1]; ++j) {
           ks.push_back(x);
           vs.push_back(val[j]);

@@ -289,8 +289,7 @@ class Engine:
         x, r, y = (np.zeros(n.value, dtype=np.uint32) for _ in range(3))
         self._check(self._lib.el_copy_links(self._ctx, _ptr(x), _ptr(r), _ptr(y), x.size, C.byref(n)),
                     "el_copy_links")
-        order = np.lexsort((y, r, x))
-        return x[order], r[order], y[order]
+        return x, r, y
 
     def export_result(self, layout: int = LAYOUT_X_TO_B) -> Tuple[np.ndarray, np.ndarray]:
         """Stream the result node through the C sink; returns (keys, values)."""

@@ -209,6 +209,7 @@ struct elo_ctx {
   vec plog_p, plog_b;
   vec* prow; /* propagations per pid */
   uint64_t s_init;
+  int need_pred, need_succ; /* the GPU maintains these CSRs only when they have readers */
   uint64_t wm_s[EL_NUM_RULE_TYPES], wm_l[EL_NUM_RULE_TYPES], wm_a[EL_NUM_RULE_TYPES], wm_p[EL_NUM_RULE_TYPES];
   uint64_t ev[EL_NUM_KERNELS][EL_NUM_EVENTS];
   vec tr_s, tr_l, tr_a; /* low 32 bits suffice for tests */
@@ -502,6 +503,18 @@ int elo_create(elo_ctx** out, const el_axioms* ax, int mode) {
     return EL_EINVAL;
   }
   copy_axioms(c, ax);
+  {
+    uint32_t i;
+    int bot = 0;
+    for (i = 0; i < ax->n_sub; ++i) bot |= ax->sub_b[i] == EL_BOTTOM;
+    for (i = 0; i < ax->n_conj; ++i) bot |= ax->conj_b[i] == EL_BOTTOM;
+    for (i = 0; i < ax->n_ex_rhs; ++i) bot |= ax->exr_b[i] == EL_BOTTOM;
+    for (i = 0; i < ax->n_ex_lhs; ++i) bot |= ax->exl_b[i] == EL_BOTTOM;
+    for (i = 0; i < ax->n_domain; ++i) bot |= ax->dom_c[i] == EL_BOTTOM;
+    for (i = 0; i < ax->n_range; ++i) bot |= ax->rng_c[i] == EL_BOTTOM;
+    c->need_succ = ax->n_chain > 0;
+    c->need_pred = ax->n_ex_lhs > 0 || ax->n_chain > 0 || bot;
+  }
   c->bits = (uint32_t*)calloc((size_t)c->N * c->W + 1, sizeof(uint32_t));
   if (!c->bits) {
     *out = c;
@@ -533,13 +546,13 @@ int elo_create(elo_ctx** out, const el_axioms* ax, int mode) {
 
 typedef struct {
   vec sx, sa, lx, lp, ay, ac, pp, pb;
-  vec jt, jb, jl, ja, jbb; /* job records */
+  vec jt, jb, jo, jl, ja, jbb; /* job records: type, list owner, offset, length, a, b */
 } cands;
 
 static void cands_free(cands* k) {
   free(k->sx.v), free(k->sa.v), free(k->lx.v), free(k->lp.v), free(k->ay.v), free(k->ac.v);
   free(k->pp.v), free(k->pb.v);
-  free(k->jt.v), free(k->jb.v), free(k->jl.v), free(k->ja.v), free(k->jbb.v);
+  free(k->jt.v), free(k->jb.v), free(k->jo.v), free(k->jl.v), free(k->ja.v), free(k->jbb.v);
 }
 
 static void emit_s(elo_ctx* c, cands* k, int kern, uint32_t x, uint32_t a) {
@@ -552,14 +565,20 @@ static void emit_l(elo_ctx* c, cands* k, int kern, uint32_t x, uint32_t p) {
   vpush(&k->lx, x);
   vpush(&k->lp, p);
 }
+/* a fan-out list of len items becomes ceil(len / JOB_CHUNK) job records (as on the GPU) */
+#define JOB_CHUNK 256u
 static void emit_job(elo_ctx* c, cands* k, int kern, uint32_t type, uint32_t b, uint32_t len, uint32_t a,
                      uint32_t bb) {
-  EV(kern, EL_EV_JOB);
-  vpush(&k->jt, type);
-  vpush(&k->jb, b);
-  vpush(&k->jl, len);
-  vpush(&k->ja, a);
-  vpush(&k->jbb, bb);
+  uint32_t off;
+  for (off = 0; off < len; off += JOB_CHUNK) {
+    EV(kern, EL_EV_JOB);
+    vpush(&k->jt, type);
+    vpush(&k->jb, b);
+    vpush(&k->jo, off);
+    vpush(&k->jl, len - off < JOB_CHUNK ? len - off : JOB_CHUNK);
+    vpush(&k->ja, a);
+    vpush(&k->jbb, bb);
+  }
 }
 
 enum { JOB_PRED_S = 0, JOB_PRED_L = 1, JOB_R6A = 3 };
@@ -772,18 +791,19 @@ static void run_jobs(elo_ctx* c, cands* k) {
   size_t j;
   uint32_t q, e;
   for (j = 0; j < k->jt.n; ++j) {
-    uint32_t type = k->jt.v[j], owner = k->jb.v[j], len = k->jl.v[j], a = k->ja.v[j], b = k->jbb.v[j];
+    uint32_t type = k->jt.v[j], owner = k->jb.v[j], o0 = k->jo.v[j], len = k->jl.v[j], a = k->ja.v[j],
+             b = k->jbb.v[j];
     EV(K, EL_EV_JOB);
     if (type == JOB_PRED_S) {
       for (q = 0; q < len; ++q) {
-        uint32_t xp = c->pred[owner].v[q];
+        uint32_t xp = c->pred[owner].v[o0 + q];
         EV(K, EL_EV_ENT);
         EV(K, EL_EV_TEST);
         if (!bit(c, xp, b)) emit_s(c, k, K, xp, b);
       }
     } else if (type == JOB_PRED_L) {
       for (q = 0; q < len; ++q) {
-        uint32_t xp = c->pred[owner].v[q];
+        uint32_t xp = c->pred[owner].v[o0 + q];
         EV(K, EL_EV_ENT);
         EV(K, EL_EV_HASH);
         if (!hs_has(&c->links, lkey(a, xp))) emit_l(c, k, K, xp, a);
@@ -791,7 +811,7 @@ static void run_jobs(elo_ctx* c, cands* k) {
     } else { /* JOB_R6A */
       uint32_t X = a, r = b;
       for (q = 0; q < len; ++q) {
-        uint32_t qq = c->succ[owner].v[q], s2 = c->pair_role[qq], Z = c->pair_y[qq];
+        uint32_t qq = c->succ[owner].v[o0 + q], s2 = c->pair_role[qq], Z = c->pair_y[qq];
         EV(K, EL_EV_ENT);
         EVN(K, EL_EV_ENT, 2);
         EV(K, EL_EV_ROW);
@@ -836,22 +856,24 @@ static void expand_p(elo_ctx* c, cands* k, uint64_t pb, uint64_t pe) {
   }
 }
 
-/* analytic events of one CSR merge (same formula as the GPU host side) */
-static void merge_events(elo_ctx* c, uint64_t nrows, uint64_t old_n, uint64_t nn) {
+/* analytic events of the CSR merges of one superstep (same formula as the GPU host side):
+ * one scan over the delta counts of all four CSRs (S, PR, SC, PP), then per merged CSR the
+ * row offsets, the moved entries and the placed delta entries */
+static void merge_seg_events(elo_ctx* c, uint64_t nrows, uint64_t old_n, uint64_t nn) {
   uint64_t n1 = nrows + 1;
-  EVN(EL_K_SCAN, EL_EV_ENT, 2 * n1);
   EVN(EL_K_MERGE_PTR, EL_EV_ENT, 3 * n1);
-  if (old_n) {
-    EVN(EL_K_SCATTER_OLD, EL_EV_TRIG, old_n);
-    EVN(EL_K_SCATTER_OLD, EL_EV_ENT, old_n);
-    EVN(EL_K_SCATTER_OLD, EL_EV_EMIT, old_n);
-  }
-  if (nn) {
-    EVN(EL_K_SCATTER_NEW, EL_EV_TRIG, nn);
-    EVN(EL_K_SCATTER_NEW, EL_EV_ENT, nn);
-    EVN(EL_K_SCATTER_NEW, EL_EV_RMW, nn);
-    EVN(EL_K_SCATTER_NEW, EL_EV_EMIT, nn);
-  }
+  EVN(EL_K_SCATTER_OLD, EL_EV_TRIG, old_n);
+  EVN(EL_K_SCATTER_OLD, EL_EV_ENT, old_n);
+  EVN(EL_K_SCATTER_OLD, EL_EV_EMIT, old_n);
+  EVN(EL_K_SCATTER_NEW, EL_EV_TRIG, nn);
+  EVN(EL_K_SCATTER_NEW, EL_EV_ENT, nn);
+  EVN(EL_K_SCATTER_NEW, EL_EV_RMW, nn);
+  EVN(EL_K_SCATTER_NEW, EL_EV_EMIT, nn);
+}
+
+static void merge_scan_events(elo_ctx* c) {
+  uint64_t tot = 2 * ((uint64_t)c->N + 1) + 2 * ((uint64_t)c->P + 1);
+  EVN(EL_K_SCAN, EL_EV_ENT, 2 * tot);
 }
 
 static int superstep(elo_ctx* c, uint32_t mask, uint64_t sb, uint64_t se, uint64_t lb, uint64_t le,
@@ -919,12 +941,15 @@ static int superstep(elo_ctx* c, uint32_t mask, uint64_t sb, uint64_t se, uint64
     }
   }
   cands_free(&k);
-  if (c->slog_x.n > s0) merge_events(c, c->N, s0, c->slog_x.n - s0);
-  if (c->llog_x.n > l0) {
-    if (c->P) merge_events(c, c->P, l0, c->llog_x.n - l0);
-    merge_events(c, c->N, l0, c->llog_x.n - l0);
+  /* the S-row CSR is not read during saturation (built lazily for export) */
+  {
+    int m_pr = c->llog_x.n > l0 && c->P && c->need_pred, m_sc = c->llog_x.n > l0 && c->need_succ;
+    int m_pp = c->plog_p.n > p0;
+    if (m_pr || m_sc || m_pp) merge_scan_events(c);
+    if (m_pr) merge_seg_events(c, c->P, l0, c->llog_x.n - l0);
+    if (m_sc) merge_seg_events(c, c->N, l0, c->llog_x.n - l0);
   }
-  if (c->plog_p.n > p0) merge_events(c, c->P, p0, c->plog_p.n - p0);
+  if (c->plog_p.n > p0) merge_seg_events(c, c->P, p0, c->plog_p.n - p0);
   return c->slog_x.n > s0 || c->llog_x.n > l0 || c->alog_y.n > a0 || c->plog_p.n > p0;
 }
 
@@ -1022,7 +1047,6 @@ int elo_init(elo_ctx* c) {
     }
   }
   c->s_init = c->slog_x.n;
-  merge_events(c, c->N, 0, c->s_init);
   return EL_OK;
 }
 
