@@ -137,6 +137,7 @@ struct DState {
   const uint32_t *sc_ptr, *sc_val;  // successors per X
   uint32_t* dcnt;  // all CSR delta counts, one array: [S rows | PR | SC | PP]
   uint32_t off_s, off_pr, off_sc, off_pp;
+  uint32_t need_pred, need_succ;  // CSRs with readers: only those get delta counts
   uint32_t *cs_x, *cs_a, cs_cap;
   uint32_t *cl_x, *cl_p, cl_cap;
   uint32_t *ca_y, *ca_c, ca_cap;
@@ -787,7 +788,8 @@ __global__ void k_expand_a(DIndex ix, DState st, uint32_t a_begin, uint32_t a_en
 
 // Dedup S candidates against the bit rows; new facts go to the log (the versioned
 // ZADD of every Lua kernel, e.g. Type1_1AxiomProcessorBase.java:36-41).
-__global__ void k_commit_s(DIndex ix, DState st, uint32_t n) {
+__global__ void k_commit_s(DIndex ix, DState st, const uint32_t* n_ptr, uint32_t cap) {
+  const uint32_t n = min(*n_ptr, cap);  // candidate count of this step, read on the device
   __shared__ uint32_t lx[QS_CAP], la[QS_CAP];
   __shared__ uint32_t ln, lbase;
   if (threadIdx.x == 0) ln = 0;
@@ -832,7 +834,8 @@ __global__ void k_commit_s(DIndex ix, DState st, uint32_t n) {
 
 // Dedup link candidates against the link set (checkAndInsertScript,
 // RolePairHandler.java:133-168); new links feed the predecessor/successor CSRs.
-__global__ void k_commit_l(DIndex ix, DState st, uint32_t n) {
+__global__ void k_commit_l(DIndex ix, DState st, const uint32_t* n_ptr, uint32_t cap) {
+  const uint32_t n = min(*n_ptr, cap);  // candidate count of this step, read on the device
   __shared__ uint32_t lx[QL_CAP], lp[QL_CAP];
   __shared__ uint32_t ln, lbase;
   if (threadIdx.x == 0) ln = 0;
@@ -850,10 +853,10 @@ __global__ void k_commit_l(DIndex ix, DState st, uint32_t n) {
       nw = hash_insert(st.lhash, st.lmask, link_key(p, x));
       if (nw) {
         ev.v[EL_EV_EMIT]++;
-        atomicAdd(st.dcnt + st.off_sc + x, 1u);
+        if (st.need_succ) atomicAdd(st.dcnt + st.off_sc + x, 1u);
       }
     }
-    wave_keyed_atomic(st.dcnt, st.off_pr + p, nw, false);  // hub pids: many new preds per step
+    if (st.need_pred) wave_keyed_atomic(st.dcnt, st.off_pr + p, nw, false);  // hub pids: many new preds
     const uint32_t off = lds_reserve(&ln, nw);
     if (nw) {
       lx[off] = x;
@@ -876,7 +879,8 @@ __global__ void k_commit_l(DIndex ix, DState st, uint32_t n) {
   ev_flush(st.ev, EL_K_COMMIT_L, ev);
 }
 
-__global__ void k_commit_a(DIndex ix, DState st, uint32_t n) {
+__global__ void k_commit_a(DIndex ix, DState st, const uint32_t* n_ptr, uint32_t cap) {
+  const uint32_t n = min(*n_ptr, cap);  // candidate count of this step, read on the device
   Ev ev;
   const uint32_t stride = gridDim.x * blockDim.x;
   for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
@@ -918,7 +922,8 @@ __global__ void k_expand_p(DIndex ix, DState st, uint32_t begin, uint32_t end) {
 }
 
 // Dedup propagation candidates (checkAndInsertScript, Type3_1AxiomProcessorBase.java:88-121)
-__global__ void k_commit_p(DIndex ix, DState st, uint32_t n) {
+__global__ void k_commit_p(DIndex ix, DState st, const uint32_t* n_ptr, uint32_t cap) {
+  const uint32_t n = min(*n_ptr, cap);  // candidate count of this step, read on the device
   Ev ev;
   const uint32_t stride = gridDim.x * blockDim.x;
   for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
@@ -947,7 +952,8 @@ struct MergeSeg {
   uint32_t off;             // segment offset in dcnt / dscan
   uint32_t n1;              // rows + 1
   uint32_t n_old;           // existing entries
-  uint32_t begin, end;      // delta range in the log
+  uint32_t begin;           // delta = log[begin, *end_ptr)
+  const uint32_t* end_ptr;  // device log counter (the host learns it only after the step)
   uint32_t keyed;           // hub rows possible: aggregate same-row counter updates per wave
 };
 struct MergeArgs {
@@ -960,6 +966,7 @@ struct MergeArgs {
 // blockIdx.x grid-strides over that segment.
 __global__ void k_merge_ptr(MergeArgs m, const uint32_t* __restrict__ dscan) {
   const MergeSeg g = m.seg[blockIdx.y];
+  if (*g.end_ptr == g.begin) return;  // nothing new: the host does not swap this CSR either
   const uint32_t stride = gridDim.x * blockDim.x, base = dscan[g.off];
   for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < g.n1; j += stride)
     g.ptr2[j] = g.ptr[j] + dscan[g.off + j] - base;
@@ -968,6 +975,7 @@ __global__ void k_merge_ptr(MergeArgs m, const uint32_t* __restrict__ dscan) {
 // existing entry j of row x moves by the number of delta entries in rows < x
 __global__ void k_scatter_old(MergeArgs m, const uint32_t* __restrict__ dscan) {
   const MergeSeg g = m.seg[blockIdx.y];
+  if (*g.end_ptr == g.begin) return;
   const uint32_t stride = gridDim.x * blockDim.x, base = dscan[g.off];
   const uint32_t* __restrict__ ds = dscan + g.off;
   for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < g.n_old; j += stride) {
@@ -981,7 +989,7 @@ __global__ void k_scatter_old(MergeArgs m, const uint32_t* __restrict__ dscan) {
 // delta entries fill the tail of their row; the counts are consumed back to zero
 __global__ void k_scatter_new(MergeArgs m, uint32_t* dcnt) {
   const MergeSeg g = m.seg[blockIdx.y];
-  const uint32_t stride = gridDim.x * blockDim.x, n = g.end - g.begin;
+  const uint32_t stride = gridDim.x * blockDim.x, n = *g.end_ptr - g.begin;
   for (uint32_t base = blockIdx.x * blockDim.x; base < n; base += stride) {
     const uint32_t i = base + threadIdx.x;
     const bool on = i < n;
@@ -1208,6 +1216,8 @@ struct el_ctx {
     s.off_pr = (uint32_t)(PR.dcnt - dcnt_all);
     s.off_sc = (uint32_t)(SC.dcnt - dcnt_all);
     s.off_pp = (uint32_t)(PP.dcnt - dcnt_all);
+    s.need_pred = need_pred ? 1u : 0u;
+    s.need_succ = need_succ ? 1u : 0u;
     s.cs_x = cs_x;
     s.cs_a = cs_a;
     s.cs_cap = (uint32_t)cs_cap;
@@ -1281,9 +1291,11 @@ struct el_ctx {
   struct MergeReq {
     DevCsr* c;
     const uint32_t *lx, *lv;
-    uint64_t old_n, begin, end;
+    uint64_t old_n, begin;
+    const uint32_t* end_ptr;  // device log counter
   };
-  void merge_all(const std::vector<MergeReq>& reqs, bool account = true);
+  void launch_merges(const std::vector<MergeReq>& reqs);
+  void finish_merges(const std::vector<MergeReq>& reqs, const std::vector<uint64_t>& ends, bool account);
   void ensure_s_csr();
   void rehash_links(uint64_t cap);
   void rehash_acts(uint64_t cap);
@@ -1452,11 +1464,11 @@ void el_ctx::rehash_props(uint64_t cap) {
 }
 
 // Rebuild every CSR with new entries: one scan over all delta counts, then one launch
-// each of k_merge_ptr / k_scatter_old / k_scatter_new over all merged segments.
-void el_ctx::merge_all(const std::vector<MergeReq>& reqs, bool account) {
+// each of k_merge_ptr / k_scatter_old / k_scatter_new over all segments.  The delta
+// sizes are read on the device (a segment without new entries skips itself), so the
+// merges are enqueued in the same superstep without a host round trip.
+void el_ctx::launch_merges(const std::vector<MergeReq>& reqs) {
   if (reqs.empty()) return;
-  uint64_t saved_ev[EL_NUM_KERNELS][EL_NUM_EVENTS];
-  if (!account) memcpy(saved_ev, host_ev, sizeof host_ev);
   MergeArgs m{};
   m.nseg = (uint32_t)reqs.size();
   for (uint32_t k = 0; k < m.nseg; ++k) {
@@ -1474,25 +1486,15 @@ void el_ctx::merge_all(const std::vector<MergeReq>& reqs, bool account) {
     g.n1 = r.c->nrows + 1;
     g.n_old = (uint32_t)r.old_n;
     g.begin = (uint32_t)r.begin;
-    g.end = (uint32_t)r.end;
+    g.end_ptr = r.end_ptr;
     g.keyed = r.c == &PR ? 1u : 0u;
     m.max_rows = std::max(m.max_rows, g.n1);
     m.max_old = std::max(m.max_old, g.n_old);
-    m.max_new = std::max(m.max_new, g.end - g.begin);
-    host_ev[EL_K_MERGE_PTR][EL_EV_ENT] += 3ull * g.n1;            // read ptr, dscan; write ptr2
-    host_ev[EL_K_SCATTER_OLD][EL_EV_TRIG] += g.n_old;             // read (row, val)
-    host_ev[EL_K_SCATTER_OLD][EL_EV_ENT] += g.n_old;              // read dscan[row]
-    host_ev[EL_K_SCATTER_OLD][EL_EV_EMIT] += g.n_old;             // write (row2, val2)
-    host_ev[EL_K_SCATTER_NEW][EL_EV_TRIG] += g.end - g.begin;     // read log pair
-    host_ev[EL_K_SCATTER_NEW][EL_EV_ENT] += g.end - g.begin;      // read ptr2[x + 1]
-    host_ev[EL_K_SCATTER_NEW][EL_EV_RMW] += g.end - g.begin;      // consume the delta count
-    host_ev[EL_K_SCATTER_NEW][EL_EV_EMIT] += g.end - g.begin;     // write (row2, val2)
   }
   size_t tb = scan_tmp_bytes;
   launch(EL_K_SCAN, [&] {
     HIPCHK(hipcub::DeviceScan::ExclusiveSum(scan_tmp, tb, dcnt_all, dscan_all, (uint32_t)dcnt_total, stream));
   });
-  host_ev[EL_K_SCAN][EL_EV_ENT] += 2ull * dcnt_total;  // read dcnt, write dscan
   launch(EL_K_MERGE_PTR, [&] {
     hipLaunchKernelGGL(k_merge_ptr, dim3(grid_for(m.max_rows, 512), m.nseg), dim3(BLOCK), 0, stream, m, dscan_all);
   });
@@ -1501,17 +1503,35 @@ void el_ctx::merge_all(const std::vector<MergeReq>& reqs, bool account) {
       hipLaunchKernelGGL(k_scatter_old, dim3(grid_for(m.max_old, 512), m.nseg), dim3(BLOCK), 0, stream, m,
                          dscan_all);
     });
-  if (m.max_new)
-    launch(EL_K_SCATTER_NEW, [&] {
-      hipLaunchKernelGGL(k_scatter_new, dim3(grid_for(m.max_new, 512), m.nseg), dim3(BLOCK), 0, stream, m,
-                         dcnt_all);
-    });
-  for (const MergeReq& r : reqs) {
+  launch(EL_K_SCATTER_NEW, [&] {
+    hipLaunchKernelGGL(k_scatter_new, dim3(512, m.nseg), dim3(BLOCK), 0, stream, m, dcnt_all);
+  });
+}
+
+// After the step's sync: account the merges that did work and swap their buffers.
+void el_ctx::finish_merges(const std::vector<MergeReq>& reqs, const std::vector<uint64_t>& ends, bool account) {
+  bool any = false;
+  for (size_t k = 0; k < reqs.size(); ++k) {
+    const MergeReq& r = reqs[k];
+    const uint64_t nn = ends[k] - r.begin;
+    if (!nn) continue;
+    any = true;
+    if (account) {
+      const uint64_t n1 = r.c->nrows + 1, old_n = r.old_n;
+      host_ev[EL_K_MERGE_PTR][EL_EV_ENT] += 3ull * n1;  // read ptr, dscan; write ptr2
+      host_ev[EL_K_SCATTER_OLD][EL_EV_TRIG] += old_n;   // read (row, val)
+      host_ev[EL_K_SCATTER_OLD][EL_EV_ENT] += old_n;    // read dscan[row]
+      host_ev[EL_K_SCATTER_OLD][EL_EV_EMIT] += old_n;   // write (row2, val2)
+      host_ev[EL_K_SCATTER_NEW][EL_EV_TRIG] += nn;      // read log pair
+      host_ev[EL_K_SCATTER_NEW][EL_EV_ENT] += nn;       // read ptr2[x + 1]
+      host_ev[EL_K_SCATTER_NEW][EL_EV_RMW] += nn;       // consume the delta count
+      host_ev[EL_K_SCATTER_NEW][EL_EV_EMIT] += nn;      // write (row2, val2)
+    }
     std::swap(r.c->ptr, r.c->ptr2);
     std::swap(r.c->row, r.c->row2);
     std::swap(r.c->val, r.c->val2);
   }
-  if (!account) memcpy(host_ev, saved_ev, sizeof host_ev);
+  if (any && account) host_ev[EL_K_SCAN][EL_EV_ENT] += 2ull * dcnt_total;  // read dcnt, write dscan
 }
 
 // Bring the S-row CSR up to date with the fact log (export path, not counted as saturation).
@@ -1520,28 +1540,56 @@ void el_ctx::ensure_s_csr() {
   hipLaunchKernelGGL(k_count_rows, dim3(grid_for(s_count - s_csr_count)), dim3(BLOCK), 0, stream, S.dcnt,
                      slog_x, (uint32_t)s_csr_count, (uint32_t)s_count);
   HIPCHK(hipGetLastError());
-  merge_all({{&S, slog_x, slog_a, s_csr_count, s_csr_count, s_count}}, false);
-  s_csr_count = s_count;
+  std::vector<MergeReq> reqs{{&S, slog_x, slog_a, s_csr_count, s_csr_count, &ctr->s_log}};
+  uint64_t saved_launch[EL_NUM_KERNELS];
+  memcpy(saved_launch, launches, sizeof launches);
+  launch_merges(reqs);
   sync();
+  memcpy(launches, saved_launch, sizeof launches);  // export work is not saturation work
+  finish_merges(reqs, {s_count}, false);
+  s_csr_count = s_count;
 }
 
-// One Jacobi superstep over the given trigger ranges.  Returns true if anything new.
+// One Jacobi superstep over the given trigger ranges; one host sync.  Returns true if
+// anything new.  Generation, commit and CSR merges are enqueued back to back: commits
+// and merges read their counts on the device.  Capacities are kept ahead of demand
+// (logs ≥ count + candidate capacity); if a candidate or job buffer still overflowed,
+// the step is completed by re-running generation over the same triggers with larger
+// buffers (already committed facts are filtered out, so the result is exact).
 bool el_ctx::superstep(uint32_t mask, uint64_t sb, uint64_t se, uint64_t lb, uint64_t le,
                        uint64_t ab, uint64_t ae, uint64_t pb, uint64_t pe) {
   const bool do_a = (mask & M_RRNG) && ae > ab;
   const bool do_p = (mask & M_R4P) && pe > pb;
   if (!(se > sb || le > lb || do_a || do_p)) return false;
-  // ---- generation (read-only on the state; re-run after growing a buffer)
-  HIPCHK(hipMemcpyAsync(ev_backup, ev, EV_WORDS * sizeof(unsigned long long), hipMemcpyDeviceToDevice, stream));
-  uint64_t saved_launch[EL_NUM_KERNELS];
-  memcpy(saved_launch, launches, sizeof launches);
-  for (;;) {
+  const uint64_t s0 = s_count, l0 = l_count, a0 = a_count, p0 = p_count;
+  for (int attempt = 0;; ++attempt) {
+    // ---- capacities: every candidate could be new
+    auto grow_log = [&](uint64_t used, uint64_t add, uint64_t& cap, uint32_t*& a, uint32_t*& b) {
+      if (used + add <= cap) return;
+      uint64_t c = next_pow2(used + add + (used + add) / 2);
+      dgrow(a, used, c);
+      dgrow(b, used, c);
+      cap = c;
+    };
+    grow_log(s_count, cs_cap, slog_cap, slog_x, slog_a);
+    if (slog_cap > S.cap) S.grow(s_csr_count, slog_cap);
+    grow_log(l_count, cl_cap, llog_cap, llog_x, llog_p);
+    if (llog_cap > PR.cap) PR.grow(l_count, llog_cap);
+    if (llog_cap > SC.cap) SC.grow(l_count, llog_cap);
+    if (2 * (l_count + cl_cap) > lhash_cap) rehash_links(next_pow2(4 * (l_count + cl_cap)));
+    grow_log(a_count, ca_cap, alog_cap, alog_y, alog_c);
+    if (2 * (a_count + ca_cap) > ahash_cap) rehash_acts(next_pow2(4 * (a_count + ca_cap)));
+    grow_log(p_count, cp_cap, plog_cap, plog_p, plog_b);
+    if (plog_cap > PP.cap) PP.grow(p_count, plog_cap);
+    if (2 * (p_count + cp_cap) > phash_cap) rehash_props(next_pow2(4 * (p_count + cp_cap)));
+
+    // ---- generation (reads only the state of step t-1)
     HIPCHK(hipMemsetAsync(&ctr->cand_s, 0, 8 * sizeof(uint32_t), stream));
     DState st = dstate();
     if (se > sb)
       launch(EL_K_EXPAND_S, [&] {
         hipLaunchKernelGGL(k_expand_s, dim3(grid_for(se - sb)), dim3(BLOCK), 0, stream, ix, st,
-                           (uint32_t)sb, (uint32_t)se, mask, (uint32_t)a_count);
+                           (uint32_t)sb, (uint32_t)se, mask, (uint32_t)a0);
       });
     if (le > lb)
       launch(EL_K_EXPAND_L, [&] {
@@ -1561,96 +1609,64 @@ bool el_ctx::superstep(uint32_t mask, uint64_t sb, uint64_t se, uint64_t lb, uin
     launch(EL_K_JOBS, [&] {
       hipLaunchKernelGGL(k_jobs, dim3(1024), dim3(BLOCK), 0, stream, ix, st);
     });
+    // ---- commit (counts read on the device)
+    launch(EL_K_COMMIT_S, [&] {
+      hipLaunchKernelGGL(k_commit_s, dim3(grid_for(cs_cap)), dim3(BLOCK), 0, stream, ix, st, &ctr->cand_s,
+                         (uint32_t)cs_cap);
+    });
+    launch(EL_K_COMMIT_L, [&] {
+      hipLaunchKernelGGL(k_commit_l, dim3(grid_for(cl_cap)), dim3(BLOCK), 0, stream, ix, st, &ctr->cand_l,
+                         (uint32_t)cl_cap);
+    });
+    if (hx.rng.a.size())
+      launch(EL_K_COMMIT_A, [&] {
+        hipLaunchKernelGGL(k_commit_a, dim3(grid_for(ca_cap, 64)), dim3(BLOCK), 0, stream, ix, st, &ctr->cand_a,
+                           (uint32_t)ca_cap);
+      });
+    if (hx.exl.a.size())
+      launch(EL_K_COMMIT_P, [&] {
+        hipLaunchKernelGGL(k_commit_p, dim3(grid_for(cp_cap, 256)), dim3(BLOCK), 0, stream, ix, st, &ctr->cand_p,
+                           (uint32_t)cp_cap);
+      });
+    // ---- merge the new links / propagations into their CSRs (S rows: lazily, for export)
+    std::vector<MergeReq> reqs;
+    if (hx.P && need_pred) reqs.push_back({&PR, llog_p, llog_x, l_count, l_count, &ctr->l_log});
+    if (need_succ) reqs.push_back({&SC, llog_x, llog_p, l_count, l_count, &ctr->l_log});
+    if (hx.exl.a.size()) reqs.push_back({&PP, plog_p, plog_b, p_count, p_count, &ctr->p_log});
+    launch_merges(reqs);
     sync();
     read_counters();
-    bool redo = false;
+    std::vector<uint64_t> ends;
+    for (const MergeReq& r : reqs) ends.push_back(r.end_ptr == &ctr->l_log ? hc.l_log : hc.p_log);
+    finish_merges(reqs, ends, true);
+    s_count = hc.s_log;
+    l_count = hc.l_log;
+    a_count = hc.a_log;
+    p_count = hc.p_log;
+    // ---- keep the buffers ahead of demand; complete the step if one overflowed
+    bool overflow = false;
     auto regrow2 = [&](uint32_t need, uint64_t& cap, uint32_t*& a, uint32_t*& b) {
-      if (need <= cap) return;
-      cap = next_pow2((uint64_t)need + need / 4);
+      if (2ull * need <= cap) return;
+      overflow |= need > cap;
+      cap = next_pow2(2ull * need + 1024);
       dfree(a);
       dfree(b);
       a = dalloc<uint32_t>(cap);
       b = dalloc<uint32_t>(cap);
-      redo = true;
     };
-    if (hc.jobs > job_cap) {
-      job_cap = next_pow2((uint64_t)hc.jobs + hc.jobs / 4);
-      dfree(jobs);
-      jobs = dalloc<uint4>(job_cap);
-      redo = true;
-    }
     regrow2(hc.cand_s, cs_cap, cs_x, cs_a);
     regrow2(hc.cand_l, cl_cap, cl_x, cl_p);
     regrow2(hc.cand_a, ca_cap, ca_y, ca_c);
     regrow2(hc.cand_p, cp_cap, cp_p, cp_b);
-    if (!redo) break;
-    // restore counters: the retried generation must count exactly once
-    HIPCHK(hipMemcpyAsync(ev, ev_backup, EV_WORDS * sizeof(unsigned long long), hipMemcpyDeviceToDevice, stream));
-    memcpy(launches, saved_launch, sizeof launches);
+    if (2ull * hc.jobs > job_cap) {
+      overflow |= hc.jobs > job_cap;
+      job_cap = next_pow2(2ull * hc.jobs + 1024);
+      dfree(jobs);
+      jobs = dalloc<uint4>(job_cap);
+    }
+    if (!overflow) break;
   }
-  const uint64_t cand_s = hc.cand_s, cand_l = hc.cand_l, cand_a = hc.cand_a, cand_p = hc.cand_p;
-  if (cand_s + cand_l + cand_a + cand_p == 0) return false;
-
-  // ---- capacities for the commit (new facts <= candidates)
-  auto grow_log = [&](uint64_t used, uint64_t add, uint64_t& cap, uint32_t*& a, uint32_t*& b) {
-    if (used + add <= cap) return;
-    uint64_t c = next_pow2(used + add + (used + add) / 2);
-    dgrow(a, used, c);
-    dgrow(b, used, c);
-    cap = c;
-  };
-  grow_log(s_count, cand_s, slog_cap, slog_x, slog_a);
-  if (s_count + cand_s > S.cap) S.grow(s_count, slog_cap);
-  grow_log(l_count, cand_l, llog_cap, llog_x, llog_p);
-  if (l_count + cand_l > PR.cap) PR.grow(l_count, llog_cap);
-  if (l_count + cand_l > SC.cap) SC.grow(l_count, llog_cap);
-  if (2 * (l_count + cand_l) > lhash_cap) rehash_links(next_pow2(4 * (l_count + cand_l)));
-  grow_log(a_count, cand_a + 64, alog_cap, alog_y, alog_c);
-  if (2 * (a_count + cand_a) > ahash_cap) rehash_acts(next_pow2(4 * (a_count + cand_a)));
-  grow_log(p_count, cand_p, plog_cap, plog_p, plog_b);
-  if (p_count + cand_p > PP.cap) PP.grow(p_count, plog_cap);
-  if (2 * (p_count + cand_p) > phash_cap) rehash_props(next_pow2(4 * (p_count + cand_p)));
-
-  // ---- commit
-  DState st = dstate();
-  if (cand_s)
-    launch(EL_K_COMMIT_S, [&] {
-      hipLaunchKernelGGL(k_commit_s, dim3(grid_for(cand_s)), dim3(BLOCK), 0, stream, ix, st,
-                         (uint32_t)cand_s);
-    });
-  if (cand_l)
-    launch(EL_K_COMMIT_L, [&] {
-      hipLaunchKernelGGL(k_commit_l, dim3(grid_for(cand_l)), dim3(BLOCK), 0, stream, ix, st,
-                         (uint32_t)cand_l);
-    });
-  if (cand_a)
-    launch(EL_K_COMMIT_A, [&] {
-      hipLaunchKernelGGL(k_commit_a, dim3(grid_for(cand_a)), dim3(BLOCK), 0, stream, ix, st,
-                         (uint32_t)cand_a);
-    });
-  if (cand_p)
-    launch(EL_K_COMMIT_P, [&] {
-      hipLaunchKernelGGL(k_commit_p, dim3(grid_for(cand_p)), dim3(BLOCK), 0, stream, ix, st,
-                         (uint32_t)cand_p);
-    });
-  sync();
-  read_counters();
-  const uint64_t s_new = hc.s_log, l_new = hc.l_log, a_new = hc.a_log, p_new = hc.p_log;
-  // ---- merge deltas into the CSRs
-  // (the S-row CSR is not read during saturation: built lazily for export)
-  std::vector<MergeReq> reqs;
-  if (l_new > l_count) {
-    if (hx.P && need_pred) reqs.push_back({&PR, llog_p, llog_x, l_count, l_count, l_new});
-    if (need_succ) reqs.push_back({&SC, llog_x, llog_p, l_count, l_count, l_new});
-  }
-  if (p_new > p_count) reqs.push_back({&PP, plog_p, plog_b, p_count, p_count, p_new});
-  merge_all(reqs);
-  const bool changed = s_new > s_count || l_new > l_count || a_new > a_count || p_new > p_count;
-  s_count = s_new;
-  l_count = l_new;
-  a_count = a_new;
-  p_count = p_new;
-  return changed;
+  return s_count > s0 || l_count > l0 || a_count > a0 || p_count > p0;
 }
 
 void el_ctx::fill_stats(el_stats* out, double ms) {
