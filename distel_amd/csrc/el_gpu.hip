@@ -1170,6 +1170,7 @@ struct el_ctx {
 
   // host mirrors
   DCounters hc{};
+  DCounters* hc_pinned = nullptr;  // async counter readback target (hipHostMalloc)
   uint64_t s_count = 0, l_count = 0, a_count = 0, p_count = 0, s_init = 0;
   uint64_t wm_s[EL_NUM_RULE_TYPES] = {}, wm_l[EL_NUM_RULE_TYPES] = {}, wm_a[EL_NUM_RULE_TYPES] = {},
            wm_p[EL_NUM_RULE_TYPES] = {};
@@ -1340,6 +1341,8 @@ void el_ctx::free_state() {
   dfree(ca_c);
   dfree(jobs);
   dfree(ctr);
+  if (hc_pinned) (void)hipHostFree(hc_pinned);
+  hc_pinned = nullptr;
   dfree(ev);
   dfree(ev_backup);
   if (scan_tmp) (void)hipFree(scan_tmp);
@@ -1395,6 +1398,7 @@ void el_ctx::alloc_state() {
   job_cap = std::max<uint64_t>(1u << 20, 2 * N);
   jobs = dalloc<uint4>(job_cap);
   ctr = dalloc<DCounters>(1);
+  HIPCHK(hipHostMalloc((void**)&hc_pinned, sizeof(DCounters), hipHostMallocDefault));
   ev = dalloc<unsigned long long>(EV_WORDS);
   ev_backup = dalloc<unsigned long long>(EV_WORDS);
   size_t b1 = 0;
@@ -1583,8 +1587,7 @@ bool el_ctx::superstep(uint32_t mask, uint64_t sb, uint64_t se, uint64_t lb, uin
     if (plog_cap > PP.cap) PP.grow(p_count, plog_cap);
     if (2 * (p_count + cp_cap) > phash_cap) rehash_props(next_pow2(4 * (p_count + cp_cap)));
 
-    // ---- generation (reads only the state of step t-1)
-    HIPCHK(hipMemsetAsync(&ctr->cand_s, 0, 8 * sizeof(uint32_t), stream));
+    // ---- generation (reads only the state of step t-1; candidate counters are zero here)
     DState st = dstate();
     if (se > sb)
       launch(EL_K_EXPAND_S, [&] {
@@ -1628,6 +1631,10 @@ bool el_ctx::superstep(uint32_t mask, uint64_t sb, uint64_t se, uint64_t lb, uin
         hipLaunchKernelGGL(k_commit_p, dim3(grid_for(cp_cap, 256)), dim3(BLOCK), 0, stream, ix, st, &ctr->cand_p,
                            (uint32_t)cp_cap);
       });
+    // counters are final once the commits ran: copy them out, then zero the candidate
+    // counters for the next step — all on the stream, so the step ends with ONE sync
+    HIPCHK(hipMemcpyAsync(hc_pinned, ctr, sizeof(DCounters), hipMemcpyDeviceToHost, stream));
+    HIPCHK(hipMemsetAsync(&ctr->cand_s, 0, 8 * sizeof(uint32_t), stream));
     // ---- merge the new links / propagations into their CSRs (S rows: lazily, for export)
     std::vector<MergeReq> reqs;
     if (hx.P && need_pred) reqs.push_back({&PR, llog_p, llog_x, l_count, l_count, &ctr->l_log});
@@ -1635,7 +1642,7 @@ bool el_ctx::superstep(uint32_t mask, uint64_t sb, uint64_t se, uint64_t lb, uin
     if (hx.exl.a.size()) reqs.push_back({&PP, plog_p, plog_b, p_count, p_count, &ctr->p_log});
     launch_merges(reqs);
     sync();
-    read_counters();
+    hc = *hc_pinned;
     std::vector<uint64_t> ends;
     for (const MergeReq& r : reqs) ends.push_back(r.end_ptr == &ctr->l_log ? hc.l_log : hc.p_log);
     finish_merges(reqs, ends, true);
