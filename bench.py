@@ -14,8 +14,9 @@ barrier and the max-over-ranks timing.
 
 Extra objects on the JSON line:
   roofline      dominant kernel (largest Σ time in a profiled classification):
-                algorithmic bytes per launch ÷ average launch time (HIP events on
-                the engine's stream), against the 8 TB/s HBM peak
+                algorithmic bytes per launch (all work phases the launch carries) ÷
+                average launch time (HIP events on the engine's stream), against the
+                8 TB/s HBM peak
   cpu_baseline  the CPU oracle (oracle/el_oracle.c, 1 thread, same Jacobi
                 algorithm) on the same workload; the Java/Redis reference cannot run
                 on this image (no JVM, no redis-server)
@@ -99,8 +100,16 @@ def main():
         pst = peng.saturate()
         ks = peng.kernel_stats()
         peng.close()
-        timed = [k for k in ks if k["launches"] and k["ms"] > 0]
-        dom = max(timed, key=lambda k: k["ms"])
+        # one row per launch: phases that share a launch (el_kernel_stat.group) add their bytes
+        launches = {}
+        for k in ks:
+            g = launches.setdefault(k["group"], {"kernel": k["group"].split(":")[0], "launches": 0, "ms": 0.0,
+                                                 "bytes": 0})
+            g["bytes"] += k["bytes"]
+            if k["kernel"] == k["group"]:
+                g["launches"], g["ms"] = k["launches"], k["ms"]
+        timed = [g for g in launches.values() if g["launches"] and g["ms"] > 0]
+        dom = max(timed, key=lambda g: g["ms"])
         per_launch_bytes = dom["bytes"] / dom["launches"]
         avg_ms = dom["ms"] / dom["launches"]
         achieved = per_launch_bytes / (avg_ms * 1e-3) / 1e9
@@ -109,8 +118,8 @@ def main():
                     "kernel": dom["kernel"], "bytes_per_launch": int(per_launch_bytes),
                     "avg_launch_us": round(avg_ms * 1e3, 3), "launches": dom["launches"],
                     "profiled_ms": round(pst["ms"], 3)}
-        kernels = {k["kernel"]: {"launches": k["launches"], "ms": round(k["ms"], 4), "bytes": k["bytes"]}
-                   for k in ks if k["launches"]}
+        kernels = {g["kernel"]: {"launches": g["launches"], "ms": round(g["ms"], 4), "bytes": g["bytes"]}
+                   for g in launches.values() if g["launches"]}
 
     cpu = None
     if rank == 0 and not args.no_cpu:

@@ -6,20 +6,22 @@
 // barrier (CommunicationHandler.java:49-84).  Here the whole state lives in HBM:
 //
 //   S(X)      dense bit rows, N × W uint32 words      (dedup: atomicOr, test: 1 word)
-//             + CSR of the facts by row X             (iteration of S(Y) for CR4)
 //             + append-only fact log                  (semi-naive Δ = log[wm, end))
+//             + CSR of the facts by row X, built lazily for export only
 //   R(r)      link set {(X, pid)} as an open-addressing hash of 64-bit keys,
 //             pid = dense (role, filler) pair id (el_index.cpp), + predecessor
 //             CSR keyed by pid and successor CSR keyed by X, + link log
+//   CR4       propagation set {((r, Y), B)} (hash) + log + CSR keyed by pid
 //
-// One Jacobi superstep t (all rules, or one rule type for el_step):
-//   generation  k_expand_s (Δ S-facts), k_expand_l (Δ links), k_expand_a (Δ range
-//               activations) and k_jobs (wide fan-outs) read ONLY the state of
+// One Jacobi superstep t (all rules, or one rule type for el_step) = 5 launches:
+//   generation  k_expand (roles: Δ S-facts, Δ links, Δ range activations, leftover
+//               propagations) and k_jobs (wide fan-outs) read ONLY the state of
 //               step t-1 and append candidate facts that are not yet present;
-//   commit      k_commit_s / k_commit_l / k_commit_a dedup the candidates against
-//               the bit rows / hash sets and append the new ones to the logs;
-//   merge       per-row delta counts → hipcub exclusive scan → k_merge_ptr,
-//               k_scatter_old, k_scatter_new rebuild the three CSRs.
+//   commit      k_commit (roles: S, links, activations, propagations) dedups the
+//               candidates against the bit rows / hash sets, appends the new ones
+//               to the logs and publishes the counters to pinned host memory;
+//   merge       per-row delta counts → k_scan_merge (single-pass scan + new row
+//               offsets), k_scatter_old, k_scatter_new rebuild the CSRs.
 // Generation never writes state, so a step can be re-run after growing a buffer,
 // and the delta of every step is exactly {candidates} \ S_{t-1}: the same sets
 // and the same algorithmic event counts as the CPU oracle (oracle/el_oracle.c).
@@ -31,6 +33,7 @@
 #include <hipcub/hipcub.hpp>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cstdio>
 #include <cstring>
@@ -114,7 +117,7 @@ constexpr size_t EV_WORDS = (size_t)EL_NUM_KERNELS * EL_NUM_EVENTS * EV_SLOTS;
 struct DCounters {
   uint32_t s_log, l_log, a_log, p_log;
   uint32_t cand_s, cand_l, cand_a, jobs;
-  uint32_t cand_p, pad1, pad2, pad3;
+  uint32_t cand_p, pad1, ticket, seq;  // ticket: k_scan_merge tiles; seq: host copy only
 };
 
 struct DState {
@@ -471,12 +474,10 @@ __global__ void k_init(DIndex ix, DState st) {
 //  CR1  Type1_1AxiomProcessorBase.java:22-43      CR2  Type1_2AxiomProcessorBase.java:45-66
 //  CR3  Type2AxiomProcessorBase.java:45-75        CR4½ Type3_1AxiomProcessorBase.java:194-239
 //  ⊥    TypeBottomAxiomProcessorBase.java:62-123  range RolePairHandler.java:471-479 + K10
-__global__ void k_expand_s(DIndex ix, DState st, uint32_t begin, uint32_t end, uint32_t mask,
-                           uint32_t a_end) {
-  __shared__ BlockQ q;
-  q_init(q);
+__device__ void expand_s(const DIndex& ix, const DState& st, BlockQ& q, uint32_t bid, uint32_t nb,
+                         uint32_t begin, uint32_t end, uint32_t mask, uint32_t a_end) {
   Ev ev;
-  for (uint32_t base = begin + blockIdx.x * blockDim.x; base < end; base += gridDim.x * blockDim.x) {
+  for (uint32_t base = begin + bid * blockDim.x; base < end; base += nb * blockDim.x) {
     const uint32_t i = base + threadIdx.x;
     if (i < end) {
       const uint32_t X = st.slog_x[i], A = st.slog_a[i];
@@ -581,15 +582,15 @@ __global__ void k_expand_s(DIndex ix, DState st, uint32_t begin, uint32_t end, u
   ev_flush(st.ev, EL_K_EXPAND_S, ev);
 }
 
+
 // Rules triggered by new links (X, pid = (r, Y)) = link log[begin, end).
 //  CR4½ Type3_2AxiomProcessorBase.java:67-96,182-224   CR5 Type4AxiomProcessorBase.java:38-76
 //  CR6  Type5AxiomProcessorBase.java:115-154           ⊥   RolePairHandler.java:358-372
 //  domain/range RolePairHandler.java:456-491
-__global__ void k_expand_l(DIndex ix, DState st, uint32_t begin, uint32_t end, uint32_t mask) {
-  __shared__ BlockQ q;
-  q_init(q);
+__device__ void expand_l(const DIndex& ix, const DState& st, BlockQ& q, uint32_t bid, uint32_t nb,
+                         uint32_t begin, uint32_t end, uint32_t mask) {
   Ev ev;
-  for (uint32_t base = begin + blockIdx.x * blockDim.x; base < end; base += gridDim.x * blockDim.x) {
+  for (uint32_t base = begin + bid * blockDim.x; base < end; base += nb * blockDim.x) {
     const uint32_t i = base + threadIdx.x;
     if (i < end) {
       const uint32_t X = st.llog_x[i], pid = st.llog_p[i];
@@ -760,13 +761,11 @@ __global__ void k_jobs(DIndex ix, DState st) {
 
 // Range activations (Y, C) = act log[a_begin, a_end): every X with Y ∈ S(X) gets C
 // (ScriptsCollection.insertClassAssertions1 :45-62 copies result[Y] into result[C]).
-__global__ void k_expand_a(DIndex ix, DState st, uint32_t a_begin, uint32_t a_end) {
-  __shared__ BlockQ q;
-  q_init(q);
+__device__ void expand_a(const DIndex& ix, const DState& st, BlockQ& q, uint32_t bid, uint32_t nb,
+                         uint32_t a_begin, uint32_t a_end) {
   Ev ev;
-  const uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x;
-  if (tid == 0) ev.v[EL_EV_TRIG] += a_end - a_begin;
-  for (uint32_t base = blockIdx.x * blockDim.x; base < ix.N; base += gridDim.x * blockDim.x) {
+  if (bid == 0 && threadIdx.x == 0) ev.v[EL_EV_TRIG] += a_end - a_begin;
+  for (uint32_t base = bid * blockDim.x; base < ix.N; base += nb * blockDim.x) {
     const uint32_t x = base + threadIdx.x;
     if (x < ix.N) {
       for (uint32_t k = a_begin; k < a_end; ++k) {
@@ -786,16 +785,24 @@ __global__ void k_expand_a(DIndex ix, DState st, uint32_t a_begin, uint32_t a_en
   ev_flush(st.ev, EL_K_EXPAND_A, ev);
 }
 
+// LDS staging of the commit roles (one role per block)
+struct CommitLds {
+  uint32_t x[QS_CAP > QL_CAP ? QS_CAP : QL_CAP], v[QS_CAP > QL_CAP ? QS_CAP : QL_CAP];
+  uint32_t n, base;
+};
+
 // Dedup S candidates against the bit rows; new facts go to the log (the versioned
 // ZADD of every Lua kernel, e.g. Type1_1AxiomProcessorBase.java:36-41).
-__global__ void k_commit_s(DIndex ix, DState st, const uint32_t* n_ptr, uint32_t cap) {
-  const uint32_t n = min(*n_ptr, cap);  // candidate count of this step, read on the device
-  __shared__ uint32_t lx[QS_CAP], la[QS_CAP];
-  __shared__ uint32_t ln, lbase;
+__device__ void commit_s(const DIndex& ix, const DState& st, CommitLds& sm, uint32_t bid, uint32_t nb,
+                         uint32_t n) {
+  uint32_t* lx = sm.x;
+  uint32_t* la = sm.v;
+  uint32_t& ln = sm.n;
+  uint32_t& lbase = sm.base;
   if (threadIdx.x == 0) ln = 0;
   __syncthreads();
   Ev ev;
-  for (uint32_t base = blockIdx.x * blockDim.x; base < n; base += gridDim.x * blockDim.x) {
+  for (uint32_t base = bid * blockDim.x; base < n; base += nb * blockDim.x) {
     const uint32_t i = base + threadIdx.x;
     bool nw = false;
     uint32_t x = 0, a = 0;
@@ -816,7 +823,7 @@ __global__ void k_commit_s(DIndex ix, DState st, const uint32_t* n_ptr, uint32_t
       la[off] = a;
     }
     __syncthreads();
-    if (ln > QS_CAP / 2 || base + gridDim.x * blockDim.x >= n) {
+    if (ln > QS_CAP / 2 || base + nb * blockDim.x >= n) {
       const uint32_t cnt = ln;
       if (threadIdx.x == 0) lbase = cnt ? atomicAdd(&st.ctr->s_log, cnt) : 0u;
       __syncthreads();
@@ -834,14 +841,16 @@ __global__ void k_commit_s(DIndex ix, DState st, const uint32_t* n_ptr, uint32_t
 
 // Dedup link candidates against the link set (checkAndInsertScript,
 // RolePairHandler.java:133-168); new links feed the predecessor/successor CSRs.
-__global__ void k_commit_l(DIndex ix, DState st, const uint32_t* n_ptr, uint32_t cap) {
-  const uint32_t n = min(*n_ptr, cap);  // candidate count of this step, read on the device
-  __shared__ uint32_t lx[QL_CAP], lp[QL_CAP];
-  __shared__ uint32_t ln, lbase;
+__device__ void commit_l(const DIndex& ix, const DState& st, CommitLds& sm, uint32_t bid, uint32_t nb,
+                         uint32_t n) {
+  uint32_t* lx = sm.x;
+  uint32_t* lp = sm.v;
+  uint32_t& ln = sm.n;
+  uint32_t& lbase = sm.base;
   if (threadIdx.x == 0) ln = 0;
   __syncthreads();
   Ev ev;
-  for (uint32_t base = blockIdx.x * blockDim.x; base < n; base += gridDim.x * blockDim.x) {
+  for (uint32_t base = bid * blockDim.x; base < n; base += nb * blockDim.x) {
     const uint32_t i = base + threadIdx.x;
     bool nw = false;
     uint32_t x = 0, p = 0;
@@ -863,7 +872,7 @@ __global__ void k_commit_l(DIndex ix, DState st, const uint32_t* n_ptr, uint32_t
       lp[off] = p;
     }
     __syncthreads();
-    if (ln > QL_CAP / 2 || base + gridDim.x * blockDim.x >= n) {
+    if (ln > QL_CAP / 2 || base + nb * blockDim.x >= n) {
       const uint32_t cnt = ln;
       if (threadIdx.x == 0) lbase = cnt ? atomicAdd(&st.ctr->l_log, cnt) : 0u;
       __syncthreads();
@@ -879,11 +888,10 @@ __global__ void k_commit_l(DIndex ix, DState st, const uint32_t* n_ptr, uint32_t
   ev_flush(st.ev, EL_K_COMMIT_L, ev);
 }
 
-__global__ void k_commit_a(DIndex ix, DState st, const uint32_t* n_ptr, uint32_t cap) {
-  const uint32_t n = min(*n_ptr, cap);  // candidate count of this step, read on the device
+__device__ void commit_a(const DIndex& ix, const DState& st, uint32_t bid, uint32_t nb, uint32_t n) {
   Ev ev;
-  const uint32_t stride = gridDim.x * blockDim.x;
-  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+  const uint32_t stride = nb * blockDim.x;
+  for (uint32_t i = bid * blockDim.x + threadIdx.x; i < n; i += stride) {
     const uint32_t y = st.ca_y[i], c = st.ca_c[i];
     ev.v[EL_EV_TRIG]++;
     ev.v[EL_EV_HASH]++;
@@ -902,11 +910,10 @@ __global__ void k_commit_a(DIndex ix, DState st, const uint32_t* n_ptr, uint32_t
 // New CR4 propagations ((r, Y), B) = prop log[begin, end) × existing predecessors of (r, Y)
 // (per-rule stepping: Type3_2AxiomProcessor part 1, ΔB × all X).  In fused saturation the
 // fan-out happens when the propagation is generated (M_R4D), so this kernel is idle there.
-__global__ void k_expand_p(DIndex ix, DState st, uint32_t begin, uint32_t end) {
-  __shared__ BlockQ q;
-  q_init(q);
+__device__ void expand_p(const DIndex& ix, const DState& st, BlockQ& q, uint32_t bid, uint32_t nb,
+                         uint32_t begin, uint32_t end) {
   Ev ev;
-  for (uint32_t base = begin + blockIdx.x * blockDim.x; base < end; base += gridDim.x * blockDim.x) {
+  for (uint32_t base = begin + bid * blockDim.x; base < end; base += nb * blockDim.x) {
     const uint32_t i = base + threadIdx.x;
     if (i < end) {
       const uint32_t pid = st.plog_p[i], B = st.plog_b[i];
@@ -922,11 +929,10 @@ __global__ void k_expand_p(DIndex ix, DState st, uint32_t begin, uint32_t end) {
 }
 
 // Dedup propagation candidates (checkAndInsertScript, Type3_1AxiomProcessorBase.java:88-121)
-__global__ void k_commit_p(DIndex ix, DState st, const uint32_t* n_ptr, uint32_t cap) {
-  const uint32_t n = min(*n_ptr, cap);  // candidate count of this step, read on the device
+__device__ void commit_p(const DIndex& ix, const DState& st, uint32_t bid, uint32_t nb, uint32_t n) {
   Ev ev;
-  const uint32_t stride = gridDim.x * blockDim.x;
-  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+  const uint32_t stride = nb * blockDim.x;
+  for (uint32_t i = bid * blockDim.x + threadIdx.x; i < n; i += stride) {
     const uint32_t pid = st.cp_p[i], b = st.cp_b[i];
     ev.v[EL_EV_TRIG]++;
     ev.v[EL_EV_HASH]++;
@@ -942,9 +948,96 @@ __global__ void k_commit_p(DIndex ix, DState st, const uint32_t* n_ptr, uint32_t
   ev_flush(st.ev, EL_K_COMMIT_P, ev);
 }
 
+// Generation of one superstep in ONE launch: blocks [0, gs) take ΔS triggers, then gl
+// blocks Δlinks, ga blocks range activations, gp blocks leftover propagations.  The roles
+// read only state t-1 and append to disjoint candidate queues, so they run side by side.
+struct ExpandArgs {
+  uint32_t gs, gl, ga, gp;
+  uint32_t sb, se, lb, le, ab, ae, pb, pe;
+  uint32_t mask, a_end;
+};
+__global__ void k_expand(DIndex ix, DState st, ExpandArgs a) {
+  __shared__ BlockQ q;
+  q_init(q);
+  uint32_t b = blockIdx.x;
+  if (b < a.gs) {
+    expand_s(ix, st, q, b, a.gs, a.sb, a.se, a.mask, a.a_end);
+    return;
+  }
+  b -= a.gs;
+  if (b < a.gl) {
+    expand_l(ix, st, q, b, a.gl, a.lb, a.le, a.mask);
+    return;
+  }
+  b -= a.gl;
+  if (b < a.ga) {
+    expand_a(ix, st, q, b, a.ga, a.ab, a.ae);
+    return;
+  }
+  expand_p(ix, st, q, b - a.ga, a.gp, a.pb, a.pe);
+}
+
+// Commit of one superstep in ONE launch (roles as in k_expand: S, links, activations,
+// propagations; each dedups into its own set).  The last block to finish publishes the
+// step's counters to pinned host memory and zeroes the candidate counters for the next
+// step, so the host learns everything with the step's single sync.
+// Blocks that finished are counted in 16 sharded words, then per shard in one word: a
+// single same-address counter hit by every block of a 2k-block launch would serialise.
+constexpr uint32_t DONE_SHARDS = 16;
+struct CommitArgs {
+  uint32_t gs, gl, ga, gp;
+  uint32_t cs_cap, cl_cap, ca_cap, cp_cap;
+  DCounters* host;  // device view of the pinned host copy
+  uint32_t* done;   // [DONE_SHARDS + 1] zero between launches
+  uint32_t seq;     // written last to host->seq: the host spins on it
+};
+__global__ void k_commit(DIndex ix, DState st, CommitArgs a) {
+  __shared__ CommitLds sm;
+  __shared__ uint32_t last;
+  uint32_t b = blockIdx.x;
+  if (b < a.gs) {
+    commit_s(ix, st, sm, b, a.gs, min(st.ctr->cand_s, a.cs_cap));
+  } else if ((b -= a.gs) < a.gl) {
+    commit_l(ix, st, sm, b, a.gl, min(st.ctr->cand_l, a.cl_cap));
+  } else if ((b -= a.gl) < a.ga) {
+    commit_a(ix, st, b, a.ga, min(st.ctr->cand_a, a.ca_cap));
+  } else {
+    commit_p(ix, st, b - a.ga, a.gp, min(st.ctr->cand_p, a.cp_cap));
+  }
+  // The barrier waits for this block's memory operations; every counter update is a
+  // returning device-scope atomic, so it has been performed before the block reports done.
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const uint32_t sh = blockIdx.x % DONE_SHARDS;
+    const uint32_t in_shard = (gridDim.x - 1 - sh) / DONE_SHARDS + 1;
+    const uint32_t shards = min(gridDim.x, DONE_SHARDS);
+    last = 0;
+    if (__hip_atomic_fetch_add(a.done + sh, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == in_shard - 1)
+      last = __hip_atomic_fetch_add(a.done + DONE_SHARDS, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+             shards - 1;
+  }
+  __syncthreads();
+  if (last) {
+    constexpr uint32_t NW = sizeof(DCounters) / 4 - 1;  // every word but seq
+    if (threadIdx.x < NW) {
+      uint32_t* dc = reinterpret_cast<uint32_t*>(st.ctr);
+      const uint32_t v = __hip_atomic_load(dc + threadIdx.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      reinterpret_cast<volatile uint32_t*>(a.host)[threadIdx.x] = v;
+      if (threadIdx.x >= 4) dc[threadIdx.x] = 0;  // cand_*, jobs for the next step
+    }
+    if (threadIdx.x <= DONE_SHARDS) a.done[threadIdx.x] = 0;
+    __threadfence_system();
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      reinterpret_cast<volatile uint32_t*>(a.host)[NW] = a.seq;  // counters are visible first
+      __threadfence_system();
+    }
+  }
+}
+
 // CSR merges of one superstep, all CSRs at once (segments: S, PR, SC, PP).  The delta
-// counts of every CSR sit in one array, scanned once; segment k's offsets are
-// dscan[off_k + x] - dscan[off_k].
+// counts of every CSR sit in one array; each segment is scanned on its own, so dscan is
+// segment-local.
 struct MergeSeg {
   const uint32_t *ptr, *row, *val;
   uint32_t *ptr2, *row2, *val2;
@@ -962,25 +1055,135 @@ struct MergeArgs {
   uint32_t max_rows, max_old, max_new;
 };
 
-// blockIdx.y selects the segment (uniform per block: its descriptor is loaded once);
-// blockIdx.x grid-strides over that segment.
-__global__ void k_merge_ptr(MergeArgs m, const uint32_t* __restrict__ dscan) {
-  const MergeSeg g = m.seg[blockIdx.y];
-  if (*g.end_ptr == g.begin) return;  // nothing new: the host does not swap this CSR either
-  const uint32_t stride = gridDim.x * blockDim.x, base = dscan[g.off];
-  for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < g.n1; j += stride)
-    g.ptr2[j] = g.ptr[j] + dscan[g.off + j] - base;
+// Single-pass scan of the delta counts fused with the new row offsets: replaces a library
+// scan (two launches) plus a pointer kernel.  Each segment (one CSR) is scanned on its own,
+// so dscan is segment-local and ptr2 = ptr + dscan.  Tiles are handed out by an atomic
+// ticket, so every predecessor tile of a block is owned by a block that is already running
+// (decoupled look-back cannot wait on an unscheduled block).  Look-back flags carry the
+// launch epoch: stale words from earlier launches never match, so they need no reset.
+constexpr uint32_t SCAN_ITEMS = 8;
+constexpr uint32_t SCAN_TILE = 256 * SCAN_ITEMS;
+constexpr uint32_t FLAG_AGG = 1, FLAG_INC = 2;
+struct ScanArgs {
+  uint32_t tile0[5];  // first global tile of segment k; tile0[nseg] = total tiles
+  uint32_t epoch;
+  unsigned long long* flags;
+  uint32_t* ticket;
+};
+
+__device__ __forceinline__ unsigned long long flag_word(uint32_t epoch, uint32_t state, uint32_t v) {
+  return ((unsigned long long)((epoch << 2) | state) << 32) | v;
+}
+
+__global__ void __launch_bounds__(256) k_scan_merge(MergeArgs m, ScanArgs sa, const uint32_t* __restrict__ dcnt,
+                                                    uint32_t* __restrict__ dscan) {
+  __shared__ uint32_t buf[SCAN_TILE];
+  __shared__ uint32_t wtot[4];
+  __shared__ uint32_t s_tile, s_excl;
+  const uint32_t tid = threadIdx.x, lane = tid & 63u, wv = tid >> 6;
+  if (tid == 0) s_tile = atomicAdd(sa.ticket, 1u);
+  __syncthreads();
+  const uint32_t t = __builtin_amdgcn_readfirstlane(s_tile), total = sa.tile0[m.nseg];
+  if (t == total - 1 && tid == 0) *sa.ticket = 0;  // every other tile is already taken
+  uint32_t k = 0;
+  while (k + 1 < m.nseg && sa.tile0[k + 1] <= t) ++k;
+  const MergeSeg& g = m.seg[k];
+  if (*g.end_ptr == g.begin) return;  // nothing new in this CSR: none of its tiles scans
+  const uint32_t lt = t - sa.tile0[k], r0 = lt * SCAN_TILE;
+  const uint32_t* __restrict__ dc = dcnt + g.off;
+#pragma unroll
+  for (uint32_t i = 0; i < SCAN_ITEMS; ++i) {
+    const uint32_t idx = r0 + i * 256 + tid;
+    buf[i * 256 + tid] = idx < g.n1 ? dc[idx] : 0u;
+  }
+  __syncthreads();
+  uint32_t v[SCAN_ITEMS], run = 0;
+#pragma unroll
+  for (uint32_t j = 0; j < SCAN_ITEMS; ++j) {
+    v[j] = run;
+    run += buf[tid * SCAN_ITEMS + j];
+  }
+  // wave-inclusive scan of the per-thread totals
+  uint32_t inc = run;
+#pragma unroll
+  for (uint32_t o = 1; o < 64; o <<= 1) {
+    const uint32_t y = __shfl_up(inc, o);
+    if (lane >= o) inc += y;
+  }
+  if (lane == 63) wtot[wv] = inc;
+  __syncthreads();
+  uint32_t wbase = 0, agg = 0;
+#pragma unroll
+  for (uint32_t w = 0; w < 4; ++w) {
+    if (w < wv) wbase += wtot[w];
+    agg += wtot[w];
+  }
+  if (wv == 0) {  // look-back over the segment's earlier tiles, 64 at a time
+    unsigned long long* fl = sa.flags;
+    const uint32_t ep = sa.epoch & 0x3fffffffu;
+    uint32_t excl = 0;
+    if (lt == 0) {
+      if (lane == 0) __hip_atomic_store(fl + t, flag_word(ep, FLAG_INC, agg), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+      if (lane == 0) __hip_atomic_store(fl + t, flag_word(ep, FLAG_AGG, agg), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const int64_t lo = sa.tile0[k];
+      int64_t j = (int64_t)t - 1;
+      while (true) {
+        const int64_t idx = j - (int64_t)lane;
+        const bool valid = idx >= lo;
+        uint32_t state = valid ? 0u : FLAG_INC, val = 0;
+        while (true) {
+          if (valid && state == 0) {
+            const unsigned long long f = __hip_atomic_load(fl + idx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const uint32_t hi = (uint32_t)(f >> 32);
+            if ((hi >> 2) == ep) {
+              state = hi & 3u;
+              val = (uint32_t)f;
+            }
+          }
+          if (__ballot(state == 0) == 0) break;
+        }
+        const unsigned long long incm = __ballot(state == FLAG_INC);
+        if (incm) {
+          const uint32_t first = (uint32_t)__ffsll((long long)incm) - 1;
+          excl += (uint32_t)wave_sum(lane <= first ? val : 0u);
+          break;
+        }
+        excl += (uint32_t)wave_sum(val);
+        j -= 64;
+      }
+      if (lane == 0)
+        __hip_atomic_store(fl + t, flag_word(ep, FLAG_INC, excl + agg), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (lane == 0) s_excl = excl;
+  }
+  __syncthreads();
+  const uint32_t tbase = s_excl + wbase + inc - run;
+#pragma unroll
+  for (uint32_t j = 0; j < SCAN_ITEMS; ++j) buf[tid * SCAN_ITEMS + j] = tbase + v[j];
+  __syncthreads();
+  uint32_t* __restrict__ ds = dscan + g.off;
+#pragma unroll
+  for (uint32_t i = 0; i < SCAN_ITEMS; ++i) {
+    const uint32_t idx = r0 + i * 256 + tid;
+    if (idx < g.n1) {
+      const uint32_t d = buf[i * 256 + tid];
+      ds[idx] = d;
+      g.ptr2[idx] = g.ptr[idx] + d;
+    }
+  }
 }
 
 // existing entry j of row x moves by the number of delta entries in rows < x
+// (blockIdx.y selects the segment; blockIdx.x grid-strides over it)
 __global__ void k_scatter_old(MergeArgs m, const uint32_t* __restrict__ dscan) {
   const MergeSeg g = m.seg[blockIdx.y];
   if (*g.end_ptr == g.begin) return;
-  const uint32_t stride = gridDim.x * blockDim.x, base = dscan[g.off];
+  const uint32_t stride = gridDim.x * blockDim.x;
   const uint32_t* __restrict__ ds = dscan + g.off;
   for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < g.n_old; j += stride) {
     const uint32_t x = g.row[j];
-    const uint32_t d = j + ds[x] - base;
+    const uint32_t d = j + ds[x];
     g.row2[d] = x;
     g.val2[d] = g.val[j];
   }
@@ -1029,6 +1232,25 @@ __global__ void k_rehash(unsigned long long* t, unsigned long long mask, const u
 }
 
 // ---------------------------------------------------------------- host side
+
+// Launch that carries a work phase: expand roles run in k_expand (timed as EXPAND_S),
+// commit roles in k_commit (COMMIT_S), the scan and the new row offsets in k_scan_merge.
+uint32_t kernel_group(int k) {
+  switch (k) {
+    case EL_K_EXPAND_L:
+    case EL_K_EXPAND_A:
+    case EL_K_EXPAND_P:
+      return EL_K_EXPAND_S;
+    case EL_K_COMMIT_L:
+    case EL_K_COMMIT_A:
+    case EL_K_COMMIT_P:
+      return EL_K_COMMIT_S;
+    case EL_K_MERGE_PTR:
+      return EL_K_SCAN;
+    default:
+      return (uint32_t)k;
+  }
+}
 
 template <class T>
 T* dalloc(size_t n) {
@@ -1163,14 +1385,17 @@ struct el_ctx {
   uint64_t job_cap = 0;
   DCounters* ctr = nullptr;
   unsigned long long* ev = nullptr;
-  unsigned long long* ev_backup = nullptr;
   unsigned long long hev[EL_NUM_KERNELS][EL_NUM_EVENTS] = {};
-  void* scan_tmp = nullptr;
-  size_t scan_tmp_bytes = 0;
+  unsigned long long* scan_flags = nullptr;  // k_scan_merge look-back words (epoch-tagged)
+  uint32_t* commit_done = nullptr;           // k_commit finished-block counters
+  uint64_t scan_tiles = 0;
+  uint32_t scan_epoch = 0;
 
   // host mirrors
   DCounters hc{};
-  DCounters* hc_pinned = nullptr;  // async counter readback target (hipHostMalloc)
+  DCounters* hc_pinned = nullptr;  // counters published by k_commit (hipHostMalloc)
+  DCounters* hc_dev = nullptr;     // device view of hc_pinned
+  uint32_t commit_seq = 0;         // k_commit launches so far (published with the counters)
   uint64_t s_count = 0, l_count = 0, a_count = 0, p_count = 0, s_init = 0;
   uint64_t wm_s[EL_NUM_RULE_TYPES] = {}, wm_l[EL_NUM_RULE_TYPES] = {}, wm_a[EL_NUM_RULE_TYPES] = {},
            wm_p[EL_NUM_RULE_TYPES] = {};
@@ -1273,6 +1498,27 @@ struct el_ctx {
     pending.clear();
   }
   void read_counters() { HIPCHK(hipMemcpy(&hc, ctr, sizeof(DCounters), hipMemcpyDeviceToHost)); }
+  // Wait until k_commit #seq has published the step's counters (the merge kernels of the
+  // step may still be running: the next step is enqueued behind them on the stream).
+  void wait_commit(uint32_t seq) {
+    volatile DCounters* p = hc_pinned;
+    for (uint64_t it = 1;; ++it) {
+      if (p->seq == seq) break;
+      if ((it & 1023) == 0) {  // a faulted or finished stream must not leave us spinning
+        const hipError_t e = hipStreamQuery(stream);
+        if (e == hipSuccess) {
+          if (p->seq == seq) break;
+          throw std::runtime_error("k_commit did not publish its counters");
+        }
+        if (e != hipErrorNotReady) HIPCHK(e);
+      }
+      __builtin_ia32_pause();
+    }
+    std::atomic_thread_fence(std::memory_order_acquire);
+    uint32_t* h = reinterpret_cast<uint32_t*>(&hc);
+    const volatile uint32_t* src = reinterpret_cast<const volatile uint32_t*>(hc_pinned);
+    for (size_t i = 0; i < sizeof(DCounters) / 4; ++i) h[i] = src[i];
+  }
   void read_events() {
     std::vector<unsigned long long> h(EV_WORDS);
     HIPCHK(hipMemcpy(h.data(), ev, EV_WORDS * sizeof(unsigned long long), hipMemcpyDeviceToHost));
@@ -1344,9 +1590,8 @@ void el_ctx::free_state() {
   if (hc_pinned) (void)hipHostFree(hc_pinned);
   hc_pinned = nullptr;
   dfree(ev);
-  dfree(ev_backup);
-  if (scan_tmp) (void)hipFree(scan_tmp);
-  scan_tmp = nullptr;
+  dfree(scan_flags);
+  dfree(commit_done);
 }
 
 void el_ctx::alloc_state() {
@@ -1398,14 +1643,18 @@ void el_ctx::alloc_state() {
   job_cap = std::max<uint64_t>(1u << 20, 2 * N);
   jobs = dalloc<uint4>(job_cap);
   ctr = dalloc<DCounters>(1);
-  HIPCHK(hipHostMalloc((void**)&hc_pinned, sizeof(DCounters), hipHostMallocDefault));
+  // coherent: k_commit's stores reach the host while later kernels of the step still run
+  HIPCHK(hipHostMalloc((void**)&hc_pinned, sizeof(DCounters), hipHostMallocCoherent | hipHostMallocMapped));
+  memset(hc_pinned, 0, sizeof(DCounters));
+  commit_seq = 0;
   ev = dalloc<unsigned long long>(EV_WORDS);
-  ev_backup = dalloc<unsigned long long>(EV_WORDS);
-  size_t b1 = 0;
-  HIPCHK(hipcub::DeviceScan::ExclusiveSum(nullptr, b1, (uint32_t*)nullptr, (uint32_t*)nullptr,
-                                          (uint32_t)dcnt_total, stream));
-  scan_tmp_bytes = b1;
-  HIPCHK(hipMalloc(&scan_tmp, b1 ? b1 : 1));
+  HIPCHK(hipHostGetDevicePointer((void**)&hc_dev, hc_pinned, 0));
+  scan_tiles = 0;
+  for (uint64_t rows : {N, P, N, P}) scan_tiles += (rows + 1 + SCAN_TILE - 1) / SCAN_TILE;
+  scan_flags = dalloc<unsigned long long>(scan_tiles);
+  commit_done = dalloc<uint32_t>(DONE_SHARDS + 1);
+  HIPCHK(hipMemset(scan_flags, 0, scan_tiles * sizeof(unsigned long long)));
+  scan_epoch = 0;
 }
 
 void el_ctx::reset_state() {
@@ -1420,6 +1669,7 @@ void el_ctx::reset_state() {
   PR.reset(stream);
   SC.reset(stream);
   HIPCHK(hipMemsetAsync(ctr, 0, sizeof(DCounters), stream));
+  HIPCHK(hipMemsetAsync(commit_done, 0, (DONE_SHARDS + 1) * sizeof(uint32_t), stream));
   HIPCHK(hipMemsetAsync(ev, 0, EV_WORDS * sizeof(unsigned long long), stream));
   s_count = l_count = a_count = p_count = s_init = s_csr_count = 0;
   for (int r = 0; r < EL_NUM_RULE_TYPES; ++r) wm_s[r] = wm_l[r] = wm_a[r] = wm_p[r] = 0;
@@ -1467,8 +1717,8 @@ void el_ctx::rehash_props(uint64_t cap) {
     });
 }
 
-// Rebuild every CSR with new entries: one scan over all delta counts, then one launch
-// each of k_merge_ptr / k_scatter_old / k_scatter_new over all segments.  The delta
+// Rebuild every CSR with new entries: one launch each of k_scan_merge / k_scatter_old /
+// k_scatter_new over all segments.  The delta
 // sizes are read on the device (a segment without new entries skips itself), so the
 // merges are enqueued in the same superstep without a host round trip.
 void el_ctx::launch_merges(const std::vector<MergeReq>& reqs) {
@@ -1495,12 +1745,24 @@ void el_ctx::launch_merges(const std::vector<MergeReq>& reqs) {
     m.max_rows = std::max(m.max_rows, g.n1);
     m.max_old = std::max(m.max_old, g.n_old);
   }
-  size_t tb = scan_tmp_bytes;
+  ScanArgs sa{};
+  uint32_t tiles = 0;
+  for (uint32_t k = 0; k < m.nseg; ++k) {
+    sa.tile0[k] = tiles;
+    tiles += (m.seg[k].n1 + SCAN_TILE - 1) / SCAN_TILE;
+  }
+  sa.tile0[m.nseg] = tiles;
+  if (tiles > scan_tiles) throw std::runtime_error("scan tile overflow");
+  if (++scan_epoch >= (1u << 30)) {  // epoch field is 30 bits: restart from clean flags
+    HIPCHK(hipMemsetAsync(scan_flags, 0, scan_tiles * sizeof(unsigned long long), stream));
+    scan_epoch = 1;
+  }
+  sa.epoch = scan_epoch;
+  sa.flags = scan_flags;
+  sa.ticket = &ctr->ticket;
   launch(EL_K_SCAN, [&] {
-    HIPCHK(hipcub::DeviceScan::ExclusiveSum(scan_tmp, tb, dcnt_all, dscan_all, (uint32_t)dcnt_total, stream));
-  });
-  launch(EL_K_MERGE_PTR, [&] {
-    hipLaunchKernelGGL(k_merge_ptr, dim3(grid_for(m.max_rows, 512), m.nseg), dim3(BLOCK), 0, stream, m, dscan_all);
+    hipLaunchKernelGGL(k_scan_merge, dim3(tiles), dim3(256), 0, stream, m, sa, (const uint32_t*)dcnt_all,
+                       dscan_all);
   });
   if (m.max_old)
     launch(EL_K_SCATTER_OLD, [&] {
@@ -1567,7 +1829,13 @@ bool el_ctx::superstep(uint32_t mask, uint64_t sb, uint64_t se, uint64_t lb, uin
   if (!(se > sb || le > lb || do_a || do_p)) return false;
   const uint64_t s0 = s_count, l0 = l_count, a0 = a_count, p0 = p_count;
   for (int attempt = 0;; ++attempt) {
-    // ---- capacities: every candidate could be new
+    // ---- capacities: every candidate could be new.  Growth copies device arrays outside
+    // the stream, so the previous step's merges must have finished first.
+    const bool grow = s_count + cs_cap > slog_cap || slog_cap > S.cap || l_count + cl_cap > llog_cap ||
+                      llog_cap > PR.cap || llog_cap > SC.cap || 2 * (l_count + cl_cap) > lhash_cap ||
+                      a_count + ca_cap > alog_cap || 2 * (a_count + ca_cap) > ahash_cap ||
+                      p_count + cp_cap > plog_cap || plog_cap > PP.cap || 2 * (p_count + cp_cap) > phash_cap;
+    if (grow) sync();
     auto grow_log = [&](uint64_t used, uint64_t add, uint64_t& cap, uint32_t*& a, uint32_t*& b) {
       if (used + add <= cap) return;
       uint64_t c = next_pow2(used + add + (used + add) / 2);
@@ -1589,60 +1857,43 @@ bool el_ctx::superstep(uint32_t mask, uint64_t sb, uint64_t se, uint64_t lb, uin
 
     // ---- generation (reads only the state of step t-1; candidate counters are zero here)
     DState st = dstate();
-    if (se > sb)
-      launch(EL_K_EXPAND_S, [&] {
-        hipLaunchKernelGGL(k_expand_s, dim3(grid_for(se - sb)), dim3(BLOCK), 0, stream, ix, st,
-                           (uint32_t)sb, (uint32_t)se, mask, (uint32_t)a0);
-      });
-    if (le > lb)
-      launch(EL_K_EXPAND_L, [&] {
-        hipLaunchKernelGGL(k_expand_l, dim3(grid_for(le - lb)), dim3(BLOCK), 0, stream, ix, st,
-                           (uint32_t)lb, (uint32_t)le, mask);
-      });
-    if (do_a)
-      launch(EL_K_EXPAND_A, [&] {
-        hipLaunchKernelGGL(k_expand_a, dim3(grid_for(hx.N)), dim3(BLOCK), 0, stream, ix, st,
-                           (uint32_t)ab, (uint32_t)ae);
-      });
-    if (do_p)
-      launch(EL_K_EXPAND_P, [&] {
-        hipLaunchKernelGGL(k_expand_p, dim3(grid_for(pe - pb)), dim3(BLOCK), 0, stream, ix, st,
-                           (uint32_t)pb, (uint32_t)pe);
-      });
+    ExpandArgs ea{};
+    ea.gs = se > sb ? grid_for(se - sb) : 0u;
+    ea.gl = le > lb ? grid_for(le - lb) : 0u;
+    ea.ga = do_a ? grid_for(hx.N) : 0u;
+    ea.gp = do_p ? grid_for(pe - pb) : 0u;
+    ea.sb = (uint32_t)sb, ea.se = (uint32_t)se, ea.lb = (uint32_t)lb, ea.le = (uint32_t)le;
+    ea.ab = (uint32_t)ab, ea.ae = (uint32_t)ae, ea.pb = (uint32_t)pb, ea.pe = (uint32_t)pe;
+    ea.mask = mask;
+    ea.a_end = (uint32_t)a0;
+    launch(EL_K_EXPAND_S, [&] {
+      hipLaunchKernelGGL(k_expand, dim3(ea.gs + ea.gl + ea.ga + ea.gp), dim3(BLOCK), 0, stream, ix, st, ea);
+    });
     launch(EL_K_JOBS, [&] {
       hipLaunchKernelGGL(k_jobs, dim3(1024), dim3(BLOCK), 0, stream, ix, st);
     });
-    // ---- commit (counts read on the device)
+    // ---- commit (counts read on the device); its last block publishes the counters to
+    // pinned host memory and zeroes the candidate counters, so the step ends with ONE sync
+    CommitArgs ca{};
+    ca.gs = grid_for(cs_cap);
+    ca.gl = grid_for(cl_cap);
+    ca.ga = hx.rng.a.size() ? grid_for(ca_cap, 64) : 0u;
+    ca.gp = hx.exl.a.size() ? grid_for(cp_cap, 256) : 0u;
+    ca.cs_cap = (uint32_t)cs_cap, ca.cl_cap = (uint32_t)cl_cap;
+    ca.ca_cap = (uint32_t)ca_cap, ca.cp_cap = (uint32_t)cp_cap;
+    ca.host = hc_dev;
+    ca.done = commit_done;
+    ca.seq = ++commit_seq;
     launch(EL_K_COMMIT_S, [&] {
-      hipLaunchKernelGGL(k_commit_s, dim3(grid_for(cs_cap)), dim3(BLOCK), 0, stream, ix, st, &ctr->cand_s,
-                         (uint32_t)cs_cap);
+      hipLaunchKernelGGL(k_commit, dim3(ca.gs + ca.gl + ca.ga + ca.gp), dim3(BLOCK), 0, stream, ix, st, ca);
     });
-    launch(EL_K_COMMIT_L, [&] {
-      hipLaunchKernelGGL(k_commit_l, dim3(grid_for(cl_cap)), dim3(BLOCK), 0, stream, ix, st, &ctr->cand_l,
-                         (uint32_t)cl_cap);
-    });
-    if (hx.rng.a.size())
-      launch(EL_K_COMMIT_A, [&] {
-        hipLaunchKernelGGL(k_commit_a, dim3(grid_for(ca_cap, 64)), dim3(BLOCK), 0, stream, ix, st, &ctr->cand_a,
-                           (uint32_t)ca_cap);
-      });
-    if (hx.exl.a.size())
-      launch(EL_K_COMMIT_P, [&] {
-        hipLaunchKernelGGL(k_commit_p, dim3(grid_for(cp_cap, 256)), dim3(BLOCK), 0, stream, ix, st, &ctr->cand_p,
-                           (uint32_t)cp_cap);
-      });
-    // counters are final once the commits ran: copy them out, then zero the candidate
-    // counters for the next step — all on the stream, so the step ends with ONE sync
-    HIPCHK(hipMemcpyAsync(hc_pinned, ctr, sizeof(DCounters), hipMemcpyDeviceToHost, stream));
-    HIPCHK(hipMemsetAsync(&ctr->cand_s, 0, 8 * sizeof(uint32_t), stream));
     // ---- merge the new links / propagations into their CSRs (S rows: lazily, for export)
     std::vector<MergeReq> reqs;
     if (hx.P && need_pred) reqs.push_back({&PR, llog_p, llog_x, l_count, l_count, &ctr->l_log});
     if (need_succ) reqs.push_back({&SC, llog_x, llog_p, l_count, l_count, &ctr->l_log});
     if (hx.exl.a.size()) reqs.push_back({&PP, plog_p, plog_b, p_count, p_count, &ctr->p_log});
     launch_merges(reqs);
-    sync();
-    hc = *hc_pinned;
+    wait_commit(ca.seq);
     std::vector<uint64_t> ends;
     for (const MergeReq& r : reqs) ends.push_back(r.end_ptr == &ctr->l_log ? hc.l_log : hc.p_log);
     finish_merges(reqs, ends, true);
@@ -1654,6 +1905,7 @@ bool el_ctx::superstep(uint32_t mask, uint64_t sb, uint64_t se, uint64_t lb, uin
     bool overflow = false;
     auto regrow2 = [&](uint32_t need, uint64_t& cap, uint32_t*& a, uint32_t*& b) {
       if (2ull * need <= cap) return;
+      sync();  // the step's kernels are still queued: free nothing under them
       overflow |= need > cap;
       cap = next_pow2(2ull * need + 1024);
       dfree(a);
@@ -1666,6 +1918,7 @@ bool el_ctx::superstep(uint32_t mask, uint64_t sb, uint64_t se, uint64_t lb, uin
     regrow2(hc.cand_a, ca_cap, ca_y, ca_c);
     regrow2(hc.cand_p, cp_cap, cp_p, cp_b);
     if (2ull * hc.jobs > job_cap) {
+      sync();
       overflow |= hc.jobs > job_cap;
       job_cap = next_pow2(2ull * hc.jobs + 1024);
       dfree(jobs);
@@ -1960,6 +2213,7 @@ int el_kernel_stats(el_ctx* c, el_kernel_stat* out, int n) {
         s.bytes += s.events[e] * width[e];
       }
       s.ms = c->kms[k];
+      s.group = kernel_group(k);
       out[k] = s;
     }
     return EL_OK;

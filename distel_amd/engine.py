@@ -21,12 +21,14 @@ LIB_PATH = os.path.join(_HERE, "lib", "libel_gpu.so")
 EL_OK, EL_EINVAL, EL_ENOMEM, EL_EHIP, EL_ESTATE, EL_ERANGE = 0, -1, -2, -3, -4, -5
 LAYOUT_X_TO_B, LAYOUT_B_TO_X = 0, 1
 
-KERNEL_NAMES = ["k_expand_s", "k_expand_l", "k_jobs", "k_expand_a", "k_commit_s", "k_commit_l", "k_commit_a",
-                "hipcub_scan", "k_merge_ptr", "k_scatter_old", "k_scatter_new", "k_init", "k_rehash",
-                "k_expand_p", "k_commit_p"]
+# work phases (el_kernel); "kernel:role" where several phases share one launch
+KERNEL_NAMES = ["k_expand:s", "k_expand:l", "k_jobs", "k_expand:a", "k_commit:s", "k_commit:l", "k_commit:a",
+                "k_scan_merge:scan", "k_scan_merge:ptr", "k_scatter_old", "k_scatter_new", "k_init", "k_rehash",
+                "k_expand:p", "k_commit:p"]
 EVENT_NAMES = ["trig", "row", "ent", "test", "hash", "emit", "job", "rmw"]
 EVENT_BYTES = [8, 8, 4, 4, 8, 8, 16, 8]
 NUM_KERNELS = len(KERNEL_NAMES)
+ABI_VERSION = 2  # include/el_gpu.h EL_ABI_VERSION
 NUM_EVENTS = len(EVENT_NAMES)
 
 
@@ -78,7 +80,7 @@ class _ElStats(C.Structure):
 
 class _ElKernelStat(C.Structure):
     _fields_ = [("launches", C.c_uint64), ("events", C.c_uint64 * NUM_EVENTS), ("bytes", C.c_uint64),
-                ("ms", C.c_double)]
+                ("ms", C.c_double), ("group", C.c_uint32)]
 
 
 _SINK = C.CFUNCTYPE(C.c_int, C.c_void_p, _u32p, _u32p, C.c_size_t)
@@ -103,6 +105,8 @@ def load_library(path: Optional[str] = None) -> C.CDLL:
     lib = C.CDLL(p)
     P = C.c_void_p
     lib.el_abi_version.restype = C.c_int
+    if lib.el_abi_version() != ABI_VERSION:
+        raise ElError(EL_EHIP, f"{p}: ABI version {lib.el_abi_version()} != {ABI_VERSION} (rebuild)")
     lib.el_device_count.argtypes = [C.POINTER(C.c_int)]
     lib.el_create.argtypes = [C.POINTER(P), C.POINTER(_ElConfig)]
     lib.el_load.argtypes = [P, C.POINTER(_ElAxioms)]
@@ -239,6 +243,7 @@ class Engine:
         for k in range(NUM_KERNELS):
             s = arr[k]
             out.append(dict(kernel=KERNEL_NAMES[k], launches=int(s.launches), bytes=int(s.bytes), ms=float(s.ms),
+                            group=KERNEL_NAMES[int(s.group)],
                             events={EVENT_NAMES[e]: int(s.events[e]) for e in range(NUM_EVENTS)}))
         return out
 

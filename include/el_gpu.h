@@ -42,7 +42,7 @@
 extern "C" {
 #endif
 
-#define EL_ABI_VERSION 1
+#define EL_ABI_VERSION 2
 
 /* return codes */
 #define EL_OK        0
@@ -139,24 +139,27 @@ typedef struct el_config {
   uint32_t flags;        /* reserved, must be 0 */
 } el_config;
 
-/* Kernel ids for el_kernel_stats: one row per __global__ kernel (names match
- * the rocprofv3 kernel trace), plus the hipcub scan used by the CSR merges. */
+/* Work-phase ids for el_kernel_stats.  Several phases share one launch: the
+ * generation roles run in k_expand, the commit roles in k_commit, the scan and the
+ * new row offsets in k_scan_merge (names as in the rocprofv3 kernel trace).  A
+ * phase's events are its own; launches and ms are reported on the phase that
+ * names the launch (el_kernel_stat.group). */
 typedef enum el_kernel {
-  EL_K_EXPAND_S = 0,     /* k_expand_s:  ΔS-triggered CR1, CR2, CR3, CR4 half-1, ⊥ (Y side), range */
-  EL_K_EXPAND_L = 1,     /* k_expand_l:  Δlink-triggered CR4 half-2, CR5, CR6, ⊥, domain/range */
+  EL_K_EXPAND_S = 0,     /* k_expand, ΔS role:   CR1, CR2, CR3, CR4 half-1, ⊥ (Y side), range */
+  EL_K_EXPAND_L = 1,     /* k_expand, Δlink role: CR4 half-2, CR5, CR6, ⊥, domain/range */
   EL_K_JOBS = 2,         /* k_jobs:      fan-out over predecessor / successor lists */
-  EL_K_EXPAND_A = 3,     /* k_expand_a:  range activations, column sweep of S */
-  EL_K_COMMIT_S = 4,     /* k_commit_s:  bit-row atomicOr dedup + ΔS append */
-  EL_K_COMMIT_L = 5,     /* k_commit_l:  link hash-set dedup + Δlink append */
-  EL_K_COMMIT_A = 6,     /* k_commit_a:  activation set dedup */
-  EL_K_SCAN = 7,         /* hipcub exclusive scan of per-row delta counts */
-  EL_K_MERGE_PTR = 8,    /* k_merge_ptr: new row offsets */
+  EL_K_EXPAND_A = 3,     /* k_expand, activation role: column sweep of S */
+  EL_K_COMMIT_S = 4,     /* k_commit, S role:    bit-row atomicOr dedup + ΔS append */
+  EL_K_COMMIT_L = 5,     /* k_commit, link role: link hash-set dedup + Δlink append */
+  EL_K_COMMIT_A = 6,     /* k_commit, activation role: activation set dedup */
+  EL_K_SCAN = 7,         /* k_scan_merge: single-pass scan of the per-row delta counts */
+  EL_K_MERGE_PTR = 8,    /* k_scan_merge: new row offsets */
   EL_K_SCATTER_OLD = 9,  /* k_scatter_old: move existing CSR entries */
   EL_K_SCATTER_NEW = 10, /* k_scatter_new: place delta entries */
   EL_K_INIT = 11,        /* k_init:      S(X) = {X, ⊤} */
   EL_K_REHASH = 12,      /* k_rehash:    link / activation / propagation set growth */
-  EL_K_EXPAND_P = 13,    /* k_expand_p:  new CR4 propagations × predecessors (per-rule stepping) */
-  EL_K_COMMIT_P = 14,    /* k_commit_p:  CR4 propagation set dedup ("Yr" -> B, T3_2 DB0) */
+  EL_K_EXPAND_P = 13,    /* k_expand, propagation role: new CR4 propagations × predecessors */
+  EL_K_COMMIT_P = 14,    /* k_commit, propagation role: CR4 propagation set dedup ("Yr" -> B) */
   EL_NUM_KERNELS = 15
 } el_kernel;
 
@@ -178,6 +181,7 @@ typedef struct el_kernel_stat {
   uint64_t events[EL_NUM_EVENTS];
   uint64_t bytes;        /* algorithmic bytes = Σ events × width above */
   double ms;             /* Σ HIP-event time (only with config.profile = 1) */
+  uint32_t group;        /* phase whose launches / ms include this phase's work */
 } el_kernel_stat;
 
 typedef struct el_stats {

@@ -39,7 +39,7 @@ def test_exports_every_symbol(lib):
 
 
 def test_abi_version(lib):
-    assert lib.el_abi_version() == 1
+    assert lib.el_abi_version() == 2
 
 
 def test_no_device_fails_loudly(lib):
