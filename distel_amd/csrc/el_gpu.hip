@@ -110,15 +110,26 @@ struct DIndex {
 };
 
 // Event counters live in their own array, EV_SLOTS copies per (kernel, event) so the
-// per-block flushes of a launch spread over 16 addresses (host sums the slots).
+// per-block flushes of a launch spread over 16 separate cache lines (host sums the slots).
 constexpr int EV_SLOTS = 16;
 constexpr size_t EV_WORDS = (size_t)EL_NUM_KERNELS * EL_NUM_EVENTS * EV_SLOTS;
 
+// Step counters.  On the device every counter sits on a 256-B line of its own: appends of
+// different queues then do not serialise on one L2 line (MI355X_MICROARCH.md, "fanin":
+// ≈12 ns per atomic on one line).  The host copy (HCounters) is compact.
+constexpr uint32_t CTR_STRIDE = 64;  // words
+#define EL_COUNTERS(X) X(s_log) X(l_log) X(a_log) X(p_log) X(cand_s) X(cand_l) X(cand_a) X(jobs) \
+  X(cand_p) X(pad1) X(ticket) X(seq)
+#define EL_CTR_DEV(n) uint32_t n; uint32_t n##_pad[CTR_STRIDE - 1];
+#define EL_CTR_HOST(n) uint32_t n;
 struct DCounters {
-  uint32_t s_log, l_log, a_log, p_log;
-  uint32_t cand_s, cand_l, cand_a, jobs;
-  uint32_t cand_p, pad1, ticket, seq;  // ticket: k_scan_merge tiles; seq: host copy only
+  EL_COUNTERS(EL_CTR_DEV)
 };
+struct HCounters {  // ticket: k_scan_merge tile dispenser; seq: host copy only
+  EL_COUNTERS(EL_CTR_HOST)
+};
+constexpr uint32_t NUM_CTRS = sizeof(HCounters) / 4;
+static_assert(sizeof(DCounters) == NUM_CTRS * CTR_STRIDE * 4, "counter layout");
 
 struct DState {
   uint32_t* bits;
@@ -147,7 +158,7 @@ struct DState {
   uint4* jobs;
   uint32_t job_cap;
   DCounters* ctr;
-  unsigned long long* ev;  // [kernel][event][EV_SLOTS]
+  unsigned long long* ev;  // [EV_SLOTS][kernel][event]: a slot's words are far from the others'
 };
 
 // ---------------------------------------------------------------- device helpers
@@ -182,7 +193,7 @@ __device__ __forceinline__ void ev_flush(unsigned long long* evg, int k, const E
   }
   __syncthreads();
   if (threadIdx.x < EL_NUM_EVENTS && sev[threadIdx.x])
-    atomicAdd(&evg[((size_t)k * EL_NUM_EVENTS + threadIdx.x) * EV_SLOTS + (blockIdx.x % EV_SLOTS)],
+    atomicAdd(&evg[((size_t)(blockIdx.x % EV_SLOTS) * EL_NUM_KERNELS + k) * EL_NUM_EVENTS + threadIdx.x],
               sev[threadIdx.x]);
 }
 
@@ -440,6 +451,30 @@ __device__ __forceinline__ void q_maybe_flush(BlockQ& q, const DState& st) {
 }
 
 // ---------------------------------------------------------------- kernels
+
+// State reset for el_init in one launch (instead of a dozen fill launches): each segment
+// is filled with a repeated 32-bit pattern, 16 B per store.
+struct FillSeg {
+  void* p;
+  uint64_t bytes;
+  uint32_t pattern;
+};
+struct FillArgs {
+  FillSeg seg[16];
+  uint32_t n;
+};
+__global__ void k_fill(FillArgs f) {
+  const uint64_t tid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x, stride = (uint64_t)gridDim.x * blockDim.x;
+  for (uint32_t k = 0; k < f.n; ++k) {
+    const FillSeg g = f.seg[k];
+    const uint32_t v = g.pattern;
+    uint4* q = reinterpret_cast<uint4*>(g.p);
+    const uint64_t n16 = g.bytes / 16;
+    for (uint64_t i = tid; i < n16; i += stride) q[i] = make_uint4(v, v, v, v);
+    uint8_t* b = reinterpret_cast<uint8_t*>(g.p);
+    for (uint64_t i = n16 * 16 + tid; i < g.bytes; i += stride) b[i] = (uint8_t)(v >> (8 * (i & 3)));
+  }
+}
 
 // S(X) = {X, ⊤} for classes and individuals, {X} for ⊤, ⊥ and datatypes
 // (AxiomLoader.java:1237-1245 classes, :1281-1289 individuals).
@@ -987,8 +1022,8 @@ constexpr uint32_t DONE_SHARDS = 16;
 struct CommitArgs {
   uint32_t gs, gl, ga, gp;
   uint32_t cs_cap, cl_cap, ca_cap, cp_cap;
-  DCounters* host;  // device view of the pinned host copy
-  uint32_t* done;   // [DONE_SHARDS + 1] zero between launches
+  HCounters* host;  // device view of the pinned host copy
+  uint32_t* done;   // [(DONE_SHARDS + 1) * CTR_STRIDE], zero between launches
   uint32_t seq;     // written last to host->seq: the host spins on it
 };
 __global__ void k_commit(DIndex ix, DState st, CommitArgs a) {
@@ -1012,20 +1047,21 @@ __global__ void k_commit(DIndex ix, DState st, CommitArgs a) {
     const uint32_t in_shard = (gridDim.x - 1 - sh) / DONE_SHARDS + 1;
     const uint32_t shards = min(gridDim.x, DONE_SHARDS);
     last = 0;
-    if (__hip_atomic_fetch_add(a.done + sh, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == in_shard - 1)
-      last = __hip_atomic_fetch_add(a.done + DONE_SHARDS, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
-             shards - 1;
+    if (__hip_atomic_fetch_add(a.done + sh * CTR_STRIDE, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+        in_shard - 1)
+      last = __hip_atomic_fetch_add(a.done + DONE_SHARDS * CTR_STRIDE, 1u, __ATOMIC_RELAXED,
+                                    __HIP_MEMORY_SCOPE_AGENT) == shards - 1;
   }
   __syncthreads();
   if (last) {
-    constexpr uint32_t NW = sizeof(DCounters) / 4 - 1;  // every word but seq
+    constexpr uint32_t NW = NUM_CTRS - 1;  // every counter but seq
     if (threadIdx.x < NW) {
-      uint32_t* dc = reinterpret_cast<uint32_t*>(st.ctr);
-      const uint32_t v = __hip_atomic_load(dc + threadIdx.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      uint32_t* dc = reinterpret_cast<uint32_t*>(st.ctr) + threadIdx.x * CTR_STRIDE;
+      const uint32_t v = __hip_atomic_load(dc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       reinterpret_cast<volatile uint32_t*>(a.host)[threadIdx.x] = v;
-      if (threadIdx.x >= 4) dc[threadIdx.x] = 0;  // cand_*, jobs for the next step
+      if (threadIdx.x >= 4) *dc = 0;  // cand_*, jobs for the next step
     }
-    if (threadIdx.x <= DONE_SHARDS) a.done[threadIdx.x] = 0;
+    if (threadIdx.x <= DONE_SHARDS) a.done[threadIdx.x * CTR_STRIDE] = 0;
     __threadfence_system();
     __syncthreads();
     if (threadIdx.x == 0) {
@@ -1392,9 +1428,9 @@ struct el_ctx {
   uint32_t scan_epoch = 0;
 
   // host mirrors
-  DCounters hc{};
-  DCounters* hc_pinned = nullptr;  // counters published by k_commit (hipHostMalloc)
-  DCounters* hc_dev = nullptr;     // device view of hc_pinned
+  HCounters hc{};
+  HCounters* hc_pinned = nullptr;  // counters published by k_commit (hipHostMalloc)
+  HCounters* hc_dev = nullptr;     // device view of hc_pinned
   uint32_t commit_seq = 0;         // k_commit launches so far (published with the counters)
   uint64_t s_count = 0, l_count = 0, a_count = 0, p_count = 0, s_init = 0;
   uint64_t wm_s[EL_NUM_RULE_TYPES] = {}, wm_l[EL_NUM_RULE_TYPES] = {}, wm_a[EL_NUM_RULE_TYPES] = {},
@@ -1497,11 +1533,16 @@ struct el_ctx {
     }
     pending.clear();
   }
-  void read_counters() { HIPCHK(hipMemcpy(&hc, ctr, sizeof(DCounters), hipMemcpyDeviceToHost)); }
+  void read_counters() {
+    static thread_local std::vector<uint32_t> tmp(sizeof(DCounters) / 4);
+    HIPCHK(hipMemcpy(tmp.data(), ctr, sizeof(DCounters), hipMemcpyDeviceToHost));
+    uint32_t* h = reinterpret_cast<uint32_t*>(&hc);
+    for (uint32_t i = 0; i < NUM_CTRS; ++i) h[i] = tmp[i * CTR_STRIDE];
+  }
   // Wait until k_commit #seq has published the step's counters (the merge kernels of the
   // step may still be running: the next step is enqueued behind them on the stream).
   void wait_commit(uint32_t seq) {
-    volatile DCounters* p = hc_pinned;
+    volatile HCounters* p = hc_pinned;
     for (uint64_t it = 1;; ++it) {
       if (p->seq == seq) break;
       if ((it & 1023) == 0) {  // a faulted or finished stream must not leave us spinning
@@ -1517,7 +1558,7 @@ struct el_ctx {
     std::atomic_thread_fence(std::memory_order_acquire);
     uint32_t* h = reinterpret_cast<uint32_t*>(&hc);
     const volatile uint32_t* src = reinterpret_cast<const volatile uint32_t*>(hc_pinned);
-    for (size_t i = 0; i < sizeof(DCounters) / 4; ++i) h[i] = src[i];
+    for (size_t i = 0; i < NUM_CTRS; ++i) h[i] = src[i];
   }
   void read_events() {
     std::vector<unsigned long long> h(EV_WORDS);
@@ -1525,7 +1566,7 @@ struct el_ctx {
     for (int k = 0; k < EL_NUM_KERNELS; ++k)
       for (int e = 0; e < EL_NUM_EVENTS; ++e) {
         unsigned long long t = 0;
-        for (int q = 0; q < EV_SLOTS; ++q) t += h[((size_t)k * EL_NUM_EVENTS + e) * EV_SLOTS + q];
+        for (int q = 0; q < EV_SLOTS; ++q) t += h[((size_t)q * EL_NUM_KERNELS + k) * EL_NUM_EVENTS + e];
         hev[k][e] = t;
       }
   }
@@ -1644,33 +1685,34 @@ void el_ctx::alloc_state() {
   jobs = dalloc<uint4>(job_cap);
   ctr = dalloc<DCounters>(1);
   // coherent: k_commit's stores reach the host while later kernels of the step still run
-  HIPCHK(hipHostMalloc((void**)&hc_pinned, sizeof(DCounters), hipHostMallocCoherent | hipHostMallocMapped));
-  memset(hc_pinned, 0, sizeof(DCounters));
+  HIPCHK(hipHostMalloc((void**)&hc_pinned, sizeof(HCounters), hipHostMallocCoherent | hipHostMallocMapped));
+  memset(hc_pinned, 0, sizeof(HCounters));
   commit_seq = 0;
   ev = dalloc<unsigned long long>(EV_WORDS);
   HIPCHK(hipHostGetDevicePointer((void**)&hc_dev, hc_pinned, 0));
   scan_tiles = 0;
   for (uint64_t rows : {N, P, N, P}) scan_tiles += (rows + 1 + SCAN_TILE - 1) / SCAN_TILE;
   scan_flags = dalloc<unsigned long long>(scan_tiles);
-  commit_done = dalloc<uint32_t>(DONE_SHARDS + 1);
+  commit_done = dalloc<uint32_t>((DONE_SHARDS + 1) * CTR_STRIDE);
   HIPCHK(hipMemset(scan_flags, 0, scan_tiles * sizeof(unsigned long long)));
   scan_epoch = 0;
 }
 
 void el_ctx::reset_state() {
-  HIPCHK(hipMemsetAsync(bits, 0, hx.N * W * sizeof(uint32_t), stream));
-  HIPCHK(hipMemsetAsync(lhash, 0xff, lhash_cap * sizeof(unsigned long long), stream));
-  HIPCHK(hipMemsetAsync(ahash, 0xff, ahash_cap * sizeof(unsigned long long), stream));
-  HIPCHK(hipMemsetAsync(has_act, 0, hx.N, stream));
-  HIPCHK(hipMemsetAsync(phash, 0xff, phash_cap * sizeof(unsigned long long), stream));
-  PP.reset(stream);
-  HIPCHK(hipMemsetAsync(dcnt_all, 0, dcnt_total * sizeof(uint32_t), stream));
-  S.reset(stream);
-  PR.reset(stream);
-  SC.reset(stream);
-  HIPCHK(hipMemsetAsync(ctr, 0, sizeof(DCounters), stream));
-  HIPCHK(hipMemsetAsync(commit_done, 0, (DONE_SHARDS + 1) * sizeof(uint32_t), stream));
-  HIPCHK(hipMemsetAsync(ev, 0, EV_WORDS * sizeof(unsigned long long), stream));
+  FillArgs f{};
+  auto add = [&](void* p, uint64_t bytes, uint32_t pattern) { f.seg[f.n++] = FillSeg{p, bytes, pattern}; };
+  add(bits, hx.N * W * sizeof(uint32_t), 0u);
+  add(lhash, lhash_cap * sizeof(unsigned long long), ~0u);
+  add(ahash, ahash_cap * sizeof(unsigned long long), ~0u);
+  add(has_act, hx.N, 0u);
+  add(phash, phash_cap * sizeof(unsigned long long), ~0u);
+  add(dcnt_all, dcnt_total * sizeof(uint32_t), 0u);
+  for (DevCsr* c : {&S, &PR, &SC, &PP}) add(c->ptr, (c->nrows + 1) * sizeof(uint32_t), 0u);
+  add(ctr, sizeof(DCounters), 0u);
+  add(commit_done, (DONE_SHARDS + 1) * CTR_STRIDE * sizeof(uint32_t), 0u);
+  add(ev, EV_WORDS * sizeof(unsigned long long), 0u);
+  hipLaunchKernelGGL(k_fill, dim3(1024), dim3(BLOCK), 0, stream, f);
+  HIPCHK(hipGetLastError());
   s_count = l_count = a_count = p_count = s_init = s_csr_count = 0;
   for (int r = 0; r < EL_NUM_RULE_TYPES; ++r) wm_s[r] = wm_l[r] = wm_a[r] = wm_p[r] = 0;
   memset(launches, 0, sizeof launches);
