@@ -209,36 +209,35 @@ __device__ __forceinline__ uint32_t wave_append(uint32_t* counter, bool pred) {
   return pred ? base + rank : NONE;
 }
 
-// Keyed counter update: lanes of a wave that hit the same counter (a hub row) share one
-// atomic.  Up to two distinct keys per wave are aggregated, the rest go one by one.  Only
-// used where hub rows exist (predecessor lists keyed by pid): for mostly-distinct keys the
-// rounds are pure overhead.
+// Keyed counter update: the lanes of a wave are grouped by key (a match-any built from
+// ballots: ALU work only, one round per distinct key), then ONE atomic instruction is issued
+// in which each group's first lane adds the group size; the members read their slot from
+// the returned value by a shuffle.  Same-key lanes of one atomic instruction would
+// otherwise serialise at the L2 atomic unit, and hub rows (a pid that gains hundreds of
+// predecessors in a step) make that the common case.
 // Returns, per lane, the value an individual atomic on that lane would have returned
 // in some serialisation (old + rank for add, old - rank for sub).
 __device__ __forceinline__ uint32_t wave_keyed_atomic(uint32_t* base, uint32_t key, bool pred, bool sub) {
   unsigned long long pending = __ballot(pred);
+  if (pending == 0) return 0;
   const uint32_t lane = lane_id();
-  uint32_t result = 0;
-#pragma unroll
-  for (int round = 0; round < 2; ++round) {
-    if (pending == 0) return result;
+  const unsigned long long lt = (1ull << lane) - 1ull;
+  uint32_t rank = 0, cnt = 0, src = lane;
+  while (pending) {
     const int leader = __ffsll((long long)pending) - 1;
     const uint32_t lkey = __shfl(key, leader);
     const unsigned long long same = __ballot(pred && key == lkey) & pending;
-    uint32_t old = 0;
-    if ((int)lane == leader) {
-      const uint32_t k = (uint32_t)__popcll(same);
-      old = sub ? atomicSub(base + lkey, k) : atomicAdd(base + lkey, k);
-    }
-    old = __shfl(old, leader);
     if ((same >> lane) & 1ull) {
-      const uint32_t rank = (uint32_t)__popcll(same & ((1ull << lane) - 1ull));
-      result = sub ? old - rank : old + rank;
+      src = (uint32_t)leader;
+      rank = (uint32_t)__popcll(same & lt);
+      if ((int)lane == leader) cnt = (uint32_t)__popcll(same);
     }
     pending &= ~same;
   }
-  if ((pending >> lane) & 1ull) result = sub ? atomicSub(base + key, 1u) : atomicAdd(base + key, 1u);
-  return result;
+  uint32_t old = 0;
+  if (cnt) old = sub ? atomicSub(base + key, cnt) : atomicAdd(base + key, cnt);
+  old = __shfl(old, (int)src);
+  return sub ? old - rank : old + rank;
 }
 
 __device__ __forceinline__ bool test_bit(const uint32_t* bits, uint64_t W, uint32_t x, uint32_t b) {
@@ -977,8 +976,8 @@ __device__ void commit_p(const DIndex& ix, const DState& st, uint32_t bid, uint3
       ev.v[EL_EV_EMIT]++;
       st.plog_p[slot] = pid;
       st.plog_b[slot] = b;
-      atomicAdd(st.dcnt + st.off_pp + pid, 1u);
     }
+    wave_keyed_atomic(st.dcnt, st.off_pp + pid, nw, false);
   }
   ev_flush(st.ev, EL_K_COMMIT_P, ev);
 }
@@ -1432,6 +1431,9 @@ struct el_ctx {
   HCounters* hc_pinned = nullptr;  // counters published by k_commit (hipHostMalloc)
   HCounters* hc_dev = nullptr;     // device view of hc_pinned
   uint32_t commit_seq = 0;         // k_commit launches so far (published with the counters)
+  bool stats_stale = false;        // el_init ran without a sync: `last` is filled on demand
+  unsigned long long* ev_host = nullptr;  // pinned copy of ev
+  bool events_queued = false;
   uint64_t s_count = 0, l_count = 0, a_count = 0, p_count = 0, s_init = 0;
   uint64_t wm_s[EL_NUM_RULE_TYPES] = {}, wm_l[EL_NUM_RULE_TYPES] = {}, wm_a[EL_NUM_RULE_TYPES] = {},
            wm_p[EL_NUM_RULE_TYPES] = {};
@@ -1560,9 +1562,17 @@ struct el_ctx {
     const volatile uint32_t* src = reinterpret_cast<const volatile uint32_t*>(hc_pinned);
     for (size_t i = 0; i < NUM_CTRS; ++i) h[i] = src[i];
   }
+  // Event counters travel with the stream (pinned target): a caller that syncs anyway
+  // enqueues them first and sums after its sync, without a second round trip.
+  void enqueue_events() {
+    HIPCHK(hipMemcpyAsync(ev_host, ev, EV_WORDS * sizeof(unsigned long long), hipMemcpyDeviceToHost, stream));
+    events_queued = true;
+  }
   void read_events() {
-    std::vector<unsigned long long> h(EV_WORDS);
-    HIPCHK(hipMemcpy(h.data(), ev, EV_WORDS * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+    if (!events_queued) enqueue_events();
+    sync();
+    events_queued = false;
+    const unsigned long long* h = ev_host;
     for (int k = 0; k < EL_NUM_KERNELS; ++k)
       for (int e = 0; e < EL_NUM_EVENTS; ++e) {
         unsigned long long t = 0;
@@ -1630,6 +1640,9 @@ void el_ctx::free_state() {
   dfree(ctr);
   if (hc_pinned) (void)hipHostFree(hc_pinned);
   hc_pinned = nullptr;
+  if (ev_host) (void)hipHostFree(ev_host);
+  ev_host = nullptr;
+  events_queued = false;
   dfree(ev);
   dfree(scan_flags);
   dfree(commit_done);
@@ -1689,6 +1702,7 @@ void el_ctx::alloc_state() {
   memset(hc_pinned, 0, sizeof(HCounters));
   commit_seq = 0;
   ev = dalloc<unsigned long long>(EV_WORDS);
+  HIPCHK(hipHostMalloc((void**)&ev_host, EV_WORDS * sizeof(unsigned long long), hipHostMallocDefault));
   HIPCHK(hipHostGetDevicePointer((void**)&hc_dev, hc_pinned, 0));
   scan_tiles = 0;
   for (uint64_t rows : {N, P, N, P}) scan_tiles += (rows + 1 + SCAN_TILE - 1) / SCAN_TILE;
@@ -1783,7 +1797,7 @@ void el_ctx::launch_merges(const std::vector<MergeReq>& reqs) {
     g.n_old = (uint32_t)r.old_n;
     g.begin = (uint32_t)r.begin;
     g.end_ptr = r.end_ptr;
-    g.keyed = r.c == &PR ? 1u : 0u;
+    g.keyed = (r.c == &PR || r.c == &PP) ? 1u : 0u;
     m.max_rows = std::max(m.max_rows, g.n1);
     m.max_old = std::max(m.max_old, g.n_old);
   }
@@ -1988,6 +2002,7 @@ void el_ctx::fill_stats(el_stats* out, double ms) {
   st.bytes = bytes;
   st.ms = ms;
   last = st;
+  stats_stale = false;
   if (out) *out = st;
 }
 
@@ -2161,13 +2176,16 @@ int el_init(el_ctx* c) {
     c->launch(EL_K_INIT, [&] {
       hipLaunchKernelGGL(k_init, dim3(grid_for(c->hx.N)), dim3(BLOCK), 0, c->stream, c->ix, st);
     });
-    c->sync();
-    c->read_counters();
-    c->s_count = c->hc.s_log;
-    c->s_init = c->s_count;
+    // k_init appends X for every concept and ⊤ for classes and individuals other than ⊤/⊥:
+    // the count is known on the host, so the first superstep is enqueued without a sync
+    uint64_t n = c->hx.N;
+    for (uint32_t x = 0; x < c->hx.N; ++x)
+      n += x != EL_TOP && x != EL_BOTTOM && c->hx.kind[x] != EL_KIND_DATATYPE;
+    c->s_count = n;
+    c->s_init = n;
     c->s_csr_count = 0;
     c->inited = true;
-    c->fill_stats(nullptr, 0.0);
+    c->stats_stale = true;
     return EL_OK;
   });
 }
@@ -2226,8 +2244,8 @@ int el_saturate(el_ctx* c, el_stats* stats) {
       c->wm_a[r] = c->a_count;
       c->wm_p[r] = c->p_count;
     }
+    c->enqueue_events();  // hc is current (published by the last k_commit); events ride along
     c->sync();
-    c->read_counters();
     double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     c->fill_stats(stats, ms);
     return EL_OK;
@@ -2236,6 +2254,13 @@ int el_saturate(el_ctx* c, el_stats* stats) {
 
 int el_get_stats(el_ctx* c, el_stats* stats) {
   if (!c || !stats) return EL_EINVAL;
+  if (c->stats_stale)
+    return guarded(c, [&] {
+      c->sync();
+      c->fill_stats(stats, 0.0);
+      c->stats_stale = false;
+      return EL_OK;
+    });
   *stats = c->last;
   return EL_OK;
 }
