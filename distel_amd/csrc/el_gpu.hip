@@ -109,10 +109,13 @@ struct DIndex {
   uint32_t has_range;
 };
 
-// Event counters live in their own array, EV_SLOTS copies per (kernel, event) so the
-// per-block flushes of a launch spread over 16 separate cache lines (host sums the slots).
-constexpr int EV_SLOTS = 16;
-constexpr size_t EV_WORDS = (size_t)EL_NUM_KERNELS * EL_NUM_EVENTS * EV_SLOTS;
+// Event counters: one partial row per block index, updated with plain read-modify-writes
+// (a block index is unique within a launch and launches on the stream do not overlap), so
+// counting costs no atomics at all; blocks beyond EV_BLOCKS share an atomic overflow row.
+// k_ev_reduce folds the rows into EV_TOTAL words when the host asks.
+constexpr uint32_t EV_BLOCKS = 4096;
+constexpr size_t EV_TOTAL = (size_t)EL_NUM_KERNELS * EL_NUM_EVENTS;
+constexpr size_t EV_WORDS = (EV_BLOCKS + 1) * EV_TOTAL;
 
 // Step counters.  On the device every counter sits on a 256-B line of its own: appends of
 // different queues then do not serialise on one L2 line (MI355X_MICROARCH.md, "fanin":
@@ -158,7 +161,7 @@ struct DState {
   uint4* jobs;
   uint32_t job_cap;
   DCounters* ctr;
-  unsigned long long* ev;  // [EV_SLOTS][kernel][event]: a slot's words are far from the others'
+  unsigned long long* ev;  // [EV_BLOCKS + 1][kernel][event] per-block partials
 };
 
 // ---------------------------------------------------------------- device helpers
@@ -179,6 +182,11 @@ __device__ __forceinline__ unsigned long long wave_sum(uint32_t x) {
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
   return v;
 }
+__device__ __forceinline__ unsigned long long wave_sum_u64(unsigned long long v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  return v;
+}
 
 // Block-level reduction of the event counters: one LDS atomic per wave, then one global
 // atomic per (event, block) into a sharded slot.  Every thread of the block must call it.
@@ -192,9 +200,24 @@ __device__ __forceinline__ void ev_flush(unsigned long long* evg, int k, const E
     if (lane_id() == 0 && s) atomicAdd(&sev[i], s);
   }
   __syncthreads();
-  if (threadIdx.x < EL_NUM_EVENTS && sev[threadIdx.x])
-    atomicAdd(&evg[((size_t)(blockIdx.x % EV_SLOTS) * EL_NUM_KERNELS + k) * EL_NUM_EVENTS + threadIdx.x],
-              sev[threadIdx.x]);
+  if (threadIdx.x < EL_NUM_EVENTS && sev[threadIdx.x]) {
+    if (blockIdx.x < EV_BLOCKS) {
+      evg[((size_t)blockIdx.x * EL_NUM_KERNELS + k) * EL_NUM_EVENTS + threadIdx.x] += sev[threadIdx.x];
+    } else {
+      atomicAdd(&evg[((size_t)EV_BLOCKS * EL_NUM_KERNELS + k) * EL_NUM_EVENTS + threadIdx.x], sev[threadIdx.x]);
+    }
+  }
+}
+
+// out[w] = Σ_slots ev[slot][w]: one block per word
+__global__ void k_ev_reduce(const unsigned long long* __restrict__ ev, unsigned long long* __restrict__ out) {
+  __shared__ unsigned long long part[4];
+  unsigned long long s = 0;
+  for (uint32_t q = threadIdx.x; q <= EV_BLOCKS; q += blockDim.x) s += ev[(size_t)q * EV_TOTAL + blockIdx.x];
+  s = wave_sum_u64(s);
+  if (lane_id() == 0) part[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) out[blockIdx.x] = part[0] + part[1] + part[2] + part[3];
 }
 
 // Wave-aggregated append: one atomic per wave; returns this lane's slot when pred.
@@ -1432,7 +1455,8 @@ struct el_ctx {
   HCounters* hc_dev = nullptr;     // device view of hc_pinned
   uint32_t commit_seq = 0;         // k_commit launches so far (published with the counters)
   bool stats_stale = false;        // el_init ran without a sync: `last` is filled on demand
-  unsigned long long* ev_host = nullptr;  // pinned copy of ev
+  unsigned long long* ev_sum = nullptr;   // k_ev_reduce output
+  unsigned long long* ev_host = nullptr;  // pinned copy of ev_sum
   bool events_queued = false;
   uint64_t s_count = 0, l_count = 0, a_count = 0, p_count = 0, s_init = 0;
   uint64_t wm_s[EL_NUM_RULE_TYPES] = {}, wm_l[EL_NUM_RULE_TYPES] = {}, wm_a[EL_NUM_RULE_TYPES] = {},
@@ -1565,7 +1589,9 @@ struct el_ctx {
   // Event counters travel with the stream (pinned target): a caller that syncs anyway
   // enqueues them first and sums after its sync, without a second round trip.
   void enqueue_events() {
-    HIPCHK(hipMemcpyAsync(ev_host, ev, EV_WORDS * sizeof(unsigned long long), hipMemcpyDeviceToHost, stream));
+    hipLaunchKernelGGL(k_ev_reduce, dim3(EV_TOTAL), dim3(256), 0, stream, ev, ev_sum);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipMemcpyAsync(ev_host, ev_sum, EV_TOTAL * sizeof(unsigned long long), hipMemcpyDeviceToHost, stream));
     events_queued = true;
   }
   void read_events() {
@@ -1574,11 +1600,7 @@ struct el_ctx {
     events_queued = false;
     const unsigned long long* h = ev_host;
     for (int k = 0; k < EL_NUM_KERNELS; ++k)
-      for (int e = 0; e < EL_NUM_EVENTS; ++e) {
-        unsigned long long t = 0;
-        for (int q = 0; q < EV_SLOTS; ++q) t += h[((size_t)q * EL_NUM_KERNELS + k) * EL_NUM_EVENTS + e];
-        hev[k][e] = t;
-      }
+      for (int e = 0; e < EL_NUM_EVENTS; ++e) hev[k][e] = h[(size_t)k * EL_NUM_EVENTS + e];
   }
 
   void free_state();
@@ -1640,6 +1662,7 @@ void el_ctx::free_state() {
   dfree(ctr);
   if (hc_pinned) (void)hipHostFree(hc_pinned);
   hc_pinned = nullptr;
+  dfree(ev_sum);
   if (ev_host) (void)hipHostFree(ev_host);
   ev_host = nullptr;
   events_queued = false;
@@ -1702,7 +1725,8 @@ void el_ctx::alloc_state() {
   memset(hc_pinned, 0, sizeof(HCounters));
   commit_seq = 0;
   ev = dalloc<unsigned long long>(EV_WORDS);
-  HIPCHK(hipHostMalloc((void**)&ev_host, EV_WORDS * sizeof(unsigned long long), hipHostMallocDefault));
+  ev_sum = dalloc<unsigned long long>(EV_TOTAL);
+  HIPCHK(hipHostMalloc((void**)&ev_host, EV_TOTAL * sizeof(unsigned long long), hipHostMallocDefault));
   HIPCHK(hipHostGetDevicePointer((void**)&hc_dev, hc_pinned, 0));
   scan_tiles = 0;
   for (uint64_t rows : {N, P, N, P}) scan_tiles += (rows + 1 + SCAN_TILE - 1) / SCAN_TILE;

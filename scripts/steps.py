@@ -1,0 +1,37 @@
+#!/usr/bin/env python3
+"""Per-superstep kernel times of one classification from a rocprofv3 kernel trace.
+Usage: scripts/steps.py gpurun_out/TAG/prof/run_kernel_trace.csv [classification index]"""
+import collections
+import csv
+import re
+import sys
+
+rows = list(csv.DictReader(open(sys.argv[1])))
+rows.sort(key=lambda r: int(r["Start_Timestamp"]))
+which = int(sys.argv[2]) if len(sys.argv) > 2 else 2
+idx = [i for i, r in enumerate(rows) if "k_fill" in r["Kernel_Name"]] + [len(rows)]
+seg = rows[idx[which]:idx[which + 1]]
+
+
+def nm(s):
+    m = re.search(r"(k_\w+)", s)
+    return m.group(0) if m else "other"
+
+
+step, table, tot = -1, collections.defaultdict(dict), collections.Counter()
+t0, t1 = int(seg[0]["Start_Timestamp"]), max(int(r["End_Timestamp"]) for r in seg)
+for r in seg:
+    n = nm(r["Kernel_Name"])
+    if n == "k_expand":
+        step += 1
+    d = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
+    tot[n] += d
+    if step >= 0:
+        table[step][n] = table[step].get(n, 0) + d
+cols = ["k_expand", "k_jobs", "k_commit", "k_scan_merge", "k_scatter_old", "k_scatter_new"]
+print("step " + " ".join(f"{c[2:]:>12s}" for c in cols))
+for s in sorted(table):
+    print(f"{s:4d} " + " ".join(f"{table[s].get(c, 0):12.1f}" for c in cols))
+print("span us %.1f  busy us %.1f" % ((t1 - t0) / 1e3, sum(tot.values())))
+for k, v in tot.most_common():
+    print(f"  {k:20s} {v:9.1f}")
