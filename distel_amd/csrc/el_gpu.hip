@@ -155,6 +155,8 @@ struct DState {
   uint32_t* dcnt;  // all CSR delta counts, one array: [S rows | PR | SC | PP]
   uint32_t off_s, off_pr, off_sc, off_pp;
   uint32_t need_pred, need_succ;  // CSRs with readers: only those get delta counts
+  uint32_t *rk_pr, *rk_sc, *rk_pp;  // rank of each new entry in its delta row (index: log slot - base)
+  uint32_t l_base, p_base;          // link / propagation log counts at the start of the step
   uint32_t *cs_x, *cs_a, cs_cap;
   uint32_t *cl_x, *cl_p, cl_cap;
   uint32_t *ca_y, *ca_c, ca_cap;
@@ -845,6 +847,7 @@ __device__ void expand_a(const DIndex& ix, const DState& st, BlockQ& q, uint32_t
 // LDS staging of the commit roles (one role per block)
 struct CommitLds {
   uint32_t x[QS_CAP > QL_CAP ? QS_CAP : QL_CAP], v[QS_CAP > QL_CAP ? QS_CAP : QL_CAP];
+  uint32_t r1[QL_CAP], r2[QL_CAP];  // link ranks in the predecessor / successor delta rows
   uint32_t n, base;
 };
 
@@ -919,14 +922,19 @@ __device__ void commit_l(const DIndex& ix, const DState& st, CommitLds& sm, uint
       nw = hash_insert(st.lhash, st.lmask, link_key(p, x));
       if (nw) {
         ev.v[EL_EV_EMIT]++;
-        if (st.need_succ) atomicAdd(st.dcnt + st.off_sc + x, 1u);
+        ev.v[EL_EV_ENT] += st.need_pred + st.need_succ;  // rank words for the merges
       }
     }
-    if (st.need_pred) wave_keyed_atomic(st.dcnt, st.off_pr + p, nw, false);  // hub pids: many new preds
+    // the count's old value is the link's rank among its row's new entries: the merge
+    // places it from that rank without a second atomic
+    const uint32_t rp = st.need_pred ? wave_keyed_atomic(st.dcnt, st.off_pr + p, nw, false) : 0u;
+    const uint32_t rs = st.need_succ ? wave_keyed_atomic(st.dcnt, st.off_sc + x, nw, false) : 0u;
     const uint32_t off = lds_reserve(&ln, nw);
     if (nw) {
       lx[off] = x;
       lp[off] = p;
+      sm.r1[off] = rp;
+      sm.r2[off] = rs;
     }
     __syncthreads();
     if (ln > QL_CAP / 2 || base + nb * blockDim.x >= n) {
@@ -936,6 +944,8 @@ __device__ void commit_l(const DIndex& ix, const DState& st, CommitLds& sm, uint
       for (uint32_t k = threadIdx.x; k < cnt; k += blockDim.x) {
         st.llog_x[lbase + k] = lx[k];
         st.llog_p[lbase + k] = lp[k];
+        if (st.need_pred) st.rk_pr[lbase + k - st.l_base] = sm.r1[k];
+        if (st.need_succ) st.rk_sc[lbase + k - st.l_base] = sm.r2[k];
       }
       __syncthreads();
       if (threadIdx.x == 0) ln = 0;
@@ -995,12 +1005,14 @@ __device__ void commit_p(const DIndex& ix, const DState& st, uint32_t bid, uint3
     ev.v[EL_EV_HASH]++;
     const bool nw = hash_insert(st.phash, st.pmask, link_key(pid, b));
     const uint32_t slot = wave_append(&st.ctr->p_log, nw);
+    const uint32_t rank = wave_keyed_atomic(st.dcnt, st.off_pp + pid, nw, false);
     if (nw) {
       ev.v[EL_EV_EMIT]++;
       st.plog_p[slot] = pid;
       st.plog_b[slot] = b;
+      st.rk_pp[slot - st.p_base] = rank;
+      ev.v[EL_EV_ENT]++;
     }
-    wave_keyed_atomic(st.dcnt, st.off_pp + pid, nw, false);
   }
   ev_flush(st.ev, EL_K_COMMIT_P, ev);
 }
@@ -1105,7 +1117,7 @@ struct MergeSeg {
   uint32_t n_old;           // existing entries
   uint32_t begin;           // delta = log[begin, *end_ptr)
   const uint32_t* end_ptr;  // device log counter (the host learns it only after the step)
-  uint32_t keyed;           // hub rows possible: aggregate same-row counter updates per wave
+  const uint32_t* rank;     // rank of delta entry i among its row's new entries
 };
 struct MergeArgs {
   MergeSeg seg[4];
@@ -1133,7 +1145,7 @@ __device__ __forceinline__ unsigned long long flag_word(uint32_t epoch, uint32_t
   return ((unsigned long long)((epoch << 2) | state) << 32) | v;
 }
 
-__global__ void __launch_bounds__(256) k_scan_merge(MergeArgs m, ScanArgs sa, const uint32_t* __restrict__ dcnt,
+__global__ void __launch_bounds__(256) k_scan_merge(MergeArgs m, ScanArgs sa, uint32_t* __restrict__ dcnt,
                                                     uint32_t* __restrict__ dscan) {
   __shared__ uint32_t buf[SCAN_TILE];
   __shared__ uint32_t wtot[4];
@@ -1148,11 +1160,16 @@ __global__ void __launch_bounds__(256) k_scan_merge(MergeArgs m, ScanArgs sa, co
   const MergeSeg& g = m.seg[k];
   if (*g.end_ptr == g.begin) return;  // nothing new in this CSR: none of its tiles scans
   const uint32_t lt = t - sa.tile0[k], r0 = lt * SCAN_TILE;
-  const uint32_t* __restrict__ dc = dcnt + g.off;
+  uint32_t* __restrict__ dc = dcnt + g.off;
 #pragma unroll
   for (uint32_t i = 0; i < SCAN_ITEMS; ++i) {
     const uint32_t idx = r0 + i * 256 + tid;
-    buf[i * 256 + tid] = idx < g.n1 ? dc[idx] : 0u;
+    uint32_t v = 0;
+    if (idx < g.n1) {
+      v = dc[idx];
+      if (v) dc[idx] = 0;  // consumed: the counts start from zero next step
+    }
+    buf[i * 256 + tid] = v;
   }
   __syncthreads();
   uint32_t v[SCAN_ITEMS], run = 0;
@@ -1247,33 +1264,25 @@ __global__ void k_scatter_old(MergeArgs m, const uint32_t* __restrict__ dscan) {
   }
 }
 
-// delta entries fill the tail of their row; the counts are consumed back to zero
-__global__ void k_scatter_new(MergeArgs m, uint32_t* dcnt) {
+// delta entry i of row x lands after the row's old entries, at its rank among the row's
+// new entries (recorded when its count was taken): no atomics here
+__global__ void k_scatter_new(MergeArgs m, const uint32_t* __restrict__ dscan) {
   const MergeSeg g = m.seg[blockIdx.y];
   const uint32_t stride = gridDim.x * blockDim.x, n = *g.end_ptr - g.begin;
-  for (uint32_t base = blockIdx.x * blockDim.x; base < n; base += stride) {
-    const uint32_t i = base + threadIdx.x;
-    const bool on = i < n;
-    const uint32_t x = on ? g.lx[g.begin + i] : 0u;
-    uint32_t old;
-    if (g.keyed) {
-      old = wave_keyed_atomic(dcnt + g.off, x, on, true);
-    } else {
-      old = on ? atomicSub(dcnt + g.off + x, 1u) : 0u;
-    }
-    if (on) {
-      const uint32_t pos = g.ptr2[x + 1] - old;
-      g.row2[pos] = x;
-      g.val2[pos] = g.lv[g.begin + i];
-    }
+  const uint32_t* __restrict__ ds = dscan + g.off;
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    const uint32_t x = g.lx[g.begin + i];
+    const uint32_t pos = g.ptr[x + 1] + ds[x] + g.rank[i];
+    g.row2[pos] = x;
+    g.val2[pos] = g.lv[g.begin + i];
   }
 }
 
-// per-row counts of log[begin, end) (lazy S-row CSR build for export)
-__global__ void k_count_rows(uint32_t* dcnt, const uint32_t* lx, uint32_t begin, uint32_t end) {
+// per-row counts of log[begin, end) with each entry's rank (lazy S-row CSR for export)
+__global__ void k_count_rows(uint32_t* dcnt, uint32_t* rank, const uint32_t* lx, uint32_t begin, uint32_t end) {
   const uint32_t stride = gridDim.x * blockDim.x;
   for (uint32_t i = begin + blockIdx.x * blockDim.x + threadIdx.x; i < end; i += stride)
-    atomicAdd(dcnt + lx[i], 1u);
+    rank[i - begin] = atomicAdd(dcnt + lx[i], 1u);
 }
 
 __global__ void k_pack_keys(unsigned long long* out, const uint32_t* hi, const uint32_t* lo, uint32_t n) {
@@ -1438,6 +1447,7 @@ struct el_ctx {
   bool need_succ = true;      // successor CSR has readers (CR6)
   uint32_t *cs_x = nullptr, *cs_a = nullptr, *cl_x = nullptr, *cl_p = nullptr, *ca_y = nullptr,
            *ca_c = nullptr;
+  uint32_t *rk_pr = nullptr, *rk_sc = nullptr, *rk_pp = nullptr;  // per-step ranks (cl_cap / cp_cap)
   uint64_t cs_cap = 0, cl_cap = 0, ca_cap = 0;
   uint4* jobs = nullptr;
   uint64_t job_cap = 0;
@@ -1506,6 +1516,11 @@ struct el_ctx {
     s.off_pp = (uint32_t)(PP.dcnt - dcnt_all);
     s.need_pred = need_pred ? 1u : 0u;
     s.need_succ = need_succ ? 1u : 0u;
+    s.rk_pr = rk_pr;
+    s.rk_sc = rk_sc;
+    s.rk_pp = rk_pp;
+    s.l_base = (uint32_t)l_count;
+    s.p_base = (uint32_t)p_count;
     s.cs_x = cs_x;
     s.cs_a = cs_a;
     s.cs_cap = (uint32_t)cs_cap;
@@ -1613,6 +1628,7 @@ struct el_ctx {
     const uint32_t *lx, *lv;
     uint64_t old_n, begin;
     const uint32_t* end_ptr;  // device log counter
+    const uint32_t* rank;     // rank of each delta entry in its row (index: log slot - begin)
   };
   void launch_merges(const std::vector<MergeReq>& reqs);
   void finish_merges(const std::vector<MergeReq>& reqs, const std::vector<uint64_t>& ends, bool account);
@@ -1646,6 +1662,9 @@ void el_ctx::free_state() {
   dfree(plog_b);
   dfree(cp_p);
   dfree(cp_b);
+  dfree(rk_pr);
+  dfree(rk_sc);
+  dfree(rk_pp);
   S.release();
   PR.release();
   SC.release();
@@ -1697,6 +1716,7 @@ void el_ctx::alloc_state() {
   cp_cap = plog_cap;
   cp_p = dalloc<uint32_t>(cp_cap);
   cp_b = dalloc<uint32_t>(cp_cap);
+  rk_pp = dalloc<uint32_t>(cp_cap);
   dcnt_total = 2 * (N + 1) + 2 * (P + 1);
   dcnt_all = dalloc<uint32_t>(dcnt_total);
   dscan_all = dalloc<uint32_t>(dcnt_total);
@@ -1715,6 +1735,8 @@ void el_ctx::alloc_state() {
   cs_a = dalloc<uint32_t>(cs_cap);
   cl_x = dalloc<uint32_t>(cl_cap);
   cl_p = dalloc<uint32_t>(cl_cap);
+  rk_pr = dalloc<uint32_t>(cl_cap);
+  rk_sc = dalloc<uint32_t>(cl_cap);
   ca_y = dalloc<uint32_t>(ca_cap);
   ca_c = dalloc<uint32_t>(ca_cap);
   job_cap = std::max<uint64_t>(1u << 20, 2 * N);
@@ -1821,7 +1843,7 @@ void el_ctx::launch_merges(const std::vector<MergeReq>& reqs) {
     g.n_old = (uint32_t)r.old_n;
     g.begin = (uint32_t)r.begin;
     g.end_ptr = r.end_ptr;
-    g.keyed = (r.c == &PR || r.c == &PP) ? 1u : 0u;
+    g.rank = r.rank;
     m.max_rows = std::max(m.max_rows, g.n1);
     m.max_old = std::max(m.max_old, g.n_old);
   }
@@ -1841,8 +1863,7 @@ void el_ctx::launch_merges(const std::vector<MergeReq>& reqs) {
   sa.flags = scan_flags;
   sa.ticket = &ctr->ticket;
   launch(EL_K_SCAN, [&] {
-    hipLaunchKernelGGL(k_scan_merge, dim3(tiles), dim3(256), 0, stream, m, sa, (const uint32_t*)dcnt_all,
-                       dscan_all);
+    hipLaunchKernelGGL(k_scan_merge, dim3(tiles), dim3(256), 0, stream, m, sa, dcnt_all, dscan_all);
   });
   if (m.max_old)
     launch(EL_K_SCATTER_OLD, [&] {
@@ -1850,49 +1871,49 @@ void el_ctx::launch_merges(const std::vector<MergeReq>& reqs) {
                          dscan_all);
     });
   launch(EL_K_SCATTER_NEW, [&] {
-    hipLaunchKernelGGL(k_scatter_new, dim3(512, m.nseg), dim3(BLOCK), 0, stream, m, dcnt_all);
+    hipLaunchKernelGGL(k_scatter_new, dim3(512, m.nseg), dim3(BLOCK), 0, stream, m, (const uint32_t*)dscan_all);
   });
 }
 
 // After the step's sync: account the merges that did work and swap their buffers.
 void el_ctx::finish_merges(const std::vector<MergeReq>& reqs, const std::vector<uint64_t>& ends, bool account) {
-  bool any = false;
   for (size_t k = 0; k < reqs.size(); ++k) {
     const MergeReq& r = reqs[k];
     const uint64_t nn = ends[k] - r.begin;
     if (!nn) continue;
-    any = true;
     if (account) {
       const uint64_t n1 = r.c->nrows + 1, old_n = r.old_n;
-      host_ev[EL_K_MERGE_PTR][EL_EV_ENT] += 3ull * n1;  // read ptr, dscan; write ptr2
+      host_ev[EL_K_SCAN][EL_EV_ENT] += 3ull * n1;       // read + zero dcnt, write dscan
+      host_ev[EL_K_MERGE_PTR][EL_EV_ENT] += 2ull * n1;  // read ptr, write ptr2
       host_ev[EL_K_SCATTER_OLD][EL_EV_TRIG] += old_n;   // read (row, val)
       host_ev[EL_K_SCATTER_OLD][EL_EV_ENT] += old_n;    // read dscan[row]
       host_ev[EL_K_SCATTER_OLD][EL_EV_EMIT] += old_n;   // write (row2, val2)
       host_ev[EL_K_SCATTER_NEW][EL_EV_TRIG] += nn;      // read log pair
-      host_ev[EL_K_SCATTER_NEW][EL_EV_ENT] += nn;       // read ptr2[x + 1]
-      host_ev[EL_K_SCATTER_NEW][EL_EV_RMW] += nn;       // consume the delta count
+      host_ev[EL_K_SCATTER_NEW][EL_EV_ENT] += 3 * nn;   // read rank, ptr[x + 1], dscan[x]
       host_ev[EL_K_SCATTER_NEW][EL_EV_EMIT] += nn;      // write (row2, val2)
     }
     std::swap(r.c->ptr, r.c->ptr2);
     std::swap(r.c->row, r.c->row2);
     std::swap(r.c->val, r.c->val2);
   }
-  if (any && account) host_ev[EL_K_SCAN][EL_EV_ENT] += 2ull * dcnt_total;  // read dcnt, write dscan
 }
 
 // Bring the S-row CSR up to date with the fact log (export path, not counted as saturation).
 void el_ctx::ensure_s_csr() {
   if (s_csr_count == s_count) return;
-  hipLaunchKernelGGL(k_count_rows, dim3(grid_for(s_count - s_csr_count)), dim3(BLOCK), 0, stream, S.dcnt,
+  sync();  // the saturation's last merges may still be running
+  uint32_t* rank = dalloc<uint32_t>(s_count - s_csr_count);
+  hipLaunchKernelGGL(k_count_rows, dim3(grid_for(s_count - s_csr_count)), dim3(BLOCK), 0, stream, S.dcnt, rank,
                      slog_x, (uint32_t)s_csr_count, (uint32_t)s_count);
   HIPCHK(hipGetLastError());
-  std::vector<MergeReq> reqs{{&S, slog_x, slog_a, s_csr_count, s_csr_count, &ctr->s_log}};
+  std::vector<MergeReq> reqs{{&S, slog_x, slog_a, s_csr_count, s_csr_count, &ctr->s_log, rank}};
   uint64_t saved_launch[EL_NUM_KERNELS];
   memcpy(saved_launch, launches, sizeof launches);
   launch_merges(reqs);
   sync();
   memcpy(launches, saved_launch, sizeof launches);  // export work is not saturation work
   finish_merges(reqs, {s_count}, false);
+  dfree(rank);
   s_csr_count = s_count;
 }
 
@@ -1969,9 +1990,9 @@ bool el_ctx::superstep(uint32_t mask, uint64_t sb, uint64_t se, uint64_t lb, uin
     });
     // ---- merge the new links / propagations into their CSRs (S rows: lazily, for export)
     std::vector<MergeReq> reqs;
-    if (hx.P && need_pred) reqs.push_back({&PR, llog_p, llog_x, l_count, l_count, &ctr->l_log});
-    if (need_succ) reqs.push_back({&SC, llog_x, llog_p, l_count, l_count, &ctr->l_log});
-    if (hx.exl.a.size()) reqs.push_back({&PP, plog_p, plog_b, p_count, p_count, &ctr->p_log});
+    if (hx.P && need_pred) reqs.push_back({&PR, llog_p, llog_x, l_count, l_count, &ctr->l_log, rk_pr});
+    if (need_succ) reqs.push_back({&SC, llog_x, llog_p, l_count, l_count, &ctr->l_log, rk_sc});
+    if (hx.exl.a.size()) reqs.push_back({&PP, plog_p, plog_b, p_count, p_count, &ctr->p_log, rk_pp});
     launch_merges(reqs);
     wait_commit(ca.seq);
     std::vector<uint64_t> ends;
@@ -1983,6 +2004,12 @@ bool el_ctx::superstep(uint32_t mask, uint64_t sb, uint64_t se, uint64_t lb, uin
     p_count = hc.p_log;
     // ---- keep the buffers ahead of demand; complete the step if one overflowed
     bool overflow = false;
+    auto regrow2_to = [&](uint64_t cap, uint32_t*& a, uint32_t*& b) {
+      dfree(a);
+      dfree(b);
+      a = dalloc<uint32_t>(cap);
+      b = dalloc<uint32_t>(cap);
+    };
     auto regrow2 = [&](uint32_t need, uint64_t& cap, uint32_t*& a, uint32_t*& b) {
       if (2ull * need <= cap) return;
       sync();  // the step's kernels are still queued: free nothing under them
@@ -1994,9 +2021,15 @@ bool el_ctx::superstep(uint32_t mask, uint64_t sb, uint64_t se, uint64_t lb, uin
       b = dalloc<uint32_t>(cap);
     };
     regrow2(hc.cand_s, cs_cap, cs_x, cs_a);
+    const uint64_t cl_old = cl_cap, cp_old = cp_cap;
     regrow2(hc.cand_l, cl_cap, cl_x, cl_p);
     regrow2(hc.cand_a, ca_cap, ca_y, ca_c);
     regrow2(hc.cand_p, cp_cap, cp_p, cp_b);
+    if (cl_cap != cl_old) regrow2_to(cl_cap, rk_pr, rk_sc);
+    if (cp_cap != cp_old) {
+      dfree(rk_pp);
+      rk_pp = dalloc<uint32_t>(cp_cap);
+    }
     if (2ull * hc.jobs > job_cap) {
       sync();
       overflow |= hc.jobs > job_cap;

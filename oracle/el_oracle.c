@@ -856,24 +856,19 @@ static void expand_p(elo_ctx* c, cands* k, uint64_t pb, uint64_t pe) {
   }
 }
 
-/* analytic events of the CSR merges of one superstep (same formula as the GPU host side):
- * one scan over the delta counts of all four CSRs (S, PR, SC, PP), then per merged CSR the
- * row offsets, the moved entries and the placed delta entries */
+/* analytic events of the CSR merge of one CSR with nn new entries (same formula as the GPU
+ * host side): scan of the row counts (read, zero, write), new row offsets, the moved
+ * entries, and the delta entries placed by their recorded rank */
 static void merge_seg_events(elo_ctx* c, uint64_t nrows, uint64_t old_n, uint64_t nn) {
   uint64_t n1 = nrows + 1;
-  EVN(EL_K_MERGE_PTR, EL_EV_ENT, 3 * n1);
+  EVN(EL_K_SCAN, EL_EV_ENT, 3 * n1);
+  EVN(EL_K_MERGE_PTR, EL_EV_ENT, 2 * n1);
   EVN(EL_K_SCATTER_OLD, EL_EV_TRIG, old_n);
   EVN(EL_K_SCATTER_OLD, EL_EV_ENT, old_n);
   EVN(EL_K_SCATTER_OLD, EL_EV_EMIT, old_n);
   EVN(EL_K_SCATTER_NEW, EL_EV_TRIG, nn);
-  EVN(EL_K_SCATTER_NEW, EL_EV_ENT, nn);
-  EVN(EL_K_SCATTER_NEW, EL_EV_RMW, nn);
+  EVN(EL_K_SCATTER_NEW, EL_EV_ENT, 3 * nn);
   EVN(EL_K_SCATTER_NEW, EL_EV_EMIT, nn);
-}
-
-static void merge_scan_events(elo_ctx* c) {
-  uint64_t tot = 2 * ((uint64_t)c->N + 1) + 2 * ((uint64_t)c->P + 1);
-  EVN(EL_K_SCAN, EL_EV_ENT, 2 * tot);
 }
 
 static int superstep(elo_ctx* c, uint32_t mask, uint64_t sb, uint64_t se, uint64_t lb, uint64_t le,
@@ -912,6 +907,7 @@ static int superstep(elo_ctx* c, uint32_t mask, uint64_t sb, uint64_t se, uint64
     EV(EL_K_COMMIT_L, EL_EV_HASH);
     if (hs_add(&c->links, lkey(p, x))) {
       EV(EL_K_COMMIT_L, EL_EV_EMIT);
+      EVN(EL_K_COMMIT_L, EL_EV_ENT, (uint64_t)(c->need_pred != 0) + (c->need_succ != 0)); /* merge ranks */
       vpush(&c->llog_x, x);
       vpush(&c->llog_p, p);
       vpush(&c->pred[p], x);
@@ -935,6 +931,7 @@ static int superstep(elo_ctx* c, uint32_t mask, uint64_t sb, uint64_t se, uint64
     EV(EL_K_COMMIT_P, EL_EV_HASH);
     if (hs_add(&c->props, lkey(pid, b))) {
       EV(EL_K_COMMIT_P, EL_EV_EMIT);
+      EV(EL_K_COMMIT_P, EL_EV_ENT); /* merge rank */
       vpush(&c->plog_p, pid);
       vpush(&c->plog_b, b);
       vpush(&c->prow[pid], b);
@@ -942,13 +939,8 @@ static int superstep(elo_ctx* c, uint32_t mask, uint64_t sb, uint64_t se, uint64
   }
   cands_free(&k);
   /* the S-row CSR is not read during saturation (built lazily for export) */
-  {
-    int m_pr = c->llog_x.n > l0 && c->P && c->need_pred, m_sc = c->llog_x.n > l0 && c->need_succ;
-    int m_pp = c->plog_p.n > p0;
-    if (m_pr || m_sc || m_pp) merge_scan_events(c);
-    if (m_pr) merge_seg_events(c, c->P, l0, c->llog_x.n - l0);
-    if (m_sc) merge_seg_events(c, c->N, l0, c->llog_x.n - l0);
-  }
+  if (c->llog_x.n > l0 && c->P && c->need_pred) merge_seg_events(c, c->P, l0, c->llog_x.n - l0);
+  if (c->llog_x.n > l0 && c->need_succ) merge_seg_events(c, c->N, l0, c->llog_x.n - l0);
   if (c->plog_p.n > p0) merge_seg_events(c, c->P, p0, c->plog_p.n - p0);
   return c->slog_x.n > s0 || c->llog_x.n > l0 || c->alog_y.n > a0 || c->plog_p.n > p0;
 }
