@@ -36,6 +36,7 @@
 #include <atomic>
 #include <chrono>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <stdexcept>
 #include <string>
@@ -235,7 +236,8 @@ __device__ __forceinline__ uint32_t wave_append(uint32_t* counter, bool pred) {
 }
 
 // Keyed counter update: the lanes of a wave are grouped by key (a match-any built from
-// ballots: ALU work only, one round per distinct key), then ONE atomic instruction is issued
+// ballots and v_readlane: scalar-latency ALU work, one round per distinct key — a shuffle
+// per round would put an LDS round trip on this chain), then ONE atomic instruction is issued
 // in which each group's first lane adds the group size; the members read their slot from
 // the returned value by a shuffle.  Same-key lanes of one atomic instruction would
 // otherwise serialise at the L2 atomic unit, and hub rows (a pid that gains hundreds of
@@ -246,22 +248,22 @@ __device__ __forceinline__ uint32_t wave_keyed_atomic(uint32_t* base, uint32_t k
   unsigned long long pending = __ballot(pred);
   if (pending == 0) return 0;
   const uint32_t lane = lane_id();
-  const unsigned long long lt = (1ull << lane) - 1ull;
-  uint32_t rank = 0, cnt = 0, src = lane;
-  while (pending) {
+  unsigned long long group = 0;  // this lane's key group (lanes with the same key)
+  while (pending) {              // scalar loop: leader by s_ff1, its key by v_readlane
     const int leader = __ffsll((long long)pending) - 1;
-    const uint32_t lkey = __shfl(key, leader);
+    const uint32_t lkey = __builtin_amdgcn_readlane(key, leader);
     const unsigned long long same = __ballot(pred && key == lkey) & pending;
-    if ((same >> lane) & 1ull) {
-      src = (uint32_t)leader;
-      rank = (uint32_t)__popcll(same & lt);
-      if ((int)lane == leader) cnt = (uint32_t)__popcll(same);
-    }
+    if ((same >> lane) & 1ull) group = same;
     pending &= ~same;
   }
+  const uint32_t first = pred ? (uint32_t)__ffsll((long long)group) - 1 : lane;
+  const uint32_t rank = (uint32_t)__popcll(group & ((1ull << lane) - 1ull));
   uint32_t old = 0;
-  if (cnt) old = sub ? atomicSub(base + key, cnt) : atomicAdd(base + key, cnt);
-  old = __shfl(old, (int)src);
+  if (pred && first == lane) {
+    const uint32_t cnt = (uint32_t)__popcll(group);
+    old = sub ? atomicSub(base + key, cnt) : atomicAdd(base + key, cnt);
+  }
+  old = __shfl(old, (int)first);
   return sub ? old - rank : old + rank;
 }
 
@@ -1059,6 +1061,7 @@ struct CommitArgs {
   HCounters* host;  // device view of the pinned host copy
   uint32_t* done;   // [(DONE_SHARDS + 1) * CTR_STRIDE], zero between launches
   uint32_t seq;     // written last to host->seq: the host spins on it
+  uint32_t publish; // 0: a partial launch (diagnostic split): no completion protocol
 };
 __global__ void k_commit(DIndex ix, DState st, CommitArgs a) {
   __shared__ CommitLds sm;
@@ -1075,6 +1078,7 @@ __global__ void k_commit(DIndex ix, DState st, CommitArgs a) {
   }
   // The barrier waits for this block's memory operations; every counter update is a
   // returning device-scope atomic, so it has been performed before the block reports done.
+  if (!a.publish) return;
   __syncthreads();
   if (threadIdx.x == 0) {
     const uint32_t sh = blockIdx.x % DONE_SHARDS;
@@ -1465,6 +1469,7 @@ struct el_ctx {
   HCounters* hc_dev = nullptr;     // device view of hc_pinned
   uint32_t commit_seq = 0;         // k_commit launches so far (published with the counters)
   bool stats_stale = false;        // el_init ran without a sync: `last` is filled on demand
+  bool split_commit = getenv("EL_SPLIT_COMMIT") != nullptr;  // diagnostic only
   unsigned long long* ev_sum = nullptr;   // k_ev_reduce output
   unsigned long long* ev_host = nullptr;  // pinned copy of ev_sum
   bool events_queued = false;
@@ -1985,6 +1990,14 @@ bool el_ctx::superstep(uint32_t mask, uint64_t sb, uint64_t se, uint64_t lb, uin
     ca.host = hc_dev;
     ca.done = commit_done;
     ca.seq = ++commit_seq;
+    ca.publish = 1;
+    if (split_commit) {  // diagnostic: S role alone, then the other roles (rocprof sees both)
+      CommitArgs c1 = ca;
+      c1.gl = c1.ga = c1.gp = 0;
+      c1.publish = 0;
+      hipLaunchKernelGGL(k_commit, dim3(c1.gs), dim3(BLOCK), 0, stream, ix, st, c1);
+      ca.gs = 0;
+    }
     launch(EL_K_COMMIT_S, [&] {
       hipLaunchKernelGGL(k_commit, dim3(ca.gs + ca.gl + ca.ga + ca.gp), dim3(BLOCK), 0, stream, ix, st, ca);
     });
