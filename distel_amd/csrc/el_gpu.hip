@@ -32,9 +32,16 @@
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
 
+#include <dlfcn.h>
+#include <rccl/rccl.h>  // types only: librccl is opened on first use (EL_XCHG_RCCL)
+
 #include <algorithm>
 #include <atomic>
 #include <chrono>
+#include <condition_variable>
+#include <memory>
+#include <mutex>
+#include <cstddef>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -108,6 +115,10 @@ struct DIndex {
   const uint8_t* role_has_exl;
   const uint4* meta;  // per concept A: {told_ptr, cidx_ptr, exr_ptr, exl_ptr}[A] — one 32 B span for A, A+1
   uint32_t has_range;
+  // row partition (el_config.exchange != NONE): this context owns rows [lo, hi)
+  uint32_t lo, hi;
+  uint32_t part;               // 1 = partitioned protocol (oracle/partition_model.py)
+  const uint8_t* role_chs;     // r -> r is the second role of some chain (its links are exchanged)
 };
 
 // Event counters: one partial row per block index, updated with plain read-modify-writes
@@ -122,8 +133,11 @@ constexpr size_t EV_WORDS = (EV_BLOCKS + 1) * EV_TOTAL;
 // different queues then do not serialise on one L2 line (MI355X_MICROARCH.md, "fanin":
 // ≈12 ns per atomic on one line).  The host copy (HCounters) is compact.
 constexpr uint32_t CTR_STRIDE = 64;  // words
-#define EL_COUNTERS(X) X(s_log) X(l_log) X(a_log) X(p_log) X(cand_s) X(cand_l) X(cand_a) X(jobs) \
-  X(cand_p) X(pad1) X(ticket) X(seq)
+// Counters [0, CTR_KEEP) persist across steps; the rest are per-step (zeroed by k_commit).
+// x_log / x_send / g_delta / g_max belong to the partitioned exchange (k_ximport).
+#define EL_COUNTERS(X) X(s_log) X(l_log) X(a_log) X(p_log) X(x_log) X(x_send) X(cand_s) X(cand_l) \
+  X(cand_a) X(jobs) X(cand_p) X(g_delta) X(g_max) X(g_ovf) X(ticket) X(seq)
+constexpr uint32_t CTR_KEEP = 6;
 #define EL_CTR_DEV(n) uint32_t n; uint32_t n##_pad[CTR_STRIDE - 1];
 #define EL_CTR_HOST(n) uint32_t n;
 struct DCounters {
@@ -156,8 +170,13 @@ struct DState {
   uint32_t* dcnt;  // all CSR delta counts, one array: [S rows | PR | SC | PP]
   uint32_t off_s, off_pr, off_sc, off_pp;
   uint32_t need_pred, need_succ;  // CSRs with readers: only those get delta counts
+  uint32_t succ_at_commit;        // successor counts taken by k_commit (whole-ontology mode)
   uint32_t *rk_pr, *rk_sc, *rk_pp;  // rank of each new entry in its delta row (index: log slot - base)
   uint32_t l_base, p_base;          // link / propagation log counts at the start of the step
+  // partitioned exchange: replicated chain-second link log, local send queue, import ranks
+  uint32_t *xlog_x, *xlog_p;
+  uint32_t *xs_x, *xs_p;
+  uint32_t *rk_x, x_base;
   uint32_t *cs_x, *cs_a, cs_cap;
   uint32_t *cl_x, *cl_p, cl_cap;
   uint32_t *ca_y, *ca_c, ca_cap;
@@ -507,7 +526,7 @@ __global__ void k_fill(FillArgs f) {
 __global__ void k_init(DIndex ix, DState st) {
   Ev ev;
   const uint32_t stride = gridDim.x * blockDim.x;
-  for (uint32_t x = blockIdx.x * blockDim.x + threadIdx.x; x < ix.N; x += stride) {
+  for (uint32_t x = ix.lo + blockIdx.x * blockDim.x + threadIdx.x; x < ix.hi; x += stride) {
     const bool two = x != EL_TOP && x != EL_BOTTOM && ix.kind[x] != EL_KIND_DATATYPE;
     ev.v[EL_EV_ENT]++;
     uint32_t* row = st.bits + (uint64_t)x * ix.W;
@@ -615,6 +634,11 @@ __device__ void expand_s(const DIndex& ix, const DState& st, BlockQ& q, uint32_t
         ev.v[EL_EV_ROW]++;
         const uint32_t p1 = ix.fp_ptr[X + 1];
         for (uint32_t p = ix.fp_ptr[X]; p < p1; ++p) {
+          if (ix.part) {  // partitioned: ⊥ rides the propagation set ((r, Y), ⊥) to every rank
+            ev.v[EL_EV_HASH]++;
+            emit_p(st, !hash_contains(st.phash, st.pmask, link_key(p, EL_BOTTOM)), p, EL_BOTTOM, ev);
+            continue;
+          }
           ev.v[EL_EV_ROW]++;
           const uint32_t pb = st.pr_ptr[p], pl = st.pr_ptr[p + 1] - pb;
           emit_job(st, q, pl > 0, JOB_PRED_S, pb, pl, 0, EL_BOTTOM, ev);
@@ -644,6 +668,27 @@ __device__ void expand_s(const DIndex& ix, const DState& st, BlockQ& q, uint32_t
 }
 
 
+// CR6 with the new link (X, r, Y) in second position: (X', X) ∈ R(p), p ∘ r ⊑ t  =>  (X', Y) ∈ R(t)
+// (Type5AxiomProcessorBase.java:115-154, DB4 "Xp" -> Y of RolePairHandler.java:428-443, s checked).
+__device__ __forceinline__ void r6_second(const DIndex& ix, const DState& st, BlockQ& q, uint32_t X, uint32_t r,
+                                          uint32_t Y, Ev& ev) {
+  ev.v[EL_EV_ROW]++;
+  const uint32_t h1 = ix.chs_ptr[r + 1];
+  for (uint32_t j = ix.chs_ptr[r]; j < h1; ++j) {
+    const uint32_t p = ix.chs_p[j], t = ix.chs_t[j];
+    ev.v[EL_EV_ENT] += 2;
+    const uint32_t pq = pair_lookup(ix, p, X, ev);
+    uint32_t pb = 0, pl = 0, pt = NONE;
+    if (pq != NONE) {
+      ev.v[EL_EV_ROW]++;
+      pb = st.pr_ptr[pq];
+      pl = st.pr_ptr[pq + 1] - pb;
+      if (pl) pt = pair_lookup(ix, t, Y, ev);
+    }
+    emit_job(st, q, pl > 0, JOB_PRED_L, pb, pl, pt, 0, ev);
+  }
+}
+
 // Rules triggered by new links (X, pid = (r, Y)) = link log[begin, end).
 //  CR4½ Type3_2AxiomProcessorBase.java:67-96,182-224   CR5 Type4AxiomProcessorBase.java:38-76
 //  CR6  Type5AxiomProcessorBase.java:115-154           ⊥   RolePairHandler.java:358-372
@@ -668,7 +713,7 @@ __device__ void expand_l(const DIndex& ix, const DState& st, BlockQ& q, uint32_t
           emit_s(st, q, !test_bit(st.bits, ix.W, X, B), X, B, ev);
         }
       }
-      if (mask & M_RBOT) {  // ⊥ ∈ S(Y)  =>  ⊥ ∈ S(X)
+      if ((mask & M_RBOT) && !ix.part) {  // ⊥ ∈ S(Y)  =>  ⊥ ∈ S(X)  (partitioned: via propagations)
         ev.v[EL_EV_TEST]++;
         bool nw = false;
         if (test_bit(st.bits, ix.W, Y, EL_BOTTOM)) {
@@ -697,21 +742,7 @@ __device__ void expand_l(const DIndex& ix, const DState& st, BlockQ& q, uint32_t
           sl = st.sc_ptr[Y + 1] - sb;
         }
         emit_job(st, q, first && sl > 0, JOB_R6A, sb, sl, X, r, ev);
-        ev.v[EL_EV_ROW]++;
-        const uint32_t h1 = ix.chs_ptr[r + 1];
-        for (uint32_t j = ix.chs_ptr[r]; j < h1; ++j) {  // r second: (X', X) ∈ R(p)  =>  (X', Y) ∈ R(t)
-          const uint32_t p = ix.chs_p[j], t = ix.chs_t[j];
-          ev.v[EL_EV_ENT] += 2;
-          const uint32_t pq = pair_lookup(ix, p, X, ev);
-          uint32_t pb = 0, pl = 0, pt = NONE;
-          if (pq != NONE) {
-            ev.v[EL_EV_ROW]++;
-            pb = st.pr_ptr[pq];
-            pl = st.pr_ptr[pq + 1] - pb;
-            if (pl) pt = pair_lookup(ix, t, Y, ev);
-          }
-          emit_job(st, q, pl > 0, JOB_PRED_L, pb, pl, pt, 0, ev);
-        }
+        if (!ix.part) r6_second(ix, st, q, X, r, Y, ev);  // partitioned: over the exchanged chain links
       }
       if (mask & M_RDOM) {  // domain(r) = D  =>  D ∈ S(X)   (X ≠ ⊤, not a datatype)
         ev.v[EL_EV_ROW]++;
@@ -826,9 +857,9 @@ __device__ void expand_a(const DIndex& ix, const DState& st, BlockQ& q, uint32_t
                          uint32_t a_begin, uint32_t a_end) {
   Ev ev;
   if (bid == 0 && threadIdx.x == 0) ev.v[EL_EV_TRIG] += a_end - a_begin;
-  for (uint32_t base = bid * blockDim.x; base < ix.N; base += nb * blockDim.x) {
+  for (uint32_t base = ix.lo + bid * blockDim.x; base < ix.hi; base += nb * blockDim.x) {
     const uint32_t x = base + threadIdx.x;
-    if (x < ix.N) {
+    if (x < ix.hi) {
       for (uint32_t k = a_begin; k < a_end; ++k) {
         const uint32_t Y = st.alog_y[k], C = st.alog_c[k];
         ev.v[EL_EV_TEST]++;
@@ -924,13 +955,21 @@ __device__ void commit_l(const DIndex& ix, const DState& st, CommitLds& sm, uint
       nw = hash_insert(st.lhash, st.lmask, link_key(p, x));
       if (nw) {
         ev.v[EL_EV_EMIT]++;
-        ev.v[EL_EV_ENT] += st.need_pred + st.need_succ;  // rank words for the merges
+        ev.v[EL_EV_ENT] += st.need_pred + st.succ_at_commit;  // rank words for the merges
       }
     }
     // the count's old value is the link's rank among its row's new entries: the merge
     // places it from that rank without a second atomic
     const uint32_t rp = st.need_pred ? wave_keyed_atomic(st.dcnt, st.off_pr + p, nw, false) : 0u;
-    const uint32_t rs = st.need_succ ? wave_keyed_atomic(st.dcnt, st.off_sc + x, nw, false) : 0u;
+    const uint32_t rs = st.succ_at_commit ? wave_keyed_atomic(st.dcnt, st.off_sc + x, nw, false) : 0u;
+    if (ix.part) {  // partitioned: a new link of a chain-second role goes to every rank
+      const bool xs = nw && ix.role_chs[ix.pair_role[p]];
+      const uint32_t slot = wave_append(&st.ctr->x_send, xs);
+      if (xs) {
+        st.xs_x[slot] = x;
+        st.xs_p[slot] = p;
+      }
+    }
     const uint32_t off = lds_reserve(&ln, nw);
     if (nw) {
       lx[off] = x;
@@ -947,7 +986,7 @@ __device__ void commit_l(const DIndex& ix, const DState& st, CommitLds& sm, uint
         st.llog_x[lbase + k] = lx[k];
         st.llog_p[lbase + k] = lp[k];
         if (st.need_pred) st.rk_pr[lbase + k - st.l_base] = sm.r1[k];
-        if (st.need_succ) st.rk_sc[lbase + k - st.l_base] = sm.r2[k];
+        if (st.succ_at_commit) st.rk_sc[lbase + k - st.l_base] = sm.r2[k];
       }
       __syncthreads();
       if (threadIdx.x == 0) ln = 0;
@@ -1023,10 +1062,28 @@ __device__ void commit_p(const DIndex& ix, const DState& st, uint32_t bid, uint3
 // blocks Δlinks, ga blocks range activations, gp blocks leftover propagations.  The roles
 // read only state t-1 and append to disjoint candidate queues, so they run side by side.
 struct ExpandArgs {
-  uint32_t gs, gl, ga, gp;
-  uint32_t sb, se, lb, le, ab, ae, pb, pe;
+  uint32_t gs, gl, ga, gp, gx;
+  uint32_t sb, se, lb, le, ab, ae, pb, pe, xb, xe;
   uint32_t mask, a_end;
 };
+
+// Partitioned mode: new chain-second links of every rank = xlog[begin, end) meet this
+// rank's predecessors (CR6, r second; oracle/partition_model.py Rank.step).
+__device__ void expand_x(const DIndex& ix, const DState& st, BlockQ& q, uint32_t bid, uint32_t nb,
+                         uint32_t begin, uint32_t end) {
+  Ev ev;
+  for (uint32_t base = begin + bid * blockDim.x; base < end; base += nb * blockDim.x) {
+    const uint32_t i = base + threadIdx.x;
+    if (i < end) {
+      const uint32_t X = st.xlog_x[i], pid = st.xlog_p[i];
+      ev.v[EL_EV_TRIG]++;
+      r6_second(ix, st, q, X, ix.pair_role[pid], ix.pair_y[pid], ev);
+    }
+    q_maybe_flush(q, st);
+  }
+  q_flush(q, st);
+  ev_flush(st.ev, EL_K_EXPAND_L, ev);
+}
 __global__ void k_expand(DIndex ix, DState st, ExpandArgs a) {
   __shared__ BlockQ q;
   q_init(q);
@@ -1045,40 +1102,29 @@ __global__ void k_expand(DIndex ix, DState st, ExpandArgs a) {
     expand_a(ix, st, q, b, a.ga, a.ab, a.ae);
     return;
   }
-  expand_p(ix, st, q, b - a.ga, a.gp, a.pb, a.pe);
+  b -= a.ga;
+  if (b < a.gp) {
+    expand_p(ix, st, q, b, a.gp, a.pb, a.pe);
+    return;
+  }
+  expand_x(ix, st, q, b - a.gp, a.gx, a.xb, a.xe);
 }
 
-// Commit of one superstep in ONE launch (roles as in k_expand: S, links, activations,
-// propagations; each dedups into its own set).  The last block to finish publishes the
-// step's counters to pinned host memory and zeroes the candidate counters for the next
-// step, so the host learns everything with the step's single sync.
-// Blocks that finished are counted in 16 sharded words, then per shard in one word: a
-// single same-address counter hit by every block of a 2k-block launch would serialise.
 constexpr uint32_t DONE_SHARDS = 16;
-struct CommitArgs {
-  uint32_t gs, gl, ga, gp;
-  uint32_t cs_cap, cl_cap, ca_cap, cp_cap;
+struct PubArgs {
   HCounters* host;  // device view of the pinned host copy
   uint32_t* done;   // [(DONE_SHARDS + 1) * CTR_STRIDE], zero between launches
   uint32_t seq;     // written last to host->seq: the host spins on it
-  uint32_t publish; // 0: a partial launch (diagnostic split): no completion protocol
 };
-__global__ void k_commit(DIndex ix, DState st, CommitArgs a) {
-  __shared__ CommitLds sm;
+
+// Completion protocol shared by k_commit and k_ximport: the last block of the launch runs
+// last_fn (block-wide), copies every counter but seq to the pinned host mirror (unless
+// last_fn did), then writes seq.  Every thread of every block must call it.
+template <class LastFn>
+__device__ __forceinline__ void publish_last(const DState& st, const PubArgs& a, bool copy, LastFn last_fn) {
   __shared__ uint32_t last;
-  uint32_t b = blockIdx.x;
-  if (b < a.gs) {
-    commit_s(ix, st, sm, b, a.gs, min(st.ctr->cand_s, a.cs_cap));
-  } else if ((b -= a.gs) < a.gl) {
-    commit_l(ix, st, sm, b, a.gl, min(st.ctr->cand_l, a.cl_cap));
-  } else if ((b -= a.gl) < a.ga) {
-    commit_a(ix, st, b, a.ga, min(st.ctr->cand_a, a.ca_cap));
-  } else {
-    commit_p(ix, st, b - a.ga, a.gp, min(st.ctr->cand_p, a.cp_cap));
-  }
   // The barrier waits for this block's memory operations; every counter update is a
   // returning device-scope atomic, so it has been performed before the block reports done.
-  if (!a.publish) return;
   __syncthreads();
   if (threadIdx.x == 0) {
     const uint32_t sh = blockIdx.x % DONE_SHARDS;
@@ -1091,22 +1137,182 @@ __global__ void k_commit(DIndex ix, DState st, CommitArgs a) {
                                     __HIP_MEMORY_SCOPE_AGENT) == shards - 1;
   }
   __syncthreads();
-  if (last) {
-    constexpr uint32_t NW = NUM_CTRS - 1;  // every counter but seq
-    if (threadIdx.x < NW) {
-      uint32_t* dc = reinterpret_cast<uint32_t*>(st.ctr) + threadIdx.x * CTR_STRIDE;
-      const uint32_t v = __hip_atomic_load(dc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      reinterpret_cast<volatile uint32_t*>(a.host)[threadIdx.x] = v;
-      if (threadIdx.x >= 4) *dc = 0;  // cand_*, jobs for the next step
-    }
-    if (threadIdx.x <= DONE_SHARDS) a.done[threadIdx.x * CTR_STRIDE] = 0;
+  if (!last) return;
+  last_fn();
+  __syncthreads();
+  constexpr uint32_t NW = NUM_CTRS - 1;  // every counter but seq
+  if (copy && threadIdx.x < NW) {
+    uint32_t* dc = reinterpret_cast<uint32_t*>(st.ctr) + threadIdx.x * CTR_STRIDE;
+    reinterpret_cast<volatile uint32_t*>(a.host)[threadIdx.x] =
+        __hip_atomic_load(dc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  if (threadIdx.x <= DONE_SHARDS) a.done[threadIdx.x * CTR_STRIDE] = 0;
+  __threadfence_system();
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    reinterpret_cast<volatile uint32_t*>(a.host)[NW] = a.seq;  // counters are visible first
     __threadfence_system();
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      reinterpret_cast<volatile uint32_t*>(a.host)[NW] = a.seq;  // counters are visible first
-      __threadfence_system();
+  }
+}
+
+// Block-wide: copy every counter but seq to the host mirror, then zero those in zero_mask
+// (bit i = counter i).  Each thread owns one counter, so each is read before it is zeroed.
+__device__ __forceinline__ void copy_and_zero(const DState& st, HCounters* host, uint32_t zero_mask) {
+  constexpr uint32_t NW = NUM_CTRS - 1;
+  static_assert(NW <= 32, "zero mask width");
+  if (threadIdx.x < NW) {
+    uint32_t* dc = reinterpret_cast<uint32_t*>(st.ctr) + threadIdx.x * CTR_STRIDE;
+    reinterpret_cast<volatile uint32_t*>(host)[threadIdx.x] =
+        __hip_atomic_load(dc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if ((zero_mask >> threadIdx.x) & 1u) __hip_atomic_store(dc, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
+// Commit of one superstep in ONE launch (roles as in k_expand: S, links, activations,
+// propagations; each dedups into its own set).  The last block to finish publishes the
+// step's counters to pinned host memory and zeroes the per-step counters for the next
+// step, so the host learns everything with the step's single sync.
+// Blocks that finished are counted in 16 sharded words, then per shard in one word: a
+// single same-address counter hit by every block of a 2k-block launch would serialise.
+struct CommitArgs {
+  uint32_t gs, gl, ga, gp;
+  uint32_t cs_cap, cl_cap, ca_cap, cp_cap;
+  PubArgs pub;
+  uint32_t publish; // 0: a partial launch (diagnostic split): no completion protocol
+};
+__global__ void k_commit(DIndex ix, DState st, CommitArgs a) {
+  __shared__ CommitLds sm;
+  uint32_t b = blockIdx.x;
+  if (b < a.gs) {
+    commit_s(ix, st, sm, b, a.gs, min(st.ctr->cand_s, a.cs_cap));
+  } else if ((b -= a.gs) < a.gl) {
+    commit_l(ix, st, sm, b, a.gl, min(st.ctr->cand_l, a.cl_cap));
+  } else if ((b -= a.gl) < a.ga) {
+    commit_a(ix, st, b, a.ga, min(st.ctr->cand_a, a.ca_cap));
+  } else {
+    commit_p(ix, st, b - a.ga, a.gp, min(st.ctr->cand_p, a.cp_cap));
+  }
+  if (!a.publish) return;
+  publish_last(st, a.pub, false, [&] { copy_and_zero(st, a.pub.host, ~0u << CTR_KEEP); });
+}
+
+// ---- partitioned exchange (protocol: oracle/partition_model.py)
+// Each rank's slot of the all-gather: XH header words, then up to cap records (a, b):
+// its new propagations (pid, B), then new activations (Y, C), then new chain-second
+// links (X, pid).  Records past cap wait for a larger exchange (the host redoes it).
+constexpr uint32_t XH = 16;
+enum : uint32_t { XH_NP = 0, XH_NA = 1, XH_NX = 2, XH_DS = 3, XH_DL = 4, XH_OVF = 5 };
+struct XchgArgs {
+  uint32_t* send;        // this rank's slot: XH + 2 * cap words
+  const uint32_t* recv;  // nranks slots
+  uint32_t cap, nranks, me;
+  uint32_t s0, l0, a0, p0;  // log counts at the start of the attempt
+  uint32_t cs_cap, cl_cap, ca_cap, cp_cap, job_cap;  // a candidate queue past its cap = redo
+};
+// per-step counters the import zeroes once the exchange went through: x_send, cand_*, jobs
+constexpr uint32_t XCHG_ZERO = (1u << 5) | (1u << 6) | (1u << 7) | (1u << 8) | (1u << 9) | (1u << 10);
+static_assert(offsetof(DCounters, x_send) == 5 * CTR_STRIDE * 4 && offsetof(DCounters, cand_p) == 10 * CTR_STRIDE * 4,
+              "XCHG_ZERO bits");
+
+__global__ void k_xpack(DState st, XchgArgs x) {
+  const uint32_t np = st.ctr->p_log - x.p0, na = st.ctr->a_log - x.a0, nx = st.ctr->x_send;
+  const uint32_t tot = np + na + nx, n = min(tot, x.cap);
+  if (blockIdx.x == 0 && threadIdx.x < XH) {
+    uint32_t v = 0;
+    if (threadIdx.x == XH_NP) v = np;
+    if (threadIdx.x == XH_NA) v = na;
+    if (threadIdx.x == XH_NX) v = nx;
+    if (threadIdx.x == XH_DS) v = st.ctr->s_log - x.s0;
+    if (threadIdx.x == XH_DL) v = st.ctr->l_log - x.l0;
+    if (threadIdx.x == XH_OVF)
+      v = st.ctr->cand_s > x.cs_cap || st.ctr->cand_l > x.cl_cap || st.ctr->cand_a > x.ca_cap ||
+          st.ctr->cand_p > x.cp_cap || st.ctr->jobs > x.job_cap;
+    x.send[threadIdx.x] = v;
+  }
+  uint2* rec = reinterpret_cast<uint2*>(x.send + XH);
+  for (uint32_t g = blockIdx.x * blockDim.x + threadIdx.x; g < n; g += gridDim.x * blockDim.x) {
+    uint2 r;
+    if (g < np) r = make_uint2(st.plog_p[x.p0 + g], st.plog_b[x.p0 + g]);
+    else if (g < np + na) r = make_uint2(st.alog_y[x.a0 + g - np], st.alog_c[x.a0 + g - np]);
+    else r = make_uint2(st.xs_x[g - np - na], st.xs_p[g - np - na]);
+    rec[g] = r;
+  }
+}
+
+// Import every rank's records: other ranks' propagations and activations into the
+// replicated sets (dedup), every rank's chain links (own included) into the replicated
+// chain-link log with their successor-CSR ranks.  If any rank's records exceeded the cap
+// nothing is imported (g_max tells the host; it re-runs the exchange with a larger cap).
+// The last block publishes: g_delta = Σ over ranks of all deltas (0 = global fixpoint).
+__global__ void k_ximport(DIndex ix, DState st, XchgArgs x, PubArgs pub) {
+  const uint32_t stride = XH + 2 * x.cap;
+  uint32_t gmax = 0;
+  for (uint32_t q = 0; q < x.nranks; ++q) {
+    const uint32_t* h = x.recv + (size_t)q * stride;
+    gmax = max(gmax, h[XH_NP] + h[XH_NA] + h[XH_NX]);
+  }
+  const bool ok = gmax <= x.cap;
+  const uint32_t total = ok ? x.nranks * x.cap : 0u;
+  const uint32_t gs = gridDim.x * blockDim.x;
+  for (uint32_t base = blockIdx.x * blockDim.x; base < total; base += gs) {  // wave-uniform trip count
+    const uint32_t i = base + threadIdx.x;
+    uint32_t q = 0, j = 0, np = 0, na = 0, nx = 0;
+    uint2 r = make_uint2(0, 0);
+    if (i < total) {
+      q = i / x.cap;
+      j = i - q * x.cap;
+      const uint32_t* h = x.recv + (size_t)q * stride;
+      np = h[XH_NP], na = h[XH_NA], nx = h[XH_NX];
+      if (j < np + na + nx) r = reinterpret_cast<const uint2*>(h + XH)[j];
+    }
+    const bool live = i < total && j < np + na + nx;
+    const bool is_p = live && j < np && q != x.me;
+    const bool is_a = live && j >= np && j < np + na && q != x.me;
+    const bool is_x = live && j >= np + na;
+    // propagations (unique per owner of Y, so a remote one is new unless re-imported)
+    const bool nwp = is_p && hash_insert(st.phash, st.pmask, link_key(r.x, r.y));
+    const uint32_t ps = wave_append(&st.ctr->p_log, nwp);
+    const uint32_t prk = wave_keyed_atomic(st.dcnt, st.off_pp + r.x, nwp, false);
+    if (nwp) {
+      st.plog_p[ps] = r.x;
+      st.plog_b[ps] = r.y;
+      st.rk_pp[ps - st.p_base] = prk;
+    }
+    // activations (two ranks may have made the same one)
+    const bool nwa = is_a && hash_insert(st.ahash, st.amask, link_key(r.y, r.x));
+    const uint32_t as = wave_append(&st.ctr->a_log, nwa);
+    if (nwa) {
+      st.alog_y[as] = r.x;
+      st.alog_c[as] = r.y;
+      st.has_act[r.x] = 1;
+    }
+    // chain-second links: every rank's, successor CSR keyed by the link's source
+    const uint32_t xsl = wave_append(&st.ctr->x_log, is_x);
+    const uint32_t xrk = st.need_succ ? wave_keyed_atomic(st.dcnt, st.off_sc + r.x, is_x, false) : 0u;
+    if (is_x) {
+      st.xlog_x[xsl] = r.x;
+      st.xlog_p[xsl] = r.y;
+      st.rk_x[xsl - st.x_base] = xrk;
     }
   }
+  publish_last(st, pub, false, [&] {
+    if (threadIdx.x == 0) {
+      uint32_t gd = 0, go = 0;
+      for (uint32_t q = 0; q < x.nranks; ++q) {
+        const uint32_t* h = x.recv + (size_t)q * stride;
+        gd += h[XH_NP] + h[XH_NA] + h[XH_NX] + h[XH_DS] + h[XH_DL];
+        go += h[XH_OVF];
+      }
+      auto put = [](uint32_t* w, uint32_t v) { __hip_atomic_store(w, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); };
+      put(&st.ctr->g_delta, gd);
+      put(&st.ctr->g_max, gmax);
+      put(&st.ctr->g_ovf, go);
+    }
+    __syncthreads();
+    // sent: the send queue and the candidate counters start over (on an exchange overflow
+    // the redo packs the same records again)
+    copy_and_zero(st, pub.host, ok ? XCHG_ZERO : 0u);
+  });
 }
 
 // CSR merges of one superstep, all CSRs at once (segments: S, PR, SC, PP).  The delta
@@ -1410,6 +1616,127 @@ struct PendingEvent {
   hipEvent_t a, b;
 };
 
+// ---- delta exchange transports.  allgather is stream-ordered: it
+// reads `send` after the work already queued on s and later work on s sees `recv`.
+struct Exchange {
+  int rank = 0, size = 1;
+  virtual ~Exchange() {}
+  virtual void allgather(const void* send, void* recv, size_t bytes, hipStream_t s) = 0;
+};
+
+// RCCL over xGMI.  librccl is opened on first use, so a whole-ontology context (and the
+// CPU-side ABI checks) never need it; the header provides the types only.
+struct RcclApi {
+  decltype(&ncclGetUniqueId) get_id = nullptr;
+  decltype(&ncclCommInitRank) init_rank = nullptr;
+  decltype(&ncclAllGather) all_gather = nullptr;
+  decltype(&ncclCommDestroy) destroy = nullptr;
+  decltype(&ncclGetErrorString) err = nullptr;
+};
+const RcclApi& rccl_api() {
+  static RcclApi api;
+  static std::once_flag once;
+  static std::string why;
+  std::call_once(once, [] {
+    void* h = nullptr;
+    for (const char* n : {"librccl.so.1", "librccl.so", "/opt/rocm/lib/librccl.so.1"})
+      if ((h = dlopen(n, RTLD_NOW | RTLD_GLOBAL))) break;
+    if (!h) {
+      why = dlerror() ? dlerror() : "librccl not found";
+      return;
+    }
+    api.get_id = (decltype(api.get_id))dlsym(h, "ncclGetUniqueId");
+    api.init_rank = (decltype(api.init_rank))dlsym(h, "ncclCommInitRank");
+    api.all_gather = (decltype(api.all_gather))dlsym(h, "ncclAllGather");
+    api.destroy = (decltype(api.destroy))dlsym(h, "ncclCommDestroy");
+    api.err = (decltype(api.err))dlsym(h, "ncclGetErrorString");
+  });
+  if (!api.get_id || !api.init_rank || !api.all_gather || !api.destroy || !api.err)
+    throw ElError{EL_EHIP, "RCCL unavailable: " + why};
+  return api;
+}
+#define RCCLCHK(expr)                                                                              \
+  do {                                                                                             \
+    ncclResult_t r_ = (expr);                                                                      \
+    if (r_ != ncclSuccess) throw ElError{EL_EHIP, std::string(#expr) + ": " + rccl_api().err(r_)}; \
+  } while (0)
+
+struct RcclExchange : Exchange {
+  ncclComm_t comm = nullptr;
+  RcclExchange(int r, int n, const uint8_t id[128]) {
+    rank = r;
+    size = n;
+    ncclUniqueId uid;
+    static_assert(sizeof(uid) == 128, "ncclUniqueId");
+    memcpy(&uid, id, sizeof uid);
+    RCCLCHK(rccl_api().init_rank(&comm, n, uid, r));
+  }
+  ~RcclExchange() override {
+    if (comm) (void)rccl_api().destroy(comm);
+  }
+  void allgather(const void* send, void* recv, size_t bytes, hipStream_t s) override {
+    RCCLCHK(rccl_api().all_gather(send, recv, bytes, ncclUint8, comm, s));
+  }
+};
+
+}  // namespace
+
+// In-process group: n contexts driven by n host threads (tests, and one process driving
+// several GPUs).  Peers copy each other's send buffers device-to-device between barriers.
+struct el_group {
+  int n = 0;
+  std::mutex m;
+  std::condition_variable cv;
+  int arrived = 0;
+  uint64_t gen = 0;
+  bool broken = false;
+  std::vector<const void*> src;
+  void barrier() {
+    std::unique_lock<std::mutex> lk(m);
+    if (broken) throw ElError{EL_ESTATE, "exchange group broken by a failed rank"};
+    const uint64_t g = gen;
+    if (++arrived == n) {
+      arrived = 0;
+      ++gen;
+      cv.notify_all();
+      return;
+    }
+    if (!cv.wait_for(lk, std::chrono::seconds(120), [&] { return gen != g || broken; }) || broken) {
+      broken = true;
+      cv.notify_all();
+      throw ElError{EL_ESTATE, "exchange group barrier timed out or broken"};
+    }
+  }
+  void fail() {
+    std::lock_guard<std::mutex> lk(m);
+    broken = true;
+    cv.notify_all();
+  }
+};
+
+namespace {
+struct LocalExchange : Exchange {
+  el_group* g;
+  LocalExchange(el_group* grp, int r) : g(grp) {
+    rank = r;
+    size = grp->n;
+  }
+  void allgather(const void* send, void* recv, size_t bytes, hipStream_t s) override {
+    try {
+      HIPCHK(hipStreamSynchronize(s));  // send is complete
+      g->src[rank] = send;
+      g->barrier();
+      for (int q = 0; q < size; ++q)
+        HIPCHK(hipMemcpyAsync(static_cast<char*>(recv) + (size_t)q * bytes, g->src[q], bytes,
+                              hipMemcpyDeviceToDevice, s));
+      HIPCHK(hipStreamSynchronize(s));
+      g->barrier();  // nobody reuses its send buffer before every peer has copied it
+    } catch (...) {
+      g->fail();
+      throw;
+    }
+  }
+};
 }  // namespace
 
 struct el_ctx {
@@ -1475,7 +1802,7 @@ struct el_ctx {
   bool events_queued = false;
   uint64_t s_count = 0, l_count = 0, a_count = 0, p_count = 0, s_init = 0;
   uint64_t wm_s[EL_NUM_RULE_TYPES] = {}, wm_l[EL_NUM_RULE_TYPES] = {}, wm_a[EL_NUM_RULE_TYPES] = {},
-           wm_p[EL_NUM_RULE_TYPES] = {};
+           wm_p[EL_NUM_RULE_TYPES] = {}, wm_x = 0;
   el_stats last{};
   std::vector<uint64_t> tr_s, tr_l, tr_a;
   // host-side per-kernel accounting (merge kernels, launches, times)
@@ -1485,9 +1812,25 @@ struct el_ctx {
   std::vector<PendingEvent> pending;
   std::vector<hipEvent_t> event_pool;
 
+  // row partition + delta exchange
+  int xmode = EL_XCHG_NONE;
+  uint32_t part_rank = 0, part_count = 1, cfg_lo = 0, cfg_hi = 0;
+  uint32_t lo = 0, hi = 0;  // owned rows (whole ontology: [0, N))
+  std::unique_ptr<Exchange> xchg;
+  bool use_props = false;   // propagation set in use (CR4 axioms, or ⊥ in partitioned mode)
+  uint32_t *xlog_x = nullptr, *xlog_p = nullptr;  // replicated chain-second links
+  uint64_t xlog_cap = 0, x_count = 0;
+  uint32_t *xs_x = nullptr, *xs_p = nullptr;      // this step's local chain links to send (cl_cap)
+  uint32_t* rk_x = nullptr;                       // import ranks in the successor rows (xcap * ranks)
+  uint32_t* xsend = nullptr;                      // exchange slot: XH + 2 * xcap words
+  uint32_t* xrecv = nullptr;                      // part_count slots
+  uint64_t xcap = 0;                              // records per rank per exchange (grows on overflow)
+  bool part() const { return xmode != EL_XCHG_NONE; }
+
   DState dstate() const {
     DState s{};
-    s.bits = bits;
+    // virtual row base: row x of the owned range [lo, hi) is bits + (x - lo) * W
+    s.bits = reinterpret_cast<uint32_t*>(reinterpret_cast<uintptr_t>(bits) - (uintptr_t)lo * W * sizeof(uint32_t));
     s.slog_x = slog_x;
     s.slog_a = slog_a;
     s.lhash = lhash;
@@ -1521,6 +1864,13 @@ struct el_ctx {
     s.off_pp = (uint32_t)(PP.dcnt - dcnt_all);
     s.need_pred = need_pred ? 1u : 0u;
     s.need_succ = need_succ ? 1u : 0u;
+    s.succ_at_commit = (need_succ && !part()) ? 1u : 0u;
+    s.xlog_x = xlog_x;
+    s.xlog_p = xlog_p;
+    s.xs_x = xs_x;
+    s.xs_p = xs_p;
+    s.rk_x = rk_x;
+    s.x_base = (uint32_t)x_count;
     s.rk_pr = rk_pr;
     s.rk_sc = rk_sc;
     s.rk_pp = rk_pp;
@@ -1643,6 +1993,12 @@ struct el_ctx {
   void rehash_props(uint64_t cap);
   bool superstep(uint32_t mask, uint64_t sb, uint64_t se, uint64_t lb, uint64_t le, uint64_t ab,
                  uint64_t ae, uint64_t pb, uint64_t pe);
+  // partitioned mode: one superstep + the delta exchange; returns Σ over ranks of the deltas
+  uint64_t superstep_part(uint32_t mask, uint64_t sb, uint64_t se, uint64_t lb, uint64_t le, uint64_t ab,
+                          uint64_t ae, uint64_t pb, uint64_t pe, uint64_t xb, uint64_t xe);
+  void grow_part(uint64_t new_xcap);
+  uint32_t exchange_round(uint32_t s0, uint32_t l0, uint32_t a0, uint32_t p0, std::vector<MergeReq>& reqs);
+  uint64_t remote_bound() const { return part() ? (uint64_t)(part_count - 1) * xcap : 0u; }
   void fill_stats(el_stats* st, double ms);
 };
 
@@ -1693,12 +2049,19 @@ void el_ctx::free_state() {
   dfree(ev);
   dfree(scan_flags);
   dfree(commit_done);
+  dfree(xlog_x);
+  dfree(xlog_p);
+  dfree(xs_x);
+  dfree(xs_p);
+  dfree(rk_x);
+  dfree(xsend);
+  dfree(xrecv);
 }
 
 void el_ctx::alloc_state() {
   const uint64_t N = hx.N, P = hx.P;
   W = (N + 31) / 32;
-  bits = dalloc<uint32_t>(N * W);
+  bits = dalloc<uint32_t>((uint64_t)(hi - lo) * W);  // owned rows only
   slog_cap = std::max<uint64_t>(1u << 20, 8 * N);
   slog_x = dalloc<uint32_t>(slog_cap);
   slog_a = dalloc<uint32_t>(slog_cap);
@@ -1721,7 +2084,7 @@ void el_ctx::alloc_state() {
   cp_cap = plog_cap;
   cp_p = dalloc<uint32_t>(cp_cap);
   cp_b = dalloc<uint32_t>(cp_cap);
-  rk_pp = dalloc<uint32_t>(cp_cap);
+  rk_pp = dalloc<uint32_t>(cp_cap);  // partitioned: re-sized with the exchange (grow_part)
   dcnt_total = 2 * (N + 1) + 2 * (P + 1);
   dcnt_all = dalloc<uint32_t>(dcnt_total);
   dscan_all = dalloc<uint32_t>(dcnt_total);
@@ -1761,12 +2124,25 @@ void el_ctx::alloc_state() {
   commit_done = dalloc<uint32_t>((DONE_SHARDS + 1) * CTR_STRIDE);
   HIPCHK(hipMemset(scan_flags, 0, scan_tiles * sizeof(unsigned long long)));
   scan_epoch = 0;
+  if (part()) {
+    // records per rank per all-gather; grows on demand (EL_XCHG_CAP: a smaller start, tests)
+    xcap = 1u << 12;
+    if (const char* e = getenv("EL_XCHG_CAP")) xcap = std::max<uint64_t>(1, strtoull(e, nullptr, 10));
+    xlog_cap = std::max<uint64_t>(1u << 16, (uint64_t)part_count * xcap);
+    xlog_x = dalloc<uint32_t>(xlog_cap);
+    xlog_p = dalloc<uint32_t>(xlog_cap);
+    xs_x = dalloc<uint32_t>(cl_cap);
+    xs_p = dalloc<uint32_t>(cl_cap);
+    rk_x = dalloc<uint32_t>((uint64_t)part_count * xcap);
+    xsend = dalloc<uint32_t>(XH + 2 * xcap);
+    xrecv = dalloc<uint32_t>((uint64_t)part_count * (XH + 2 * xcap));
+  }
 }
 
 void el_ctx::reset_state() {
   FillArgs f{};
   auto add = [&](void* p, uint64_t bytes, uint32_t pattern) { f.seg[f.n++] = FillSeg{p, bytes, pattern}; };
-  add(bits, hx.N * W * sizeof(uint32_t), 0u);
+  add(bits, (uint64_t)(hi - lo) * W * sizeof(uint32_t), 0u);
   add(lhash, lhash_cap * sizeof(unsigned long long), ~0u);
   add(ahash, ahash_cap * sizeof(unsigned long long), ~0u);
   add(has_act, hx.N, 0u);
@@ -1778,8 +2154,9 @@ void el_ctx::reset_state() {
   add(ev, EV_WORDS * sizeof(unsigned long long), 0u);
   hipLaunchKernelGGL(k_fill, dim3(1024), dim3(BLOCK), 0, stream, f);
   HIPCHK(hipGetLastError());
-  s_count = l_count = a_count = p_count = s_init = s_csr_count = 0;
+  s_count = l_count = a_count = p_count = s_init = s_csr_count = x_count = 0;
   for (int r = 0; r < EL_NUM_RULE_TYPES; ++r) wm_s[r] = wm_l[r] = wm_a[r] = wm_p[r] = 0;
+  wm_x = 0;
   memset(launches, 0, sizeof launches);
   memset(host_ev, 0, sizeof host_ev);
   memset(kms, 0, sizeof kms);
@@ -1987,9 +2364,7 @@ bool el_ctx::superstep(uint32_t mask, uint64_t sb, uint64_t se, uint64_t lb, uin
     ca.gp = hx.exl.a.size() ? grid_for(cp_cap, 256) : 0u;
     ca.cs_cap = (uint32_t)cs_cap, ca.cl_cap = (uint32_t)cl_cap;
     ca.ca_cap = (uint32_t)ca_cap, ca.cp_cap = (uint32_t)cp_cap;
-    ca.host = hc_dev;
-    ca.done = commit_done;
-    ca.seq = ++commit_seq;
+    ca.pub = PubArgs{hc_dev, commit_done, ++commit_seq};
     ca.publish = 1;
     if (split_commit) {  // diagnostic: S role alone, then the other roles (rocprof sees both)
       CommitArgs c1 = ca;
@@ -2007,7 +2382,7 @@ bool el_ctx::superstep(uint32_t mask, uint64_t sb, uint64_t se, uint64_t lb, uin
     if (need_succ) reqs.push_back({&SC, llog_x, llog_p, l_count, l_count, &ctr->l_log, rk_sc});
     if (hx.exl.a.size()) reqs.push_back({&PP, plog_p, plog_b, p_count, p_count, &ctr->p_log, rk_pp});
     launch_merges(reqs);
-    wait_commit(ca.seq);
+    wait_commit(ca.pub.seq);
     std::vector<uint64_t> ends;
     for (const MergeReq& r : reqs) ends.push_back(r.end_ptr == &ctr->l_log ? hc.l_log : hc.p_log);
     finish_merges(reqs, ends, true);
@@ -2041,7 +2416,7 @@ bool el_ctx::superstep(uint32_t mask, uint64_t sb, uint64_t se, uint64_t lb, uin
     if (cl_cap != cl_old) regrow2_to(cl_cap, rk_pr, rk_sc);
     if (cp_cap != cp_old) {
       dfree(rk_pp);
-      rk_pp = dalloc<uint32_t>(cp_cap);
+      rk_pp = dalloc<uint32_t>(cp_cap + remote_bound());
     }
     if (2ull * hc.jobs > job_cap) {
       sync();
@@ -2053,6 +2428,188 @@ bool el_ctx::superstep(uint32_t mask, uint64_t sb, uint64_t se, uint64_t lb, uin
     if (!overflow) break;
   }
   return s_count > s0 || l_count > l0 || a_count > a0 || p_count > p0;
+}
+
+// Exchange capacity: records per rank per all-gather (xcap) and every structure the import
+// appends to (replicated propagations / activations / chain links and their CSRs).
+void el_ctx::grow_part(uint64_t new_xcap) {
+  sync();
+  if (new_xcap > xcap) {
+    xcap = new_xcap;
+    dfree(xsend);
+    dfree(xrecv);
+    dfree(rk_x);
+    xsend = dalloc<uint32_t>(XH + 2 * xcap);
+    xrecv = dalloc<uint32_t>((uint64_t)part_count * (XH + 2 * xcap));
+    rk_x = dalloc<uint32_t>((uint64_t)part_count * xcap);
+    dfree(rk_pp);
+    rk_pp = dalloc<uint32_t>(cp_cap + remote_bound());
+  }
+  const uint64_t rb = remote_bound(), xb = (uint64_t)part_count * xcap;
+  auto grow_log = [&](uint64_t used, uint64_t need, uint64_t& cap, uint32_t*& a, uint32_t*& b) {
+    if (need <= cap) return;
+    const uint64_t c = next_pow2(need + need / 2);
+    dgrow(a, used, c);
+    dgrow(b, used, c);
+    cap = c;
+  };
+  grow_log(p_count, p_count + cp_cap + rb, plog_cap, plog_p, plog_b);
+  if (plog_cap > PP.cap) PP.grow(p_count, plog_cap);
+  if (2 * (p_count + cp_cap + rb) > phash_cap) rehash_props(next_pow2(4 * (p_count + cp_cap + rb)));
+  grow_log(a_count, a_count + ca_cap + rb, alog_cap, alog_y, alog_c);
+  if (2 * (a_count + ca_cap + rb) > ahash_cap) rehash_acts(next_pow2(4 * (a_count + ca_cap + rb)));
+  grow_log(x_count, x_count + xb, xlog_cap, xlog_x, xlog_p);
+  if (xlog_cap > SC.cap) SC.grow(x_count, xlog_cap);
+}
+
+// Pack this rank's new records, all-gather every rank's, import them, merge the CSRs.
+// Returns after the import published; hc then holds the global g_* words.
+uint32_t el_ctx::exchange_round(uint32_t s0, uint32_t l0, uint32_t a0, uint32_t p0, std::vector<MergeReq>& reqs) {
+  DState st = dstate();
+  XchgArgs xa{};
+  xa.send = xsend;
+  xa.recv = xrecv;
+  xa.cap = (uint32_t)xcap;
+  xa.nranks = part_count;
+  xa.me = part_rank;
+  xa.s0 = s0, xa.l0 = l0, xa.a0 = a0, xa.p0 = p0;
+  xa.cs_cap = (uint32_t)cs_cap, xa.cl_cap = (uint32_t)cl_cap, xa.ca_cap = (uint32_t)ca_cap;
+  xa.cp_cap = (uint32_t)cp_cap, xa.job_cap = (uint32_t)job_cap;
+  hipLaunchKernelGGL(k_xpack, dim3(grid_for(xcap, 64)), dim3(BLOCK), 0, stream, st, xa);
+  HIPCHK(hipGetLastError());
+  xchg->allgather(xsend, xrecv, (XH + 2 * xcap) * sizeof(uint32_t), stream);
+  const uint32_t seq = ++commit_seq;
+  hipLaunchKernelGGL(k_ximport, dim3(grid_for((uint64_t)part_count * xcap, 256)), dim3(BLOCK), 0, stream, ix, st,
+                     xa, PubArgs{hc_dev, commit_done, seq});
+  HIPCHK(hipGetLastError());
+  reqs.clear();
+  if (hx.P && need_pred) reqs.push_back({&PR, llog_p, llog_x, l_count, l_count, &ctr->l_log, rk_pr});
+  if (need_succ) reqs.push_back({&SC, xlog_x, xlog_p, x_count, x_count, &ctr->x_log, rk_x});
+  if (use_props) reqs.push_back({&PP, plog_p, plog_b, p_count, p_count, &ctr->p_log, rk_pp});
+  launch_merges(reqs);
+  wait_commit(seq);
+  std::vector<uint64_t> ends;
+  for (const MergeReq& r : reqs)
+    ends.push_back(r.end_ptr == &ctr->l_log ? hc.l_log : r.end_ptr == &ctr->x_log ? hc.x_log : hc.p_log);
+  finish_merges(reqs, ends, true);
+  s_count = hc.s_log;
+  l_count = hc.l_log;
+  a_count = hc.a_log;
+  p_count = hc.p_log;
+  x_count = hc.x_log;
+  return hc.g_max;
+}
+
+// One Jacobi superstep of a row partition (protocol: oracle/partition_model.py).  Every
+// rank runs it in lock-step, including ranks without local triggers: the exchange is
+// collective.  Redo decisions (exchange cap, candidate overflow) use all-gathered words,
+// so every rank takes the same branch.
+uint64_t el_ctx::superstep_part(uint32_t mask, uint64_t sb, uint64_t se, uint64_t lb, uint64_t le, uint64_t ab,
+                                uint64_t ae, uint64_t pb, uint64_t pe, uint64_t xb, uint64_t xe) {
+  uint64_t gdelta = 0;
+  std::vector<MergeReq> reqs;
+  for (int attempt = 0;; ++attempt) {
+    // ---- capacities for the local candidates (as in superstep) and the remote imports
+    const uint64_t rb = remote_bound();
+    const bool grow = s_count + cs_cap > slog_cap || slog_cap > S.cap || l_count + cl_cap > llog_cap ||
+                      llog_cap > PR.cap || 2 * (l_count + cl_cap) > lhash_cap ||
+                      a_count + ca_cap + rb > alog_cap || 2 * (a_count + ca_cap + rb) > ahash_cap ||
+                      p_count + cp_cap + rb > plog_cap || plog_cap > PP.cap ||
+                      2 * (p_count + cp_cap + rb) > phash_cap || x_count + part_count * xcap > xlog_cap ||
+                      xlog_cap > SC.cap;
+    if (grow) {
+      sync();
+      auto grow_log = [&](uint64_t used, uint64_t add, uint64_t& cap, uint32_t*& a, uint32_t*& b) {
+        if (used + add <= cap) return;
+        uint64_t c = next_pow2(used + add + (used + add) / 2);
+        dgrow(a, used, c);
+        dgrow(b, used, c);
+        cap = c;
+      };
+      grow_log(s_count, cs_cap, slog_cap, slog_x, slog_a);
+      if (slog_cap > S.cap) S.grow(s_csr_count, slog_cap);
+      grow_log(l_count, cl_cap, llog_cap, llog_x, llog_p);
+      if (llog_cap > PR.cap) PR.grow(l_count, llog_cap);
+      if (2 * (l_count + cl_cap) > lhash_cap) rehash_links(next_pow2(4 * (l_count + cl_cap)));
+      grow_part(xcap);
+    }
+    const uint32_t s0 = (uint32_t)s_count, l0 = (uint32_t)l_count, a0 = (uint32_t)a_count, p0 = (uint32_t)p_count;
+
+    // ---- generation + local commit (no publish: the import publishes for the step)
+    DState st = dstate();
+    ExpandArgs ea{};
+    const bool do_a = (mask & M_RRNG) && ae > ab;
+    const bool do_p = (mask & M_R4P) && pe > pb;
+    ea.gs = se > sb ? grid_for(se - sb) : 0u;
+    ea.gl = le > lb ? grid_for(le - lb) : 0u;
+    ea.ga = do_a ? grid_for(hi - lo) : 0u;
+    ea.gp = do_p ? grid_for(pe - pb) : 0u;
+    ea.gx = ((mask & M_R6) && xe > xb) ? grid_for(xe - xb) : 0u;
+    ea.sb = (uint32_t)sb, ea.se = (uint32_t)se, ea.lb = (uint32_t)lb, ea.le = (uint32_t)le;
+    ea.ab = (uint32_t)ab, ea.ae = (uint32_t)ae, ea.pb = (uint32_t)pb, ea.pe = (uint32_t)pe;
+    ea.xb = (uint32_t)xb, ea.xe = (uint32_t)xe;
+    ea.mask = mask;
+    ea.a_end = (uint32_t)ab;  // activations known at t-1 (the exchange appended this step's)
+    const uint32_t eg = ea.gs + ea.gl + ea.ga + ea.gp + ea.gx;
+    if (eg) {
+      launch(EL_K_EXPAND_S, [&] { hipLaunchKernelGGL(k_expand, dim3(eg), dim3(BLOCK), 0, stream, ix, st, ea); });
+      launch(EL_K_JOBS, [&] { hipLaunchKernelGGL(k_jobs, dim3(1024), dim3(BLOCK), 0, stream, ix, st); });
+    }
+    CommitArgs ca{};
+    ca.gs = grid_for(cs_cap);
+    ca.gl = grid_for(cl_cap);
+    ca.ga = hx.rng.a.size() ? grid_for(ca_cap, 64) : 0u;
+    ca.gp = use_props ? grid_for(cp_cap, 256) : 0u;
+    ca.cs_cap = (uint32_t)cs_cap, ca.cl_cap = (uint32_t)cl_cap;
+    ca.ca_cap = (uint32_t)ca_cap, ca.cp_cap = (uint32_t)cp_cap;
+    ca.publish = 0;
+    launch(EL_K_COMMIT_S, [&] {
+      hipLaunchKernelGGL(k_commit, dim3(ca.gs + ca.gl + ca.ga + ca.gp), dim3(BLOCK), 0, stream, ix, st, ca);
+    });
+
+    // ---- delta exchange; a too-small exchange imports nothing and is redone larger
+    uint32_t gmax = exchange_round(s0, l0, a0, p0, reqs);
+    if (gmax > xcap) {
+      grow_part(next_pow2(gmax));
+      gmax = exchange_round(s0, l0, a0, p0, reqs);
+      if (gmax > xcap) throw std::runtime_error("exchange overflow after growth");
+    }
+    gdelta += hc.g_delta;
+
+    // ---- candidate queues: grow ahead of demand; a global overflow re-runs generation
+    auto regrow2 = [&](uint32_t need, uint64_t& cap, uint32_t*& a, uint32_t*& b) {
+      if (2ull * need <= cap) return false;
+      sync();
+      cap = next_pow2(2ull * need + 1024);
+      dfree(a);
+      dfree(b);
+      a = dalloc<uint32_t>(cap);
+      b = dalloc<uint32_t>(cap);
+      return true;
+    };
+    regrow2(hc.cand_s, cs_cap, cs_x, cs_a);
+    if (regrow2(hc.cand_l, cl_cap, cl_x, cl_p)) {
+      dfree(rk_pr);
+      dfree(xs_x);
+      dfree(xs_p);
+      rk_pr = dalloc<uint32_t>(cl_cap);
+      xs_x = dalloc<uint32_t>(cl_cap);
+      xs_p = dalloc<uint32_t>(cl_cap);
+    }
+    regrow2(hc.cand_a, ca_cap, ca_y, ca_c);
+    if (regrow2(hc.cand_p, cp_cap, cp_p, cp_b)) {
+      dfree(rk_pp);
+      rk_pp = dalloc<uint32_t>(cp_cap + remote_bound());
+    }
+    if (2ull * hc.jobs > job_cap) {
+      sync();
+      job_cap = next_pow2(2ull * hc.jobs + 1024);
+      dfree(jobs);
+      jobs = dalloc<uint4>(job_cap);
+    }
+    if (hc.g_ovf == 0) break;
+  }
+  return gdelta;
 }
 
 void el_ctx::fill_stats(el_stats* out, double ms) {
@@ -2129,6 +2686,20 @@ int el_create(el_ctx** out, const el_config* cfg) {
     }
     c->device = cfg->device;
     c->profile = cfg->profile;
+    c->xmode = cfg->exchange;
+    if (c->xmode != EL_XCHG_NONE) {
+      const bool bad = (c->xmode != EL_XCHG_LOCAL && c->xmode != EL_XCHG_RCCL) || cfg->part_count < 1 ||
+                       cfg->part_rank >= cfg->part_count || cfg->row_hi < cfg->row_lo ||
+                       (c->xmode == EL_XCHG_LOCAL && (!cfg->group || cfg->group->n != (int)cfg->part_count));
+      if (bad) {
+        delete c;
+        return EL_EINVAL;
+      }
+      c->part_rank = cfg->part_rank;
+      c->part_count = cfg->part_count;
+      c->cfg_lo = cfg->row_lo;
+      c->cfg_hi = cfg->row_hi;
+    }
   }
   int n = 0;
   if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) {
@@ -2141,14 +2712,42 @@ int el_create(el_ctx** out, const el_config* cfg) {
   }
   int rc = guarded(c, [&] {
     HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+    if (c->xmode == EL_XCHG_LOCAL) c->xchg.reset(new LocalExchange(cfg->group, (int)c->part_rank));
+    if (c->xmode == EL_XCHG_RCCL)  // collective: every rank of the group calls el_create
+      c->xchg.reset(new RcclExchange((int)c->part_rank, (int)c->part_count, cfg->rccl_id));
     return EL_OK;
   });
   if (rc != EL_OK) {
+    if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
     return rc;
   }
   *out = c;
   return EL_OK;
+}
+
+int el_group_create(el_group** g, int n) {
+  if (!g || n < 1) return EL_EINVAL;
+  el_group* p = new (std::nothrow) el_group();
+  if (!p) return EL_ENOMEM;
+  p->n = n;
+  p->src.assign(n, nullptr);
+  *g = p;
+  return EL_OK;
+}
+
+void el_group_destroy(el_group* g) { delete g; }
+
+int el_rccl_unique_id(uint8_t out[128]) {
+  if (!out) return EL_EINVAL;
+  try {
+    ncclUniqueId id;
+    RCCLCHK(rccl_api().get_id(&id));
+    memcpy(out, &id, 128);
+    return EL_OK;
+  } catch (...) {
+    return EL_EHIP;
+  }
 }
 
 int el_load(el_ctx* c, const el_axioms* ax) {
@@ -2229,7 +2828,29 @@ int el_load(el_ctx* c, const el_axioms* ax) {
             has0(ax->exl_b, ax->n_ex_lhs) || has0(ax->dom_c, ax->n_domain) || has0(ax->rng_c, ax->n_range);
       c->need_succ = !h.chf.a.empty();
       c->need_pred = !h.exl.a.empty() || c->need_succ || bot;
+      c->use_props = !h.exl.a.empty() || (c->part() && bot);
     }
+    // owned rows: the configured range, or the equal split of [0, N)
+    if (c->part()) {
+      if (c->cfg_lo == 0 && c->cfg_hi == 0) {
+        c->lo = (uint32_t)((uint64_t)h.N * c->part_rank / c->part_count);
+        c->hi = (uint32_t)((uint64_t)h.N * (c->part_rank + 1) / c->part_count);
+      } else {
+        if (c->cfg_hi > h.N) return fail(c, EL_EINVAL, "partition rows beyond n_concepts");
+        c->lo = c->cfg_lo;
+        c->hi = c->cfg_hi;
+      }
+      std::vector<uint8_t> chs(h.R + 1, 0);
+      for (uint32_t r = 0; r < h.R; ++r) chs[r] = h.chs.ptr[r + 1] > h.chs.ptr[r];
+      d.role_chs = up8(chs);
+    } else {
+      c->lo = 0;
+      c->hi = h.N;
+      d.role_chs = nullptr;
+    }
+    d.lo = c->lo;
+    d.hi = c->hi;
+    d.part = c->part() ? 1u : 0u;
     c->alloc_state();
     c->loaded = true;
     c->inited = false;
@@ -2244,12 +2865,13 @@ int el_init(el_ctx* c) {
     c->reset_state();
     DState st = c->dstate();
     c->launch(EL_K_INIT, [&] {
-      hipLaunchKernelGGL(k_init, dim3(grid_for(c->hx.N)), dim3(BLOCK), 0, c->stream, c->ix, st);
+      hipLaunchKernelGGL(k_init, dim3(grid_for(c->hi - c->lo)), dim3(BLOCK), 0, c->stream, c->ix, st);
     });
-    // k_init appends X for every concept and ⊤ for classes and individuals other than ⊤/⊥:
-    // the count is known on the host, so the first superstep is enqueued without a sync
-    uint64_t n = c->hx.N;
-    for (uint32_t x = 0; x < c->hx.N; ++x)
+    // k_init appends X for every owned concept and ⊤ for classes and individuals other
+    // than ⊤/⊥: the count is known on the host, so the first superstep is enqueued
+    // without a sync
+    uint64_t n = c->hi - c->lo;
+    for (uint32_t x = c->lo; x < c->hi; ++x)
       n += x != EL_TOP && x != EL_BOTTOM && c->hx.kind[x] != EL_KIND_DATATYPE;
     c->s_count = n;
     c->s_init = n;
@@ -2263,6 +2885,7 @@ int el_init(el_ctx* c) {
 int el_step(el_ctx* c, el_rule rule, int* changed) {
   if (!c || !changed || (int)rule < 0 || (int)rule >= EL_NUM_RULE_TYPES) return EL_EINVAL;
   if (!c->inited) return fail(c, EL_ESTATE, "el_step before el_init");
+  if (c->part()) return fail(c, EL_ESTATE, "el_step needs a whole-ontology context (use el_saturate)");
   return guarded(c, [&] {
     const int r = (int)rule;
     const uint64_t se = c->s_count, le = c->l_count, ae = c->a_count, pe = c->p_count;
@@ -2296,7 +2919,24 @@ int el_saturate(el_ctx* c, el_stats* stats) {
     c->tr_s.clear();
     c->tr_l.clear();
     c->tr_a.clear();
+    if (c->part()) {  // collective: every rank runs the same supersteps (global delta)
+      constexpr uint32_t mask = (M_ALL & ~M_R4D) | M_R4P;
+      uint64_t xb = 0;
+      for (int r = 0; r < EL_NUM_RULE_TYPES; ++r) pb = std::min(pb, c->wm_p[r]);
+      xb = std::min<uint64_t>(c->x_count, c->wm_x);
+      for (;;) {
+        const uint64_t se = c->s_count, le = c->l_count, ae = c->a_count, pe2 = c->p_count, xe = c->x_count;
+        c->tr_s.push_back(se - sb);
+        c->tr_l.push_back(le - lb);
+        c->tr_a.push_back(ae - ab);
+        const uint64_t g = c->superstep_part(mask, sb, se, lb, le, ab, ae, pb, pe2, xb, xe);
+        sb = se, lb = le, ab = ae, pb = pe2, xb = xe;
+        if (g == 0) break;
+      }
+      c->wm_x = c->x_count;
+    }
     for (;;) {
+      if (c->part()) break;
       const uint64_t se = c->s_count, le = c->l_count, ae = c->a_count;
       if (se == sb && le == lb && ae == ab && pb == pe) break;
       c->tr_s.push_back(se - sb);
@@ -2373,6 +3013,7 @@ int el_get_subsumers(el_ctx* c, uint32_t x, uint32_t* out, size_t cap, size_t* n
   if (!c || !n) return EL_EINVAL;
   if (!c->inited) return fail(c, EL_ESTATE, "no state");
   if (x >= c->hx.N) return fail(c, EL_EINVAL, "concept id out of range");
+  if (x < c->lo || x >= c->hi) return fail(c, EL_EINVAL, "row not owned by this partition");
   return guarded(c, [&] {
     c->sync();
     c->ensure_s_csr();

@@ -28,7 +28,8 @@ KERNEL_NAMES = ["k_expand:s", "k_expand:l", "k_jobs", "k_expand:a", "k_commit:s"
 EVENT_NAMES = ["trig", "row", "ent", "test", "hash", "emit", "job", "rmw"]
 EVENT_BYTES = [8, 8, 4, 4, 8, 8, 16, 8]
 NUM_KERNELS = len(KERNEL_NAMES)
-ABI_VERSION = 2  # include/el_gpu.h EL_ABI_VERSION
+ABI_VERSION = 3  # include/el_gpu.h EL_ABI_VERSION
+XCHG_NONE, XCHG_LOCAL, XCHG_RCCL = 0, 1, 2
 NUM_EVENTS = len(EVENT_NAMES)
 
 
@@ -69,7 +70,9 @@ class _ElAxioms(C.Structure):
 
 
 class _ElConfig(C.Structure):
-    _fields_ = [("device", C.c_int), ("profile", C.c_int), ("flags", C.c_uint32)]
+    _fields_ = [("device", C.c_int), ("profile", C.c_int), ("flags", C.c_uint32), ("exchange", C.c_int),
+                ("part_rank", C.c_uint32), ("part_count", C.c_uint32), ("row_lo", C.c_uint32),
+                ("row_hi", C.c_uint32), ("group", C.c_void_p), ("rccl_id", C.c_uint8 * 128)]
 
 
 class _ElStats(C.Structure):
@@ -88,7 +91,8 @@ _SINK = C.CFUNCTYPE(C.c_int, C.c_void_p, _u32p, _u32p, C.c_size_t)
 EXPORTED_SYMBOLS = [
     "el_abi_version", "el_device_count", "el_create", "el_load", "el_init", "el_step", "el_saturate",
     "el_get_stats", "el_kernel_stats", "el_superstep_trace", "el_get_subsumers", "el_copy_facts",
-    "el_copy_links", "el_export_result", "el_last_error", "el_destroy",
+    "el_copy_links", "el_export_result", "el_last_error", "el_destroy", "el_group_create", "el_group_destroy",
+    "el_rccl_unique_id",
 ]
 
 _lib: Optional[C.CDLL] = None
@@ -125,6 +129,10 @@ def load_library(path: Optional[str] = None) -> C.CDLL:
     lib.el_last_error.restype = C.c_char_p
     lib.el_destroy.argtypes = [P]
     lib.el_destroy.restype = None
+    lib.el_group_create.argtypes = [C.POINTER(P), C.c_int]
+    lib.el_group_destroy.argtypes = [P]
+    lib.el_group_destroy.restype = None
+    lib.el_rccl_unique_id.argtypes = [C.POINTER(C.c_uint8 * 128)]
     if path is None:
         _lib = lib
     return lib
@@ -178,16 +186,62 @@ class Stats(dict):
                      activations=s.activations, propagations=s.propagations, bytes=s.bytes, ms=s.ms)
 
 
+class Partition:
+    """Row partition of one engine: this rank owns S(X) for X in
+    [row_lo, row_hi) (0, 0 = the equal split) and all-gathers its deltas each superstep."""
+
+    def __init__(self, rank: int, count: int, exchange: int, group: "Optional[LocalGroup]" = None,
+                 rccl_id: Optional[bytes] = None, rows: Tuple[int, int] = (0, 0)):
+        self.rank, self.count, self.exchange, self.group, self.rccl_id, self.rows = (
+            rank, count, exchange, group, rccl_id, rows)
+
+
+class LocalGroup:
+    """In-process exchange group (EL_XCHG_LOCAL): n engines driven by n threads."""
+
+    def __init__(self, n: int):
+        self._lib = load_library()
+        self.ptr = C.c_void_p()
+        rc = self._lib.el_group_create(C.byref(self.ptr), int(n))
+        if rc != EL_OK:
+            raise ElError(rc, "el_group_create failed")
+        self.n = n
+
+    def close(self) -> None:
+        if self.ptr:
+            self._lib.el_group_destroy(self.ptr)
+            self.ptr = C.c_void_p()
+
+
+def rccl_unique_id() -> bytes:
+    """ncclUniqueId for EL_XCHG_RCCL (rank 0 makes it; the launcher broadcasts it)."""
+    lib = load_library()
+    buf = (C.c_uint8 * 128)()
+    rc = lib.el_rccl_unique_id(C.byref(buf))
+    if rc != EL_OK:
+        raise ElError(rc, "el_rccl_unique_id failed (RCCL unavailable)")
+    return bytes(buf)
+
+
 class Engine:
     """One GPU saturation context (one DistEL rule cluster), on one device."""
 
-    def __init__(self, device: int = 0, profile: bool = False):
+    def __init__(self, device: int = 0, profile: bool = False, partition: Optional[Partition] = None):
         self._lib = load_library()
         self._ctx = C.c_void_p()
         cfg = _ElConfig(device, 1 if profile else 0, 0)
+        if partition is not None:
+            cfg.exchange = partition.exchange
+            cfg.part_rank, cfg.part_count = partition.rank, partition.count
+            cfg.row_lo, cfg.row_hi = partition.rows
+            if partition.group is not None:
+                cfg.group = partition.group.ptr
+            if partition.rccl_id is not None:
+                C.memmove(cfg.rccl_id, partition.rccl_id, 128)
         rc = self._lib.el_create(C.byref(self._ctx), C.byref(cfg))
         if rc != EL_OK:
-            raise ElError(rc, f"el_create(device={device}) failed: no usable HIP device")
+            raise ElError(rc, f"el_create(device={device}) failed: no usable HIP device or bad partition")
+        self.partition = partition
         self.ax: Optional[Axioms] = None
 
     def _check(self, rc: int, what: str) -> None:
@@ -310,6 +364,55 @@ class Engine:
         if not ks:
             return np.zeros(0, np.uint32), np.zeros(0, np.uint32)
         return np.concatenate(ks), np.concatenate(vs)
+
+
+def classify_partitioned(ax: Axioms, parts: int, devices: Optional[List[int]] = None,
+                         rows: Optional[List[Tuple[int, int]]] = None) -> Tuple[List[Engine], List[Stats]]:
+    """Row-partitioned classification in ONE process: ``parts`` engines (one per thread,
+    on ``devices`` round-robin, default all on device 0) exchanging their deltas through an
+    in-process group (EL_XCHG_LOCAL).  The union of the engines' rows is the closure."""
+    import threading
+    devices = devices or [0]
+    group = LocalGroup(parts)
+    engs = [Engine(device=devices[q % len(devices)],
+                   partition=Partition(q, parts, XCHG_LOCAL, group=group, rows=rows[q] if rows else (0, 0)))
+            for q in range(parts)]
+    engs[0]._group = group  # keep the group alive as long as the engines
+    for e in engs:
+        e.load(ax)
+    stats: List[Optional[Stats]] = [None] * parts
+    errs: List[BaseException] = []
+
+    def run(q: int) -> None:
+        try:
+            engs[q].init()
+            stats[q] = engs[q].saturate()
+        except BaseException as exc:  # noqa: BLE001 — re-raised below
+            errs.append(exc)
+    th = [threading.Thread(target=run, args=(q,)) for q in range(parts)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    if errs:
+        raise errs[0]
+    return engs, stats  # type: ignore[return-value]
+
+
+def merge_facts(engs: List[Engine]) -> Tuple[np.ndarray, np.ndarray]:
+    """Union of the partitions' S facts, sorted by (x, a)."""
+    parts = [e.facts() for e in engs]
+    x = np.concatenate([p[0] for p in parts])
+    a = np.concatenate([p[1] for p in parts])
+    o = np.lexsort((a, x))
+    return x[o], a[o]
+
+
+def merge_links(engs: List[Engine]) -> Tuple[np.ndarray, np.ndarray, np.ndarray]:
+    parts = [e.links() for e in engs]
+    x, r, y = (np.concatenate([p[i] for p in parts]) for i in range(3))
+    o = np.lexsort((y, r, x))
+    return x[o], r[o], y[o]
 
 
 def classify(ax: Axioms, device: int = 0, profile: bool = False) -> Tuple[Engine, Stats]:

@@ -42,7 +42,7 @@
 extern "C" {
 #endif
 
-#define EL_ABI_VERSION 2
+#define EL_ABI_VERSION 3
 
 /* return codes */
 #define EL_OK        0
@@ -133,10 +133,29 @@ typedef struct el_axioms {
   const uint32_t* rng_c;
 } el_axioms;
 
+/* Row partition of the concept space.  A partitioned context owns the
+ * rows S(X), X in [row_lo, row_hi), and the links (X, r, Y) of those X; CR4 propagations,
+ * range activations and the links of chain-second roles are replicated.  Every
+ * superstep all-gathers each rank's new propagations / activations / chain links (the
+ * delta exchange) and the per-rank delta counts, whose sum is the termination test
+ * (replaces the "anything new?" broadcast, CommunicationHandler.java:49-84).  All ranks
+ * of a group must call el_init / el_saturate together (they are collective). */
+#define EL_XCHG_NONE  0   /* whole ontology, no partition (the default) */
+#define EL_XCHG_LOCAL 1   /* in-process group: one context per thread (el_group_create) */
+#define EL_XCHG_RCCL  2   /* one context per process/GPU, RCCL all-gather over xGMI */
+
+typedef struct el_group el_group;
+
 typedef struct el_config {
   int device;            /* HIP device ordinal (one context per GPU / rank) */
   int profile;           /* 1 = record per-kernel HIP-event times (el_kernel_stats) */
   uint32_t flags;        /* reserved, must be 0 */
+  int exchange;          /* EL_XCHG_*; NONE ignores every field below */
+  uint32_t part_rank;    /* this context's rank in [0, part_count) */
+  uint32_t part_count;   /* ranks in the group */
+  uint32_t row_lo, row_hi;  /* owned rows; row_lo = row_hi = 0: the equal split of [0, N) */
+  el_group* group;       /* EL_XCHG_LOCAL: shared by the group's contexts */
+  uint8_t rccl_id[128];  /* EL_XCHG_RCCL: ncclUniqueId made by el_rccl_unique_id on rank 0 */
 } el_config;
 
 /* Work-phase ids for el_kernel_stats.  Several phases share one launch: the
@@ -208,6 +227,11 @@ int el_abi_version(void);
 int el_device_count(int* n);
 
 int el_create(el_ctx** ctx, const el_config* cfg);
+/* in-process exchange group for EL_XCHG_LOCAL (n contexts on n threads) */
+int el_group_create(el_group** g, int n);
+void el_group_destroy(el_group* g);
+/* RCCL unique id for EL_XCHG_RCCL (rank 0 makes it, the launcher broadcasts it) */
+int el_rccl_unique_id(uint8_t out[128]);
 int el_load(el_ctx* ctx, const el_axioms* ax);
 int el_init(el_ctx* ctx);
 int el_step(el_ctx* ctx, el_rule rule, int* changed);

@@ -39,7 +39,40 @@ def test_exports_every_symbol(lib):
 
 
 def test_abi_version(lib):
-    assert lib.el_abi_version() == 2
+    from distel_amd import engine
+    assert lib.el_abi_version() == engine.ABI_VERSION == 3
+
+
+def test_config_struct_layout():
+    """The ctypes mirror of el_config matches the C layout (offset of every field)."""
+    import ctypes as C
+    from distel_amd import engine
+    src = '#include <stddef.h>\n#include <stdio.h>\n#include "el_gpu.h"\nint main(void){printf("%zu %zu %zu %zu\\n",' \
+          'offsetof(el_config, exchange), offsetof(el_config, group), offsetof(el_config, rccl_id), sizeof(el_config));}'
+    import tempfile
+    with tempfile.TemporaryDirectory() as d:
+        open(os.path.join(d, "t.c"), "w").write(src)
+        subprocess.run(["gcc", "-I", os.path.join(ROOT, "include"), "-o", os.path.join(d, "t"), os.path.join(d, "t.c")],
+                       check=True)
+        got = list(map(int, subprocess.run([os.path.join(d, "t")], capture_output=True, text=True).stdout.split()))
+    T = engine._ElConfig
+    assert got == [T.exchange.offset, T.group.offset, T.rccl_id.offset, C.sizeof(T)]
+
+
+def test_partition_config_validation(lib):
+    """Bad partition configs are refused before any device work."""
+    import ctypes as C
+    from distel_amd import engine
+    cfg = engine._ElConfig(0, 0, 0)
+    cfg.exchange, cfg.part_rank, cfg.part_count = engine.XCHG_LOCAL, 0, 2  # LOCAL without a group
+    ctx = C.c_void_p()
+    assert lib.el_create(C.byref(ctx), C.byref(cfg)) == engine.EL_EINVAL
+    cfg.exchange, cfg.part_rank, cfg.part_count = 7, 0, 1
+    assert lib.el_create(C.byref(ctx), C.byref(cfg)) == engine.EL_EINVAL
+    g = engine.LocalGroup(2)
+    cfg.exchange, cfg.part_rank, cfg.part_count, cfg.group = engine.XCHG_LOCAL, 2, 2, g.ptr  # rank out of range
+    assert lib.el_create(C.byref(ctx), C.byref(cfg)) == engine.EL_EINVAL
+    g.close()
 
 
 def test_no_device_fails_loudly(lib):

@@ -1,0 +1,125 @@
+"""GPU parity of the row-partitioned engine against the CPU oracle.
+
+Several partitioned contexts on device 0, one host thread each, exchange their deltas
+through the in-process group (EL_XCHG_LOCAL) — the same kernels and the same exchange
+protocol as one-context-per-GPU under RCCL, whose transport is checked on its own with a
+one-rank communicator.  The union of the partitions' S rows and links must be bit-exactly
+the oracle's closure (the protocol itself is pinned on the CPU by
+oracle/partition_model.py, tests/test_partition_model.py).
+"""
+import os
+
+import numpy as np
+import pytest
+
+import kat
+from distel_amd import engine, generators, ir
+
+pytestmark = pytest.mark.gpu
+
+
+def _closure(engs):
+    fx, fa = engine.merge_facts(engs)
+    lx, lr, ly = engine.merge_links(engs)
+    return fx, fa, lx, lr, ly
+
+
+def _assert_oracle(engs, ax, oracle_lib):
+    o = oracle_lib.saturate(ax, 0)
+    fx, fa, lx, lr, ly = _closure(engs)
+    ox, oa = o.facts()
+    assert np.array_equal(fx, ox) and np.array_equal(fa, oa), "S(X) differs from the oracle"
+    for g, c in zip((lx, lr, ly), o.links()):
+        assert np.array_equal(g, c), "R(r) differs from the oracle"
+    return o
+
+
+def _close(engs):
+    for e in engs:
+        e.close()
+
+
+@pytest.mark.parametrize("path", kat.kat_files(), ids=lambda p: os.path.basename(p))
+def test_kat_partitioned(path, oracle_lib):
+    ax, exp = kat.load_kat(path)
+    for parts in (1, 2, 3):
+        engs, st = engine.classify_partitioned(ax, min(parts, ax.n_concepts))
+        S, R = kat.to_sets(*engine.merge_facts(engs), *engine.merge_links(engs))
+        kat.check(exp, S, R)
+        _assert_oracle(engs, ax, oracle_lib)
+        _close(engs)
+
+
+def test_fuzz_partitioned(oracle_lib):
+    for seed in range(80):
+        ax = generators.random_small(seed, n=8 + seed % 60, n_roles=1 + seed % 5)
+        parts = 2 + seed % 3
+        engs, st = engine.classify_partitioned(ax, parts)
+        o = _assert_oracle(engs, ax, oracle_lib)
+        assert sum(s["derived"] for s in st) == o.stats()["derived"], seed
+        assert len({s["supersteps"] for s in st}) == 1  # lock-step supersteps
+        _close(engs)
+
+
+def test_uneven_and_empty_partitions(oracle_lib):
+    ax = generators.random_small(77, n=40, n_roles=3)
+    engs, st = engine.classify_partitioned(ax, 3, rows=[(0, 5), (5, 5), (5, 40)])  # rank 1 owns nothing
+    _assert_oracle(engs, ax, oracle_lib)
+    _close(engs)
+
+
+def test_exchange_overflow_regrows(oracle_lib, monkeypatch):
+    """A 2-record exchange cap overflows at once: the all-gather is redone larger."""
+    monkeypatch.setenv("EL_XCHG_CAP", "2")
+    for name in ("g1", "g5"):
+        ax = generators.workload(name, scale=0.02)
+        engs, st = engine.classify_partitioned(ax, 3)
+        _assert_oracle(engs, ax, oracle_lib)
+        _close(engs)
+
+
+@pytest.mark.parametrize("name,scale,parts", [("g1", 0.1, 2), ("g1", 0.1, 4), ("g2", 0.1, 4), ("g5", 0.05, 3),
+                                              ("g3", 0.02, 4)])
+def test_workloads_partitioned(name, scale, parts, oracle_lib):
+    ax = generators.workload(name, scale=scale)
+    engs, st = engine.classify_partitioned(ax, parts)
+    o = _assert_oracle(engs, ax, oracle_lib)
+    assert sum(s["derived"] for s in st) == o.stats()["derived"]
+    _close(engs)
+
+
+def test_replicated_copies_partitioned():
+    """OntologyMultiplier ×4 split at the copy boundaries: each partition's closure is copy
+    0's shifted (size-independent property; no oracle run at this size)."""
+    base = generators.workload("g1", scale=0.25)
+    k = 4
+    ax = ir.replicate(base, k)
+    bounds = [ir.copy_slice(base, k, i) for i in range(k)]
+    bounds[0] = (0, bounds[0][1])  # ⊥ and ⊤ (shared by the copies) live on rank 0
+    engs, st = engine.classify_partitioned(ax, k, rows=bounds)
+
+    def rows(i):
+        x, a = engs[i].facts()
+        keep = x >= 2
+        lo = ir.copy_slice(base, k, i)[0]
+        shift = lambda v: np.where(v >= 2, v.astype(np.int64) - lo, v)
+        return shift(x[keep]), shift(a[keep])
+    rx, ra = rows(0)
+    for i in range(1, k):
+        x, a = rows(i)
+        assert np.array_equal(x, rx) and np.array_equal(a, ra), i
+    ls = [len(engs[i].links()[0]) for i in range(k)]
+    assert len(set(ls)) == 1
+    _close(engs)
+
+
+def test_rccl_single_rank(oracle_lib):
+    """The RCCL transport (ncclAllGather on the engine stream) with a one-rank communicator."""
+    ax = generators.workload("g1", scale=0.05)
+    uid = engine.rccl_unique_id()
+    eng = engine.Engine(device=0, partition=engine.Partition(0, 1, engine.XCHG_RCCL, rccl_id=uid))
+    eng.load(ax)
+    eng.init()
+    st = eng.saturate()
+    _assert_oracle([eng], ax, oracle_lib)
+    eng.close()
