@@ -10,7 +10,10 @@ separately (``copyback_ms``) and never part of ``value``.
 Multi-GPU (``torch.distributed.run``): weak scaling.  Rank i classifies its own
 disjoint copy of the workload (OntologyMultiplier ×N semantics, the G4 config);
 copies share no concepts, so there is no data-path collective — only the
-barrier and the max-over-ranks timing.
+barrier and the max-over-ranks timing (``--partition copies``, the default).
+``--partition exchange`` instead loads the whole ×N ontology on every rank and runs
+the row-partitioned engine (rank i owns copy i's rows) with the per-superstep RCCL
+delta all-gather of SURVEY.md §8(e) — the path for ontologies that do not decompose.
 
 Extra objects on the JSON line:
   roofline      dominant kernel (largest Σ time in a profiled classification):
@@ -42,6 +45,21 @@ WORKLOAD_DESC = {
 }
 
 
+class _stdout_to_stderr:
+    """Route fd 1 to fd 2 for a block (native libraries write to fd 1 directly): the
+    bench's stdout carries exactly one JSON line."""
+
+    def __enter__(self):
+        sys.stdout.flush()
+        self.saved = os.dup(1)
+        os.dup2(2, 1)
+
+    def __exit__(self, *exc):
+        sys.stdout.flush()
+        os.dup2(self.saved, 1)
+        os.close(self.saved)
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -51,6 +69,9 @@ def parse():
     ap.add_argument("--scale", type=float, default=1.0)
     ap.add_argument("--no-cpu", action="store_true", help="skip the cpu_baseline leg")
     ap.add_argument("--no-profile", action="store_true", help="skip the profiled roofline pass")
+    ap.add_argument("--partition", default="copies", choices=["copies", "exchange"],
+                    help="copies: one disjoint copy per rank, no collective; exchange: row-partitioned "
+                         "engine over the ×N ontology with the RCCL delta all-gather")
     ap.add_argument("--verbose", action="store_true")
     return ap.parse_args()
 
@@ -70,10 +91,28 @@ def main():
     ax = generators.workload(args.workload, args.scale)   # this rank's copy (×world disjoint copies)
     gen_s = time.time() - t0
 
-    eng = engine.Engine(device=local if has_cuda else 0)
-    t0 = time.time()
-    eng.load(ax)  # host index build + upload: AxiomLoader's part, reported separately
-    load_s = time.time() - t0
+    if args.partition == "exchange":
+        from distel_amd import ir
+        full = ir.replicate(ax, world) if world > 1 else ax
+        rows = ir.copy_slice(ax, world, rank) if world > 1 else (0, ax.n_concepts)
+        if rank == 0:
+            rows = (0, rows[1])  # ⊥ and ⊤ live on rank 0
+        uid = engine.rccl_unique_id() if rank == 0 else None
+        if world > 1:
+            box = [uid]
+            rk.dist.broadcast_object_list(box, src=0)
+            uid = box[0]
+        with _stdout_to_stderr():  # RCCL prints its version banner on stdout at communicator init
+            eng = engine.Engine(device=local if has_cuda else 0,
+                                partition=engine.Partition(rank, world, engine.XCHG_RCCL, rccl_id=uid, rows=rows))
+        t0 = time.time()
+        eng.load(full)
+        load_s = time.time() - t0
+    else:
+        eng = engine.Engine(device=local if has_cuda else 0)
+        t0 = time.time()
+        eng.load(ax)  # host index build + upload: AxiomLoader's part, reported separately
+        load_s = time.time() - t0
 
     def classify():
         eng.init()
@@ -152,7 +191,10 @@ def main():
             "data": "synthetic",
             "config": {"workload": WORKLOAD_DESC[args.workload] + (f" ×scale {args.scale}" if args.scale != 1 else ""),
                        "concepts_per_rank": ax.n_concepts, "roles": ax.n_roles, "axioms": ax.counts(),
-                       "parallelism": f"{world} disjoint copies, one per GPU (OntologyMultiplier ×{world})"},
+                       "parallelism": (f"{world} disjoint copies, one per GPU (OntologyMultiplier ×{world})"
+                                       if args.partition == "copies" else
+                                       f"row partition of the ×{world} ontology over {world} GPUs, RCCL delta "
+                                       f"all-gather per superstep")},
             "classification_wall_s": round(ms_per_step / 1e3, 6),
             "derived_axioms": derived_all,
             "s_facts_per_rank": st["s_facts"],
