@@ -124,3 +124,55 @@ def _group(keys: np.ndarray, vals: np.ndarray) -> Dict[int, np.ndarray]:
     for ks, vs in zip(np.split(keys, cut), np.split(vals, cut)):
         out[int(ks[0])] = vs
     return out
+
+
+# ------------------------------------------------------------------ ELK diff
+def read_saxioms(path: str) -> Dict[str, set]:
+    """``X|B`` lines (``final-saxioms-distel.txt`` layout) → {X: {B}}."""
+    out: Dict[str, set] = {}
+    with open(path, encoding="utf-8") as f:
+        for line in f:
+            line = line.strip()
+            if not line or line.startswith("#"):
+                continue
+            x, b = line.rsplit("|", 1)
+            out.setdefault(x, set()).add(b)
+    return out
+
+
+BOTTOM_NAMES = ("owl:Nothing", "http://www.w3.org/2002/07/owl#Nothing", "<http://www.w3.org/2002/07/owl#Nothing>")
+
+
+def diff_results(expected: Dict[str, set], got: Dict[str, set], bottom: Optional[str] = None,
+                 top: Optional[str] = None, classes: Optional[Iterable[str]] = None) -> Tuple[int, List[str]]:
+    """Per-class comparison as ``ELClassifierTest.rearrangeAndCompareResults``
+    (kc/test/ELClassifierTest.java:363-447) / ``ResultDiffWriter.writeDiffResults``
+    (kc/output/ResultDiffWriter.java:34-99): a class differs when its superclass sets
+    differ.  ⊥ itself is skipped (:379-382); an unsatisfiable class (⊥ in either set)
+    is compared on ⊥-membership only, since ELK lists every class as its superclass and
+    DistEL only ⊥ (H4).  ``top`` (if given) is added to every expected set
+    (the reasoner's answer omits owl:Thing, :390).  Returns (differing classes, report)."""
+    keys = sorted(set(expected) | set(got)) if classes is None else sorted(classes)
+    if bottom is None:  # whichever spelling of owl:Nothing the files use
+        seen = set(expected) | set(got) | {b for v in list(expected.values()) + list(got.values()) for b in v}
+        bottom = next((b for b in BOTTOM_NAMES if b in seen), BOTTOM_NAMES[0])
+    misses, report = 0, []
+    for x in keys:
+        if x == bottom:
+            continue
+        want = set(expected.get(x, set())) | {x}
+        if top is not None:
+            want.add(top)
+        have = set(got.get(x, set())) | {x}
+        if bottom in want or bottom in have:
+            if (bottom in want) != (bottom in have):
+                misses += 1
+                report.append(f"{x} -- unsatisfiable in {'expected' if bottom in want else 'result'} only")
+            continue
+        if want != have:
+            misses += 1
+            miss, extra = sorted(want - have), sorted(have - want)
+            report.append(f"{x} -- {len(have)}, {len(want)}" + "".join(f"\n  {x} -ne- {b}" for b in miss) +
+                          "".join(f"\n\t -- {b}" for b in extra))
+    report.append(f"No of classes not equal: {misses}")
+    return misses, report

@@ -56,3 +56,28 @@ def test_write_saxioms(tmp_path, oracle_lib):
     n = rn.write_saxioms(str(p))
     text = p.read_text().splitlines()
     assert n == len(text) and "0120|0150" in text  # A (id 2) ⊑ D (id 5)
+
+
+def test_diff_results_elk_conventions(tmp_path):
+    """ResultDiffWriter-style comparison: equal sets pass; a missing / extra superclass
+    counts once per class; unsatisfiable classes compare on ⊥ only (H4)."""
+    from distel_amd.result import diff_results, read_saxioms
+    exp = {"A": {"A", "B", "owl:Thing"}, "U": {"U", "owl:Nothing", "A", "B", "C"}, "C": {"C"}}
+    got = {"A": {"A", "B", "owl:Thing"}, "U": {"U", "owl:Nothing"}, "C": {"C", "A"}}
+    misses, rep = diff_results(exp, got)
+    assert misses == 1 and "C -- " in rep[0] and rep[-1] == "No of classes not equal: 1"
+    p = tmp_path / "x.txt"
+    p.write_text("A|B\nA|A\n# comment\nC|C\n")
+    assert read_saxioms(str(p)) == {"A": {"A", "B"}, "C": {"C"}}
+
+
+def test_cli_normalize(tmp_path):
+    import os
+    from distel_amd import cli, owl
+    src = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "owl", "kat_definitions.ofn")
+    out = tmp_path / "norm.ofn"
+    assert cli.main(["normalize", src, str(out)]) == 0
+    n = owl.parse_functional(out.read_text())
+    a = owl.to_axioms(n)                               # already normal: types without normalizing
+    b = owl.to_axioms(owl.normalize(owl.parse_functional(open(src).read())))
+    assert a.counts() == b.counts()
