@@ -135,9 +135,10 @@ constexpr size_t EV_WORDS = (EV_BLOCKS + 1) * EV_TOTAL;
 constexpr uint32_t CTR_STRIDE = 64;  // words
 // Counters [0, CTR_KEEP) persist across steps; the rest are per-step (zeroed by k_commit).
 // x_log / x_send / g_delta / g_max belong to the partitioned exchange (k_ximport).
-#define EL_COUNTERS(X) X(s_log) X(l_log) X(a_log) X(p_log) X(x_log) X(x_send) X(cand_s) X(cand_l) \
-  X(cand_a) X(jobs) X(cand_p) X(g_delta) X(g_max) X(g_ovf) X(ticket) X(seq)
-constexpr uint32_t CTR_KEEP = 6;
+// ov_* count the entries of this step that did not fit their slack row (gapped CSRs below).
+#define EL_COUNTERS(X) X(s_log) X(l_log) X(a_log) X(p_log) X(x_log) X(x_send) X(ov_pr) X(ov_sc) X(ov_pp) \
+  X(cand_s) X(cand_l) X(cand_a) X(jobs) X(cand_p) X(g_delta) X(g_max) X(g_ovf) X(ticket) X(seq)
+constexpr uint32_t CTR_KEEP = 9;
 #define EL_CTR_DEV(n) uint32_t n; uint32_t n##_pad[CTR_STRIDE - 1];
 #define EL_CTR_HOST(n) uint32_t n;
 struct DCounters {
@@ -148,6 +149,30 @@ struct HCounters {  // ticket: k_scan_merge tile dispenser; seq: host copy only
 };
 constexpr uint32_t NUM_CTRS = sizeof(HCounters) / 4;
 static_assert(sizeof(DCounters) == NUM_CTRS * CTR_STRIDE * 4, "counter layout");
+
+// Gapped ("slack") CSR: row r owns the slots [start[r], start[r+1]) and holds len[r]
+// entries.  An entry is appended where its row's keyed atomic on len places it, so a
+// superstep needs no CSR merge; an entry past its row's capacity goes to the overflow
+// queue (row, value, rank) and the host re-lays out the rows (gap_cap) before the next
+// step reads them.  Readers of step t see len at the end of step t-1 (appends happen only
+// in commit / import launches, which no reader shares).
+struct DGap {
+  const uint32_t* start;  // rows + 1
+  uint32_t* len;          // rows
+  uint32_t* val;
+  uint32_t* ovq;          // 3 words per overflowing entry
+  uint32_t ovq_cap;
+  uint32_t* ov_count;     // DCounters::ov_*
+};
+
+// row r of a gapped CSR as (begin, length); a CSR the ontology never fills is not allocated
+// and reads as empty rows
+__device__ __forceinline__ uint2 gap_row(const DGap& g, uint32_t r) {
+  return g.start ? make_uint2(g.start[r], g.len[r]) : make_uint2(0u, 0u);
+}
+
+// capacity of a row with n entries after a re-layout (the CPU oracle mirrors it)
+__host__ __device__ constexpr uint32_t gap_cap(uint32_t n) { return 4 * n + 16; }
 
 struct DState {
   uint32_t* bits;
@@ -162,21 +187,16 @@ struct DState {
   unsigned long long* phash;  // CR4 propagations (pid, B)
   unsigned long long pmask;
   uint32_t *plog_p, *plog_b;
-  const uint32_t *pp_ptr, *pp_val;  // propagations per pid (CSR, current)
+  DGap pp;                          // propagations per pid
   uint32_t *cp_p, *cp_b, cp_cap;
   const uint32_t *s_ptr, *s_val;    // S rows (CSR, current)
-  const uint32_t *pr_ptr, *pr_val;  // predecessors per pid
-  const uint32_t *sc_ptr, *sc_val;  // successors per X
-  uint32_t* dcnt;  // all CSR delta counts, one array: [S rows | PR | SC | PP]
-  uint32_t off_s, off_pr, off_sc, off_pp;
+  DGap pr;                          // predecessors per pid
+  DGap sc;                          // successors per X (chain-second links in partitioned mode)
   uint32_t need_pred, need_succ;  // CSRs with readers: only those get delta counts
   uint32_t succ_at_commit;        // successor counts taken by k_commit (whole-ontology mode)
-  uint32_t *rk_pr, *rk_sc, *rk_pp;  // rank of each new entry in its delta row (index: log slot - base)
-  uint32_t l_base, p_base;          // link / propagation log counts at the start of the step
   // partitioned exchange: replicated chain-second link log, local send queue, import ranks
   uint32_t *xlog_x, *xlog_p;
   uint32_t *xs_x, *xs_p;
-  uint32_t *rk_x, x_base;
   uint32_t *cs_x, *cs_a, cs_cap;
   uint32_t *cl_x, *cl_p, cl_cap;
   uint32_t *ca_y, *ca_c, ca_cap;
@@ -284,6 +304,31 @@ __device__ __forceinline__ uint32_t wave_keyed_atomic(uint32_t* base, uint32_t k
   }
   old = __shfl(old, (int)first);
   return sub ? old - rank : old + rank;
+}
+
+// Append v to row `row` of a gapped CSR (every lane calls it; pred selects the lanes that
+// append).  Events: the len atomic (RMW), the row bounds (ROW), the value (ENT); an entry
+// past the row's capacity writes a 3-word overflow record instead (3 ENT).
+__device__ __forceinline__ void gap_append(const DGap& g, uint32_t row, uint32_t v, bool pred, uint32_t* ev) {
+  const uint32_t rank = wave_keyed_atomic(g.len, row, pred, false);
+  bool ovf = false;
+  if (pred) {
+    ev[EL_EV_RMW]++;
+    ev[EL_EV_ROW]++;
+    ev[EL_EV_ENT]++;
+    const uint32_t s = g.start[row] + rank;
+    ovf = s >= g.start[row + 1];
+    if (!ovf) g.val[s] = v;
+  }
+  const uint32_t q = wave_append(g.ov_count, ovf);
+  if (ovf) {
+    ev[EL_EV_ENT] += 2;
+    if (q < g.ovq_cap) {
+      g.ovq[3 * (size_t)q] = row;
+      g.ovq[3 * (size_t)q + 1] = v;
+      g.ovq[3 * (size_t)q + 2] = rank;
+    }
+  }
 }
 
 __device__ __forceinline__ bool test_bit(const uint32_t* bits, uint64_t W, uint32_t x, uint32_t b) {
@@ -622,8 +667,9 @@ __device__ void expand_s(const DIndex& ix, const DState& st, BlockQ& q, uint32_t
             fresh = !hash_contains(st.phash, st.pmask, link_key(pid, B));
             if (fresh && (mask & M_R4D)) {  // fused mode: B reaches today's predecessors now
               ev.v[EL_EV_ROW]++;
-              pb = st.pr_ptr[pid];
-              pl = st.pr_ptr[pid + 1] - pb;
+              const uint2 row = gap_row(st.pr, pid);
+              pb = row.x;
+              pl = row.y;
             }
           }
           emit_p(st, fresh, pid, B, ev);
@@ -640,8 +686,8 @@ __device__ void expand_s(const DIndex& ix, const DState& st, BlockQ& q, uint32_t
             continue;
           }
           ev.v[EL_EV_ROW]++;
-          const uint32_t pb = st.pr_ptr[p], pl = st.pr_ptr[p + 1] - pb;
-          emit_job(st, q, pl > 0, JOB_PRED_S, pb, pl, 0, EL_BOTTOM, ev);
+          const uint2 row = gap_row(st.pr, p);
+          emit_job(st, q, row.y > 0, JOB_PRED_S, row.x, row.y, 0, EL_BOTTOM, ev);
         }
       }
       if ((mask & M_RRNG) && ix.has_range) {  // Y=A ∈ S(X) new, active range (Y, C)  =>  C ∈ S(X)
@@ -681,8 +727,9 @@ __device__ __forceinline__ void r6_second(const DIndex& ix, const DState& st, Bl
     uint32_t pb = 0, pl = 0, pt = NONE;
     if (pq != NONE) {
       ev.v[EL_EV_ROW]++;
-      pb = st.pr_ptr[pq];
-      pl = st.pr_ptr[pq + 1] - pb;
+      const uint2 row = gap_row(st.pr, pq);
+      pb = row.x;
+      pl = row.y;
       if (pl) pt = pair_lookup(ix, t, Y, ev);
     }
     emit_job(st, q, pl > 0, JOB_PRED_L, pb, pl, pt, 0, ev);
@@ -705,9 +752,11 @@ __device__ void expand_l(const DIndex& ix, const DState& st, BlockQ& q, uint32_t
       ev.v[EL_EV_ENT] += 2;
       if (mask & M_R4L) {  // (X, Y) ∈ R(r) new, propagation ((r, Y), B)  =>  B ∈ S(X)
         ev.v[EL_EV_ROW]++;   // (Type3_2AxiomProcessorBase.java:67-96, part 2: all B × ΔX)
-        const uint32_t g1 = st.pp_ptr[pid + 1];
-        for (uint32_t j = st.pp_ptr[pid]; j < g1; ++j) {
-          const uint32_t B = st.pp_val[j];
+        // (no propagation CSR when the ontology has no ∃r.A ⊑ B: every row is empty)
+        const uint2 row = gap_row(st.pp, pid);
+        const uint32_t g0 = row.x, g1 = row.x + row.y;
+        for (uint32_t j = g0; j < g1; ++j) {
+          const uint32_t B = st.pp.val[j];
           ev.v[EL_EV_ENT]++;
           ev.v[EL_EV_TEST]++;
           emit_s(st, q, !test_bit(st.bits, ix.W, X, B), X, B, ev);
@@ -738,8 +787,9 @@ __device__ void expand_l(const DIndex& ix, const DState& st, BlockQ& q, uint32_t
         uint32_t sb = 0, sl = 0;
         if (first) {  // r first: (Y, Z) ∈ R(s)  =>  (X, Z) ∈ R(t)
           ev.v[EL_EV_ROW]++;
-          sb = st.sc_ptr[Y];
-          sl = st.sc_ptr[Y + 1] - sb;
+          const uint2 row = gap_row(st.sc, Y);
+          sb = row.x;
+          sl = row.y;
         }
         emit_job(st, q, first && sl > 0, JOB_R6A, sb, sl, X, r, ev);
         if (!ix.part) r6_second(ix, st, q, X, r, Y, ev);  // partitioned: over the exchanged chain links
@@ -809,14 +859,14 @@ __global__ void k_jobs(DIndex ix, DState st) {
       if (lane == 0) ev.v[EL_EV_JOB]++;
       if (type == JOB_PRED_S) {
         for (uint32_t k = lane; k < len; k += 64) {
-          const uint32_t xp = st.pr_val[begin + k];
+          const uint32_t xp = st.pr.val[begin + k];
           ev.v[EL_EV_ENT]++;
           ev.v[EL_EV_TEST]++;
           emit_s(st, q, !test_bit(st.bits, ix.W, xp, b), xp, b, ev);
         }
       } else if (type == JOB_PRED_L) {
         for (uint32_t k = lane; k < len; k += 64) {
-          const uint32_t xp = st.pr_val[begin + k];
+          const uint32_t xp = st.pr.val[begin + k];
           ev.v[EL_EV_ENT]++;
           ev.v[EL_EV_HASH]++;
           emit_l(st, q, !hash_contains(st.lhash, st.lmask, link_key(a, xp)), xp, a, ev);
@@ -824,7 +874,7 @@ __global__ void k_jobs(DIndex ix, DState st) {
       } else {  // JOB_R6A
         const uint32_t X = a, r = b;
         for (uint32_t k = lane; k < len; k += 64) {
-          const uint32_t sq = st.sc_val[begin + k];
+          const uint32_t sq = st.sc.val[begin + k];
           ev.v[EL_EV_ENT]++;
           const uint32_t s2 = ix.pair_role[sq], Z = ix.pair_y[sq];
           ev.v[EL_EV_ENT] += 2;
@@ -880,7 +930,6 @@ __device__ void expand_a(const DIndex& ix, const DState& st, BlockQ& q, uint32_t
 // LDS staging of the commit roles (one role per block)
 struct CommitLds {
   uint32_t x[QS_CAP > QL_CAP ? QS_CAP : QL_CAP], v[QS_CAP > QL_CAP ? QS_CAP : QL_CAP];
-  uint32_t r1[QL_CAP], r2[QL_CAP];  // link ranks in the predecessor / successor delta rows
   uint32_t n, base;
 };
 
@@ -953,15 +1002,11 @@ __device__ void commit_l(const DIndex& ix, const DState& st, CommitLds& sm, uint
       ev.v[EL_EV_TRIG]++;
       ev.v[EL_EV_HASH]++;
       nw = hash_insert(st.lhash, st.lmask, link_key(p, x));
-      if (nw) {
-        ev.v[EL_EV_EMIT]++;
-        ev.v[EL_EV_ENT] += st.need_pred + st.succ_at_commit;  // rank words for the merges
-      }
+      if (nw) ev.v[EL_EV_EMIT]++;
     }
-    // the count's old value is the link's rank among its row's new entries: the merge
-    // places it from that rank without a second atomic
-    const uint32_t rp = st.need_pred ? wave_keyed_atomic(st.dcnt, st.off_pr + p, nw, false) : 0u;
-    const uint32_t rs = st.succ_at_commit ? wave_keyed_atomic(st.dcnt, st.off_sc + x, nw, false) : 0u;
+    // the new link joins its predecessor / successor rows in place
+    if (st.need_pred) gap_append(st.pr, p, x, nw, ev.v);
+    if (st.succ_at_commit) gap_append(st.sc, x, p, nw, ev.v);
     if (ix.part) {  // partitioned: a new link of a chain-second role goes to every rank
       const bool xs = nw && ix.role_chs[ix.pair_role[p]];
       const uint32_t slot = wave_append(&st.ctr->x_send, xs);
@@ -974,8 +1019,6 @@ __device__ void commit_l(const DIndex& ix, const DState& st, CommitLds& sm, uint
     if (nw) {
       lx[off] = x;
       lp[off] = p;
-      sm.r1[off] = rp;
-      sm.r2[off] = rs;
     }
     __syncthreads();
     if (ln > QL_CAP / 2 || base + nb * blockDim.x >= n) {
@@ -985,8 +1028,6 @@ __device__ void commit_l(const DIndex& ix, const DState& st, CommitLds& sm, uint
       for (uint32_t k = threadIdx.x; k < cnt; k += blockDim.x) {
         st.llog_x[lbase + k] = lx[k];
         st.llog_p[lbase + k] = lp[k];
-        if (st.need_pred) st.rk_pr[lbase + k - st.l_base] = sm.r1[k];
-        if (st.succ_at_commit) st.rk_sc[lbase + k - st.l_base] = sm.r2[k];
       }
       __syncthreads();
       if (threadIdx.x == 0) ln = 0;
@@ -1027,7 +1068,8 @@ __device__ void expand_p(const DIndex& ix, const DState& st, BlockQ& q, uint32_t
       const uint32_t pid = st.plog_p[i], B = st.plog_b[i];
       ev.v[EL_EV_TRIG]++;
       ev.v[EL_EV_ROW]++;
-      const uint32_t pb = st.pr_ptr[pid], pl = st.pr_ptr[pid + 1] - pb;
+      const uint2 row = gap_row(st.pr, pid);
+      const uint32_t pb = row.x, pl = row.y;
       emit_job(st, q, pl > 0, JOB_PRED_S, pb, pl, 0, B, ev);
     }
     q_maybe_flush(q, st);
@@ -1046,13 +1088,11 @@ __device__ void commit_p(const DIndex& ix, const DState& st, uint32_t bid, uint3
     ev.v[EL_EV_HASH]++;
     const bool nw = hash_insert(st.phash, st.pmask, link_key(pid, b));
     const uint32_t slot = wave_append(&st.ctr->p_log, nw);
-    const uint32_t rank = wave_keyed_atomic(st.dcnt, st.off_pp + pid, nw, false);
+    gap_append(st.pp, pid, b, nw, ev.v);
     if (nw) {
       ev.v[EL_EV_EMIT]++;
       st.plog_p[slot] = pid;
       st.plog_b[slot] = b;
-      st.rk_pp[slot - st.p_base] = rank;
-      ev.v[EL_EV_ENT]++;
     }
   }
   ev_flush(st.ev, EL_K_COMMIT_P, ev);
@@ -1210,8 +1250,9 @@ struct XchgArgs {
   uint32_t cs_cap, cl_cap, ca_cap, cp_cap, job_cap;  // a candidate queue past its cap = redo
 };
 // per-step counters the import zeroes once the exchange went through: x_send, cand_*, jobs
-constexpr uint32_t XCHG_ZERO = (1u << 5) | (1u << 6) | (1u << 7) | (1u << 8) | (1u << 9) | (1u << 10);
-static_assert(offsetof(DCounters, x_send) == 5 * CTR_STRIDE * 4 && offsetof(DCounters, cand_p) == 10 * CTR_STRIDE * 4,
+constexpr uint32_t XCHG_ZERO = (1u << 5) | (1u << 9) | (1u << 10) | (1u << 11) | (1u << 12) | (1u << 13);
+static_assert(offsetof(DCounters, x_send) == 5 * CTR_STRIDE * 4 && offsetof(DCounters, cand_s) == 9 * CTR_STRIDE * 4 &&
+                  offsetof(DCounters, cand_p) == 13 * CTR_STRIDE * 4,
               "XCHG_ZERO bits");
 
 __global__ void k_xpack(DState st, XchgArgs x) {
@@ -1245,6 +1286,7 @@ __global__ void k_xpack(DState st, XchgArgs x) {
 // nothing is imported (g_max tells the host; it re-runs the exchange with a larger cap).
 // The last block publishes: g_delta = Σ over ranks of all deltas (0 = global fixpoint).
 __global__ void k_ximport(DIndex ix, DState st, XchgArgs x, PubArgs pub) {
+  Ev ev;  // not accounted (the import has no oracle counterpart)
   const uint32_t stride = XH + 2 * x.cap;
   uint32_t gmax = 0;
   for (uint32_t q = 0; q < x.nranks; ++q) {
@@ -1272,11 +1314,10 @@ __global__ void k_ximport(DIndex ix, DState st, XchgArgs x, PubArgs pub) {
     // propagations (unique per owner of Y, so a remote one is new unless re-imported)
     const bool nwp = is_p && hash_insert(st.phash, st.pmask, link_key(r.x, r.y));
     const uint32_t ps = wave_append(&st.ctr->p_log, nwp);
-    const uint32_t prk = wave_keyed_atomic(st.dcnt, st.off_pp + r.x, nwp, false);
+    gap_append(st.pp, r.x, r.y, nwp, ev.v);
     if (nwp) {
       st.plog_p[ps] = r.x;
       st.plog_b[ps] = r.y;
-      st.rk_pp[ps - st.p_base] = prk;
     }
     // activations (two ranks may have made the same one)
     const bool nwa = is_a && hash_insert(st.ahash, st.amask, link_key(r.y, r.x));
@@ -1288,11 +1329,10 @@ __global__ void k_ximport(DIndex ix, DState st, XchgArgs x, PubArgs pub) {
     }
     // chain-second links: every rank's, successor CSR keyed by the link's source
     const uint32_t xsl = wave_append(&st.ctr->x_log, is_x);
-    const uint32_t xrk = st.need_succ ? wave_keyed_atomic(st.dcnt, st.off_sc + r.x, is_x, false) : 0u;
+    if (st.need_succ) gap_append(st.sc, r.x, r.y, is_x, ev.v);
     if (is_x) {
       st.xlog_x[xsl] = r.x;
       st.xlog_p[xsl] = r.y;
-      st.rk_x[xsl - st.x_base] = xrk;
     }
   }
   publish_last(st, pub, false, [&] {
@@ -1328,6 +1368,7 @@ struct MergeSeg {
   uint32_t begin;           // delta = log[begin, *end_ptr)
   const uint32_t* end_ptr;  // device log counter (the host learns it only after the step)
   const uint32_t* rank;     // rank of delta entry i among its row's new entries
+  const uint32_t* gap_len;  // non-null: scan gap_cap(gap_len[r]) into ptr2 (gapped-CSR re-layout)
 };
 struct MergeArgs {
   MergeSeg seg[4];
@@ -1368,14 +1409,16 @@ __global__ void __launch_bounds__(256) k_scan_merge(MergeArgs m, ScanArgs sa, ui
   uint32_t k = 0;
   while (k + 1 < m.nseg && sa.tile0[k + 1] <= t) ++k;
   const MergeSeg& g = m.seg[k];
-  if (*g.end_ptr == g.begin) return;  // nothing new in this CSR: none of its tiles scans
+  if (!g.gap_len && *g.end_ptr == g.begin) return;  // nothing new in this CSR: none of its tiles scans
   const uint32_t lt = t - sa.tile0[k], r0 = lt * SCAN_TILE;
   uint32_t* __restrict__ dc = dcnt + g.off;
 #pragma unroll
   for (uint32_t i = 0; i < SCAN_ITEMS; ++i) {
     const uint32_t idx = r0 + i * 256 + tid;
     uint32_t v = 0;
-    if (idx < g.n1) {
+    if (g.gap_len) {
+      if (idx + 1 < g.n1) v = gap_cap(g.gap_len[idx]);  // row capacities of the new layout
+    } else if (idx < g.n1) {
       v = dc[idx];
       if (v) dc[idx] = 0;  // consumed: the counts start from zero next step
     }
@@ -1453,8 +1496,12 @@ __global__ void __launch_bounds__(256) k_scan_merge(MergeArgs m, ScanArgs sa, ui
     const uint32_t idx = r0 + i * 256 + tid;
     if (idx < g.n1) {
       const uint32_t d = buf[i * 256 + tid];
-      ds[idx] = d;
-      g.ptr2[idx] = g.ptr[idx] + d;
+      if (g.gap_len) {
+        g.ptr2[idx] = d;
+      } else {
+        ds[idx] = d;
+        g.ptr2[idx] = g.ptr[idx] + d;
+      }
     }
   }
 }
@@ -1506,6 +1553,43 @@ __global__ void k_rehash(unsigned long long* t, unsigned long long mask, const u
   const uint32_t stride = gridDim.x * blockDim.x;
   for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
     hash_insert(t, mask, link_key(kp[i], kx[i]));
+}
+
+// el_init after a classification: only the words the fact log names can be non-zero, and
+// when the log is small next to the matrix, clearing those words beats streaming it all
+__global__ void k_clear_logged(uint32_t* bits_base, uint64_t W, const uint32_t* __restrict__ lx,
+                               const uint32_t* __restrict__ la, uint32_t n) {
+  const uint32_t stride = gridDim.x * blockDim.x;
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
+    bits_base[(uint64_t)lx[i] * W + (la[i] >> 5)] = 0u;
+}
+
+// ---- gapped-CSR layout kernels (rare: initial layout, re-layout after an overflow)
+__global__ void k_gap_init(uint32_t* start, uint32_t* len, uint32_t rows) {
+  const uint32_t stride = gridDim.x * blockDim.x;
+  for (uint32_t r = blockIdx.x * blockDim.x + threadIdx.x; r <= rows; r += stride) {
+    start[r] = r * gap_cap(0);
+    if (r < rows) len[r] = 0;
+  }
+}
+
+// one wave per row: the in-place entries of row r move to its new slots
+__global__ void k_gap_move(const uint32_t* __restrict__ s_old, const uint32_t* __restrict__ len,
+                           const uint32_t* __restrict__ v_old, const uint32_t* __restrict__ s_new,
+                           uint32_t* __restrict__ v_new, uint32_t rows) {
+  const uint32_t lane = threadIdx.x & 63u, waves = gridDim.x * (blockDim.x >> 6);
+  for (uint32_t r = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); r < rows; r += waves) {
+    const uint32_t b = s_old[r], n = min(len[r], s_old[r + 1] - b), d = s_new[r];
+    for (uint32_t k = lane; k < n; k += 64) v_new[d + k] = v_old[b + k];
+  }
+}
+
+// overflow records (row, value, rank) land at their rank in the new layout
+__global__ void k_gap_ovf(const uint32_t* __restrict__ q, uint32_t n, const uint32_t* __restrict__ s_new,
+                          uint32_t* __restrict__ v_new) {
+  const uint32_t stride = gridDim.x * blockDim.x;
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
+    v_new[s_new[q[3 * (size_t)i]] + q[3 * (size_t)i + 2]] = q[3 * (size_t)i + 1];
 }
 
 // ---------------------------------------------------------------- host side
@@ -1608,6 +1692,46 @@ struct DevCsr {
     dfree(row2);
     dfree(val2);
     dcnt = dscan = nullptr;
+  }
+};
+
+// Gapped CSR (DGap) on the host side: the layout buffers, the overflow queue, scan scratch.
+struct GapCsr {
+  uint32_t rows = 0;
+  uint32_t *start = nullptr, *start2 = nullptr, *len = nullptr;
+  uint32_t *val = nullptr, *val2 = nullptr;
+  uint64_t val_cap = 0, val2_cap = 0;
+  uint32_t* ovq = nullptr;
+  uint64_t ovq_cap = 0;
+  bool live = false;  // maintained for this ontology (it has readers)
+  void alloc(uint32_t n, uint64_t ovq_entries) {
+    rows = n;
+    start = dalloc<uint32_t>(n + 1);
+    start2 = dalloc<uint32_t>(n + 1);
+    len = dalloc<uint32_t>(n);
+    val_cap = (uint64_t)gap_cap(0) * n;
+    val = dalloc<uint32_t>(val_cap);
+    live = true;
+    set_ovq(ovq_entries);
+  }
+  void set_ovq(uint64_t entries) {
+    if (!live || entries <= ovq_cap) return;
+    dfree(ovq);
+    ovq_cap = entries;
+    ovq = dalloc<uint32_t>(3 * entries);
+  }
+  void release() {
+    dfree(start);
+    dfree(start2);
+    dfree(len);
+    dfree(val);
+    dfree(val2);
+    dfree(ovq);
+    val_cap = val2_cap = ovq_cap = 0;
+    live = false;
+  }
+  DGap view(uint32_t* ov_count) const {
+    return DGap{start, len, val, ovq, (uint32_t)ovq_cap, ov_count};
   }
 };
 
@@ -1770,7 +1894,9 @@ struct el_ctx {
   uint64_t plog_cap = 0;
   uint32_t *cp_p = nullptr, *cp_b = nullptr;
   uint64_t cp_cap = 0;
-  DevCsr S, PR, SC, PP;
+  DevCsr S;            // S rows, built lazily for export (merge kernels)
+  GapCsr PR, SC, PP;   // predecessors per pid, successors per X, propagations per pid
+  uint32_t* pin_word = nullptr;  // pinned scratch for the rare synchronous readbacks
   uint32_t *dcnt_all = nullptr, *dscan_all = nullptr;
   uint64_t dcnt_total = 0;
   uint64_t s_csr_count = 0;   // S-row CSR is built lazily (only export reads it)
@@ -1778,7 +1904,6 @@ struct el_ctx {
   bool need_succ = true;      // successor CSR has readers (CR6)
   uint32_t *cs_x = nullptr, *cs_a = nullptr, *cl_x = nullptr, *cl_p = nullptr, *ca_y = nullptr,
            *ca_c = nullptr;
-  uint32_t *rk_pr = nullptr, *rk_sc = nullptr, *rk_pp = nullptr;  // per-step ranks (cl_cap / cp_cap)
   uint64_t cs_cap = 0, cl_cap = 0, ca_cap = 0;
   uint4* jobs = nullptr;
   uint64_t job_cap = 0;
@@ -1821,11 +1946,21 @@ struct el_ctx {
   uint32_t *xlog_x = nullptr, *xlog_p = nullptr;  // replicated chain-second links
   uint64_t xlog_cap = 0, x_count = 0;
   uint32_t *xs_x = nullptr, *xs_p = nullptr;      // this step's local chain links to send (cl_cap)
-  uint32_t* rk_x = nullptr;                       // import ranks in the successor rows (xcap * ranks)
   uint32_t* xsend = nullptr;                      // exchange slot: XH + 2 * xcap words
   uint32_t* xrecv = nullptr;                      // part_count slots
   uint64_t xcap = 0;                              // records per rank per exchange (grows on overflow)
   bool part() const { return xmode != EL_XCHG_NONE; }
+  bool bits_logged = false;  // every set bit of the matrix is in the fact log (not after el_load)
+
+  // launch shapes (workgroups per role): a workgroup costs dispatch time even when its
+  // grid-stride loop is empty, so the capacity-sized roles are capped
+  static uint32_t env_u32(const char* n, uint32_t d) {
+    const char* e = getenv(n);
+    return e ? (uint32_t)std::max(1ul, strtoul(e, nullptr, 10)) : d;
+  }
+  uint32_t tune_commit = env_u32("EL_COMMIT_BLOCKS", 1024);
+  uint32_t tune_jobs = env_u32("EL_JOBS_BLOCKS", 1024);
+  uint32_t tune_scatter = env_u32("EL_SCATTER_BLOCKS", 512);
 
   DState dstate() const {
     DState s{};
@@ -1846,22 +1981,14 @@ struct el_ctx {
     s.pmask = phash_cap - 1;
     s.plog_p = plog_p;
     s.plog_b = plog_b;
-    s.pp_ptr = PP.ptr;
-    s.pp_val = PP.val;
+    s.pp = PP.view(&ctr->ov_pp);
     s.cp_p = cp_p;
     s.cp_b = cp_b;
     s.cp_cap = (uint32_t)cp_cap;
     s.s_ptr = S.ptr;
     s.s_val = S.val;
-    s.pr_ptr = PR.ptr;
-    s.pr_val = PR.val;
-    s.sc_ptr = SC.ptr;
-    s.sc_val = SC.val;
-    s.dcnt = dcnt_all;
-    s.off_s = (uint32_t)(S.dcnt - dcnt_all);
-    s.off_pr = (uint32_t)(PR.dcnt - dcnt_all);
-    s.off_sc = (uint32_t)(SC.dcnt - dcnt_all);
-    s.off_pp = (uint32_t)(PP.dcnt - dcnt_all);
+    s.pr = PR.view(&ctr->ov_pr);
+    s.sc = SC.view(&ctr->ov_sc);
     s.need_pred = need_pred ? 1u : 0u;
     s.need_succ = need_succ ? 1u : 0u;
     s.succ_at_commit = (need_succ && !part()) ? 1u : 0u;
@@ -1869,13 +1996,7 @@ struct el_ctx {
     s.xlog_p = xlog_p;
     s.xs_x = xs_x;
     s.xs_p = xs_p;
-    s.rk_x = rk_x;
-    s.x_base = (uint32_t)x_count;
-    s.rk_pr = rk_pr;
-    s.rk_sc = rk_sc;
-    s.rk_pp = rk_pp;
-    s.l_base = (uint32_t)l_count;
-    s.p_base = (uint32_t)p_count;
+
     s.cs_x = cs_x;
     s.cs_a = cs_a;
     s.cs_cap = (uint32_t)cs_cap;
@@ -1997,9 +2118,11 @@ struct el_ctx {
   uint64_t superstep_part(uint32_t mask, uint64_t sb, uint64_t se, uint64_t lb, uint64_t le, uint64_t ab,
                           uint64_t ae, uint64_t pb, uint64_t pe, uint64_t xb, uint64_t xe);
   void grow_part(uint64_t new_xcap);
-  uint32_t exchange_round(uint32_t s0, uint32_t l0, uint32_t a0, uint32_t p0, std::vector<MergeReq>& reqs);
+  uint32_t exchange_round(uint32_t s0, uint32_t l0, uint32_t a0, uint32_t p0);
   uint64_t remote_bound() const { return part() ? (uint64_t)(part_count - 1) * xcap : 0u; }
   void fill_stats(el_stats* st, double ms);
+  void gap_rebuild(GapCsr& g, uint32_t n_ovf, uint64_t entries);
+  void gap_rebuild_all();
 };
 
 void el_ctx::free_index() {
@@ -2023,9 +2146,6 @@ void el_ctx::free_state() {
   dfree(plog_b);
   dfree(cp_p);
   dfree(cp_b);
-  dfree(rk_pr);
-  dfree(rk_sc);
-  dfree(rk_pp);
   S.release();
   PR.release();
   SC.release();
@@ -2053,15 +2173,17 @@ void el_ctx::free_state() {
   dfree(xlog_p);
   dfree(xs_x);
   dfree(xs_p);
-  dfree(rk_x);
   dfree(xsend);
   dfree(xrecv);
+  if (pin_word) (void)hipHostFree(pin_word);
+  pin_word = nullptr;
 }
 
 void el_ctx::alloc_state() {
   const uint64_t N = hx.N, P = hx.P;
   W = (N + 31) / 32;
   bits = dalloc<uint32_t>((uint64_t)(hi - lo) * W);  // owned rows only
+  bits_logged = false;
   slog_cap = std::max<uint64_t>(1u << 20, 8 * N);
   slog_x = dalloc<uint32_t>(slog_cap);
   slog_a = dalloc<uint32_t>(slog_cap);
@@ -2084,27 +2206,27 @@ void el_ctx::alloc_state() {
   cp_cap = plog_cap;
   cp_p = dalloc<uint32_t>(cp_cap);
   cp_b = dalloc<uint32_t>(cp_cap);
-  rk_pp = dalloc<uint32_t>(cp_cap);  // partitioned: re-sized with the exchange (grow_part)
-  dcnt_total = 2 * (N + 1) + 2 * (P + 1);
+  dcnt_total = N + 1;  // the S-row CSR (export) is the only merged CSR
   dcnt_all = dalloc<uint32_t>(dcnt_total);
   dscan_all = dalloc<uint32_t>(dcnt_total);
-  uint64_t o = 0;
-  S.alloc((uint32_t)N, slog_cap, dcnt_all + o, dscan_all + o);
-  o += N + 1;
-  PR.alloc((uint32_t)P, llog_cap, dcnt_all + o, dscan_all + o);
-  o += P + 1;
-  SC.alloc((uint32_t)N, llog_cap, dcnt_all + o, dscan_all + o);
-  o += N + 1;
-  PP.alloc((uint32_t)P, plog_cap, dcnt_all + o, dscan_all + o);
+  S.alloc((uint32_t)N, slog_cap, dcnt_all, dscan_all);
   cs_cap = std::max<uint64_t>(1u << 20, 4 * N);
   cl_cap = cs_cap;
+  if (part()) {
+    // records per rank per all-gather; grows on demand (EL_XCHG_CAP: a smaller start, tests)
+    xcap = 1u << 12;
+    if (const char* e = getenv("EL_XCHG_CAP")) xcap = std::max<uint64_t>(1, strtoull(e, nullptr, 10));
+  }
+  // gapped CSRs, only where the rules read them; overflow queues hold a step's appends
+  if (P && need_pred) PR.alloc((uint32_t)P, cl_cap);
+  if (need_succ) SC.alloc((uint32_t)N, part() ? (uint64_t)part_count * xcap : cl_cap);
+  if (use_props) PP.alloc((uint32_t)P, cp_cap + remote_bound());
+  HIPCHK(hipHostMalloc((void**)&pin_word, sizeof(uint32_t), hipHostMallocDefault));
   ca_cap = 1u << 12;
   cs_x = dalloc<uint32_t>(cs_cap);
   cs_a = dalloc<uint32_t>(cs_cap);
   cl_x = dalloc<uint32_t>(cl_cap);
   cl_p = dalloc<uint32_t>(cl_cap);
-  rk_pr = dalloc<uint32_t>(cl_cap);
-  rk_sc = dalloc<uint32_t>(cl_cap);
   ca_y = dalloc<uint32_t>(ca_cap);
   ca_c = dalloc<uint32_t>(ca_cap);
   job_cap = std::max<uint64_t>(1u << 20, 2 * N);
@@ -2119,21 +2241,17 @@ void el_ctx::alloc_state() {
   HIPCHK(hipHostMalloc((void**)&ev_host, EV_TOTAL * sizeof(unsigned long long), hipHostMallocDefault));
   HIPCHK(hipHostGetDevicePointer((void**)&hc_dev, hc_pinned, 0));
   scan_tiles = 0;
-  for (uint64_t rows : {N, P, N, P}) scan_tiles += (rows + 1 + SCAN_TILE - 1) / SCAN_TILE;
+  scan_tiles = (std::max(N, P) + 1 + SCAN_TILE - 1) / SCAN_TILE;  // S rows or a gapped CSR re-layout
   scan_flags = dalloc<unsigned long long>(scan_tiles);
   commit_done = dalloc<uint32_t>((DONE_SHARDS + 1) * CTR_STRIDE);
   HIPCHK(hipMemset(scan_flags, 0, scan_tiles * sizeof(unsigned long long)));
   scan_epoch = 0;
   if (part()) {
-    // records per rank per all-gather; grows on demand (EL_XCHG_CAP: a smaller start, tests)
-    xcap = 1u << 12;
-    if (const char* e = getenv("EL_XCHG_CAP")) xcap = std::max<uint64_t>(1, strtoull(e, nullptr, 10));
     xlog_cap = std::max<uint64_t>(1u << 16, (uint64_t)part_count * xcap);
     xlog_x = dalloc<uint32_t>(xlog_cap);
     xlog_p = dalloc<uint32_t>(xlog_cap);
     xs_x = dalloc<uint32_t>(cl_cap);
     xs_p = dalloc<uint32_t>(cl_cap);
-    rk_x = dalloc<uint32_t>((uint64_t)part_count * xcap);
     xsend = dalloc<uint32_t>(XH + 2 * xcap);
     xrecv = dalloc<uint32_t>((uint64_t)part_count * (XH + 2 * xcap));
   }
@@ -2142,18 +2260,36 @@ void el_ctx::alloc_state() {
 void el_ctx::reset_state() {
   FillArgs f{};
   auto add = [&](void* p, uint64_t bytes, uint32_t pattern) { f.seg[f.n++] = FillSeg{p, bytes, pattern}; };
-  add(bits, (uint64_t)(hi - lo) * W * sizeof(uint32_t), 0u);
+  const uint64_t matrix_bytes = (uint64_t)(hi - lo) * W * sizeof(uint32_t);
+  if (bits_logged && s_count * 64 < matrix_bytes) {  // one 64-B line per logged fact vs. the whole matrix
+    hipLaunchKernelGGL(k_clear_logged, dim3(grid_for(s_count)), dim3(BLOCK), 0, stream, dstate().bits, W, slog_x,
+                       slog_a, (uint32_t)s_count);
+    HIPCHK(hipGetLastError());
+  } else {
+    add(bits, matrix_bytes, 0u);
+  }
+  bits_logged = true;  // from here on every set bit is in the fact log (k_init and k_commit append)
   add(lhash, lhash_cap * sizeof(unsigned long long), ~0u);
   add(ahash, ahash_cap * sizeof(unsigned long long), ~0u);
   add(has_act, hx.N, 0u);
   add(phash, phash_cap * sizeof(unsigned long long), ~0u);
   add(dcnt_all, dcnt_total * sizeof(uint32_t), 0u);
-  for (DevCsr* c : {&S, &PR, &SC, &PP}) add(c->ptr, (c->nrows + 1) * sizeof(uint32_t), 0u);
+  add(S.ptr, (S.nrows + 1) * sizeof(uint32_t), 0u);
   add(ctr, sizeof(DCounters), 0u);
   add(commit_done, (DONE_SHARDS + 1) * CTR_STRIDE * sizeof(uint32_t), 0u);
   add(ev, EV_WORDS * sizeof(unsigned long long), 0u);
   hipLaunchKernelGGL(k_fill, dim3(1024), dim3(BLOCK), 0, stream, f);
   HIPCHK(hipGetLastError());
+  for (GapCsr* g : {&PR, &SC, &PP}) {
+    if (!g->live) continue;
+    if (g->val_cap < (uint64_t)gap_cap(0) * g->rows) {  // (a re-layout may have shrunk nothing: val only grows)
+      dfree(g->val);
+      g->val_cap = (uint64_t)gap_cap(0) * g->rows;
+      g->val = dalloc<uint32_t>(g->val_cap);
+    }
+    hipLaunchKernelGGL(k_gap_init, dim3(grid_for(g->rows + 1)), dim3(BLOCK), 0, stream, g->start, g->len, g->rows);
+    HIPCHK(hipGetLastError());
+  }
   s_count = l_count = a_count = p_count = s_init = s_csr_count = x_count = 0;
   for (int r = 0; r < EL_NUM_RULE_TYPES; ++r) wm_s[r] = wm_l[r] = wm_a[r] = wm_p[r] = 0;
   wm_x = 0;
@@ -2249,11 +2385,11 @@ void el_ctx::launch_merges(const std::vector<MergeReq>& reqs) {
   });
   if (m.max_old)
     launch(EL_K_SCATTER_OLD, [&] {
-      hipLaunchKernelGGL(k_scatter_old, dim3(grid_for(m.max_old, 512), m.nseg), dim3(BLOCK), 0, stream, m,
+      hipLaunchKernelGGL(k_scatter_old, dim3(grid_for(m.max_old, tune_scatter), m.nseg), dim3(BLOCK), 0, stream, m,
                          dscan_all);
     });
   launch(EL_K_SCATTER_NEW, [&] {
-    hipLaunchKernelGGL(k_scatter_new, dim3(512, m.nseg), dim3(BLOCK), 0, stream, m, (const uint32_t*)dscan_all);
+    hipLaunchKernelGGL(k_scatter_new, dim3(tune_scatter, m.nseg), dim3(BLOCK), 0, stream, m, (const uint32_t*)dscan_all);
   });
 }
 
@@ -2313,11 +2449,11 @@ bool el_ctx::superstep(uint32_t mask, uint64_t sb, uint64_t se, uint64_t lb, uin
   const uint64_t s0 = s_count, l0 = l_count, a0 = a_count, p0 = p_count;
   for (int attempt = 0;; ++attempt) {
     // ---- capacities: every candidate could be new.  Growth copies device arrays outside
-    // the stream, so the previous step's merges must have finished first.
+    // the stream, so the previous step's kernels must have finished first.
     const bool grow = s_count + cs_cap > slog_cap || slog_cap > S.cap || l_count + cl_cap > llog_cap ||
-                      llog_cap > PR.cap || llog_cap > SC.cap || 2 * (l_count + cl_cap) > lhash_cap ||
-                      a_count + ca_cap > alog_cap || 2 * (a_count + ca_cap) > ahash_cap ||
-                      p_count + cp_cap > plog_cap || plog_cap > PP.cap || 2 * (p_count + cp_cap) > phash_cap;
+                      2 * (l_count + cl_cap) > lhash_cap || a_count + ca_cap > alog_cap ||
+                      2 * (a_count + ca_cap) > ahash_cap || p_count + cp_cap > plog_cap ||
+                      2 * (p_count + cp_cap) > phash_cap;
     if (grow) sync();
     auto grow_log = [&](uint64_t used, uint64_t add, uint64_t& cap, uint32_t*& a, uint32_t*& b) {
       if (used + add <= cap) return;
@@ -2329,13 +2465,10 @@ bool el_ctx::superstep(uint32_t mask, uint64_t sb, uint64_t se, uint64_t lb, uin
     grow_log(s_count, cs_cap, slog_cap, slog_x, slog_a);
     if (slog_cap > S.cap) S.grow(s_csr_count, slog_cap);
     grow_log(l_count, cl_cap, llog_cap, llog_x, llog_p);
-    if (llog_cap > PR.cap) PR.grow(l_count, llog_cap);
-    if (llog_cap > SC.cap) SC.grow(l_count, llog_cap);
     if (2 * (l_count + cl_cap) > lhash_cap) rehash_links(next_pow2(4 * (l_count + cl_cap)));
     grow_log(a_count, ca_cap, alog_cap, alog_y, alog_c);
     if (2 * (a_count + ca_cap) > ahash_cap) rehash_acts(next_pow2(4 * (a_count + ca_cap)));
     grow_log(p_count, cp_cap, plog_cap, plog_p, plog_b);
-    if (plog_cap > PP.cap) PP.grow(p_count, plog_cap);
     if (2 * (p_count + cp_cap) > phash_cap) rehash_props(next_pow2(4 * (p_count + cp_cap)));
 
     // ---- generation (reads only the state of step t-1; candidate counters are zero here)
@@ -2353,13 +2486,13 @@ bool el_ctx::superstep(uint32_t mask, uint64_t sb, uint64_t se, uint64_t lb, uin
       hipLaunchKernelGGL(k_expand, dim3(ea.gs + ea.gl + ea.ga + ea.gp), dim3(BLOCK), 0, stream, ix, st, ea);
     });
     launch(EL_K_JOBS, [&] {
-      hipLaunchKernelGGL(k_jobs, dim3(1024), dim3(BLOCK), 0, stream, ix, st);
+      hipLaunchKernelGGL(k_jobs, dim3(tune_jobs), dim3(BLOCK), 0, stream, ix, st);
     });
     // ---- commit (counts read on the device); its last block publishes the counters to
     // pinned host memory and zeroes the candidate counters, so the step ends with ONE sync
     CommitArgs ca{};
-    ca.gs = grid_for(cs_cap);
-    ca.gl = grid_for(cl_cap);
+    ca.gs = grid_for(cs_cap, tune_commit);
+    ca.gl = grid_for(cl_cap, tune_commit);
     ca.ga = hx.rng.a.size() ? grid_for(ca_cap, 64) : 0u;
     ca.gp = hx.exl.a.size() ? grid_for(cp_cap, 256) : 0u;
     ca.cs_cap = (uint32_t)cs_cap, ca.cl_cap = (uint32_t)cl_cap;
@@ -2376,28 +2509,16 @@ bool el_ctx::superstep(uint32_t mask, uint64_t sb, uint64_t se, uint64_t lb, uin
     launch(EL_K_COMMIT_S, [&] {
       hipLaunchKernelGGL(k_commit, dim3(ca.gs + ca.gl + ca.ga + ca.gp), dim3(BLOCK), 0, stream, ix, st, ca);
     });
-    // ---- merge the new links / propagations into their CSRs (S rows: lazily, for export)
-    std::vector<MergeReq> reqs;
-    if (hx.P && need_pred) reqs.push_back({&PR, llog_p, llog_x, l_count, l_count, &ctr->l_log, rk_pr});
-    if (need_succ) reqs.push_back({&SC, llog_x, llog_p, l_count, l_count, &ctr->l_log, rk_sc});
-    if (hx.exl.a.size()) reqs.push_back({&PP, plog_p, plog_b, p_count, p_count, &ctr->p_log, rk_pp});
-    launch_merges(reqs);
+    // the new links / propagations are already in their (gapped) CSR rows; S rows are
+    // built lazily, for export only
     wait_commit(ca.pub.seq);
-    std::vector<uint64_t> ends;
-    for (const MergeReq& r : reqs) ends.push_back(r.end_ptr == &ctr->l_log ? hc.l_log : hc.p_log);
-    finish_merges(reqs, ends, true);
     s_count = hc.s_log;
     l_count = hc.l_log;
     a_count = hc.a_log;
     p_count = hc.p_log;
+    gap_rebuild_all();  // rows that outgrew their slack get a new layout before anyone reads them
     // ---- keep the buffers ahead of demand; complete the step if one overflowed
     bool overflow = false;
-    auto regrow2_to = [&](uint64_t cap, uint32_t*& a, uint32_t*& b) {
-      dfree(a);
-      dfree(b);
-      a = dalloc<uint32_t>(cap);
-      b = dalloc<uint32_t>(cap);
-    };
     auto regrow2 = [&](uint32_t need, uint64_t& cap, uint32_t*& a, uint32_t*& b) {
       if (2ull * need <= cap) return;
       sync();  // the step's kernels are still queued: free nothing under them
@@ -2409,15 +2530,12 @@ bool el_ctx::superstep(uint32_t mask, uint64_t sb, uint64_t se, uint64_t lb, uin
       b = dalloc<uint32_t>(cap);
     };
     regrow2(hc.cand_s, cs_cap, cs_x, cs_a);
-    const uint64_t cl_old = cl_cap, cp_old = cp_cap;
     regrow2(hc.cand_l, cl_cap, cl_x, cl_p);
     regrow2(hc.cand_a, ca_cap, ca_y, ca_c);
     regrow2(hc.cand_p, cp_cap, cp_p, cp_b);
-    if (cl_cap != cl_old) regrow2_to(cl_cap, rk_pr, rk_sc);
-    if (cp_cap != cp_old) {
-      dfree(rk_pp);
-      rk_pp = dalloc<uint32_t>(cp_cap + remote_bound());
-    }
+    PR.set_ovq(cl_cap);  // overflow queues hold one step's appends
+    SC.set_ovq(part() ? (uint64_t)part_count * xcap : cl_cap);
+    PP.set_ovq(cp_cap + remote_bound());
     if (2ull * hc.jobs > job_cap) {
       sync();
       overflow |= hc.jobs > job_cap;
@@ -2438,12 +2556,10 @@ void el_ctx::grow_part(uint64_t new_xcap) {
     xcap = new_xcap;
     dfree(xsend);
     dfree(xrecv);
-    dfree(rk_x);
     xsend = dalloc<uint32_t>(XH + 2 * xcap);
     xrecv = dalloc<uint32_t>((uint64_t)part_count * (XH + 2 * xcap));
-    rk_x = dalloc<uint32_t>((uint64_t)part_count * xcap);
-    dfree(rk_pp);
-    rk_pp = dalloc<uint32_t>(cp_cap + remote_bound());
+    if (SC.live) SC.set_ovq((uint64_t)part_count * xcap);
+    if (PP.live) PP.set_ovq(cp_cap + remote_bound());
   }
   const uint64_t rb = remote_bound(), xb = (uint64_t)part_count * xcap;
   auto grow_log = [&](uint64_t used, uint64_t need, uint64_t& cap, uint32_t*& a, uint32_t*& b) {
@@ -2454,17 +2570,15 @@ void el_ctx::grow_part(uint64_t new_xcap) {
     cap = c;
   };
   grow_log(p_count, p_count + cp_cap + rb, plog_cap, plog_p, plog_b);
-  if (plog_cap > PP.cap) PP.grow(p_count, plog_cap);
   if (2 * (p_count + cp_cap + rb) > phash_cap) rehash_props(next_pow2(4 * (p_count + cp_cap + rb)));
   grow_log(a_count, a_count + ca_cap + rb, alog_cap, alog_y, alog_c);
   if (2 * (a_count + ca_cap + rb) > ahash_cap) rehash_acts(next_pow2(4 * (a_count + ca_cap + rb)));
   grow_log(x_count, x_count + xb, xlog_cap, xlog_x, xlog_p);
-  if (xlog_cap > SC.cap) SC.grow(x_count, xlog_cap);
 }
 
 // Pack this rank's new records, all-gather every rank's, import them, merge the CSRs.
 // Returns after the import published; hc then holds the global g_* words.
-uint32_t el_ctx::exchange_round(uint32_t s0, uint32_t l0, uint32_t a0, uint32_t p0, std::vector<MergeReq>& reqs) {
+uint32_t el_ctx::exchange_round(uint32_t s0, uint32_t l0, uint32_t a0, uint32_t p0) {
   DState st = dstate();
   XchgArgs xa{};
   xa.send = xsend;
@@ -2482,21 +2596,13 @@ uint32_t el_ctx::exchange_round(uint32_t s0, uint32_t l0, uint32_t a0, uint32_t 
   hipLaunchKernelGGL(k_ximport, dim3(grid_for((uint64_t)part_count * xcap, 256)), dim3(BLOCK), 0, stream, ix, st,
                      xa, PubArgs{hc_dev, commit_done, seq});
   HIPCHK(hipGetLastError());
-  reqs.clear();
-  if (hx.P && need_pred) reqs.push_back({&PR, llog_p, llog_x, l_count, l_count, &ctr->l_log, rk_pr});
-  if (need_succ) reqs.push_back({&SC, xlog_x, xlog_p, x_count, x_count, &ctr->x_log, rk_x});
-  if (use_props) reqs.push_back({&PP, plog_p, plog_b, p_count, p_count, &ctr->p_log, rk_pp});
-  launch_merges(reqs);
   wait_commit(seq);
-  std::vector<uint64_t> ends;
-  for (const MergeReq& r : reqs)
-    ends.push_back(r.end_ptr == &ctr->l_log ? hc.l_log : r.end_ptr == &ctr->x_log ? hc.x_log : hc.p_log);
-  finish_merges(reqs, ends, true);
   s_count = hc.s_log;
   l_count = hc.l_log;
   a_count = hc.a_log;
   p_count = hc.p_log;
   x_count = hc.x_log;
+  gap_rebuild_all();
   return hc.g_max;
 }
 
@@ -2507,16 +2613,13 @@ uint32_t el_ctx::exchange_round(uint32_t s0, uint32_t l0, uint32_t a0, uint32_t 
 uint64_t el_ctx::superstep_part(uint32_t mask, uint64_t sb, uint64_t se, uint64_t lb, uint64_t le, uint64_t ab,
                                 uint64_t ae, uint64_t pb, uint64_t pe, uint64_t xb, uint64_t xe) {
   uint64_t gdelta = 0;
-  std::vector<MergeReq> reqs;
   for (int attempt = 0;; ++attempt) {
     // ---- capacities for the local candidates (as in superstep) and the remote imports
     const uint64_t rb = remote_bound();
     const bool grow = s_count + cs_cap > slog_cap || slog_cap > S.cap || l_count + cl_cap > llog_cap ||
-                      llog_cap > PR.cap || 2 * (l_count + cl_cap) > lhash_cap ||
-                      a_count + ca_cap + rb > alog_cap || 2 * (a_count + ca_cap + rb) > ahash_cap ||
-                      p_count + cp_cap + rb > plog_cap || plog_cap > PP.cap ||
-                      2 * (p_count + cp_cap + rb) > phash_cap || x_count + part_count * xcap > xlog_cap ||
-                      xlog_cap > SC.cap;
+                      2 * (l_count + cl_cap) > lhash_cap || a_count + ca_cap + rb > alog_cap || 2 * (a_count + ca_cap + rb) > ahash_cap ||
+                      p_count + cp_cap + rb > plog_cap || 2 * (p_count + cp_cap + rb) > phash_cap ||
+                      x_count + part_count * xcap > xlog_cap;
     if (grow) {
       sync();
       auto grow_log = [&](uint64_t used, uint64_t add, uint64_t& cap, uint32_t*& a, uint32_t*& b) {
@@ -2529,7 +2632,6 @@ uint64_t el_ctx::superstep_part(uint32_t mask, uint64_t sb, uint64_t se, uint64_
       grow_log(s_count, cs_cap, slog_cap, slog_x, slog_a);
       if (slog_cap > S.cap) S.grow(s_csr_count, slog_cap);
       grow_log(l_count, cl_cap, llog_cap, llog_x, llog_p);
-      if (llog_cap > PR.cap) PR.grow(l_count, llog_cap);
       if (2 * (l_count + cl_cap) > lhash_cap) rehash_links(next_pow2(4 * (l_count + cl_cap)));
       grow_part(xcap);
     }
@@ -2553,11 +2655,11 @@ uint64_t el_ctx::superstep_part(uint32_t mask, uint64_t sb, uint64_t se, uint64_
     const uint32_t eg = ea.gs + ea.gl + ea.ga + ea.gp + ea.gx;
     if (eg) {
       launch(EL_K_EXPAND_S, [&] { hipLaunchKernelGGL(k_expand, dim3(eg), dim3(BLOCK), 0, stream, ix, st, ea); });
-      launch(EL_K_JOBS, [&] { hipLaunchKernelGGL(k_jobs, dim3(1024), dim3(BLOCK), 0, stream, ix, st); });
+      launch(EL_K_JOBS, [&] { hipLaunchKernelGGL(k_jobs, dim3(tune_jobs), dim3(BLOCK), 0, stream, ix, st); });
     }
     CommitArgs ca{};
-    ca.gs = grid_for(cs_cap);
-    ca.gl = grid_for(cl_cap);
+    ca.gs = grid_for(cs_cap, tune_commit);
+    ca.gl = grid_for(cl_cap, tune_commit);
     ca.ga = hx.rng.a.size() ? grid_for(ca_cap, 64) : 0u;
     ca.gp = use_props ? grid_for(cp_cap, 256) : 0u;
     ca.cs_cap = (uint32_t)cs_cap, ca.cl_cap = (uint32_t)cl_cap;
@@ -2568,10 +2670,10 @@ uint64_t el_ctx::superstep_part(uint32_t mask, uint64_t sb, uint64_t se, uint64_
     });
 
     // ---- delta exchange; a too-small exchange imports nothing and is redone larger
-    uint32_t gmax = exchange_round(s0, l0, a0, p0, reqs);
+    uint32_t gmax = exchange_round(s0, l0, a0, p0);
     if (gmax > xcap) {
       grow_part(next_pow2(gmax));
-      gmax = exchange_round(s0, l0, a0, p0, reqs);
+      gmax = exchange_round(s0, l0, a0, p0);
       if (gmax > xcap) throw std::runtime_error("exchange overflow after growth");
     }
     gdelta += hc.g_delta;
@@ -2589,18 +2691,14 @@ uint64_t el_ctx::superstep_part(uint32_t mask, uint64_t sb, uint64_t se, uint64_
     };
     regrow2(hc.cand_s, cs_cap, cs_x, cs_a);
     if (regrow2(hc.cand_l, cl_cap, cl_x, cl_p)) {
-      dfree(rk_pr);
       dfree(xs_x);
       dfree(xs_p);
-      rk_pr = dalloc<uint32_t>(cl_cap);
       xs_x = dalloc<uint32_t>(cl_cap);
       xs_p = dalloc<uint32_t>(cl_cap);
+      PR.set_ovq(cl_cap);
     }
     regrow2(hc.cand_a, ca_cap, ca_y, ca_c);
-    if (regrow2(hc.cand_p, cp_cap, cp_p, cp_b)) {
-      dfree(rk_pp);
-      rk_pp = dalloc<uint32_t>(cp_cap + remote_bound());
-    }
+    if (regrow2(hc.cand_p, cp_cap, cp_p, cp_b)) PP.set_ovq(cp_cap + remote_bound());
     if (2ull * hc.jobs > job_cap) {
       sync();
       job_cap = next_pow2(2ull * hc.jobs + 1024);
@@ -2610,6 +2708,77 @@ uint64_t el_ctx::superstep_part(uint32_t mask, uint64_t sb, uint64_t se, uint64_
     if (hc.g_ovf == 0) break;
   }
   return gdelta;
+}
+
+// Re-lay out a gapped CSR whose rows overflowed this step: every row gets gap_cap(len)
+// slots (exclusive scan), its in-place entries move, the overflow records land at their
+// rank.  Events mirror the CPU oracle (same formula as a CSR merge with `entries` - n_ovf
+// moved and n_ovf placed entries).
+void el_ctx::gap_rebuild(GapCsr& g, uint32_t n_ovf, uint64_t entries) {
+  if (n_ovf > g.ovq_cap) throw std::runtime_error("gapped-CSR overflow queue overrun");
+  const uint32_t R = g.rows;
+  // Σ_r gap_cap(len[r]) with Σ len = entries: the host sizes the new layout without a readback
+  const uint64_t total = 4 * entries + (uint64_t)gap_cap(0) * R;
+  if (total > 0xffffffffull) throw ElError{EL_ENOMEM, "gapped CSR beyond 2^32 slots"};
+  if (total > g.val2_cap) {
+    sync();
+    dfree(g.val2);
+    g.val2_cap = total + total / 2;
+    g.val2 = dalloc<uint32_t>(g.val2_cap);
+  }
+  // new row starts: the single-pass look-back scan of k_scan_merge over gap_cap(len)
+  MergeArgs m{};
+  m.nseg = 1;
+  m.seg[0].ptr2 = g.start2;
+  m.seg[0].n1 = R + 1;
+  m.seg[0].gap_len = g.len;
+  ScanArgs sa{};
+  const uint32_t tiles = (R + 1 + SCAN_TILE - 1) / SCAN_TILE;
+  if (tiles > scan_tiles) throw std::runtime_error("scan tile overflow");
+  sa.tile0[0] = 0;
+  sa.tile0[1] = tiles;
+  if (++scan_epoch >= (1u << 30)) {
+    HIPCHK(hipMemsetAsync(scan_flags, 0, scan_tiles * sizeof(unsigned long long), stream));
+    scan_epoch = 1;
+  }
+  sa.epoch = scan_epoch;
+  sa.flags = scan_flags;
+  sa.ticket = &ctr->ticket;
+  launch(EL_K_SCAN, [&] {
+    hipLaunchKernelGGL(k_scan_merge, dim3(tiles), dim3(256), 0, stream, m, sa, dcnt_all, dscan_all);
+  });
+  launch(EL_K_SCATTER_OLD, [&] {
+    hipLaunchKernelGGL(k_gap_move, dim3(grid_for((uint64_t)R * 64, 1024)), dim3(BLOCK), 0, stream, g.start, g.len,
+                       g.val, g.start2, g.val2, R);
+  });
+  if (n_ovf)
+    launch(EL_K_SCATTER_NEW, [&] {
+      hipLaunchKernelGGL(k_gap_ovf, dim3(grid_for(n_ovf)), dim3(BLOCK), 0, stream, g.ovq, n_ovf, g.start2, g.val2);
+    });
+  std::swap(g.start, g.start2);
+  std::swap(g.val, g.val2);
+  std::swap(g.val_cap, g.val2_cap);
+  const uint64_t n1 = (uint64_t)R + 1, moved = entries - n_ovf;
+  host_ev[EL_K_SCAN][EL_EV_ENT] += 3 * n1;        // read len, write caps, scan
+  host_ev[EL_K_MERGE_PTR][EL_EV_ENT] += 2 * n1;   // old and new row starts
+  host_ev[EL_K_SCATTER_OLD][EL_EV_TRIG] += moved;
+  host_ev[EL_K_SCATTER_OLD][EL_EV_ENT] += moved;
+  host_ev[EL_K_SCATTER_OLD][EL_EV_EMIT] += moved;
+  host_ev[EL_K_SCATTER_NEW][EL_EV_TRIG] += n_ovf;
+  host_ev[EL_K_SCATTER_NEW][EL_EV_ENT] += 3ull * n_ovf;
+  host_ev[EL_K_SCATTER_NEW][EL_EV_EMIT] += n_ovf;
+}
+
+void el_ctx::gap_rebuild_all() {
+  const uint32_t ov[3] = {hc.ov_pr, hc.ov_sc, hc.ov_pp};
+  if (!(ov[0] | ov[1] | ov[2])) return;
+  GapCsr* gs[3] = {&PR, &SC, &PP};
+  const uint64_t entries[3] = {l_count, part() ? x_count : l_count, p_count};
+  for (int i = 0; i < 3; ++i)
+    if (ov[i]) gap_rebuild(*gs[i], ov[i], entries[i]);
+  // the overflow counters start over (stream-ordered after the re-layout kernels)
+  HIPCHK(hipMemsetAsync(&ctr->ov_pr, 0, 3 * CTR_STRIDE * sizeof(uint32_t), stream));
+  hc.ov_pr = hc.ov_sc = hc.ov_pp = 0;
 }
 
 void el_ctx::fill_stats(el_stats* out, double ms) {

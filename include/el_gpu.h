@@ -171,10 +171,10 @@ typedef enum el_kernel {
   EL_K_COMMIT_S = 4,     /* k_commit, S role:    bit-row atomicOr dedup + ΔS append */
   EL_K_COMMIT_L = 5,     /* k_commit, link role: link hash-set dedup + Δlink append */
   EL_K_COMMIT_A = 6,     /* k_commit, activation role: activation set dedup */
-  EL_K_SCAN = 7,         /* k_scan_merge: single-pass scan of the per-row delta counts */
-  EL_K_MERGE_PTR = 8,    /* k_scan_merge: new row offsets */
-  EL_K_SCATTER_OLD = 9,  /* k_scatter_old: move existing CSR entries */
-  EL_K_SCATTER_NEW = 10, /* k_scatter_new: place delta entries */
+  EL_K_SCAN = 7,         /* k_gap_caps: re-layout of a gapped CSR whose rows overflowed: row capacities */
+  EL_K_MERGE_PTR = 8,    /*   … and their scan into new row starts (library scan, carried by k_gap_caps) */
+  EL_K_SCATTER_OLD = 9,  /* k_gap_move: in-place entries to their new rows */
+  EL_K_SCATTER_NEW = 10, /* k_gap_ovf: overflow entries placed at their rank */
   EL_K_INIT = 11,        /* k_init:      S(X) = {X, ⊤} */
   EL_K_REHASH = 12,      /* k_rehash:    link / activation / propagation set growth */
   EL_K_EXPAND_P = 13,    /* k_expand, propagation role: new CR4 propagations × predecessors */

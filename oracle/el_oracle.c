@@ -210,6 +210,10 @@ struct elo_ctx {
   vec* prow; /* propagations per pid */
   uint64_t s_init;
   int need_pred, need_succ; /* the GPU maintains these CSRs only when they have readers */
+  /* slack capacities of the GPU's gapped CSR rows (predecessors, successors, propagations)
+   * and this step's entries past them: the GPU re-lays out a CSR after a step with any */
+  uint32_t *cap_pr, *cap_sc, *cap_pp;
+  uint64_t ov_pr, ov_sc, ov_pp;
   uint64_t wm_s[EL_NUM_RULE_TYPES], wm_l[EL_NUM_RULE_TYPES], wm_a[EL_NUM_RULE_TYPES], wm_p[EL_NUM_RULE_TYPES];
   uint64_t ev[EL_NUM_KERNELS][EL_NUM_EVENTS];
   vec tr_s, tr_l, tr_a; /* low 32 bits suffice for tests */
@@ -228,6 +232,9 @@ static int setbit(elo_ctx* c, uint32_t x, uint32_t b) { /* returns 1 if newly se
   *w |= m;
   return 1;
 }
+
+/* gapped-CSR row capacity after a re-layout: gap_cap() in distel_amd/csrc/el_gpu.hip */
+#define GAP_CAP(n) (4u * (uint32_t)(n) + 16u)
 
 #define EV(k, e) (c->ev[(k)][(e)]++)
 #define EVN(k, e, n) (c->ev[(k)][(e)] += (n))
@@ -526,6 +533,14 @@ int elo_create(elo_ctx** out, const el_axioms* ax, int mode) {
   c->succ = (vec*)calloc(c->N, sizeof(vec));
   c->has_act = (uint8_t*)calloc(c->N, 1);
   c->prow = (vec*)calloc(c->P ? c->P : 1, sizeof(vec));
+  c->cap_pr = (uint32_t*)malloc((c->P ? c->P : 1) * sizeof(uint32_t));
+  c->cap_pp = (uint32_t*)malloc((c->P ? c->P : 1) * sizeof(uint32_t));
+  c->cap_sc = (uint32_t*)malloc((c->N ? c->N : 1) * sizeof(uint32_t));
+  {
+    uint32_t q;
+    for (q = 0; q < (c->P ? c->P : 1); ++q) c->cap_pr[q] = c->cap_pp[q] = GAP_CAP(0);
+    for (q = 0; q < c->N; ++q) c->cap_sc[q] = GAP_CAP(0);
+  }
   hs_init(&c->props, 1024);
   hs_init(&c->links, 1024);
   hs_init(&c->acts, 64);
@@ -856,9 +871,22 @@ static void expand_p(elo_ctx* c, cands* k, uint64_t pb, uint64_t pe) {
   }
 }
 
-/* analytic events of the CSR merge of one CSR with nn new entries (same formula as the GPU
- * host side): scan of the row counts (read, zero, write), new row offsets, the moved
- * entries, and the delta entries placed by their recorded rank */
+/* append of one entry to a gapped CSR row holding n entries with capacity cap (gap_append
+ * on the GPU): the len atomic, the row bounds, the value; past the capacity a 3-word
+ * overflow record */
+static void gap_append_ev(elo_ctx* c, int K, uint64_t n, uint32_t cap, uint64_t* ov) {
+  EV(K, EL_EV_RMW);
+  EV(K, EL_EV_ROW);
+  EV(K, EL_EV_ENT);
+  if (n >= cap) {
+    EVN(K, EL_EV_ENT, 2);
+    ++*ov;
+  }
+}
+
+/* analytic events of a re-layout (and formerly of a CSR merge) with old_n moved and nn
+ * placed entries (same formula as the GPU host side): the row capacities and their scan,
+ * old and new row starts, the moved entries, and the overflow entries placed by rank */
 static void merge_seg_events(elo_ctx* c, uint64_t nrows, uint64_t old_n, uint64_t nn) {
   uint64_t n1 = nrows + 1;
   EVN(EL_K_SCAN, EL_EV_ENT, 3 * n1);
@@ -869,6 +897,14 @@ static void merge_seg_events(elo_ctx* c, uint64_t nrows, uint64_t old_n, uint64_
   EVN(EL_K_SCATTER_NEW, EL_EV_TRIG, nn);
   EVN(EL_K_SCATTER_NEW, EL_EV_ENT, 3 * nn);
   EVN(EL_K_SCATTER_NEW, EL_EV_EMIT, nn);
+}
+
+static void gap_step_end(elo_ctx* c, const vec* rows, uint32_t R, uint32_t* cap, uint64_t* ov, uint64_t entries) {
+  uint32_t r;
+  if (!*ov) return;
+  merge_seg_events(c, R, entries - *ov, *ov);
+  for (r = 0; r < R; ++r) cap[r] = GAP_CAP(rows[r].n);
+  *ov = 0;
 }
 
 static int superstep(elo_ctx* c, uint32_t mask, uint64_t sb, uint64_t se, uint64_t lb, uint64_t le,
@@ -907,7 +943,8 @@ static int superstep(elo_ctx* c, uint32_t mask, uint64_t sb, uint64_t se, uint64
     EV(EL_K_COMMIT_L, EL_EV_HASH);
     if (hs_add(&c->links, lkey(p, x))) {
       EV(EL_K_COMMIT_L, EL_EV_EMIT);
-      EVN(EL_K_COMMIT_L, EL_EV_ENT, (uint64_t)(c->need_pred != 0) + (c->need_succ != 0)); /* merge ranks */
+      if (c->need_pred) gap_append_ev(c, EL_K_COMMIT_L, c->pred[p].n, c->cap_pr[p], &c->ov_pr);
+      if (c->need_succ) gap_append_ev(c, EL_K_COMMIT_L, c->succ[x].n, c->cap_sc[x], &c->ov_sc);
       vpush(&c->llog_x, x);
       vpush(&c->llog_p, p);
       vpush(&c->pred[p], x);
@@ -931,17 +968,18 @@ static int superstep(elo_ctx* c, uint32_t mask, uint64_t sb, uint64_t se, uint64
     EV(EL_K_COMMIT_P, EL_EV_HASH);
     if (hs_add(&c->props, lkey(pid, b))) {
       EV(EL_K_COMMIT_P, EL_EV_EMIT);
-      EV(EL_K_COMMIT_P, EL_EV_ENT); /* merge rank */
+      gap_append_ev(c, EL_K_COMMIT_P, c->prow[pid].n, c->cap_pp[pid], &c->ov_pp);
       vpush(&c->plog_p, pid);
       vpush(&c->plog_b, b);
       vpush(&c->prow[pid], b);
     }
   }
   cands_free(&k);
-  /* the S-row CSR is not read during saturation (built lazily for export) */
-  if (c->llog_x.n > l0 && c->P && c->need_pred) merge_seg_events(c, c->P, l0, c->llog_x.n - l0);
-  if (c->llog_x.n > l0 && c->need_succ) merge_seg_events(c, c->N, l0, c->llog_x.n - l0);
-  if (c->plog_p.n > p0) merge_seg_events(c, c->P, p0, c->plog_p.n - p0);
+  /* the S-row CSR is not read during saturation (built lazily for export); a gapped CSR
+   * with overflowing rows is re-laid out */
+  gap_step_end(c, c->pred, c->P, c->cap_pr, &c->ov_pr, c->llog_x.n);
+  gap_step_end(c, c->succ, c->N, c->cap_sc, &c->ov_sc, c->llog_x.n);
+  gap_step_end(c, c->prow, c->P, c->cap_pp, &c->ov_pp, c->plog_p.n);
   return c->slog_x.n > s0 || c->llog_x.n > l0 || c->alog_y.n > a0 || c->plog_p.n > p0;
 }
 
@@ -1221,6 +1259,7 @@ void elo_destroy(elo_ctx* c) {
     for (i = 0; i < c->P; ++i) free(c->prow[i].v);
   free(c->prow), free(c->props.t), free(c->plog_p.v), free(c->plog_b.v);
   free(c->srow), free(c->succ), free(c->pred), free(c->has_act);
+  free(c->cap_pr), free(c->cap_sc), free(c->cap_pp);
   free(c->slog_x.v), free(c->slog_a.v), free(c->llog_x.v), free(c->llog_p.v);
   free(c->alog_y.v), free(c->alog_c.v), free(c->tr_s.v), free(c->tr_l.v), free(c->tr_a.v);
   free(c->links.t), free(c->acts.t), free(c->cube);
