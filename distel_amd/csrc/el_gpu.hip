@@ -136,8 +136,9 @@ constexpr uint32_t CTR_STRIDE = 64;  // words
 // Counters [0, CTR_KEEP) persist across steps; the rest are per-step (zeroed by k_commit).
 // x_log / x_send / g_delta / g_max belong to the partitioned exchange (k_ximport).
 // ov_* count the entries of this step that did not fit their slack row (gapped CSRs below).
+// cand_t counts the CR1 told-closure candidates (committed first, by k_commit_told).
 #define EL_COUNTERS(X) X(s_log) X(l_log) X(a_log) X(p_log) X(x_log) X(x_send) X(ov_pr) X(ov_sc) X(ov_pp) \
-  X(cand_s) X(cand_l) X(cand_a) X(jobs) X(cand_p) X(g_delta) X(g_max) X(g_ovf) X(ticket) X(seq)
+  X(cand_s) X(cand_l) X(cand_a) X(jobs) X(cand_p) X(cand_t) X(g_delta) X(g_max) X(g_ovf) X(ticket) X(seq)
 constexpr uint32_t CTR_KEEP = 9;
 #define EL_CTR_DEV(n) uint32_t n; uint32_t n##_pad[CTR_STRIDE - 1];
 #define EL_CTR_HOST(n) uint32_t n;
@@ -177,6 +178,7 @@ __host__ __device__ constexpr uint32_t gap_cap(uint32_t n) { return 4 * n + 16; 
 struct DState {
   uint32_t* bits;
   uint32_t *slog_x, *slog_a;
+  uint8_t* slog_f;  // 1: the fact came out of a CR1 told closure (its own closure is already out)
   unsigned long long* lhash;
   unsigned long long lmask;
   uint32_t *llog_x, *llog_p;
@@ -198,6 +200,7 @@ struct DState {
   uint32_t *xlog_x, *xlog_p;
   uint32_t *xs_x, *xs_p;
   uint32_t *cs_x, *cs_a, cs_cap;
+  uint32_t *ct_x, *ct_a, ct_cap;  // CR1 told-closure candidates
   uint32_t *cl_x, *cl_p, cl_cap;
   uint32_t *ca_y, *ca_c, ca_cap;
   uint4* jobs;
@@ -384,25 +387,9 @@ __device__ __forceinline__ uint32_t pair_lookup(const DIndex& ix, uint32_t r, ui
   return NONE;
 }
 
-// Block-level staging of appended records in LDS.  A single global append counter
-// saturates at ~88 atomics/us (MI355X_MICROARCH.md, row "dequeue"), so candidates are
-// reserved with an LDS atomic per wave and published with ONE global atomic per block
-// flush (>= QS_CAP/2 records).  A full LDS queue spills straight to global memory.
-constexpr uint32_t QS_CAP = 1024;  // S candidates (x, a)
-constexpr uint32_t QL_CAP = 1024;  // link candidates (x, pid)
-constexpr uint32_t QJ_CAP = 256;   // fan-out jobs
-
-struct BlockQ {
-  uint4 jb[QJ_CAP];
-  uint32_t sx[QS_CAP], sa[QS_CAP];
-  uint32_t lx[QL_CAP], lp[QL_CAP];
-  uint32_t ns, nl, nj, bs, bl, bj;
-};
-
-__device__ __forceinline__ void q_init(BlockQ& q) {
-  if (threadIdx.x == 0) q.ns = q.nl = q.nj = 0;
-  __syncthreads();
-}
+// LDS staging of the commit roles (new facts / links of a block round)
+constexpr uint32_t QS_CAP = 1024;
+constexpr uint32_t QL_CAP = 1024;
 
 // LDS slot for each predicated lane (one LDS atomic per wave)
 __device__ __forceinline__ uint32_t lds_reserve(uint32_t* qn, bool pred) {
@@ -415,51 +402,107 @@ __device__ __forceinline__ uint32_t lds_reserve(uint32_t* qn, bool pred) {
   return pred ? off + (uint32_t)__popcll(m & ((1ull << lane_id()) - 1ull)) : NONE;
 }
 
-__device__ __forceinline__ void emit_s(const DState& st, BlockQ& q, bool pred, uint32_t x, uint32_t a, Ev& ev) {
-  const uint32_t off = lds_reserve(&q.ns, pred);
-  const bool spill = pred && off >= QS_CAP;
-  if (pred) {
-    ev.v[EL_EV_EMIT]++;
-    if (!spill) {
-      q.sx[off] = x;
-      q.sa[off] = a;
+// Wave-private staging of appended records in LDS.  A single global append counter
+// serialises same-address atomics (MI355X_MICROARCH.md, "fanin": ≈12 ns each), so each
+// wave stages its candidates in its own LDS queues and publishes a full queue with ONE
+// global atomic (WQ records).  No block barrier is involved, so a wave may flush in the
+// middle of a divergent inner loop (a told closure, a fan-out row): only the wave's
+// active lanes take part, and LDS accesses of one wave execute in program order.
+constexpr uint32_t WQ = 256;   // (x, a) / (x, pid) records per wave and queue
+constexpr uint32_t WQJ = 64;   // fan-out job records per wave
+
+struct WaveQ {
+  uint32_t sx[WQ], sa[WQ];  // S candidates
+  uint32_t tx[WQ], ta[WQ];  // CR1 told-closure candidates
+  uint32_t lx[WQ], lp[WQ];  // link candidates
+  uint4 jb[WQJ];            // fan-out jobs
+  uint32_t ns, nt, nl, nj;
+};
+struct BlockQ {
+  WaveQ w[BLOCK / 64];
+};
+
+__device__ __forceinline__ WaveQ& wave_q(BlockQ& q) { return q.w[threadIdx.x >> 6]; }
+
+__device__ __forceinline__ void q_init(BlockQ& q) {
+  WaveQ& w = wave_q(q);
+  if (lane_id() == 0) w.ns = w.nt = w.nl = w.nj = 0;
+  __syncthreads();
+}
+
+// Publish n staged records of this wave: one atomic, the active lanes copy.
+template <class T>
+__device__ __forceinline__ void wq_publish(const T* qa, const uint32_t* qb, uint32_t n, uint32_t* gcnt, T* ga,
+                                           uint32_t* gb, uint32_t gcap) {
+  if (n == 0) return;
+  const unsigned long long act = __ballot(true);
+  const int leader = __ffsll((long long)act) - 1;
+  uint32_t base = 0;
+  if ((int)lane_id() == leader) base = atomicAdd(gcnt, n);
+  base = __shfl(base, leader);
+  const uint32_t na = (uint32_t)__popcll(act), r = (uint32_t)__popcll(act & ((1ull << lane_id()) - 1ull));
+  for (uint32_t k = r; k < n; k += na) {
+    const uint32_t slot = base + k;
+    if (slot < gcap) {
+      ga[slot] = qa[k];
+      if (gb) gb[slot] = qb[k];
     }
-  }
-  const uint32_t slot = wave_append(&st.ctr->cand_s, spill);
-  if (spill && slot < st.cs_cap) {
-    st.cs_x[slot] = x;
-    st.cs_a[slot] = a;
   }
 }
 
-__device__ __forceinline__ void emit_l(const DState& st, BlockQ& q, bool pred, uint32_t x, uint32_t pid, Ev& ev) {
-  const uint32_t off = lds_reserve(&q.nl, pred);
-  const bool spill = pred && off >= QL_CAP;
+// Stage (a, b) for the predicated lanes; a full queue is published first.
+__device__ __forceinline__ void wq_push(uint32_t* qa, uint32_t* qb, uint32_t& qn, bool pred, uint32_t a, uint32_t b,
+                                        uint32_t* gcnt, uint32_t* ga, uint32_t* gb, uint32_t gcap) {
+  const unsigned long long m = __ballot(pred);
+  if (m == 0) return;
+  const uint32_t cnt = (uint32_t)__popcll(m);
+  uint32_t n = qn;
+  if (n + cnt > WQ) {
+    wq_publish(qa, qb, n, gcnt, ga, gb, gcap);
+    n = 0;
+  }
   if (pred) {
-    ev.v[EL_EV_EMIT]++;
-    if (!spill) {
-      q.lx[off] = x;
-      q.lp[off] = pid;
-    }
+    const uint32_t r = n + (uint32_t)__popcll(m & ((1ull << lane_id()) - 1ull));
+    qa[r] = a;
+    qb[r] = b;
   }
-  const uint32_t slot = wave_append(&st.ctr->cand_l, spill);
-  if (spill && slot < st.cl_cap) {
-    st.cl_x[slot] = x;
-    st.cl_p[slot] = pid;
-  }
+  if ((int)lane_id() == __ffsll((long long)__ballot(true)) - 1) qn = n + cnt;
+}
+
+__device__ __forceinline__ void emit_s(const DState& st, BlockQ& q, bool pred, uint32_t x, uint32_t a, Ev& ev) {
+  WaveQ& w = wave_q(q);
+  if (pred) ev.v[EL_EV_EMIT]++;
+  wq_push(w.sx, w.sa, w.ns, pred, x, a, &st.ctr->cand_s, st.cs_x, st.cs_a, st.cs_cap);
+}
+
+__device__ __forceinline__ void emit_t(const DState& st, BlockQ& q, bool pred, uint32_t x, uint32_t a, Ev& ev) {
+  WaveQ& w = wave_q(q);
+  if (pred) ev.v[EL_EV_EMIT]++;
+  wq_push(w.tx, w.ta, w.nt, pred, x, a, &st.ctr->cand_t, st.ct_x, st.ct_a, st.ct_cap);
+}
+
+__device__ __forceinline__ void emit_l(const DState& st, BlockQ& q, bool pred, uint32_t x, uint32_t pid, Ev& ev) {
+  WaveQ& w = wave_q(q);
+  if (pred) ev.v[EL_EV_EMIT]++;
+  wq_push(w.lx, w.lp, w.nl, pred, x, pid, &st.ctr->cand_l, st.cl_x, st.cl_p, st.cl_cap);
 }
 
 __device__ __forceinline__ void emit_job1(const DState& st, BlockQ& q, bool pred, uint32_t type, uint32_t begin,
                                           uint32_t len, uint32_t a, uint32_t b, Ev& ev) {
-  const uint32_t off = lds_reserve(&q.nj, pred);
-  const bool spill = pred && off >= QJ_CAP;
-  const uint4 rec = make_uint4(begin, len | (type << 28), a, b);
+  WaveQ& w = wave_q(q);
+  const unsigned long long m = __ballot(pred);
+  if (m == 0) return;
+  const uint32_t cnt = (uint32_t)__popcll(m);
+  uint32_t n = w.nj;
+  if (n + cnt > WQJ) {
+    wq_publish<uint4>(w.jb, nullptr, n, &st.ctr->jobs, st.jobs, nullptr, st.job_cap);
+    n = 0;
+  }
   if (pred) {
     ev.v[EL_EV_JOB]++;
-    if (!spill) q.jb[off] = rec;
+    w.jb[n + (uint32_t)__popcll(m & ((1ull << lane_id()) - 1ull))] = make_uint4(begin, len | (type << 28), a, b);
   }
-  const uint32_t slot = wave_append(&st.ctr->jobs, spill);
-  if (spill && slot < st.job_cap) st.jobs[slot] = rec;
+  if ((int)lane_id() == __ffsll((long long)__ballot(true)) - 1) w.nj = n + cnt;
 }
 
 // A fan-out list of len items becomes ceil(len / JOB_CHUNK) job records, so one hub
@@ -500,45 +543,19 @@ __device__ __forceinline__ void emit_p(const DState& st, bool pred, uint32_t pid
   }
 }
 
-// Publish the block's staged records: one global atomic per non-empty queue.
-// Every thread of the block must call this (it contains barriers).
+// Publish what this wave still has staged (every lane of the block calls it at the end
+// of its role, so the staged records of the step are all in the global queues).
 __device__ void q_flush(BlockQ& q, const DState& st) {
-  __syncthreads();
-  const uint32_t ns = min(q.ns, QS_CAP), nl = min(q.nl, QL_CAP), nj = min(q.nj, QJ_CAP);
-  if (threadIdx.x == 0) {
-    q.bs = ns ? atomicAdd(&st.ctr->cand_s, ns) : 0u;
-    q.bl = nl ? atomicAdd(&st.ctr->cand_l, nl) : 0u;
-    q.bj = nj ? atomicAdd(&st.ctr->jobs, nj) : 0u;
-  }
-  __syncthreads();
-  for (uint32_t k = threadIdx.x; k < ns; k += blockDim.x) {
-    const uint32_t slot = q.bs + k;
-    if (slot < st.cs_cap) {
-      st.cs_x[slot] = q.sx[k];
-      st.cs_a[slot] = q.sa[k];
-    }
-  }
-  for (uint32_t k = threadIdx.x; k < nl; k += blockDim.x) {
-    const uint32_t slot = q.bl + k;
-    if (slot < st.cl_cap) {
-      st.cl_x[slot] = q.lx[k];
-      st.cl_p[slot] = q.lp[k];
-    }
-  }
-  for (uint32_t k = threadIdx.x; k < nj; k += blockDim.x) {
-    const uint32_t slot = q.bj + k;
-    if (slot < st.job_cap) st.jobs[slot] = q.jb[k];
-  }
-  __syncthreads();
-  if (threadIdx.x == 0) q.ns = q.nl = q.nj = 0;
-  __syncthreads();
+  WaveQ& w = wave_q(q);
+  wq_publish(w.sx, w.sa, w.ns, &st.ctr->cand_s, st.cs_x, st.cs_a, st.cs_cap);
+  wq_publish(w.tx, w.ta, w.nt, &st.ctr->cand_t, st.ct_x, st.ct_a, st.ct_cap);
+  wq_publish(w.lx, w.lp, w.nl, &st.ctr->cand_l, st.cl_x, st.cl_p, st.cl_cap);
+  wq_publish<uint4>(w.jb, nullptr, w.nj, &st.ctr->jobs, st.jobs, nullptr, st.job_cap);
+  if (lane_id() == 0) w.ns = w.nt = w.nl = w.nj = 0;
 }
 
-// Called by every thread after each block-uniform loop round.
-__device__ __forceinline__ void q_maybe_flush(BlockQ& q, const DState& st) {
-  __syncthreads();
-  if (q.ns > QS_CAP / 2 || q.nl > QL_CAP / 2 || q.nj > QJ_CAP / 2) q_flush(q, st);
-}
+// The wave queues publish themselves when full: nothing to do between loop rounds.
+__device__ __forceinline__ void q_maybe_flush(BlockQ&, const DState&) {}
 
 // ---------------------------------------------------------------- kernels
 
@@ -584,11 +601,13 @@ __global__ void k_init(DIndex ix, DState st) {
     uint32_t s0 = wave_append(&st.ctr->s_log, true);
     st.slog_x[s0] = x;
     st.slog_a[s0] = x;
+    st.slog_f[s0] = 0;
     ev.v[EL_EV_EMIT]++;
     uint32_t s1 = wave_append(&st.ctr->s_log, two);
     if (two) {
       st.slog_x[s1] = x;
       st.slog_a[s1] = EL_TOP;
+      st.slog_f[s1] = 0;
       ev.v[EL_EV_EMIT]++;
     }
   }
@@ -608,13 +627,15 @@ __device__ void expand_s(const DIndex& ix, const DState& st, BlockQ& q, uint32_t
       const uint32_t X = st.slog_x[i], A = st.slog_a[i];
       ev.v[EL_EV_TRIG]++;
       const uint4 m0 = ix.meta[A], m1 = ix.meta[A + 1];  // the four CSR rows of A at once
-      if (mask & M_R1) {  // A ∈ S(X), A ⊑ B  =>  B ∈ S(X)
+      // A ∈ S(X), A ⊑* B  =>  B ∈ S(X), over the told closure at once; a fact that came out
+      // of a closure is not re-expanded (its closure is a subset of the one that produced it)
+      if ((mask & M_R1) && !st.slog_f[i]) {
         ev.v[EL_EV_ROW]++;
         for (uint32_t j = m0.x; j < m1.x; ++j) {
           const uint32_t B = ix.told_b[j];
           ev.v[EL_EV_ENT]++;
           ev.v[EL_EV_TEST]++;
-          emit_s(st, q, !test_bit(st.bits, ix.W, X, B), X, B, ev);
+          emit_t(st, q, !test_bit(st.bits, ix.W, X, B), X, B, ev);
         }
       }
       if (mask & M_R2) {  // A1..An ∈ S(X), ⊓Ai ⊑ B  =>  B ∈ S(X)
@@ -935,8 +956,10 @@ struct CommitLds {
 
 // Dedup S candidates against the bit rows; new facts go to the log (the versioned
 // ZADD of every Lua kernel, e.g. Type1_1AxiomProcessorBase.java:36-41).
+// (x, a) = the candidate queue; flag = slog_f of the facts it adds; kev = the work phase
 __device__ void commit_s(const DIndex& ix, const DState& st, CommitLds& sm, uint32_t bid, uint32_t nb,
-                         uint32_t n) {
+                         uint32_t n, const uint32_t* __restrict__ qx, const uint32_t* __restrict__ qa,
+                         uint8_t flag, int kev) {
   uint32_t* lx = sm.x;
   uint32_t* la = sm.v;
   uint32_t& ln = sm.n;
@@ -949,8 +972,8 @@ __device__ void commit_s(const DIndex& ix, const DState& st, CommitLds& sm, uint
     bool nw = false;
     uint32_t x = 0, a = 0;
     if (i < n) {
-      x = st.cs_x[i];
-      a = st.cs_a[i];
+      x = qx[i];
+      a = qa[i];
       ev.v[EL_EV_TRIG]++;
       ev.v[EL_EV_RMW]++;
       const uint32_t m = 1u << (a & 31u);
@@ -972,13 +995,14 @@ __device__ void commit_s(const DIndex& ix, const DState& st, CommitLds& sm, uint
       for (uint32_t k = threadIdx.x; k < cnt; k += blockDim.x) {
         st.slog_x[lbase + k] = lx[k];
         st.slog_a[lbase + k] = la[k];
+        st.slog_f[lbase + k] = flag;
       }
       __syncthreads();
       if (threadIdx.x == 0) ln = 0;
       __syncthreads();
     }
   }
-  ev_flush(st.ev, EL_K_COMMIT_S, ev);
+  ev_flush(st.ev, kev, ev);
 }
 
 // Dedup link candidates against the link set (checkAndInsertScript,
@@ -1195,6 +1219,14 @@ __device__ __forceinline__ void publish_last(const DState& st, const PubArgs& a,
   }
 }
 
+// The CR1 told-closure candidates of a superstep, committed before every other candidate
+// (a fact that is also a closure candidate is therefore marked closed, whatever else
+// derived it — the same order as the CPU oracle, so per-step deltas and events agree).
+__global__ void k_commit_told(DIndex ix, DState st, uint32_t cap) {
+  __shared__ CommitLds sm;
+  commit_s(ix, st, sm, blockIdx.x, gridDim.x, min(st.ctr->cand_t, cap), st.ct_x, st.ct_a, 1, EL_K_COMMIT_T);
+}
+
 // Block-wide: copy every counter but seq to the host mirror, then zero those in zero_mask
 // (bit i = counter i).  Each thread owns one counter, so each is read before it is zeroed.
 __device__ __forceinline__ void copy_and_zero(const DState& st, HCounters* host, uint32_t zero_mask) {
@@ -1224,7 +1256,7 @@ __global__ void k_commit(DIndex ix, DState st, CommitArgs a) {
   __shared__ CommitLds sm;
   uint32_t b = blockIdx.x;
   if (b < a.gs) {
-    commit_s(ix, st, sm, b, a.gs, min(st.ctr->cand_s, a.cs_cap));
+    commit_s(ix, st, sm, b, a.gs, min(st.ctr->cand_s, a.cs_cap), st.cs_x, st.cs_a, 0, EL_K_COMMIT_S);
   } else if ((b -= a.gs) < a.gl) {
     commit_l(ix, st, sm, b, a.gl, min(st.ctr->cand_l, a.cl_cap));
   } else if ((b -= a.gl) < a.ga) {
@@ -1247,12 +1279,12 @@ struct XchgArgs {
   const uint32_t* recv;  // nranks slots
   uint32_t cap, nranks, me;
   uint32_t s0, l0, a0, p0;  // log counts at the start of the attempt
-  uint32_t cs_cap, cl_cap, ca_cap, cp_cap, job_cap;  // a candidate queue past its cap = redo
+  uint32_t cs_cap, cl_cap, ca_cap, cp_cap, job_cap, ct_cap;  // a candidate queue past its cap = redo
 };
 // per-step counters the import zeroes once the exchange went through: x_send, cand_*, jobs
-constexpr uint32_t XCHG_ZERO = (1u << 5) | (1u << 9) | (1u << 10) | (1u << 11) | (1u << 12) | (1u << 13);
+constexpr uint32_t XCHG_ZERO = (1u << 5) | (1u << 9) | (1u << 10) | (1u << 11) | (1u << 12) | (1u << 13) | (1u << 14);
 static_assert(offsetof(DCounters, x_send) == 5 * CTR_STRIDE * 4 && offsetof(DCounters, cand_s) == 9 * CTR_STRIDE * 4 &&
-                  offsetof(DCounters, cand_p) == 13 * CTR_STRIDE * 4,
+                  offsetof(DCounters, cand_t) == 14 * CTR_STRIDE * 4,
               "XCHG_ZERO bits");
 
 __global__ void k_xpack(DState st, XchgArgs x) {
@@ -1267,7 +1299,7 @@ __global__ void k_xpack(DState st, XchgArgs x) {
     if (threadIdx.x == XH_DL) v = st.ctr->l_log - x.l0;
     if (threadIdx.x == XH_OVF)
       v = st.ctr->cand_s > x.cs_cap || st.ctr->cand_l > x.cl_cap || st.ctr->cand_a > x.ca_cap ||
-          st.ctr->cand_p > x.cp_cap || st.ctr->jobs > x.job_cap;
+          st.ctr->cand_p > x.cp_cap || st.ctr->jobs > x.job_cap || st.ctr->cand_t > x.ct_cap;
     x.send[threadIdx.x] = v;
   }
   uint2* rec = reinterpret_cast<uint2*>(x.send + XH);
@@ -1878,7 +1910,10 @@ struct el_ctx {
   uint32_t* bits = nullptr;
   uint64_t W = 0;
   uint32_t *slog_x = nullptr, *slog_a = nullptr;
+  uint8_t* slog_f = nullptr;  // told-closure flags of the facts (slog_cap)
   uint64_t slog_cap = 0;
+  uint32_t *ct_x = nullptr, *ct_a = nullptr;  // CR1 told-closure candidates
+  uint64_t ct_cap = 0;
   unsigned long long* lhash = nullptr;
   uint64_t lhash_cap = 0;
   uint32_t *llog_x = nullptr, *llog_p = nullptr;
@@ -1950,7 +1985,8 @@ struct el_ctx {
   uint32_t* xrecv = nullptr;                      // part_count slots
   uint64_t xcap = 0;                              // records per rank per exchange (grows on overflow)
   bool part() const { return xmode != EL_XCHG_NONE; }
-  bool bits_logged = false;  // every set bit of the matrix is in the fact log (not after el_load)
+  bool bits_logged = false;
+  bool trace_cands = getenv("EL_TRACE_CANDS") != nullptr;  // every set bit of the matrix is in the fact log (not after el_load)
 
   // launch shapes (workgroups per role): a workgroup costs dispatch time even when its
   // grid-stride loop is empty, so the capacity-sized roles are capped
@@ -1968,6 +2004,10 @@ struct el_ctx {
     s.bits = reinterpret_cast<uint32_t*>(reinterpret_cast<uintptr_t>(bits) - (uintptr_t)lo * W * sizeof(uint32_t));
     s.slog_x = slog_x;
     s.slog_a = slog_a;
+    s.slog_f = slog_f;
+    s.ct_x = ct_x;
+    s.ct_a = ct_a;
+    s.ct_cap = (uint32_t)ct_cap;
     s.lhash = lhash;
     s.lmask = lhash_cap - 1;
     s.llog_x = llog_x;
@@ -2134,6 +2174,9 @@ void el_ctx::free_state() {
   dfree(bits);
   dfree(slog_x);
   dfree(slog_a);
+  dfree(slog_f);
+  dfree(ct_x);
+  dfree(ct_a);
   dfree(lhash);
   dfree(llog_x);
   dfree(llog_p);
@@ -2187,6 +2230,7 @@ void el_ctx::alloc_state() {
   slog_cap = std::max<uint64_t>(1u << 20, 8 * N);
   slog_x = dalloc<uint32_t>(slog_cap);
   slog_a = dalloc<uint32_t>(slog_cap);
+  slog_f = dalloc<uint8_t>(slog_cap);
   llog_cap = std::max<uint64_t>(1u << 20, 4 * N);
   llog_x = dalloc<uint32_t>(llog_cap);
   llog_p = dalloc<uint32_t>(llog_cap);
@@ -2225,6 +2269,10 @@ void el_ctx::alloc_state() {
   ca_cap = 1u << 12;
   cs_x = dalloc<uint32_t>(cs_cap);
   cs_a = dalloc<uint32_t>(cs_cap);
+  // the first superstep emits the whole told closure of every concept (its init fact X ∈ S(X))
+  ct_cap = std::max<uint64_t>(cs_cap, next_pow2(2 * (uint64_t)hx.told.a.size() + 1024));
+  ct_x = dalloc<uint32_t>(ct_cap);
+  ct_a = dalloc<uint32_t>(ct_cap);
   cl_x = dalloc<uint32_t>(cl_cap);
   cl_p = dalloc<uint32_t>(cl_cap);
   ca_y = dalloc<uint32_t>(ca_cap);
@@ -2450,7 +2498,7 @@ bool el_ctx::superstep(uint32_t mask, uint64_t sb, uint64_t se, uint64_t lb, uin
   for (int attempt = 0;; ++attempt) {
     // ---- capacities: every candidate could be new.  Growth copies device arrays outside
     // the stream, so the previous step's kernels must have finished first.
-    const bool grow = s_count + cs_cap > slog_cap || slog_cap > S.cap || l_count + cl_cap > llog_cap ||
+    const bool grow = s_count + cs_cap + ct_cap > slog_cap || slog_cap > S.cap || l_count + cl_cap > llog_cap ||
                       2 * (l_count + cl_cap) > lhash_cap || a_count + ca_cap > alog_cap ||
                       2 * (a_count + ca_cap) > ahash_cap || p_count + cp_cap > plog_cap ||
                       2 * (p_count + cp_cap) > phash_cap;
@@ -2462,7 +2510,11 @@ bool el_ctx::superstep(uint32_t mask, uint64_t sb, uint64_t se, uint64_t lb, uin
       dgrow(b, used, c);
       cap = c;
     };
-    grow_log(s_count, cs_cap, slog_cap, slog_x, slog_a);
+    {
+      const uint64_t old_cap = slog_cap;
+      grow_log(s_count, cs_cap + ct_cap, slog_cap, slog_x, slog_a);
+      if (slog_cap != old_cap) dgrow(slog_f, s_count, slog_cap);
+    }
     if (slog_cap > S.cap) S.grow(s_csr_count, slog_cap);
     grow_log(l_count, cl_cap, llog_cap, llog_x, llog_p);
     if (2 * (l_count + cl_cap) > lhash_cap) rehash_links(next_pow2(4 * (l_count + cl_cap)));
@@ -2499,6 +2551,10 @@ bool el_ctx::superstep(uint32_t mask, uint64_t sb, uint64_t se, uint64_t lb, uin
     ca.ca_cap = (uint32_t)ca_cap, ca.cp_cap = (uint32_t)cp_cap;
     ca.pub = PubArgs{hc_dev, commit_done, ++commit_seq};
     ca.publish = 1;
+    launch(EL_K_COMMIT_T, [&] {  // CR1 told-closure candidates first (see k_commit_told)
+      hipLaunchKernelGGL(k_commit_told, dim3(grid_for(ct_cap, tune_commit)), dim3(BLOCK), 0, stream, ix, st,
+                         (uint32_t)ct_cap);
+    });
     if (split_commit) {  // diagnostic: S role alone, then the other roles (rocprof sees both)
       CommitArgs c1 = ca;
       c1.gl = c1.ga = c1.gp = 0;
@@ -2512,6 +2568,10 @@ bool el_ctx::superstep(uint32_t mask, uint64_t sb, uint64_t se, uint64_t lb, uin
     // the new links / propagations are already in their (gapped) CSR rows; S rows are
     // built lazily, for export only
     wait_commit(ca.pub.seq);
+    if (trace_cands)  // diagnostic (EL_TRACE_CANDS): candidates vs. new facts per step
+      fprintf(stderr, "step cand_t %u cand_s %u new_s %llu cand_l %u new_l %llu cand_p %u jobs %u\n", hc.cand_t, hc.cand_s,
+              (unsigned long long)(hc.s_log - s_count), hc.cand_l, (unsigned long long)(hc.l_log - l_count), hc.cand_p,
+              hc.jobs);
     s_count = hc.s_log;
     l_count = hc.l_log;
     a_count = hc.a_log;
@@ -2530,6 +2590,7 @@ bool el_ctx::superstep(uint32_t mask, uint64_t sb, uint64_t se, uint64_t lb, uin
       b = dalloc<uint32_t>(cap);
     };
     regrow2(hc.cand_s, cs_cap, cs_x, cs_a);
+    regrow2(hc.cand_t, ct_cap, ct_x, ct_a);
     regrow2(hc.cand_l, cl_cap, cl_x, cl_p);
     regrow2(hc.cand_a, ca_cap, ca_y, ca_c);
     regrow2(hc.cand_p, cp_cap, cp_p, cp_b);
@@ -2588,7 +2649,7 @@ uint32_t el_ctx::exchange_round(uint32_t s0, uint32_t l0, uint32_t a0, uint32_t 
   xa.me = part_rank;
   xa.s0 = s0, xa.l0 = l0, xa.a0 = a0, xa.p0 = p0;
   xa.cs_cap = (uint32_t)cs_cap, xa.cl_cap = (uint32_t)cl_cap, xa.ca_cap = (uint32_t)ca_cap;
-  xa.cp_cap = (uint32_t)cp_cap, xa.job_cap = (uint32_t)job_cap;
+  xa.cp_cap = (uint32_t)cp_cap, xa.job_cap = (uint32_t)job_cap, xa.ct_cap = (uint32_t)ct_cap;
   hipLaunchKernelGGL(k_xpack, dim3(grid_for(xcap, 64)), dim3(BLOCK), 0, stream, st, xa);
   HIPCHK(hipGetLastError());
   xchg->allgather(xsend, xrecv, (XH + 2 * xcap) * sizeof(uint32_t), stream);
@@ -2616,7 +2677,7 @@ uint64_t el_ctx::superstep_part(uint32_t mask, uint64_t sb, uint64_t se, uint64_
   for (int attempt = 0;; ++attempt) {
     // ---- capacities for the local candidates (as in superstep) and the remote imports
     const uint64_t rb = remote_bound();
-    const bool grow = s_count + cs_cap > slog_cap || slog_cap > S.cap || l_count + cl_cap > llog_cap ||
+    const bool grow = s_count + cs_cap + ct_cap > slog_cap || slog_cap > S.cap || l_count + cl_cap > llog_cap ||
                       2 * (l_count + cl_cap) > lhash_cap || a_count + ca_cap + rb > alog_cap || 2 * (a_count + ca_cap + rb) > ahash_cap ||
                       p_count + cp_cap + rb > plog_cap || 2 * (p_count + cp_cap + rb) > phash_cap ||
                       x_count + part_count * xcap > xlog_cap;
@@ -2629,7 +2690,11 @@ uint64_t el_ctx::superstep_part(uint32_t mask, uint64_t sb, uint64_t se, uint64_
         dgrow(b, used, c);
         cap = c;
       };
-      grow_log(s_count, cs_cap, slog_cap, slog_x, slog_a);
+      {
+        const uint64_t old_cap = slog_cap;
+        grow_log(s_count, cs_cap + ct_cap, slog_cap, slog_x, slog_a);
+        if (slog_cap != old_cap) dgrow(slog_f, s_count, slog_cap);
+      }
       if (slog_cap > S.cap) S.grow(s_csr_count, slog_cap);
       grow_log(l_count, cl_cap, llog_cap, llog_x, llog_p);
       if (2 * (l_count + cl_cap) > lhash_cap) rehash_links(next_pow2(4 * (l_count + cl_cap)));
@@ -2665,6 +2730,10 @@ uint64_t el_ctx::superstep_part(uint32_t mask, uint64_t sb, uint64_t se, uint64_
     ca.cs_cap = (uint32_t)cs_cap, ca.cl_cap = (uint32_t)cl_cap;
     ca.ca_cap = (uint32_t)ca_cap, ca.cp_cap = (uint32_t)cp_cap;
     ca.publish = 0;
+    launch(EL_K_COMMIT_T, [&] {
+      hipLaunchKernelGGL(k_commit_told, dim3(grid_for(ct_cap, tune_commit)), dim3(BLOCK), 0, stream, ix, st,
+                         (uint32_t)ct_cap);
+    });
     launch(EL_K_COMMIT_S, [&] {
       hipLaunchKernelGGL(k_commit, dim3(ca.gs + ca.gl + ca.ga + ca.gp), dim3(BLOCK), 0, stream, ix, st, ca);
     });
@@ -2690,6 +2759,7 @@ uint64_t el_ctx::superstep_part(uint32_t mask, uint64_t sb, uint64_t se, uint64_
       return true;
     };
     regrow2(hc.cand_s, cs_cap, cs_x, cs_a);
+    regrow2(hc.cand_t, ct_cap, ct_x, ct_a);
     if (regrow2(hc.cand_l, cl_cap, cl_x, cl_p)) {
       dfree(xs_x);
       dfree(xs_p);

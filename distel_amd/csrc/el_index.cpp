@@ -74,7 +74,33 @@ std::string build_index(const el_axioms& ax, HostIndex& o) {
       CHECK(bad_c(ax.sub_a[i]) || bad_c(ax.sub_b[i]), "sub", i);
       if (ax.sub_a[i] != ax.sub_b[i]) t.push_back({ax.sub_a[i], ax.sub_b[i], 0});
     }
-    o.told = make_csr(N, t, false);
+    // CR1 fires the whole told closure at once: a new A ∈ S(X) emits every B reachable from
+    // A over A ⊑ B axioms, so a taxonomy of depth d costs one superstep instead of d
+    // (facts that came out of a closure are not re-expanded: their closure is a subset).
+    const Csr told = make_csr(N, t, false);
+    std::vector<uint32_t> stamp(N, 0), queue;
+    queue.reserve(64);
+    o.told.ptr.assign(N + 1, 0);
+    o.told.a.clear();
+    for (uint32_t a = 0; a < N; ++a) {
+      const size_t base = o.told.a.size();
+      queue.clear();
+      queue.push_back(a);
+      stamp[a] = a + 1;
+      for (size_t h = 0; h < queue.size(); ++h) {
+        const uint32_t u = queue[h];
+        for (uint32_t j = told.ptr[u]; j < told.ptr[u + 1]; ++j) {
+          const uint32_t v = told.a[j];
+          if (stamp[v] == a + 1) continue;
+          stamp[v] = a + 1;
+          queue.push_back(v);
+          o.told.a.push_back(v);
+        }
+      }
+      std::sort(o.told.a.begin() + base, o.told.a.end());
+      if (o.told.a.size() > 0xffffffffull) return "told closure beyond 2^32 entries";
+      o.told.ptr[a + 1] = (uint32_t)o.told.a.size();
+    }
   }
   // CR2 conjunctions: operands sorted/unique per conjunction, conj ids in input order
   {

@@ -26,7 +26,7 @@ struct HostIndex {
   uint32_t P = 0;   // (role, filler) pairs = link targets
   std::vector<uint8_t> kind;          // EntityType digit per concept
 
-  Csr told;       // A -> B                      CR1  (told(A), B != A)
+  Csr told;       // A -> B, B ∈ told*(A)        CR1  (transitive closure of A ⊑ B, B != A)
   Csr cidx;       // A -> conj id c              CR2  conjunct index (AxiomLoader.java:931-941, DB3)
   Csr conj;       // c -> operands (sorted)      CR2
   std::vector<uint32_t> conj_b;     // c -> B

@@ -179,7 +179,8 @@ typedef enum el_kernel {
   EL_K_REHASH = 12,      /* k_rehash:    link / activation / propagation set growth */
   EL_K_EXPAND_P = 13,    /* k_expand, propagation role: new CR4 propagations × predecessors */
   EL_K_COMMIT_P = 14,    /* k_commit, propagation role: CR4 propagation set dedup ("Yr" -> B) */
-  EL_NUM_KERNELS = 15
+  EL_K_COMMIT_T = 15,    /* k_commit_told: CR1 told-closure candidates, committed first */
+  EL_NUM_KERNELS = 16
 } el_kernel;
 
 /* Algorithmic event counters; identical in the CPU oracle. */

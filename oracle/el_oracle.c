@@ -78,6 +78,11 @@ typedef struct {
   uint32_t k, a, b;
 } trip;
 
+static int u32_cmp(const void* x, const void* y) {
+  const uint32_t p = *(const uint32_t*)x, q = *(const uint32_t*)y;
+  return p < q ? -1 : p > q;
+}
+
 static int trip_cmp(const void* x, const void* y) {
   const trip *p = (const trip*)x, *q = (const trip*)y;
   if (p->k != q->k) return p->k < q->k ? -1 : 1;
@@ -190,6 +195,7 @@ struct elo_ctx {
   uint32_t *cp_ptr, *cp_ops, *cp_b;
   /* indexes */
   csr told, cidx, conj, exr, exl, psup, chf, chs, dom, rng;
+  csr toldc;        /* told closure: A -> every B reachable over A ⊑ B axioms (B != A) */
   uint32_t* conj_b;
   uint32_t *fp_ptr, *pair_role, *pair_y;
   uint8_t* role_has_exl;
@@ -198,6 +204,7 @@ struct elo_ctx {
   /* state */
   uint32_t* bits;
   vec slog_x, slog_a;
+  vec slog_f; /* 1: the fact came from a CR1 told closure, so its own closure is already out */
   vec* srow;
   hset links;
   vec llog_x, llog_p;
@@ -284,6 +291,36 @@ static int build_index(elo_ctx* c, const el_axioms* ax) {
   for (n = 0, i = 0; i < ax->n_sub; ++i)
     if (ax->sub_a[i] != ax->sub_b[i]) t[n++] = (trip){ax->sub_a[i], ax->sub_b[i], 0};
   c->told = csr_build(N, t, n);
+  {
+    /* told closure by a BFS from every concept (stamped visits) */
+    uint32_t* stamp = (uint32_t*)calloc(N, sizeof(uint32_t));
+    uint32_t* q = (uint32_t*)malloc(N * sizeof(uint32_t));
+    vec out = {0, 0, 0};
+    uint32_t A;
+    c->toldc.ptr = (uint32_t*)calloc(N + 1, sizeof(uint32_t));
+    for (A = 0; A < N; ++A) {
+      uint32_t h = 0, tl = 0, st = A + 1, base = (uint32_t)out.n, z;
+      stamp[A] = st;
+      q[tl++] = A;
+      while (h < tl) {
+        uint32_t u = q[h++], jj;
+        for (jj = c->told.ptr[u]; jj < c->told.ptr[u + 1]; ++jj) {
+          uint32_t v = c->told.a[jj];
+          if (stamp[v] == st) continue;
+          stamp[v] = st;
+          q[tl++] = v;
+          vpush(&out, v);
+        }
+      }
+      (void)z;
+      qsort(out.v + base, out.n - base, sizeof(uint32_t), u32_cmp);  /* sorted, as every index row */
+      c->toldc.ptr[A + 1] = (uint32_t)out.n;
+    }
+    c->toldc.a = out.v ? out.v : (uint32_t*)malloc(4);
+    c->toldc.b = NULL;
+    free(stamp);
+    free(q);
+  }
 
   /* CR2: sorted unique operands per conjunction, conj ids in input order */
   c->conj.ptr = (uint32_t*)calloc(ax->n_conj + 1, sizeof(uint32_t));
@@ -561,12 +598,13 @@ int elo_create(elo_ctx** out, const el_axioms* ax, int mode) {
 
 typedef struct {
   vec sx, sa, lx, lp, ay, ac, pp, pb;
+  vec s1x, s1a; /* CR1 told-closure candidates: committed after every other S candidate */
   vec jt, jb, jo, jl, ja, jbb; /* job records: type, list owner, offset, length, a, b */
 } cands;
 
 static void cands_free(cands* k) {
   free(k->sx.v), free(k->sa.v), free(k->lx.v), free(k->lp.v), free(k->ay.v), free(k->ac.v);
-  free(k->pp.v), free(k->pb.v);
+  free(k->pp.v), free(k->pb.v), free(k->s1x.v), free(k->s1a.v);
   free(k->jt.v), free(k->jb.v), free(k->jo.v), free(k->jl.v), free(k->ja.v), free(k->jbb.v);
 }
 
@@ -619,13 +657,21 @@ static void expand_s(elo_ctx* c, cands* k, uint32_t mask, uint64_t b, uint64_t e
   for (i = b; i < e; ++i) {
     uint32_t X = c->slog_x.v[i], A = c->slog_a.v[i];
     EV(K, EL_EV_TRIG);
+    /* CR1 over the told closure (Type1_1AxiomProcessorBase.java:22-43 applied transitively at
+     * once, as the GPU index does): a fact that came out of a closure is not re-expanded */
     if (mask & M_R1) {
-      EV(K, EL_EV_ROW);
-      for (j = c->told.ptr[A]; j < c->told.ptr[A + 1]; ++j) {
-        uint32_t B = c->told.a[j];
-        EV(K, EL_EV_ENT);
-        EV(K, EL_EV_TEST);
-        if (!bit(c, X, B)) emit_s(c, k, K, X, B);
+      if (!c->slog_f.v[i]) {
+        EV(K, EL_EV_ROW);
+        for (j = c->toldc.ptr[A]; j < c->toldc.ptr[A + 1]; ++j) {
+          uint32_t B = c->toldc.a[j];
+          EV(K, EL_EV_ENT);
+          EV(K, EL_EV_TEST);
+          if (!bit(c, X, B)) {
+            EV(K, EL_EV_EMIT);
+            vpush(&k->s1x, X);
+            vpush(&k->s1a, B);
+          }
+        }
       }
     }
     if (mask & M_R2) {
@@ -921,11 +967,24 @@ static int superstep(elo_ctx* c, uint32_t mask, uint64_t sb, uint64_t se, uint64
   if (do_a) expand_a(c, &k, ab, ae);
   if (do_p) expand_p(c, &k, pb, pe);
   run_jobs(c, &k);
-  if (k.sx.n + k.lx.n + k.ay.n + k.pp.n == 0) {
+  if (k.sx.n + k.s1x.n + k.lx.n + k.ay.n + k.pp.n == 0) {
     cands_free(&k);
     return 0;
   }
-  /* commit */
+  /* commit: the CR1 closure candidates first (k_commit_told on the GPU), so a fact that is
+   * also a closure candidate is marked closed whatever else derived it */
+  for (i = 0; i < k.s1x.n; ++i) {
+    uint32_t x = k.s1x.v[i], a = k.s1a.v[i];
+    EV(EL_K_COMMIT_T, EL_EV_TRIG);
+    EV(EL_K_COMMIT_T, EL_EV_RMW);
+    if (setbit(c, x, a)) {
+      EV(EL_K_COMMIT_T, EL_EV_EMIT);
+      vpush(&c->slog_x, x);
+      vpush(&c->slog_a, a);
+      vpush(&c->slog_f, 1);
+      vpush(&c->srow[x], a);
+    }
+  }
   for (i = 0; i < k.sx.n; ++i) {
     uint32_t x = k.sx.v[i], a = k.sa.v[i];
     EV(EL_K_COMMIT_S, EL_EV_TRIG);
@@ -934,6 +993,7 @@ static int superstep(elo_ctx* c, uint32_t mask, uint64_t sb, uint64_t se, uint64
       EV(EL_K_COMMIT_S, EL_EV_EMIT);
       vpush(&c->slog_x, x);
       vpush(&c->slog_a, a);
+      vpush(&c->slog_f, 0);
       vpush(&c->srow[x], a);
     }
   }
@@ -1066,6 +1126,7 @@ int elo_init(elo_ctx* c) {
     setbit(c, x, x);
     vpush(&c->slog_x, x);
     vpush(&c->slog_a, x);
+    vpush(&c->slog_f, 0);
     vpush(&c->srow[x], x);
     if (two) {
       EV(EL_K_INIT, EL_EV_RMW);
@@ -1073,6 +1134,7 @@ int elo_init(elo_ctx* c) {
       setbit(c, x, EL_TOP);
       vpush(&c->slog_x, x);
       vpush(&c->slog_a, EL_TOP);
+      vpush(&c->slog_f, 0);
       vpush(&c->srow[x], EL_TOP);
     }
   }
@@ -1244,7 +1306,7 @@ const char* elo_error(const elo_ctx* c) { return c ? c->err : "null"; }
 void elo_destroy(elo_ctx* c) {
   uint32_t i;
   if (!c) return;
-  csr_free(&c->told), csr_free(&c->cidx), csr_free(&c->exr), csr_free(&c->exl);
+  csr_free(&c->told), csr_free(&c->toldc), csr_free(&c->cidx), csr_free(&c->exr), csr_free(&c->exl);
   csr_free(&c->psup), csr_free(&c->chf), csr_free(&c->chs), csr_free(&c->dom), csr_free(&c->rng);
   free(c->conj.ptr), free(c->conj.a), free(c->conj_b);
   free(c->fp_ptr), free(c->pair_role), free(c->pair_y), free(c->role_has_exl);
@@ -1260,7 +1322,7 @@ void elo_destroy(elo_ctx* c) {
   free(c->prow), free(c->props.t), free(c->plog_p.v), free(c->plog_b.v);
   free(c->srow), free(c->succ), free(c->pred), free(c->has_act);
   free(c->cap_pr), free(c->cap_sc), free(c->cap_pp);
-  free(c->slog_x.v), free(c->slog_a.v), free(c->llog_x.v), free(c->llog_p.v);
+  free(c->slog_x.v), free(c->slog_a.v), free(c->slog_f.v), free(c->llog_x.v), free(c->llog_p.v);
   free(c->alog_y.v), free(c->alog_c.v), free(c->tr_s.v), free(c->tr_l.v), free(c->tr_a.v);
   free(c->links.t), free(c->acts.t), free(c->cube);
   free((void*)c->ax.sub_a), free((void*)c->ax.sub_b), free((void*)c->ax.conj_ptr);
