@@ -1616,6 +1616,28 @@ __global__ void k_gap_move(const uint32_t* __restrict__ s_old, const uint32_t* _
   }
 }
 
+// rows[i] -> map[rows[i]] (pair ids after an increment re-numbered the pair universe)
+__global__ void k_remap(uint32_t* __restrict__ v, uint64_t n, const uint32_t* __restrict__ map) {
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) v[i] = map[v[i]];
+}
+
+__global__ void k_gap_count(uint32_t* __restrict__ len, const uint32_t* __restrict__ rows, uint64_t n) {
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) atomicAdd(len + rows[i], 1u);
+}
+
+// every logged entry appended to its row (the layout already fits every row)
+__global__ void k_gap_fill(DGap g, const uint32_t* __restrict__ rows, const uint32_t* __restrict__ vals, uint64_t n) {
+  uint32_t ev[EL_NUM_EVENTS] = {};
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t base = (uint64_t)blockIdx.x * blockDim.x; base < n; base += stride) {
+    const uint64_t i = base + threadIdx.x;
+    const bool p = i < n;
+    gap_append(g, p ? rows[i] : 0u, p ? vals[i] : 0u, p, ev);
+  }
+}
+
 // overflow records (row, value, rank) land at their rank in the new layout
 __global__ void k_gap_ovf(const uint32_t* __restrict__ q, uint32_t n, const uint32_t* __restrict__ s_new,
                           uint32_t* __restrict__ v_new) {
@@ -2163,7 +2185,105 @@ struct el_ctx {
   void fill_stats(el_stats* st, double ms);
   void gap_rebuild(GapCsr& g, uint32_t n_ovf, uint64_t entries);
   void gap_rebuild_all();
+  void gap_build_from_log(GapCsr& g, const uint32_t* rows, const uint32_t* vals, uint64_t n);
+  void launch_gap_scan(const uint32_t* len, uint32_t R, uint32_t* start_out);
+  std::string install_index(el::HostIndex&& h);
+  void migrate_state(uint32_t N0, const std::vector<uint32_t>& pmap);
+  el::AxiomStore store;  // the loaded axioms (increments append to them)
 };
+
+// Upload the indexes of hx and derive what the kernels need from them (which CSRs have
+// readers, the owned rows).  The state is not touched.
+std::string el_ctx::install_index(el::HostIndex&& hnew) {
+  hx = std::move(hnew);
+  const el::HostIndex& h = hx;
+  auto up32 = [&](const std::vector<uint32_t>& v) {
+    uint32_t* p = dupload(v);
+    index_bufs.push_back(p);
+    return (const uint32_t*)p;
+  };
+  auto up8 = [&](const std::vector<uint8_t>& v) {
+    uint8_t* p = dupload(v);
+    index_bufs.push_back(p);
+    return (const uint8_t*)p;
+  };
+  DIndex& d = ix;
+  d.N = h.N;
+  d.R = h.R;
+  d.P = h.P;
+  d.W = (h.N + 31) / 32;
+  d.kind = up8(h.kind);
+  d.told_ptr = up32(h.told.ptr);
+  d.told_b = up32(h.told.a);
+  d.cidx_ptr = up32(h.cidx.ptr);
+  d.cidx_c = up32(h.cidx.a);
+  d.conj_ptr = up32(h.conj.ptr);
+  d.conj_ops = up32(h.conj.a);
+  d.conj_b = up32(h.conj_b);
+  d.exr_ptr = up32(h.exr.ptr);
+  d.exr_pid = up32(h.exr.a);
+  d.exl_ptr = up32(h.exl.ptr);
+  d.exl_r = up32(h.exl.a);
+  d.exl_b = up32(h.exl.b);
+  d.fp_ptr = up32(h.fp_ptr);
+  d.pair_role = up32(h.pair_role);
+  d.pair_y = up32(h.pair_y);
+  d.psup_ptr = up32(h.psup.ptr);
+  d.psup_pid = up32(h.psup.a);
+  d.chf_ptr = up32(h.chf.ptr);
+  d.chf_s = up32(h.chf.a);
+  d.chf_t = up32(h.chf.b);
+  d.chs_ptr = up32(h.chs.ptr);
+  d.chs_p = up32(h.chs.a);
+  d.chs_t = up32(h.chs.b);
+  d.dom_ptr = up32(h.dom.ptr);
+  d.dom_c = up32(h.dom.a);
+  d.rng_ptr = up32(h.rng.ptr);
+  d.rng_c = up32(h.rng.a);
+  d.role_has_exl = up8(h.role_has_exl);
+  {
+    std::vector<uint32_t> meta(4 * (size_t)(h.N + 1));
+    for (uint32_t a = 0; a <= h.N; ++a) {
+      meta[4 * a + 0] = h.told.ptr[a];
+      meta[4 * a + 1] = h.cidx.ptr[a];
+      meta[4 * a + 2] = h.exr.ptr[a];
+      meta[4 * a + 3] = h.exl.ptr[a];
+    }
+    d.meta = (const uint4*)up32(meta);
+  }
+  d.has_range = h.rng.a.empty() ? 0u : 1u;
+  {
+    // ⊥ derivable only if some axiom mentions it (as a conclusion or a CR3 filler)
+    auto has0 = [](const std::vector<uint32_t>& v) { return std::find(v.begin(), v.end(), EL_BOTTOM) != v.end(); };
+    const bool bot = has0(store.sub_b) || has0(store.conj_b) || has0(store.exr_b) || has0(store.exl_b) ||
+                     has0(store.dom_c) || has0(store.rng_c);
+    need_succ = !h.chf.a.empty();
+    need_pred = !h.exl.a.empty() || need_succ || bot;
+    use_props = !h.exl.a.empty() || (part() && bot);
+  }
+  // owned rows: the configured range, or the equal split of [0, N)
+  if (part()) {
+    if (cfg_lo == 0 && cfg_hi == 0) {
+      lo = (uint32_t)((uint64_t)h.N * part_rank / part_count);
+      hi = (uint32_t)((uint64_t)h.N * (part_rank + 1) / part_count);
+    } else {
+      if (cfg_hi > h.N) return "partition rows beyond n_concepts";
+      lo = cfg_lo;
+      hi = cfg_hi;
+    }
+    std::vector<uint8_t> chs(h.R + 1, 0);
+    for (uint32_t r = 0; r < h.R; ++r) chs[r] = h.chs.ptr[r + 1] > h.chs.ptr[r];
+    d.role_chs = up8(chs);
+  } else {
+    lo = 0;
+    hi = h.N;
+    d.role_chs = nullptr;
+  }
+  d.lo = lo;
+  d.hi = hi;
+  d.part = part() ? 1u : 0u;
+  return "";
+}
 
 void el_ctx::free_index() {
   for (void* p : index_bufs) (void)hipFree(p);
@@ -2796,27 +2916,7 @@ void el_ctx::gap_rebuild(GapCsr& g, uint32_t n_ovf, uint64_t entries) {
     g.val2_cap = total + total / 2;
     g.val2 = dalloc<uint32_t>(g.val2_cap);
   }
-  // new row starts: the single-pass look-back scan of k_scan_merge over gap_cap(len)
-  MergeArgs m{};
-  m.nseg = 1;
-  m.seg[0].ptr2 = g.start2;
-  m.seg[0].n1 = R + 1;
-  m.seg[0].gap_len = g.len;
-  ScanArgs sa{};
-  const uint32_t tiles = (R + 1 + SCAN_TILE - 1) / SCAN_TILE;
-  if (tiles > scan_tiles) throw std::runtime_error("scan tile overflow");
-  sa.tile0[0] = 0;
-  sa.tile0[1] = tiles;
-  if (++scan_epoch >= (1u << 30)) {
-    HIPCHK(hipMemsetAsync(scan_flags, 0, scan_tiles * sizeof(unsigned long long), stream));
-    scan_epoch = 1;
-  }
-  sa.epoch = scan_epoch;
-  sa.flags = scan_flags;
-  sa.ticket = &ctr->ticket;
-  launch(EL_K_SCAN, [&] {
-    hipLaunchKernelGGL(k_scan_merge, dim3(tiles), dim3(256), 0, stream, m, sa, dcnt_all, dscan_all);
-  });
+  launch_gap_scan(g.len, R, g.start2);
   launch(EL_K_SCATTER_OLD, [&] {
     hipLaunchKernelGGL(k_gap_move, dim3(grid_for((uint64_t)R * 64, 1024)), dim3(BLOCK), 0, stream, g.start, g.len,
                        g.val, g.start2, g.val2, R);
@@ -2837,6 +2937,153 @@ void el_ctx::gap_rebuild(GapCsr& g, uint32_t n_ovf, uint64_t entries) {
   host_ev[EL_K_SCATTER_NEW][EL_EV_TRIG] += n_ovf;
   host_ev[EL_K_SCATTER_NEW][EL_EV_ENT] += 3ull * n_ovf;
   host_ev[EL_K_SCATTER_NEW][EL_EV_EMIT] += n_ovf;
+}
+
+// new row starts = exclusive scan of gap_cap(len[r]): the single-pass look-back scan of
+// k_scan_merge in its gapped mode
+void el_ctx::launch_gap_scan(const uint32_t* len, uint32_t R, uint32_t* start_out) {
+  MergeArgs m{};
+  m.nseg = 1;
+  m.seg[0].ptr2 = start_out;
+  m.seg[0].n1 = R + 1;
+  m.seg[0].gap_len = len;
+  ScanArgs sa{};
+  const uint32_t tiles = (R + 1 + SCAN_TILE - 1) / SCAN_TILE;
+  if (tiles > scan_tiles) throw std::runtime_error("scan tile overflow");
+  sa.tile0[0] = 0;
+  sa.tile0[1] = tiles;
+  if (++scan_epoch >= (1u << 30)) {
+    HIPCHK(hipMemsetAsync(scan_flags, 0, scan_tiles * sizeof(unsigned long long), stream));
+    scan_epoch = 1;
+  }
+  sa.epoch = scan_epoch;
+  sa.flags = scan_flags;
+  sa.ticket = &ctr->ticket;
+  launch(EL_K_SCAN, [&] {
+    hipLaunchKernelGGL(k_scan_merge, dim3(tiles), dim3(256), 0, stream, m, sa, dcnt_all, dscan_all);
+  });
+}
+
+// A gapped CSR laid out for, and filled with, the n logged entries (rows[i], vals[i]).
+void el_ctx::gap_build_from_log(GapCsr& g, const uint32_t* rows, const uint32_t* vals, uint64_t n) {
+  const uint32_t R = g.rows;
+  HIPCHK(hipMemsetAsync(g.len, 0, (uint64_t)R * sizeof(uint32_t), stream));
+  if (n) {
+    hipLaunchKernelGGL(k_gap_count, dim3(grid_for(n)), dim3(BLOCK), 0, stream, g.len, rows, n);
+    HIPCHK(hipGetLastError());
+  }
+  launch_gap_scan(g.len, R, g.start);
+  const uint64_t total = 4 * n + (uint64_t)gap_cap(0) * R;
+  if (total > g.val_cap) {
+    sync();
+    dfree(g.val);
+    g.val_cap = total + total / 2;
+    g.val = dalloc<uint32_t>(g.val_cap);
+  }
+  HIPCHK(hipMemsetAsync(g.len, 0, (uint64_t)R * sizeof(uint32_t), stream));
+  if (n) {
+    hipLaunchKernelGGL(k_gap_fill, dim3(grid_for(n)), dim3(BLOCK), 0, stream, g.view(&ctr->ov_pr), rows, vals, n);
+    HIPCHK(hipGetLastError());
+  }
+}
+
+// Carry a saturated state over to indexes rebuilt for old ∪ increment (el_add_axioms).
+void el_ctx::migrate_state(uint32_t N0, const std::vector<uint32_t>& pmap) {
+  const uint64_t N = hx.N, P = hx.P, W0 = W, W1 = (N + 31) / 32;
+  sync();
+  if (N != N0) {  // wider bit rows, more rows: pitched copy of the old matrix
+    uint32_t* nb = dalloc<uint32_t>(N * W1);
+    HIPCHK(hipMemsetAsync(nb, 0, N * W1 * sizeof(uint32_t), stream));
+    HIPCHK(hipMemcpy2DAsync(nb, W1 * 4, bits, W0 * 4, W0 * 4, N0, hipMemcpyDeviceToDevice, stream));
+    uint8_t* ha = dalloc<uint8_t>(N);
+    HIPCHK(hipMemsetAsync(ha, 0, N, stream));
+    HIPCHK(hipMemcpyAsync(ha, has_act, N0, hipMemcpyDeviceToDevice, stream));
+    sync();
+    dfree(bits);
+    dfree(has_act);
+    bits = nb;
+    has_act = ha;
+    W = W1;
+    S.release();
+    dfree(dcnt_all);
+    dfree(dscan_all);
+    dcnt_total = N + 1;
+    dcnt_all = dalloc<uint32_t>(dcnt_total);
+    dscan_all = dalloc<uint32_t>(dcnt_total);
+    HIPCHK(hipMemsetAsync(dcnt_all, 0, dcnt_total * sizeof(uint32_t), stream));
+    S.alloc((uint32_t)N, slog_cap, dcnt_all, dscan_all);
+  }
+  HIPCHK(hipMemsetAsync(S.ptr, 0, (N + 1) * sizeof(uint32_t), stream));
+  s_csr_count = 0;  // the export CSR is rebuilt from the log on demand
+  dfree(scan_flags);
+  scan_tiles = (std::max(N, P) + 1 + SCAN_TILE - 1) / SCAN_TILE;
+  scan_flags = dalloc<unsigned long long>(scan_tiles);
+  HIPCHK(hipMemsetAsync(scan_flags, 0, scan_tiles * sizeof(unsigned long long), stream));
+  scan_epoch = 0;
+  // pair ids in the logs, then the sets keyed by them
+  if (!pmap.empty() && (l_count || p_count)) {
+    uint32_t* dmap = dupload(pmap);
+    if (l_count) hipLaunchKernelGGL(k_remap, dim3(grid_for(l_count)), dim3(BLOCK), 0, stream, llog_p, l_count, dmap);
+    if (p_count) hipLaunchKernelGGL(k_remap, dim3(grid_for(p_count)), dim3(BLOCK), 0, stream, plog_p, p_count, dmap);
+    HIPCHK(hipGetLastError());
+    sync();
+    dfree(dmap);
+  }
+  rehash_links(lhash_cap);
+  rehash_props(phash_cap);
+  // predecessor / successor / propagation rows for the new pair and concept spaces
+  PR.release();
+  SC.release();
+  PP.release();
+  if (P && need_pred) {
+    PR.alloc((uint32_t)P, cl_cap);
+    gap_build_from_log(PR, llog_p, llog_x, l_count);
+  }
+  if (need_succ) {
+    SC.alloc((uint32_t)N, cl_cap);
+    gap_build_from_log(SC, llog_x, llog_p, l_count);
+  }
+  if (use_props) {
+    PP.alloc((uint32_t)P, cp_cap + remote_bound());
+    gap_build_from_log(PP, plog_p, plog_b, p_count);
+  }
+  // the first superstep re-emits the told closure of every fact it re-triggers
+  const uint64_t ct_need = next_pow2(2 * (uint64_t)hx.told.a.size() + 1024);
+  if (ct_need > ct_cap) {
+    dfree(ct_x);
+    dfree(ct_a);
+    ct_cap = ct_need;
+    ct_x = dalloc<uint32_t>(ct_cap);
+    ct_a = dalloc<uint32_t>(ct_cap);
+  }
+  // S(X) = {X, ⊤} for the new concepts
+  if (N > N0) {
+    const uint64_t add = 2 * (N - N0);
+    if (s_count + add + cs_cap + ct_cap > slog_cap) {
+      const uint64_t c = next_pow2(s_count + add + cs_cap + ct_cap);
+      dgrow(slog_x, s_count, c);
+      dgrow(slog_a, s_count, c);
+      dgrow(slog_f, s_count, c);
+      slog_cap = c;
+      if (slog_cap > S.cap) S.grow(0, slog_cap);
+    }
+    DIndex d = ix;
+    d.lo = N0;
+    d.hi = (uint32_t)N;
+    DState st = dstate();
+    launch(EL_K_INIT, [&] {
+      hipLaunchKernelGGL(k_init, dim3(grid_for(N - N0)), dim3(BLOCK), 0, stream, d, st);
+    });
+    uint64_t n = 0;
+    for (uint64_t x = N0; x < N; ++x) n += 1 + (x != EL_TOP && x != EL_BOTTOM && hx.kind[x] != EL_KIND_DATATYPE);
+    s_count += n;
+    s_init += n;
+  }
+  // every log re-triggers once against the new axioms, then the saturation is semi-naive again
+  for (int r = 0; r < EL_NUM_RULE_TYPES; ++r) wm_s[r] = wm_l[r] = wm_a[r] = wm_p[r] = 0;
+  wm_x = 0;
+  sync();
+  stats_stale = true;
 }
 
 void el_ctx::gap_rebuild_all() {
@@ -2992,107 +3239,64 @@ int el_rccl_unique_id(uint8_t out[128]) {
 int el_load(el_ctx* c, const el_axioms* ax) {
   if (!c || !ax) return EL_EINVAL;
   return guarded(c, [&] {
+    el::AxiomStore store;
+    std::string e = store.append(*ax);
     el::HostIndex hx;
-    std::string e = el::build_index(*ax, hx);
+    if (e.empty()) e = el::build_index(store.view(), hx);
     if (!e.empty()) return fail(c, EL_EINVAL, e);
     HIPCHK(hipStreamSynchronize(c->stream));
     c->free_state();
     c->free_index();
-    c->hx = std::move(hx);
-    const el::HostIndex& h = c->hx;
-    auto up32 = [&](const std::vector<uint32_t>& v) {
-      uint32_t* p = dupload(v);
-      c->index_bufs.push_back(p);
-      return (const uint32_t*)p;
-    };
-    auto up8 = [&](const std::vector<uint8_t>& v) {
-      uint8_t* p = dupload(v);
-      c->index_bufs.push_back(p);
-      return (const uint8_t*)p;
-    };
-    DIndex& d = c->ix;
-    d.N = h.N;
-    d.R = h.R;
-    d.P = h.P;
-    d.W = (h.N + 31) / 32;
-    d.kind = up8(h.kind);
-    d.told_ptr = up32(h.told.ptr);
-    d.told_b = up32(h.told.a);
-    d.cidx_ptr = up32(h.cidx.ptr);
-    d.cidx_c = up32(h.cidx.a);
-    d.conj_ptr = up32(h.conj.ptr);
-    d.conj_ops = up32(h.conj.a);
-    d.conj_b = up32(h.conj_b);
-    d.exr_ptr = up32(h.exr.ptr);
-    d.exr_pid = up32(h.exr.a);
-    d.exl_ptr = up32(h.exl.ptr);
-    d.exl_r = up32(h.exl.a);
-    d.exl_b = up32(h.exl.b);
-    d.fp_ptr = up32(h.fp_ptr);
-    d.pair_role = up32(h.pair_role);
-    d.pair_y = up32(h.pair_y);
-    d.psup_ptr = up32(h.psup.ptr);
-    d.psup_pid = up32(h.psup.a);
-    d.chf_ptr = up32(h.chf.ptr);
-    d.chf_s = up32(h.chf.a);
-    d.chf_t = up32(h.chf.b);
-    d.chs_ptr = up32(h.chs.ptr);
-    d.chs_p = up32(h.chs.a);
-    d.chs_t = up32(h.chs.b);
-    d.dom_ptr = up32(h.dom.ptr);
-    d.dom_c = up32(h.dom.a);
-    d.rng_ptr = up32(h.rng.ptr);
-    d.rng_c = up32(h.rng.a);
-    d.role_has_exl = up8(h.role_has_exl);
-    {
-      std::vector<uint32_t> meta(4 * (size_t)(h.N + 1));
-      for (uint32_t a = 0; a <= h.N; ++a) {
-        meta[4 * a + 0] = h.told.ptr[a];
-        meta[4 * a + 1] = h.cidx.ptr[a];
-        meta[4 * a + 2] = h.exr.ptr[a];
-        meta[4 * a + 3] = h.exl.ptr[a];
-      }
-      d.meta = (const uint4*)up32(meta);
-    }
-    d.has_range = h.rng.a.empty() ? 0u : 1u;
-    {
-      // ⊥ derivable only if some axiom mentions it (as a conclusion or a CR3 filler)
-      bool bot = false;
-      auto has0 = [](const uint32_t* v, uint32_t n) {
-        for (uint32_t i = 0; i < n; ++i)
-          if (v[i] == EL_BOTTOM) return true;
-        return false;
-      };
-      bot = has0(ax->sub_b, ax->n_sub) || has0(ax->conj_b, ax->n_conj) || has0(ax->exr_b, ax->n_ex_rhs) ||
-            has0(ax->exl_b, ax->n_ex_lhs) || has0(ax->dom_c, ax->n_domain) || has0(ax->rng_c, ax->n_range);
-      c->need_succ = !h.chf.a.empty();
-      c->need_pred = !h.exl.a.empty() || c->need_succ || bot;
-      c->use_props = !h.exl.a.empty() || (c->part() && bot);
-    }
-    // owned rows: the configured range, or the equal split of [0, N)
-    if (c->part()) {
-      if (c->cfg_lo == 0 && c->cfg_hi == 0) {
-        c->lo = (uint32_t)((uint64_t)h.N * c->part_rank / c->part_count);
-        c->hi = (uint32_t)((uint64_t)h.N * (c->part_rank + 1) / c->part_count);
-      } else {
-        if (c->cfg_hi > h.N) return fail(c, EL_EINVAL, "partition rows beyond n_concepts");
-        c->lo = c->cfg_lo;
-        c->hi = c->cfg_hi;
-      }
-      std::vector<uint8_t> chs(h.R + 1, 0);
-      for (uint32_t r = 0; r < h.R; ++r) chs[r] = h.chs.ptr[r + 1] > h.chs.ptr[r];
-      d.role_chs = up8(chs);
-    } else {
-      c->lo = 0;
-      c->hi = h.N;
-      d.role_chs = nullptr;
-    }
-    d.lo = c->lo;
-    d.hi = c->hi;
-    d.part = c->part() ? 1u : 0u;
+    c->store = std::move(store);
+    e = c->install_index(std::move(hx));
+    if (!e.empty()) return fail(c, EL_EINVAL, e);
     c->alloc_state();
     c->loaded = true;
     c->inited = false;
+    return EL_OK;
+  });
+}
+
+// Incremental classification (AxiomLoader's isIncrementalData,
+// AxiomLoader.java:119-131, 149-186): the context's ontology becomes old ∪ increment, the
+// saturated state is carried over to the new indexes (pair ids remapped, bit rows widened,
+// CSRs rebuilt from the logs), and every watermark is reset so the next el_saturate /
+// el_step re-triggers all facts once against the new axioms and then continues semi-naively.
+int el_add_axioms(el_ctx* c, const el_axioms* inc) {
+  if (!c || !inc) return EL_EINVAL;
+  if (!c->loaded) return fail(c, EL_ESTATE, "el_add_axioms before el_load");
+  if (c->part()) return fail(c, EL_ESTATE, "increments need a whole-ontology context");
+  return guarded(c, [&] {
+    el::AxiomStore store = c->store;
+    std::string e = store.append(*inc);
+    el::HostIndex hx;
+    if (e.empty()) e = el::build_index(store.view(), hx);
+    if (!e.empty()) return fail(c, EL_EINVAL, e);
+    c->sync();
+    if (!c->inited) {  // nothing saturated yet: a plain reload
+      c->free_state();
+      c->free_index();
+      c->store = std::move(store);
+      e = c->install_index(std::move(hx));
+      if (!e.empty()) return fail(c, EL_EINVAL, e);
+      c->alloc_state();
+      return EL_OK;
+    }
+    // old pair id -> new pair id (the pair universe only grows)
+    std::vector<uint32_t> pmap(c->hx.P);
+    for (uint32_t p = 0; p < c->hx.P; ++p) {
+      const uint32_t r = c->hx.pair_role[p], y = c->hx.pair_y[p];
+      uint32_t q = hx.fp_ptr[y];
+      while (q < hx.fp_ptr[y + 1] && hx.pair_role[q] != r) ++q;
+      if (q == hx.fp_ptr[y + 1]) return fail(c, EL_EHIP, "pair universe lost a pair");
+      pmap[p] = q;
+    }
+    const uint32_t N0 = c->hx.N;
+    c->free_index();
+    c->store = std::move(store);
+    e = c->install_index(std::move(hx));
+    if (!e.empty()) return fail(c, EL_EINVAL, e);
+    c->migrate_state(N0, pmap);
     return EL_OK;
   });
 }

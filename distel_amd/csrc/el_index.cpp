@@ -38,6 +38,59 @@ Csr make_csr(uint32_t rows, std::vector<std::array<uint32_t, 3>>& t, bool two) {
 
 }  // namespace
 
+std::string AxiomStore::append(const el_axioms& ax) {
+  char msg[256];
+  if (ax.n_concepts < N || ax.n_roles < R) return "an increment cannot shrink the concept or role id space";
+  if (ax.n_conj && !ax.conj_ptr) return "conj_ptr missing";
+  std::vector<uint8_t> k(kind);
+  k.resize(ax.n_concepts, EL_KIND_CLASS);
+  if (ax.concept_kind)
+    for (uint32_t i = 0; i < ax.n_concepts; ++i) {
+      if (i < N && i > EL_TOP && ax.concept_kind[i] != kind[i]) {
+        snprintf(msg, sizeof msg, "increment changes the kind of concept %u", i);
+        return msg;
+      }
+      if (i >= N) k[i] = ax.concept_kind[i];
+    }
+  auto add = [](std::vector<uint32_t>& v, const uint32_t* src, uint32_t n) {
+    if (n && src) v.insert(v.end(), src, src + n);
+  };
+  for (const uint32_t* p : {ax.sub_a, ax.sub_b})
+    if (ax.n_sub && !p) return "sub arrays missing";
+  kind = std::move(k);
+  N = ax.n_concepts;
+  R = ax.n_roles;
+  add(sub_a, ax.sub_a, ax.n_sub), add(sub_b, ax.sub_b, ax.n_sub);
+  const uint32_t base = conj_ptr.back();
+  for (uint32_t i = 0; i < ax.n_conj; ++i) conj_ptr.push_back(base + ax.conj_ptr[i + 1] - ax.conj_ptr[0]);
+  if (ax.n_conj) add(conj_ops, ax.conj_ops + ax.conj_ptr[0], ax.conj_ptr[ax.n_conj] - ax.conj_ptr[0]);
+  add(conj_b, ax.conj_b, ax.n_conj);
+  add(exr_a, ax.exr_a, ax.n_ex_rhs), add(exr_r, ax.exr_r, ax.n_ex_rhs), add(exr_b, ax.exr_b, ax.n_ex_rhs);
+  add(exl_r, ax.exl_r, ax.n_ex_lhs), add(exl_a, ax.exl_a, ax.n_ex_lhs), add(exl_b, ax.exl_b, ax.n_ex_lhs);
+  add(sr_r, ax.sr_r, ax.n_subrole), add(sr_s, ax.sr_s, ax.n_subrole);
+  add(ch_r, ax.ch_r, ax.n_chain), add(ch_s, ax.ch_s, ax.n_chain), add(ch_t, ax.ch_t, ax.n_chain);
+  add(dom_r, ax.dom_r, ax.n_domain), add(dom_c, ax.dom_c, ax.n_domain);
+  add(rng_r, ax.rng_r, ax.n_range), add(rng_c, ax.rng_c, ax.n_range);
+  return "";
+}
+
+el_axioms AxiomStore::view() const {
+  el_axioms a{};
+  auto p = [](const std::vector<uint32_t>& v) { return v.empty() ? nullptr : v.data(); };
+  a.n_concepts = N;
+  a.n_roles = R;
+  a.concept_kind = kind.empty() ? nullptr : kind.data();
+  a.n_sub = (uint32_t)sub_a.size(), a.sub_a = p(sub_a), a.sub_b = p(sub_b);
+  a.n_conj = (uint32_t)conj_b.size(), a.conj_ptr = conj_ptr.data(), a.conj_ops = p(conj_ops), a.conj_b = p(conj_b);
+  a.n_ex_rhs = (uint32_t)exr_a.size(), a.exr_a = p(exr_a), a.exr_r = p(exr_r), a.exr_b = p(exr_b);
+  a.n_ex_lhs = (uint32_t)exl_r.size(), a.exl_r = p(exl_r), a.exl_a = p(exl_a), a.exl_b = p(exl_b);
+  a.n_subrole = (uint32_t)sr_r.size(), a.sr_r = p(sr_r), a.sr_s = p(sr_s);
+  a.n_chain = (uint32_t)ch_r.size(), a.ch_r = p(ch_r), a.ch_s = p(ch_s), a.ch_t = p(ch_t);
+  a.n_domain = (uint32_t)dom_r.size(), a.dom_r = p(dom_r), a.dom_c = p(dom_c);
+  a.n_range = (uint32_t)rng_r.size(), a.rng_r = p(rng_r), a.rng_c = p(rng_c);
+  return a;
+}
+
 std::string build_index(const el_axioms& ax, HostIndex& o) {
   char msg[256];
   const uint32_t N = ax.n_concepts, R = ax.n_roles;

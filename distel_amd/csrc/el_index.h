@@ -43,6 +43,17 @@ struct HostIndex {
   std::vector<uint8_t> role_has_exl;  // r -> any ∃r.A ⊑ B
 };
 
+// Owned copy of the typed axioms (el_load copies its input; el_add_axioms appends an
+// increment: the concept and role id spaces may grow, existing ids keep their kind).
+struct AxiomStore {
+  uint32_t N = 0, R = 0;
+  std::vector<uint8_t> kind;
+  std::vector<uint32_t> sub_a, sub_b, conj_ptr{0}, conj_ops, conj_b, exr_a, exr_r, exr_b, exl_r, exl_a, exl_b,
+      sr_r, sr_s, ch_r, ch_s, ch_t, dom_r, dom_c, rng_r, rng_c;
+  std::string append(const el_axioms& ax);  // "" or an error (nothing appended then)
+  el_axioms view() const;
+};
+
 // Validates ids and builds the canonical indexes.  Returns "" on success or an
 // error message (the reference throws on unknown concepts, AxiomLoader.java:1343-1354).
 std::string build_index(const el_axioms& ax, HostIndex& out);

@@ -92,7 +92,7 @@ EXPORTED_SYMBOLS = [
     "el_abi_version", "el_device_count", "el_create", "el_load", "el_init", "el_step", "el_saturate",
     "el_get_stats", "el_kernel_stats", "el_superstep_trace", "el_get_subsumers", "el_copy_facts",
     "el_copy_links", "el_export_result", "el_last_error", "el_destroy", "el_group_create", "el_group_destroy",
-    "el_rccl_unique_id",
+    "el_rccl_unique_id", "el_add_axioms",
 ]
 
 _lib: Optional[C.CDLL] = None
@@ -115,6 +115,7 @@ def load_library(path: Optional[str] = None) -> C.CDLL:
     lib.el_create.argtypes = [C.POINTER(P), C.POINTER(_ElConfig)]
     lib.el_load.argtypes = [P, C.POINTER(_ElAxioms)]
     lib.el_init.argtypes = [P]
+    lib.el_add_axioms.argtypes = [P, C.POINTER(_ElAxioms)]
     lib.el_step.argtypes = [P, C.c_int, C.POINTER(C.c_int)]
     lib.el_saturate.argtypes = [P, C.POINTER(_ElStats)]
     lib.el_get_stats.argtypes = [P, C.POINTER(_ElStats)]
@@ -275,6 +276,13 @@ class Engine:
     def init(self) -> None:
         self._check(self._lib.el_init(self._ctx), "el_init")
 
+    def add_axioms(self, inc: Axioms) -> None:
+        """Incremental classification: the loaded ontology becomes old ∪ inc (same id spaces,
+        possibly extended); a saturated state is kept and the next saturate() continues."""
+        view = AxiomsView(inc)
+        self._check(self._lib.el_add_axioms(self._ctx, C.byref(view.struct)), "el_add_axioms")
+        self.ax = merge_axioms(self.ax, inc) if self.ax is not None else inc
+
     def step(self, rule: int) -> bool:
         ch = C.c_int(0)
         self._check(self._lib.el_step(self._ctx, int(rule), C.byref(ch)), "el_step")
@@ -364,6 +372,21 @@ class Engine:
         if not ks:
             return np.zeros(0, np.uint32), np.zeros(0, np.uint32)
         return np.concatenate(ks), np.concatenate(vs)
+
+
+def merge_axioms(a: Axioms, b: Axioms) -> Axioms:
+    """old ∪ increment as one Axioms (b's id spaces extend a's)."""
+    n = max(a.n_concepts, b.n_concepts)
+    kind = np.zeros(n, np.uint8)
+    kind[:b.n_concepts] = b.kind
+    kind[:a.n_concepts] = a.kind
+    cat = lambda x, y: np.concatenate([x, y]).astype(np.uint32)
+    conj = [(a.conj_ops[a.conj_ptr[i]:a.conj_ptr[i + 1]].tolist(), int(a.conj_b[i])) for i in range(a.n_conj)] + \
+           [(b.conj_ops[b.conj_ptr[i]:b.conj_ptr[i + 1]].tolist(), int(b.conj_b[i])) for i in range(b.n_conj)]
+    return Axioms.build(n, max(a.n_roles, b.n_roles), kind=kind, sub=cat(a.sub, b.sub), conj=conj,
+                        ex_rhs=cat(a.ex_rhs, b.ex_rhs), ex_lhs=cat(a.ex_lhs, b.ex_lhs),
+                        subrole=cat(a.subrole, b.subrole), chain=cat(a.chain, b.chain),
+                        domain=cat(a.domain, b.domain), range=cat(a.range, b.range))
 
 
 def classify_partitioned(ax: Axioms, parts: int, devices: Optional[List[int]] = None,

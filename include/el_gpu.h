@@ -235,6 +235,12 @@ void el_group_destroy(el_group* g);
 int el_rccl_unique_id(uint8_t out[128]);
 int el_load(el_ctx* ctx, const el_axioms* ax);
 int el_init(el_ctx* ctx);
+/* Incremental classification (AxiomLoader isIncrementalData, AxiomLoader.java:119-131):
+ * the ontology becomes old ∪ inc.  inc uses the same id spaces, possibly extended
+ * (n_concepts / n_roles >= the loaded ones; existing concepts keep their kind; NULL
+ * concept_kind = new concepts are classes).  A saturated state is kept and the next
+ * el_saturate / el_step continues from it.  Whole-ontology contexts only. */
+int el_add_axioms(el_ctx* ctx, const el_axioms* inc);
 int el_step(el_ctx* ctx, el_rule rule, int* changed);
 int el_saturate(el_ctx* ctx, el_stats* stats);
 int el_get_stats(el_ctx* ctx, el_stats* stats);
