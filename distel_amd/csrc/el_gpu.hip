@@ -114,6 +114,7 @@ struct DIndex {
   const uint32_t *rng_ptr, *rng_c;
   const uint8_t* role_has_exl;
   const uint4* meta;  // per concept A: {told_ptr, cidx_ptr, exr_ptr, exl_ptr}[A] — one 32 B span for A, A+1
+  const uint32_t* init_off;  // N + 1: start of concept X's init facts in an init-ordered log
   uint32_t has_range;
   // row partition (el_config.exchange != NONE): this context owns rows [lo, hi)
   uint32_t lo, hi;
@@ -584,35 +585,59 @@ __global__ void k_fill(FillArgs f) {
 }
 
 // S(X) = {X, ⊤} for classes and individuals, {X} for ⊤, ⊥ and datatypes
-// (AxiomLoader.java:1237-1245 classes, :1281-1289 individuals).
-__global__ void k_init(DIndex ix, DState st) {
+// (AxiomLoader.java:1237-1245 classes, :1281-1289 individuals), together with the told
+// closure of X — exactly what CR1 derives from the init fact X ∈ S(X) in the first
+// superstep — written without candidates: the init facts of rows [lo, hi) are the
+// contiguous log range [init_off[lo], init_off[hi]) (host prefix sums), so each thread takes
+// one log slot k, finds its row by a binary search over init_off and its fact by the offset
+// inside the row, and a wave's log stores are coalesced.  Row X's facts: X (closure flag:
+// its closure is written right here), ⊤ for classes and individuals, then told*(X) (flagged)
+// without a second ⊤.
+__global__ void k_init(DIndex ix, DState st, uint32_t lo, uint32_t hi, uint32_t base) {
   Ev ev;
+  const uint32_t o0 = ix.init_off[lo], n = ix.init_off[hi] - o0;
   const uint32_t stride = gridDim.x * blockDim.x;
-  for (uint32_t x = ix.lo + blockIdx.x * blockDim.x + threadIdx.x; x < ix.hi; x += stride) {
+  for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < n; k += stride) {
+    uint32_t a = lo, b = hi;  // the row: largest x with init_off[x] - o0 <= k
+    while (b - a > 1) {
+      const uint32_t m = (a + b) >> 1;
+      if (ix.init_off[m] - o0 <= k) a = m;
+      else b = m;
+    }
+    const uint32_t x = a, j = k - (ix.init_off[x] - o0);
     const bool two = x != EL_TOP && x != EL_BOTTOM && ix.kind[x] != EL_KIND_DATATYPE;
-    ev.v[EL_EV_ENT]++;
-    uint32_t* row = st.bits + (uint64_t)x * ix.W;
-    atomicOr(row + (x >> 5), 1u << (x & 31u));
+    const uint32_t t0 = ix.told_ptr[x], t1 = ix.told_ptr[x + 1];
+    // ⊤ (id 1) sorts first or right after ⊥ in told*(X): for classes it is already there
+    const uint32_t ptop = !two ? NONE
+                          : (t0 < t1 && ix.told_b[t0] == EL_TOP)         ? 0u
+                          : (t0 + 1 < t1 && ix.told_b[t0 + 1] == EL_TOP) ? 1u
+                                                                         : NONE;
+    uint32_t v;
+    uint8_t f = 1;
+    if (j == 0) {
+      v = x;
+      ev.v[EL_EV_ENT] += 1 + (ptop != NONE);  // the row, and the skipped closure entry
+    } else if (two && j == 1) {
+      v = EL_TOP;
+      f = 0;
+    } else {
+      uint32_t c = j - 1 - (two ? 1u : 0u);
+      if (c >= ptop) ++c;
+      v = ix.told_b[t0 + c];
+      ev.v[EL_EV_ENT]++;
+    }
+    __hip_atomic_fetch_or(st.bits + (uint64_t)x * ix.W + (v >> 5), 1u << (v & 31u), __ATOMIC_RELAXED,
+                          __HIP_MEMORY_SCOPE_AGENT);
+    st.slog_x[base + k] = x;
+    st.slog_a[base + k] = v;
+    st.slog_f[base + k] = f;
     ev.v[EL_EV_RMW]++;
-    if (two) {
-      atomicOr(row + (EL_TOP >> 5), 1u << (EL_TOP & 31u));
-      ev.v[EL_EV_RMW]++;
-    }
-    uint32_t s0 = wave_append(&st.ctr->s_log, true);
-    st.slog_x[s0] = x;
-    st.slog_a[s0] = x;
-    st.slog_f[s0] = 0;
     ev.v[EL_EV_EMIT]++;
-    uint32_t s1 = wave_append(&st.ctr->s_log, two);
-    if (two) {
-      st.slog_x[s1] = x;
-      st.slog_a[s1] = EL_TOP;
-      st.slog_f[s1] = 0;
-      ev.v[EL_EV_EMIT]++;
-    }
   }
   ev_flush(st.ev, EL_K_INIT, ev);
 }
+
+__global__ void k_set_u32(uint32_t* p, uint32_t v) { *p = v; }
 
 // Rules triggered by new S-facts (X, A) = log[begin, end).
 //  CR1  Type1_1AxiomProcessorBase.java:22-43      CR2  Type1_2AxiomProcessorBase.java:45-66
@@ -2189,7 +2214,9 @@ struct el_ctx {
   void launch_gap_scan(const uint32_t* len, uint32_t R, uint32_t* start_out);
   std::string install_index(el::HostIndex&& h);
   void migrate_state(uint32_t N0, const std::vector<uint32_t>& pmap);
+  void init_rows(uint32_t a, uint32_t b);
   el::AxiomStore store;  // the loaded axioms (increments append to them)
+  std::vector<uint32_t> init_off;  // host copy of DIndex::init_off
 };
 
 // Upload the indexes of hx and derive what the kernels need from them (which CSRs have
@@ -2252,6 +2279,18 @@ std::string el_ctx::install_index(el::HostIndex&& hnew) {
     d.meta = (const uint4*)up32(meta);
   }
   d.has_range = h.rng.a.empty() ? 0u : 1u;
+  {  // init facts per concept: X, ⊤ (classes, individuals), told*(X) without a second ⊤
+    init_off.assign(h.N + 1, 0);
+    for (uint32_t x = 0; x < h.N; ++x) {
+      const bool two = x != EL_TOP && x != EL_BOTTOM && h.kind[x] != EL_KIND_DATATYPE;
+      uint64_t n = 1 + two + (h.told.ptr[x + 1] - h.told.ptr[x]);
+      if (two && std::binary_search(h.told.a.begin() + h.told.ptr[x], h.told.a.begin() + h.told.ptr[x + 1], EL_TOP))
+        --n;
+      if ((uint64_t)init_off[x] + n > 0xffffffffull) return "init facts beyond 2^32";
+      init_off[x + 1] = init_off[x] + (uint32_t)n;
+    }
+    d.init_off = up32(init_off);
+  }
   {
     // ⊥ derivable only if some axiom mentions it (as a conclusion or a CR3 filler)
     auto has0 = [](const std::vector<uint32_t>& v) { return std::find(v.begin(), v.end(), EL_BOTTOM) != v.end(); };
@@ -2374,8 +2413,32 @@ void el_ctx::alloc_state() {
   dcnt_all = dalloc<uint32_t>(dcnt_total);
   dscan_all = dalloc<uint32_t>(dcnt_total);
   S.alloc((uint32_t)N, slog_cap, dcnt_all, dscan_all);
-  cs_cap = std::max<uint64_t>(1u << 20, 4 * N);
-  cl_cap = cs_cap;
+  // The first superstep re-triggers every init fact (the told closures included), so the
+  // candidate queues start sized for it: bounds from the index, per owned row X over
+  // F(X) = {X, ⊤} ∪ told*(X) — CR3 links Σ|exr(A)|, CR2 candidates Σ|cidx(A)|, CR4
+  // propagations Σ|exl(A)| (an overflow would re-run the step).
+  uint64_t b_link = 0, b_conj = 0, b_prop = 0;
+  {
+    auto add = [&](uint32_t a) {
+      b_link += hx.exr.ptr[a + 1] - hx.exr.ptr[a];
+      b_conj += hx.cidx.ptr[a + 1] - hx.cidx.ptr[a];
+      b_prop += hx.exl.ptr[a + 1] - hx.exl.ptr[a];
+    };
+    for (uint32_t x = lo; x < hi; ++x) {
+      add(x);
+      if (x != EL_TOP && x != EL_BOTTOM && hx.kind[x] != EL_KIND_DATATYPE) add(EL_TOP);
+      for (uint32_t j = hx.told.ptr[x]; j < hx.told.ptr[x + 1]; ++j) add(hx.told.a[j]);
+    }
+  }
+  cs_cap = std::max<uint64_t>(std::max<uint64_t>(1u << 20, 4 * N), next_pow2(b_conj + b_conj / 4));
+  cl_cap = std::max<uint64_t>(1u << 20, next_pow2(b_link + b_link / 4));
+  if (b_prop + b_prop / 4 > cp_cap) {
+    dfree(cp_p);
+    dfree(cp_b);
+    cp_cap = next_pow2(b_prop + b_prop / 4);
+    cp_p = dalloc<uint32_t>(cp_cap);
+    cp_b = dalloc<uint32_t>(cp_cap);
+  }
   if (part()) {
     // records per rank per all-gather; grows on demand (EL_XCHG_CAP: a smaller start, tests)
     xcap = 1u << 12;
@@ -2397,6 +2460,20 @@ void el_ctx::alloc_state() {
   cl_p = dalloc<uint32_t>(cl_cap);
   ca_y = dalloc<uint32_t>(ca_cap);
   ca_c = dalloc<uint32_t>(ca_cap);
+  {  // the init facts (with the told closure) and one step of candidates fit from the start
+    const uint64_t need = (uint64_t)init_off[hi] - init_off[lo] + cs_cap + ct_cap;
+    if (need > slog_cap) {
+      dfree(slog_x);
+      dfree(slog_a);
+      dfree(slog_f);
+      slog_cap = next_pow2(need);
+      slog_x = dalloc<uint32_t>(slog_cap);
+      slog_a = dalloc<uint32_t>(slog_cap);
+      slog_f = dalloc<uint8_t>(slog_cap);
+      S.release();
+      S.alloc((uint32_t)N, slog_cap, dcnt_all, dscan_all);
+    }
+  }
   job_cap = std::max<uint64_t>(1u << 20, 2 * N);
   jobs = dalloc<uint4>(job_cap);
   ctr = dalloc<DCounters>(1);
@@ -2987,6 +3064,33 @@ void el_ctx::gap_build_from_log(GapCsr& g, const uint32_t* rows, const uint32_t*
   }
 }
 
+// Init facts of the rows [a, b), appended at s_count: X, ⊤ and the told closure of X (see
+// k_init).  The counts are known on the host (init_off), so nothing is read back and the
+// first superstep is enqueued without a sync.
+void el_ctx::init_rows(uint32_t a, uint32_t b) {
+  if (b <= a) return;
+  const uint64_t n = (uint64_t)init_off[b] - init_off[a];
+  if (s_count + n + cs_cap + ct_cap > slog_cap) {
+    sync();
+    const uint64_t c = next_pow2(s_count + n + cs_cap + ct_cap);
+    dgrow(slog_x, s_count, c);
+    dgrow(slog_a, s_count, c);
+    dgrow(slog_f, s_count, c);
+    slog_cap = c;
+    if (slog_cap > S.cap) S.grow(s_csr_count, slog_cap);
+  }
+  DState st = dstate();
+  launch(EL_K_INIT, [&] {
+    hipLaunchKernelGGL(k_init, dim3(grid_for(n, 2048)), dim3(BLOCK), 0, stream, ix, st, a, b, (uint32_t)s_count);
+  });
+  hipLaunchKernelGGL(k_set_u32, dim3(1), dim3(1), 0, stream, &ctr->s_log, (uint32_t)(s_count + n));
+  HIPCHK(hipGetLastError());
+  uint64_t two = 0;  // the {X, ⊤} part: init facts proper; the closure part is derived
+  for (uint32_t x = a; x < b; ++x) two += 1 + (x != EL_TOP && x != EL_BOTTOM && hx.kind[x] != EL_KIND_DATATYPE);
+  s_count += n;
+  s_init += two;
+}
+
 // Carry a saturated state over to indexes rebuilt for old ∪ increment (el_add_axioms).
 void el_ctx::migrate_state(uint32_t N0, const std::vector<uint32_t>& pmap) {
   const uint64_t N = hx.N, P = hx.P, W0 = W, W1 = (N + 31) / 32;
@@ -3056,29 +3160,10 @@ void el_ctx::migrate_state(uint32_t N0, const std::vector<uint32_t>& pmap) {
     ct_x = dalloc<uint32_t>(ct_cap);
     ct_a = dalloc<uint32_t>(ct_cap);
   }
-  // S(X) = {X, ⊤} for the new concepts
-  if (N > N0) {
-    const uint64_t add = 2 * (N - N0);
-    if (s_count + add + cs_cap + ct_cap > slog_cap) {
-      const uint64_t c = next_pow2(s_count + add + cs_cap + ct_cap);
-      dgrow(slog_x, s_count, c);
-      dgrow(slog_a, s_count, c);
-      dgrow(slog_f, s_count, c);
-      slog_cap = c;
-      if (slog_cap > S.cap) S.grow(0, slog_cap);
-    }
-    DIndex d = ix;
-    d.lo = N0;
-    d.hi = (uint32_t)N;
-    DState st = dstate();
-    launch(EL_K_INIT, [&] {
-      hipLaunchKernelGGL(k_init, dim3(grid_for(N - N0)), dim3(BLOCK), 0, stream, d, st);
-    });
-    uint64_t n = 0;
-    for (uint64_t x = N0; x < N; ++x) n += 1 + (x != EL_TOP && x != EL_BOTTOM && hx.kind[x] != EL_KIND_DATATYPE);
-    s_count += n;
-    s_init += n;
-  }
+  // every logged fact re-expands its told closure once (the closures may have grown)
+  if (s_count) HIPCHK(hipMemsetAsync(slog_f, 0, s_count, stream));
+  // S(X) = {X, ⊤} ∪ told*(X) for the new concepts
+  if (N > N0) init_rows(N0, (uint32_t)N);
   // every log re-triggers once against the new axioms, then the saturation is semi-naive again
   for (int r = 0; r < EL_NUM_RULE_TYPES; ++r) wm_s[r] = wm_l[r] = wm_a[r] = wm_p[r] = 0;
   wm_x = 0;
@@ -3306,18 +3391,7 @@ int el_init(el_ctx* c) {
   if (!c->loaded) return fail(c, EL_ESTATE, "el_init before el_load");
   return guarded(c, [&] {
     c->reset_state();
-    DState st = c->dstate();
-    c->launch(EL_K_INIT, [&] {
-      hipLaunchKernelGGL(k_init, dim3(grid_for(c->hi - c->lo)), dim3(BLOCK), 0, c->stream, c->ix, st);
-    });
-    // k_init appends X for every owned concept and ⊤ for classes and individuals other
-    // than ⊤/⊥: the count is known on the host, so the first superstep is enqueued
-    // without a sync
-    uint64_t n = c->hi - c->lo;
-    for (uint32_t x = c->lo; x < c->hi; ++x)
-      n += x != EL_TOP && x != EL_BOTTOM && c->hx.kind[x] != EL_KIND_DATATYPE;
-    c->s_count = n;
-    c->s_init = n;
+    c->init_rows(c->lo, c->hi);
     c->s_csr_count = 0;
     c->inited = true;
     c->stats_stale = true;

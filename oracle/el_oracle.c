@@ -1118,16 +1118,21 @@ static int naive_saturate(elo_ctx* c) {
 int elo_init(elo_ctx* c) {
   uint32_t x;
   if (!c) return EL_EINVAL;
+  uint64_t init = 0;
+  /* S(X) = {X, ⊤} (classes, individuals) and the told closure of X, flagged — what CR1 would
+   * derive from the init fact in the first superstep (k_init on the GPU) */
   for (x = 0; x < c->N; ++x) {
     int two = x != EL_TOP && x != EL_BOTTOM && c->kind[x] != EL_KIND_DATATYPE;
+    uint32_t j;
     EV(EL_K_INIT, EL_EV_ENT);
     EV(EL_K_INIT, EL_EV_RMW);
     EV(EL_K_INIT, EL_EV_EMIT);
     setbit(c, x, x);
     vpush(&c->slog_x, x);
     vpush(&c->slog_a, x);
-    vpush(&c->slog_f, 0);
+    vpush(&c->slog_f, 1); /* its closure is written right here */
     vpush(&c->srow[x], x);
+    ++init;
     if (two) {
       EV(EL_K_INIT, EL_EV_RMW);
       EV(EL_K_INIT, EL_EV_EMIT);
@@ -1136,9 +1141,22 @@ int elo_init(elo_ctx* c) {
       vpush(&c->slog_a, EL_TOP);
       vpush(&c->slog_f, 0);
       vpush(&c->srow[x], EL_TOP);
+      ++init;
+    }
+    for (j = c->toldc.ptr[x]; j < c->toldc.ptr[x + 1]; ++j) {
+      uint32_t b = c->toldc.a[j];
+      EV(EL_K_INIT, EL_EV_ENT);
+      if (two && b == EL_TOP) continue;
+      EV(EL_K_INIT, EL_EV_RMW);
+      EV(EL_K_INIT, EL_EV_EMIT);
+      setbit(c, x, b);
+      vpush(&c->slog_x, x);
+      vpush(&c->slog_a, b);
+      vpush(&c->slog_f, 1);
+      vpush(&c->srow[x], b);
     }
   }
-  c->s_init = c->slog_x.n;
+  c->s_init = init;
   return EL_OK;
 }
 

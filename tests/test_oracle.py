@@ -66,7 +66,8 @@ def test_trace_sums(oracle_lib):
     ds, dl, da = o.trace()
     st = o.stats()
     assert int(ds.sum()) == st["s_facts"] and int(dl.sum()) == st["links"]
-    assert ds[0] == st["s_init"] and dl[0] == 0
+    # the first superstep's triggers: the init facts and the told closures written with them
+    assert ds[0] >= st["s_init"] and dl[0] == 0
 
 
 def test_generators_deterministic():
