@@ -60,6 +60,26 @@ class _stdout_to_stderr:
         os.close(self.saved)
 
 
+def pmc_traffic(workload: str, kernel: str):
+    """HBM bytes per launch of `kernel` from the committed PMC summary of this workload
+    (profiles/pmc/r01_pmc_<workload>.json, written by scripts/pmc_summary.py from separate
+    rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes, gfx950-corrected as MI355X_MICROARCH.md
+    prescribes).  Used only when the summary was taken on this exact kernel source; else None."""
+    import hashlib
+    path = os.path.join(ROOT, "profiles", "pmc", f"r01_pmc_{workload}.json")
+    try:
+        with open(path) as f:
+            pmc = json.load(f)
+        with open(os.path.join(ROOT, "distel_amd", "csrc", "el_gpu.hip"), "rb") as f:
+            digest = hashlib.sha256(f.read()).hexdigest()
+    except (OSError, ValueError):
+        return None
+    if pmc.get("source_sha256") != digest:
+        return None
+    k = pmc.get("kernels", {}).get(kernel)
+    return None if not k or k.get("hbm_bytes_per_dispatch") is None else int(k["hbm_bytes_per_dispatch"])
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -153,7 +173,8 @@ def main():
         avg_ms = dom["ms"] / dom["launches"]
         achieved = per_launch_bytes / (avg_ms * 1e-3) / 1e9
         roofline = {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                    "frac": round(achieved / HBM_PEAK_GBS, 6), "traffic": None,
+                    "frac": round(achieved / HBM_PEAK_GBS, 6),
+                    "traffic": pmc_traffic(args.workload, dom["kernel"]),
                     "kernel": dom["kernel"], "bytes_per_launch": int(per_launch_bytes),
                     "avg_launch_us": round(avg_ms * 1e3, 3), "launches": dom["launches"],
                     "profiled_ms": round(pst["ms"], 3)}
