@@ -1055,7 +1055,8 @@ __device__ void commit_l(const DIndex& ix, const DState& st, CommitLds& sm, uint
     }
     // the new link joins its predecessor / successor rows in place
     if (st.need_pred) gap_append(st.pr, p, x, nw, ev.v);
-    if (st.succ_at_commit) gap_append(st.sc, x, p, nw, ev.v);
+    // successor rows are read only by CR6 with the row's role second: other links stay out
+    if (st.succ_at_commit) gap_append(st.sc, x, p, nw && ix.role_chs[ix.pair_role[p]], ev.v);
     if (ix.part) {  // partitioned: a new link of a chain-second role goes to every rank
       const bool xs = nw && ix.role_chs[ix.pair_role[p]];
       const uint32_t slot = wave_append(&st.ctr->x_send, xs);
@@ -1647,18 +1648,28 @@ __global__ void k_remap(uint32_t* __restrict__ v, uint64_t n, const uint32_t* __
   for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) v[i] = map[v[i]];
 }
 
-__global__ void k_gap_count(uint32_t* __restrict__ len, const uint32_t* __restrict__ rows, uint64_t n) {
+// keep (optional): entry i is kept iff keep[role[vals[i]]] (the successor rows' role filter)
+struct GapKeep {
+  const uint8_t* keep;
+  const uint32_t* role;
+  __device__ __forceinline__ bool operator()(uint32_t v) const { return !keep || keep[role[v]]; }
+};
+
+__global__ void k_gap_count(uint32_t* __restrict__ len, const uint32_t* __restrict__ rows,
+                            const uint32_t* __restrict__ vals, uint64_t n, GapKeep keep) {
   const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) atomicAdd(len + rows[i], 1u);
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
+    if (keep(vals[i])) atomicAdd(len + rows[i], 1u);
 }
 
 // every logged entry appended to its row (the layout already fits every row)
-__global__ void k_gap_fill(DGap g, const uint32_t* __restrict__ rows, const uint32_t* __restrict__ vals, uint64_t n) {
+__global__ void k_gap_fill(DGap g, const uint32_t* __restrict__ rows, const uint32_t* __restrict__ vals, uint64_t n,
+                           GapKeep keep) {
   uint32_t ev[EL_NUM_EVENTS] = {};
   const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
   for (uint64_t base = (uint64_t)blockIdx.x * blockDim.x; base < n; base += stride) {
     const uint64_t i = base + threadIdx.x;
-    const bool p = i < n;
+    const bool p = i < n && keep(vals[i]);
     gap_append(g, p ? rows[i] : 0u, p ? vals[i] : 0u, p, ev);
   }
 }
@@ -2210,7 +2221,8 @@ struct el_ctx {
   void fill_stats(el_stats* st, double ms);
   void gap_rebuild(GapCsr& g, uint32_t n_ovf, uint64_t entries);
   void gap_rebuild_all();
-  void gap_build_from_log(GapCsr& g, const uint32_t* rows, const uint32_t* vals, uint64_t n);
+  void gap_build_from_log(GapCsr& g, const uint32_t* rows, const uint32_t* vals, uint64_t n,
+                          const uint8_t* keep = nullptr);
   void launch_gap_scan(const uint32_t* len, uint32_t R, uint32_t* start_out);
   std::string install_index(el::HostIndex&& h);
   void migrate_state(uint32_t N0, const std::vector<uint32_t>& pmap);
@@ -2310,12 +2322,15 @@ std::string el_ctx::install_index(el::HostIndex&& hnew) {
       lo = cfg_lo;
       hi = cfg_hi;
     }
+  } else {
+    lo = 0;
+    hi = h.N;
+  }
+  if (part() || need_succ) {  // chain-second roles: their links are exchanged and feed the succ rows
     std::vector<uint8_t> chs(h.R + 1, 0);
     for (uint32_t r = 0; r < h.R; ++r) chs[r] = h.chs.ptr[r + 1] > h.chs.ptr[r];
     d.role_chs = up8(chs);
   } else {
-    lo = 0;
-    hi = h.N;
     d.role_chs = nullptr;
   }
   d.lo = lo;
@@ -3042,11 +3057,13 @@ void el_ctx::launch_gap_scan(const uint32_t* len, uint32_t R, uint32_t* start_ou
 }
 
 // A gapped CSR laid out for, and filled with, the n logged entries (rows[i], vals[i]).
-void el_ctx::gap_build_from_log(GapCsr& g, const uint32_t* rows, const uint32_t* vals, uint64_t n) {
+void el_ctx::gap_build_from_log(GapCsr& g, const uint32_t* rows, const uint32_t* vals, uint64_t n,
+                                const uint8_t* keep) {
+  const GapKeep gk{keep, keep ? ix.pair_role : nullptr};
   const uint32_t R = g.rows;
   HIPCHK(hipMemsetAsync(g.len, 0, (uint64_t)R * sizeof(uint32_t), stream));
   if (n) {
-    hipLaunchKernelGGL(k_gap_count, dim3(grid_for(n)), dim3(BLOCK), 0, stream, g.len, rows, n);
+    hipLaunchKernelGGL(k_gap_count, dim3(grid_for(n)), dim3(BLOCK), 0, stream, g.len, rows, vals, n, gk);
     HIPCHK(hipGetLastError());
   }
   launch_gap_scan(g.len, R, g.start);
@@ -3059,7 +3076,7 @@ void el_ctx::gap_build_from_log(GapCsr& g, const uint32_t* rows, const uint32_t*
   }
   HIPCHK(hipMemsetAsync(g.len, 0, (uint64_t)R * sizeof(uint32_t), stream));
   if (n) {
-    hipLaunchKernelGGL(k_gap_fill, dim3(grid_for(n)), dim3(BLOCK), 0, stream, g.view(&ctr->ov_pr), rows, vals, n);
+    hipLaunchKernelGGL(k_gap_fill, dim3(grid_for(n)), dim3(BLOCK), 0, stream, g.view(&ctr->ov_pr), rows, vals, n, gk);
     HIPCHK(hipGetLastError());
   }
 }
@@ -3145,7 +3162,7 @@ void el_ctx::migrate_state(uint32_t N0, const std::vector<uint32_t>& pmap) {
   }
   if (need_succ) {
     SC.alloc((uint32_t)N, cl_cap);
-    gap_build_from_log(SC, llog_x, llog_p, l_count);
+    gap_build_from_log(SC, llog_x, llog_p, l_count, ix.role_chs);
   }
   if (use_props) {
     PP.alloc((uint32_t)P, cp_cap + remote_bound());

@@ -1004,11 +1004,14 @@ static int superstep(elo_ctx* c, uint32_t mask, uint64_t sb, uint64_t se, uint64
     if (hs_add(&c->links, lkey(p, x))) {
       EV(EL_K_COMMIT_L, EL_EV_EMIT);
       if (c->need_pred) gap_append_ev(c, EL_K_COMMIT_L, c->pred[p].n, c->cap_pr[p], &c->ov_pr);
-      if (c->need_succ) gap_append_ev(c, EL_K_COMMIT_L, c->succ[x].n, c->cap_sc[x], &c->ov_sc);
+      /* successor rows are read only by CR6 with the row's role second: other links stay out */
+      if (c->need_succ && c->chs.ptr[c->pair_role[p] + 1] > c->chs.ptr[c->pair_role[p]]) {
+        gap_append_ev(c, EL_K_COMMIT_L, c->succ[x].n, c->cap_sc[x], &c->ov_sc);
+        vpush(&c->succ[x], p);
+      }
       vpush(&c->llog_x, x);
       vpush(&c->llog_p, p);
       vpush(&c->pred[p], x);
-      vpush(&c->succ[x], p);
     }
   }
   for (i = 0; i < k.ay.n; ++i) {
