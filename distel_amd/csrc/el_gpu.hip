@@ -214,7 +214,8 @@ struct DState {
 
 struct Ev {
   uint32_t v[EL_NUM_EVENTS];
-  __device__ Ev() {
+  uint32_t dup;  // S candidates dropped as in-wave duplicates: charged to the S commit (ev_flush)
+  __device__ Ev() : dup(0) {
 #pragma unroll
     for (int i = 0; i < EL_NUM_EVENTS; ++i) v[i] = 0;
   }
@@ -236,22 +237,29 @@ __device__ __forceinline__ unsigned long long wave_sum_u64(unsigned long long v)
 
 // Block-level reduction of the event counters: one LDS atomic per wave, then one global
 // atomic per (event, block) into a sharded slot.  Every thread of the block must call it.
+// A candidate dropped as an in-wave duplicate (emit_s) is charged to the S commit as the
+// commit would have counted it: a trigger read and a bit-word RMW that finds the bit set.
 __device__ __forceinline__ void ev_flush(unsigned long long* evg, int k, const Ev& e) {
-  __shared__ unsigned long long sev[EL_NUM_EVENTS];
-  if (threadIdx.x < EL_NUM_EVENTS) sev[threadIdx.x] = 0;
+  __shared__ unsigned long long sev[EL_NUM_EVENTS + 1];
+  if (threadIdx.x <= EL_NUM_EVENTS) sev[threadIdx.x] = 0;
   __syncthreads();
 #pragma unroll
-  for (int i = 0; i < EL_NUM_EVENTS; ++i) {
-    unsigned long long s = wave_sum(e.v[i]);
+  for (int i = 0; i <= EL_NUM_EVENTS; ++i) {
+    unsigned long long s = wave_sum(i < EL_NUM_EVENTS ? e.v[i] : e.dup);
     if (lane_id() == 0 && s) atomicAdd(&sev[i], s);
   }
   __syncthreads();
-  if (threadIdx.x < EL_NUM_EVENTS && sev[threadIdx.x]) {
+  const auto add = [&](int kk, int ev, unsigned long long v) {
     if (blockIdx.x < EV_BLOCKS) {
-      evg[((size_t)blockIdx.x * EL_NUM_KERNELS + k) * EL_NUM_EVENTS + threadIdx.x] += sev[threadIdx.x];
+      evg[((size_t)blockIdx.x * EL_NUM_KERNELS + kk) * EL_NUM_EVENTS + ev] += v;
     } else {
-      atomicAdd(&evg[((size_t)EV_BLOCKS * EL_NUM_KERNELS + k) * EL_NUM_EVENTS + threadIdx.x], sev[threadIdx.x]);
+      atomicAdd(&evg[((size_t)EV_BLOCKS * EL_NUM_KERNELS + kk) * EL_NUM_EVENTS + ev], v);
     }
+  };
+  if (threadIdx.x < EL_NUM_EVENTS && sev[threadIdx.x]) add(k, threadIdx.x, sev[threadIdx.x]);
+  if (threadIdx.x == EL_NUM_EVENTS && sev[EL_NUM_EVENTS]) {
+    add(EL_K_COMMIT_S, EL_EV_TRIG, sev[EL_NUM_EVENTS]);
+    add(EL_K_COMMIT_S, EL_EV_RMW, sev[EL_NUM_EVENTS]);
   }
 }
 
@@ -412,7 +420,16 @@ __device__ __forceinline__ uint32_t lds_reserve(uint32_t* qn, bool pred) {
 constexpr uint32_t WQ = 256;   // (x, a) / (x, pid) records per wave and queue
 constexpr uint32_t WQJ = 64;   // fan-out job records per wave
 
+// In-wave duplicate filter for S candidates: a direct-mapped cache of the wave's recent
+// (x, a) keys.  Duplicates of one conclusion within a step are common (G3 step 1: 96 M S
+// candidates for 13 M new facts — the links of one X reach fillers with overlapping
+// subsumers) and each would cost a queue slot, a global write and read and a bit-word
+// atomic; the cache drops those it still holds.  Lossy by design: a key evicted or raced
+// by another lane just reaches the commit, whose atomicOr dedups exactly.
+constexpr uint32_t DEDUP_SLOTS = 128;
+
 struct WaveQ {
+  unsigned long long seen[DEDUP_SLOTS];  // S-candidate keys (x << 32 | a), ~0 = empty
   uint32_t sx[WQ], sa[WQ];  // S candidates
   uint32_t tx[WQ], ta[WQ];  // CR1 told-closure candidates
   uint32_t lx[WQ], lp[WQ];  // link candidates
@@ -428,6 +445,7 @@ __device__ __forceinline__ WaveQ& wave_q(BlockQ& q) { return q.w[threadIdx.x >> 
 __device__ __forceinline__ void q_init(BlockQ& q) {
   WaveQ& w = wave_q(q);
   if (lane_id() == 0) w.ns = w.nt = w.nl = w.nj = 0;
+  for (uint32_t i = lane_id(); i < DEDUP_SLOTS; i += 64) w.seen[i] = ~0ull;
   __syncthreads();
 }
 
@@ -472,7 +490,18 @@ __device__ __forceinline__ void wq_push(uint32_t* qa, uint32_t* qb, uint32_t& qn
 
 __device__ __forceinline__ void emit_s(const DState& st, BlockQ& q, bool pred, uint32_t x, uint32_t a, Ev& ev) {
   WaveQ& w = wave_q(q);
-  if (pred) ev.v[EL_EV_EMIT]++;
+  if (pred) {
+    ev.v[EL_EV_EMIT]++;
+    const unsigned long long key = ((unsigned long long)x << 32) | a;
+    const uint32_t slot = ((x * 2654435761u) ^ (a * 2246822519u)) >> (32 - 7);
+    static_assert(DEDUP_SLOTS == 128, "slot = top 7 bits");
+    if (w.seen[slot] == key) {
+      pred = false;  // the wave queued (x, a) already in this launch
+      ev.dup++;
+    } else {
+      w.seen[slot] = key;
+    }
+  }
   wq_push(w.sx, w.sa, w.ns, pred, x, a, &st.ctr->cand_s, st.cs_x, st.cs_a, st.cs_cap);
 }
 
@@ -1248,8 +1277,18 @@ __device__ __forceinline__ void publish_last(const DState& st, const PubArgs& a,
 // The CR1 told-closure candidates of a superstep, committed before every other candidate
 // (a fact that is also a closure candidate is therefore marked closed, whatever else
 // derived it — the same order as the CPU oracle, so per-step deltas and events agree).
+// A generation that overflowed a candidate or job queue lost candidates: its commit is
+// skipped whole (state t-1 stays untouched) and the host re-runs the step with larger
+// queues, so every step's delta is exactly {candidates} \ S_{t-1} even then.
+__device__ __forceinline__ bool gen_overflowed(const DState& st) {
+  const DCounters* c = st.ctr;
+  return c->cand_s > st.cs_cap || c->cand_t > st.ct_cap || c->cand_l > st.cl_cap || c->cand_a > st.ca_cap ||
+         c->cand_p > st.cp_cap || c->jobs > st.job_cap;
+}
+
 __global__ void k_commit_told(DIndex ix, DState st, uint32_t cap) {
   __shared__ CommitLds sm;
+  if (gen_overflowed(st)) return;
   commit_s(ix, st, sm, blockIdx.x, gridDim.x, min(st.ctr->cand_t, cap), st.ct_x, st.ct_a, 1, EL_K_COMMIT_T);
 }
 
@@ -1281,7 +1320,9 @@ struct CommitArgs {
 __global__ void k_commit(DIndex ix, DState st, CommitArgs a) {
   __shared__ CommitLds sm;
   uint32_t b = blockIdx.x;
-  if (b < a.gs) {
+  if (gen_overflowed(st)) {
+    // nothing committed (see gen_overflowed); the counters still reach the host
+  } else if (b < a.gs) {
     commit_s(ix, st, sm, b, a.gs, min(st.ctr->cand_s, a.cs_cap), st.cs_x, st.cs_a, 0, EL_K_COMMIT_S);
   } else if ((b -= a.gs) < a.gl) {
     commit_l(ix, st, sm, b, a.gl, min(st.ctr->cand_l, a.cl_cap));
@@ -2055,6 +2096,7 @@ struct el_ctx {
   uint32_t tune_commit = env_u32("EL_COMMIT_BLOCKS", 1024);
   uint32_t tune_jobs = env_u32("EL_JOBS_BLOCKS", 1024);
   uint32_t tune_scatter = env_u32("EL_SCATTER_BLOCKS", 512);
+  bool small_queues = getenv("EL_QUEUE_CAP") != nullptr;  // tests: queues start small, grow only on demand
 
   DState dstate() const {
     DState s{};
@@ -2447,6 +2489,9 @@ void el_ctx::alloc_state() {
   }
   cs_cap = std::max<uint64_t>(std::max<uint64_t>(1u << 20, 4 * N), next_pow2(b_conj + b_conj / 4));
   cl_cap = std::max<uint64_t>(1u << 20, next_pow2(b_link + b_link / 4));
+  if (const char* e = getenv("EL_QUEUE_CAP")) {  // tests: small queues force overflowing steps
+    cs_cap = cl_cap = std::max<uint64_t>(256, next_pow2(strtoull(e, nullptr, 10)));
+  }
   if (b_prop + b_prop / 4 > cp_cap) {
     dfree(cp_p);
     dfree(cp_b);
@@ -2784,6 +2829,7 @@ bool el_ctx::superstep(uint32_t mask, uint64_t sb, uint64_t se, uint64_t lb, uin
       fprintf(stderr, "step cand_t %u cand_s %u new_s %llu cand_l %u new_l %llu cand_p %u jobs %u\n", hc.cand_t, hc.cand_s,
               (unsigned long long)(hc.s_log - s_count), hc.cand_l, (unsigned long long)(hc.l_log - l_count), hc.cand_p,
               hc.jobs);
+    const uint64_t next_trig = (hc.s_log - s_count) + (hc.l_log - l_count);  // the next step's triggers
     s_count = hc.s_log;
     l_count = hc.l_log;
     a_count = hc.a_log;
@@ -2791,6 +2837,17 @@ bool el_ctx::superstep(uint32_t mask, uint64_t sb, uint64_t se, uint64_t lb, uin
     gap_rebuild_all();  // rows that outgrew their slack get a new layout before anyone reads them
     // ---- keep the buffers ahead of demand; complete the step if one overflowed
     bool overflow = false;
+    // Each trigger of the next step fans out to a few S conclusions (G3 step 1: 25 M new links
+    // -> 88 M candidates, 3.5 per link): a queue sized ahead for that spares re-running a whole
+    // generation after an overflow (capped: an outlier step still overflows and re-runs).
+    if (const uint64_t want = std::min<uint64_t>(4 * next_trig, 1ull << 28); want > cs_cap && !small_queues) {
+      sync();
+      cs_cap = next_pow2(want);
+      dfree(cs_x);
+      dfree(cs_a);
+      cs_x = dalloc<uint32_t>(cs_cap);
+      cs_a = dalloc<uint32_t>(cs_cap);
+    }
     auto regrow2 = [&](uint32_t need, uint64_t& cap, uint32_t*& a, uint32_t*& b) {
       if (2ull * need <= cap) return;
       sync();  // the step's kernels are still queued: free nothing under them

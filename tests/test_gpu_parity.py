@@ -201,3 +201,15 @@ def test_classifier_rule_types_equals_fused(oracle_mod):
         lb = b.engine.links()
     for u, v in zip(fa + la, fb + lb):
         assert np.array_equal(u, v)
+
+
+@pytest.mark.parametrize("wl", [("g1", 0.25), ("g5", 0.05)], ids=lambda w: f"{w[0]}x{w[1]}")
+def test_queue_overflow_exact(wl, oracle_mod, monkeypatch):
+    """Candidate queues far too small (EL_QUEUE_CAP): steps overflow, their commit is skipped
+    and the step re-runs with larger queues — the closure and every per-step delta are still
+    the oracle's (the re-run's generation work is counted again, so events are not compared)."""
+    monkeypatch.setenv("EL_QUEUE_CAP", "512")
+    ax = generators.workload(wl[0], scale=wl[1])
+    eng, st = _gpu(ax)
+    _assert_same(eng, oracle_mod.saturate(ax, 0), events=False, trace=True)
+    eng.close()
