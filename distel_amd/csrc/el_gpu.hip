@@ -179,7 +179,9 @@ __host__ __device__ constexpr uint32_t gap_cap(uint32_t n) { return 4 * n + 16; 
 struct DState {
   uint32_t* bits;
   uint32_t *slog_x, *slog_a;
-  uint8_t* slog_f;  // 1: the fact came out of a CR1 told closure (its own closure is already out)
+  uint8_t* slog_f;  // 1: the fact came out of a CR1 told closure (its own closure, links and
+                    // propagations are already out); 2: an init fact X ∈ S(X) whose closure
+                    // k_init wrote (its links and propagations are not out yet); 0: neither
   unsigned long long* lhash;
   unsigned long long lmask;
   uint32_t *llog_x, *llog_p;
@@ -196,6 +198,7 @@ struct DState {
   DGap pr;                          // predecessors per pid
   DGap sc;                          // successors per X (chain-second links in partitioned mode)
   uint32_t need_pred, need_succ;  // CSRs with readers: only those get delta counts
+  uint32_t dedup;                 // in-wave S-candidate filter on (EL_DEDUP_OFF: off)
   uint32_t succ_at_commit;        // successor counts taken by k_commit (whole-ontology mode)
   // partitioned exchange: replicated chain-second link log, local send queue, import ranks
   uint32_t *xlog_x, *xlog_p;
@@ -490,8 +493,8 @@ __device__ __forceinline__ void wq_push(uint32_t* qa, uint32_t* qb, uint32_t& qn
 
 __device__ __forceinline__ void emit_s(const DState& st, BlockQ& q, bool pred, uint32_t x, uint32_t a, Ev& ev) {
   WaveQ& w = wave_q(q);
-  if (pred) {
-    ev.v[EL_EV_EMIT]++;
+  if (pred) ev.v[EL_EV_EMIT]++;
+  if (pred && st.dedup) {
     const unsigned long long key = ((unsigned long long)x << 32) | a;
     const uint32_t slot = ((x * 2654435761u) ^ (a * 2246822519u)) >> (32 - 7);
     static_assert(DEDUP_SLOTS == 128, "slot = top 7 bits");
@@ -645,6 +648,7 @@ __global__ void k_init(DIndex ix, DState st, uint32_t lo, uint32_t hi, uint32_t 
     uint8_t f = 1;
     if (j == 0) {
       v = x;
+      f = 2;  // closure written here; its links / propagations come from the first superstep
       ev.v[EL_EV_ENT] += 1 + (ptop != NONE);  // the row, and the skipped closure entry
     } else if (two && j == 1) {
       v = EL_TOP;
@@ -668,75 +672,135 @@ __global__ void k_init(DIndex ix, DState st, uint32_t lo, uint32_t hi, uint32_t 
 
 __global__ void k_set_u32(uint32_t* p, uint32_t v) { *p = v; }
 
+// Wave-cooperative loop over one CSR row per lane, [b, e) (an idle lane passes b = e): the
+// wave walks the concatenation of its lanes' rows 64 entries at a time, so a lane with a
+// long row (a told closure, the links of a whole closure) does not serialise its wave while
+// the other lanes idle.  Every lane runs every round (the emitters ballot); f(valid, owner,
+// j) gets the lane that owns entry j.  Owners are found by binary lifting over the
+// inclusive scan of the row lengths (6 lane shuffles).
+template <class F>
+__device__ __forceinline__ void wave_rows(uint32_t b, uint32_t e, F&& f) {
+  const uint32_t lane = lane_id(), len = e - b;
+  uint32_t inc = len;
+#pragma unroll
+  for (uint32_t o = 1; o < 64; o <<= 1) {
+    const uint32_t v = __shfl_up(inc, o);
+    if (lane >= o) inc += v;
+  }
+  const uint32_t total = __shfl(inc, 63), excl = inc - len;
+  for (uint32_t base = 0; base < total; base += 64) {
+    const uint32_t k = base + lane;
+    uint32_t own = 0;  // the number of lanes whose rows end at or before entry k
+#pragma unroll
+    for (uint32_t step = 32; step > 0; step >>= 1)
+      if (__shfl(inc, (int)(own + step - 1)) <= k) own += step;
+    const bool valid = k < total;
+    own = valid ? own : 0u;
+    const uint32_t j = __shfl(b, (int)own) + (k - __shfl(excl, (int)own));
+    f(valid, own, j);
+  }
+}
+
 // Rules triggered by new S-facts (X, A) = log[begin, end).
 //  CR1  Type1_1AxiomProcessorBase.java:22-43      CR2  Type1_2AxiomProcessorBase.java:45-66
 //  CR3  Type2AxiomProcessorBase.java:45-75        CR4½ Type3_1AxiomProcessorBase.java:194-239
 //  ⊥    TypeBottomAxiomProcessorBase.java:62-123  range RolePairHandler.java:471-479 + K10
+// The index rows of CR1, CR3 and CR4 half-1 (told closure, its links, its propagations) are
+// walked wave-cooperatively (wave_rows); the short CR2 rows per lane.
 __device__ void expand_s(const DIndex& ix, const DState& st, BlockQ& q, uint32_t bid, uint32_t nb,
                          uint32_t begin, uint32_t end, uint32_t mask, uint32_t a_end) {
   Ev ev;
   for (uint32_t base = begin + bid * blockDim.x; base < end; base += nb * blockDim.x) {
     const uint32_t i = base + threadIdx.x;
-    if (i < end) {
-      const uint32_t X = st.slog_x[i], A = st.slog_a[i];
+    const bool act = i < end;
+    uint32_t X = 0, A = 0, f = 1;
+    uint4 m0 = make_uint4(0, 0, 0, 0), m1 = m0;
+    if (act) {
+      X = st.slog_x[i];
+      A = st.slog_a[i];
+      f = st.slog_f[i];
       ev.v[EL_EV_TRIG]++;
-      const uint4 m0 = ix.meta[A], m1 = ix.meta[A + 1];  // the four CSR rows of A at once
-      // A ∈ S(X), A ⊑* B  =>  B ∈ S(X), over the told closure at once; a fact that came out
-      // of a closure is not re-expanded (its closure is a subset of the one that produced it)
-      if ((mask & M_R1) && !st.slog_f[i]) {
-        ev.v[EL_EV_ROW]++;
-        for (uint32_t j = m0.x; j < m1.x; ++j) {
-          const uint32_t B = ix.told_b[j];
+      m0 = ix.meta[A];  // the four CSR rows of A at once
+      m1 = ix.meta[A + 1];
+    }
+    // A ∈ S(X), A ⊑* B  =>  B ∈ S(X), over the told closure at once; a fact that came out
+    // of a closure is not re-expanded (its closure is a subset of the one that produced it)
+    {
+      const bool on = act && (mask & M_R1) && f == 0;
+      if (on) ev.v[EL_EV_ROW]++;
+      wave_rows(on ? m0.x : 0u, on ? m1.x : 0u, [&](bool v, uint32_t own, uint32_t j) {
+        const uint32_t Xo = __shfl(X, (int)own);
+        uint32_t B = 0;
+        bool nw = false;
+        if (v) {
+          B = ix.told_b[j];
           ev.v[EL_EV_ENT]++;
           ev.v[EL_EV_TEST]++;
-          emit_t(st, q, !test_bit(st.bits, ix.W, X, B), X, B, ev);
+          nw = !test_bit(st.bits, ix.W, Xo, B);
         }
-      }
-      if (mask & M_R2) {  // A1..An ∈ S(X), ⊓Ai ⊑ B  =>  B ∈ S(X)
+        emit_t(st, q, nw, Xo, B, ev);
+      });
+    }
+    if (act && (mask & M_R2)) {  // A1..An ∈ S(X), ⊓Ai ⊑ B  =>  B ∈ S(X)
+      ev.v[EL_EV_ROW]++;
+      for (uint32_t j = m0.y; j < m1.y; ++j) {
+        const uint32_t c = ix.cidx_c[j];
+        ev.v[EL_EV_ENT]++;
         ev.v[EL_EV_ROW]++;
-        for (uint32_t j = m0.y; j < m1.y; ++j) {
-          const uint32_t c = ix.cidx_c[j];
+        const uint32_t o1 = ix.conj_ptr[c + 1];
+        bool ok = true;
+        for (uint32_t k = ix.conj_ptr[c]; k < o1; ++k) {
+          const uint32_t op = ix.conj_ops[k];
           ev.v[EL_EV_ENT]++;
-          ev.v[EL_EV_ROW]++;
-          const uint32_t o1 = ix.conj_ptr[c + 1];
-          bool ok = true;
-          for (uint32_t k = ix.conj_ptr[c]; k < o1; ++k) {
-            const uint32_t op = ix.conj_ops[k];
-            ev.v[EL_EV_ENT]++;
-            if (op == A) continue;
-            ev.v[EL_EV_TEST]++;
-            if (!test_bit(st.bits, ix.W, X, op)) {
-              ok = false;
-              break;
-            }
+          if (op == A) continue;
+          ev.v[EL_EV_TEST]++;
+          if (!test_bit(st.bits, ix.W, X, op)) {
+            ok = false;
+            break;
           }
-          bool nw = false;
-          const uint32_t B = ix.conj_b[c];
-          if (ok) {
-            ev.v[EL_EV_ENT]++;
-            ev.v[EL_EV_TEST]++;
-            nw = !test_bit(st.bits, ix.W, X, B);
-          }
-          emit_s(st, q, nw, X, B, ev);
         }
+        bool nw = false;
+        const uint32_t B = ix.conj_b[c];
+        if (ok) {
+          ev.v[EL_EV_ENT]++;
+          ev.v[EL_EV_TEST]++;
+          nw = !test_bit(st.bits, ix.W, X, B);
+        }
+        emit_s(st, q, nw, X, B, ev);
       }
-      if (mask & M_R3) {  // A ∈ S(X), A ⊑ ∃r.B  =>  (X, B) ∈ R(r)
-        ev.v[EL_EV_ROW]++;
-        for (uint32_t j = m0.z; j < m1.z; ++j) {
-          const uint32_t pid = ix.exr_pid[j];
+    }
+    // CR3 / CR4 half-1 run over the told closure too (index rows exr / exl of A cover
+    // {A} ∪ told*(A)): the facts of a closure were covered by the fact that emitted it
+    const bool star = act && f != 1;
+    {  // A ∈ S(X), A ⊑ ∃r.B  =>  (X, B) ∈ R(r)
+      const bool on = star && (mask & M_R3);
+      if (on) ev.v[EL_EV_ROW]++;
+      wave_rows(on ? m0.z : 0u, on ? m1.z : 0u, [&](bool v, uint32_t own, uint32_t j) {
+        const uint32_t Xo = __shfl(X, (int)own);
+        uint32_t pid = 0;
+        bool nw = false;
+        if (v) {
+          pid = ix.exr_pid[j];
           ev.v[EL_EV_ENT]++;
           ev.v[EL_EV_HASH]++;
-          emit_l(st, q, !hash_contains(st.lhash, st.lmask, link_key(pid, X)), X, pid, ev);
+          nw = !hash_contains(st.lhash, st.lmask, link_key(pid, Xo));
         }
-      }
-      if (mask & M_R4Y) {  // A ∈ S(Y=X) new, ∃r.A ⊑ B  =>  propagation ((r, Y), B)
-        ev.v[EL_EV_ROW]++;   // (Type3_1AxiomProcessorBase.java:208-234 writes "Yr" -> B)
-        for (uint32_t j = m0.w; j < m1.w; ++j) {
-          const uint32_t r = ix.exl_r[j], B = ix.exl_b[j];
+        emit_l(st, q, nw, Xo, pid, ev);
+      });
+    }
+    {  // A ∈ S(Y=X) new, ∃r.A ⊑ B  =>  propagation ((r, Y), B)
+       // (Type3_1AxiomProcessorBase.java:208-234 writes "Yr" -> B)
+      const bool on = star && (mask & M_R4Y);
+      if (on) ev.v[EL_EV_ROW]++;
+      wave_rows(on ? m0.w : 0u, on ? m1.w : 0u, [&](bool v, uint32_t own, uint32_t j) {
+        const uint32_t Yo = __shfl(X, (int)own);
+        uint32_t pid = NONE, B = 0, pb = 0, pl = 0;
+        bool fresh = false;
+        if (v) {
+          const uint32_t r = ix.exl_r[j];
+          B = ix.exl_b[j];
           ev.v[EL_EV_ENT] += 2;
-          const uint32_t pid = pair_lookup(ix, r, X, ev);
-          bool fresh = false;
-          uint32_t pb = 0, pl = 0;
+          pid = pair_lookup(ix, r, Yo, ev);
           if (pid != NONE) {
             ev.v[EL_EV_HASH]++;
             fresh = !hash_contains(st.phash, st.pmask, link_key(pid, B));
@@ -747,38 +811,38 @@ __device__ void expand_s(const DIndex& ix, const DState& st, BlockQ& q, uint32_t
               pl = row.y;
             }
           }
-          emit_p(st, fresh, pid, B, ev);
-          emit_job(st, q, pl > 0, JOB_PRED_S, pb, pl, 0, B, ev);
         }
-      }
-      if ((mask & M_RBOT) && A == EL_BOTTOM) {  // ⊥ ∈ S(Y=X) new, (X', Y) ∈ R(*)  =>  ⊥ ∈ S(X')
+        emit_p(st, fresh, pid, B, ev);
+        emit_job(st, q, pl > 0, JOB_PRED_S, pb, pl, 0, B, ev);
+      });
+    }
+    if (act && (mask & M_RBOT) && A == EL_BOTTOM) {  // ⊥ ∈ S(Y=X) new, (X', Y) ∈ R(*)  =>  ⊥ ∈ S(X')
+      ev.v[EL_EV_ROW]++;
+      const uint32_t p1 = ix.fp_ptr[X + 1];
+      for (uint32_t p = ix.fp_ptr[X]; p < p1; ++p) {
+        if (ix.part) {  // partitioned: ⊥ rides the propagation set ((r, Y), ⊥) to every rank
+          ev.v[EL_EV_HASH]++;
+          emit_p(st, !hash_contains(st.phash, st.pmask, link_key(p, EL_BOTTOM)), p, EL_BOTTOM, ev);
+          continue;
+        }
         ev.v[EL_EV_ROW]++;
-        const uint32_t p1 = ix.fp_ptr[X + 1];
-        for (uint32_t p = ix.fp_ptr[X]; p < p1; ++p) {
-          if (ix.part) {  // partitioned: ⊥ rides the propagation set ((r, Y), ⊥) to every rank
-            ev.v[EL_EV_HASH]++;
-            emit_p(st, !hash_contains(st.phash, st.pmask, link_key(p, EL_BOTTOM)), p, EL_BOTTOM, ev);
-            continue;
-          }
-          ev.v[EL_EV_ROW]++;
-          const uint2 row = gap_row(st.pr, p);
-          emit_job(st, q, row.y > 0, JOB_PRED_S, row.x, row.y, 0, EL_BOTTOM, ev);
-        }
+        const uint2 row = gap_row(st.pr, p);
+        emit_job(st, q, row.y > 0, JOB_PRED_S, row.x, row.y, 0, EL_BOTTOM, ev);
       }
-      if ((mask & M_RRNG) && ix.has_range) {  // Y=A ∈ S(X) new, active range (Y, C)  =>  C ∈ S(X)
-        ev.v[EL_EV_ENT]++;
-        if (st.has_act[A]) {
-          for (uint32_t k = 0; k < a_end; ++k) {
-            ev.v[EL_EV_ENT] += 2;
-            const bool hit = st.alog_y[k] == A;
-            const uint32_t C = st.alog_c[k];
-            bool nw = false;
-            if (hit) {
-              ev.v[EL_EV_TEST]++;
-              nw = !test_bit(st.bits, ix.W, X, C);
-            }
-            emit_s(st, q, nw, X, C, ev);
+    }
+    if (act && (mask & M_RRNG) && ix.has_range) {  // Y=A ∈ S(X) new, active range (Y, C)  =>  C ∈ S(X)
+      ev.v[EL_EV_ENT]++;
+      if (st.has_act[A]) {
+        for (uint32_t k = 0; k < a_end; ++k) {
+          ev.v[EL_EV_ENT] += 2;
+          const bool hit = st.alog_y[k] == A;
+          const uint32_t C = st.alog_c[k];
+          bool nw = false;
+          if (hit) {
+            ev.v[EL_EV_TEST]++;
+            nw = !test_bit(st.bits, ix.W, X, C);
           }
+          emit_s(st, q, nw, X, C, ev);
         }
       }
     }
@@ -820,23 +884,38 @@ __device__ void expand_l(const DIndex& ix, const DState& st, BlockQ& q, uint32_t
   Ev ev;
   for (uint32_t base = begin + bid * blockDim.x; base < end; base += nb * blockDim.x) {
     const uint32_t i = base + threadIdx.x;
-    if (i < end) {
-      const uint32_t X = st.llog_x[i], pid = st.llog_p[i];
+    const bool act = i < end;
+    uint32_t X = 0, pid = 0, r = 0, Y = 0;
+    if (act) {
+      X = st.llog_x[i];
+      pid = st.llog_p[i];
       ev.v[EL_EV_TRIG]++;
-      const uint32_t r = ix.pair_role[pid], Y = ix.pair_y[pid];
+      r = ix.pair_role[pid];
+      Y = ix.pair_y[pid];
       ev.v[EL_EV_ENT] += 2;
-      if (mask & M_R4L) {  // (X, Y) ∈ R(r) new, propagation ((r, Y), B)  =>  B ∈ S(X)
-        ev.v[EL_EV_ROW]++;   // (Type3_2AxiomProcessorBase.java:67-96, part 2: all B × ΔX)
-        // (no propagation CSR when the ontology has no ∃r.A ⊑ B: every row is empty)
-        const uint2 row = gap_row(st.pp, pid);
-        const uint32_t g0 = row.x, g1 = row.x + row.y;
-        for (uint32_t j = g0; j < g1; ++j) {
-          const uint32_t B = st.pp.val[j];
+    }
+    {  // (X, Y) ∈ R(r) new, propagation ((r, Y), B)  =>  B ∈ S(X)
+       // (Type3_2AxiomProcessorBase.java:67-96, part 2: all B × ΔX; rows walked by the wave)
+      const bool on = act && (mask & M_R4L);
+      uint2 row = make_uint2(0u, 0u);
+      if (on) {
+        ev.v[EL_EV_ROW]++;
+        row = gap_row(st.pp, pid);  // (no propagation CSR without ∃r.A ⊑ B: rows are empty)
+      }
+      wave_rows(row.x, row.x + row.y, [&](bool v, uint32_t own, uint32_t j) {
+        const uint32_t Xo = __shfl(X, (int)own);
+        uint32_t B = 0;
+        bool nw = false;
+        if (v) {
+          B = st.pp.val[j];
           ev.v[EL_EV_ENT]++;
           ev.v[EL_EV_TEST]++;
-          emit_s(st, q, !test_bit(st.bits, ix.W, X, B), X, B, ev);
+          nw = !test_bit(st.bits, ix.W, Xo, B);
         }
-      }
+        emit_s(st, q, nw, Xo, B, ev);
+      });
+    }
+    if (act) {
       if ((mask & M_RBOT) && !ix.part) {  // ⊥ ∈ S(Y)  =>  ⊥ ∈ S(X)  (partitioned: via propagations)
         ev.v[EL_EV_TEST]++;
         bool nw = false;
@@ -2096,7 +2175,8 @@ struct el_ctx {
   uint32_t tune_commit = env_u32("EL_COMMIT_BLOCKS", 1024);
   uint32_t tune_jobs = env_u32("EL_JOBS_BLOCKS", 1024);
   uint32_t tune_scatter = env_u32("EL_SCATTER_BLOCKS", 512);
-  bool small_queues = getenv("EL_QUEUE_CAP") != nullptr;  // tests: queues start small, grow only on demand
+  bool small_queues = getenv("EL_QUEUE_CAP") != nullptr;
+  bool dedup_off = getenv("EL_DEDUP_OFF") != nullptr;  // diagnostic A/B of the in-wave filter  // tests: queues start small, grow only on demand
 
   DState dstate() const {
     DState s{};
@@ -2131,6 +2211,7 @@ struct el_ctx {
     s.sc = SC.view(&ctr->ov_sc);
     s.need_pred = need_pred ? 1u : 0u;
     s.need_succ = need_succ ? 1u : 0u;
+    s.dedup = dedup_off ? 0u : 1u;
     s.succ_at_commit = (need_succ && !part()) ? 1u : 0u;
     s.xlog_x = xlog_x;
     s.xlog_p = xlog_p;
@@ -2481,10 +2562,13 @@ void el_ctx::alloc_state() {
       b_conj += hx.cidx.ptr[a + 1] - hx.cidx.ptr[a];
       b_prop += hx.exl.ptr[a + 1] - hx.exl.ptr[a];
     };
-    for (uint32_t x = lo; x < hi; ++x) {
+    for (uint32_t x = lo; x < hi; ++x) {  // exr / exl rows already span the told closure
       add(x);
       if (x != EL_TOP && x != EL_BOTTOM && hx.kind[x] != EL_KIND_DATATYPE) add(EL_TOP);
-      for (uint32_t j = hx.told.ptr[x]; j < hx.told.ptr[x + 1]; ++j) add(hx.told.a[j]);
+      for (uint32_t j = hx.told.ptr[x]; j < hx.told.ptr[x + 1]; ++j) {
+        const uint32_t a = hx.told.a[j];
+        b_conj += hx.cidx.ptr[a + 1] - hx.cidx.ptr[a];  // the closure's facts still run CR2
+      }
     }
   }
   cs_cap = std::max<uint64_t>(std::max<uint64_t>(1u << 20, 4 * N), next_pow2(b_conj + b_conj / 4));

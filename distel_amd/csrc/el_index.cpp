@@ -254,6 +254,36 @@ std::string build_index(const el_axioms& ax, HostIndex& o) {
     }
     o.exl = make_csr(N, t, true);
   }
+  // CR3 and CR4 half-1 over the told closure: row A holds the entries of every
+  // B ∈ {A} ∪ told*(A).  A fact A new in S(X) then emits the links / propagations of its
+  // whole closure in the superstep that emits the closure itself, and the closure's facts
+  // (flagged) skip CR3 / CR4 half-1: one superstep less on every CR4 -> CR1 -> CR3 path.
+  {
+    auto star = [&](const Csr& c, bool two) {
+      Csr s;
+      s.ptr.assign(N + 1, 0);
+      std::vector<uint64_t> row;
+      for (uint32_t a = 0; a < N; ++a) {
+        row.clear();
+        auto add = [&](uint32_t u) {
+          for (uint32_t j = c.ptr[u]; j < c.ptr[u + 1]; ++j)
+            row.push_back(((uint64_t)c.a[j] << 32) | (two ? c.b[j] : 0u));
+        };
+        add(a);
+        for (uint32_t j = o.told.ptr[a]; j < o.told.ptr[a + 1]; ++j) add(o.told.a[j]);
+        std::sort(row.begin(), row.end());
+        row.erase(std::unique(row.begin(), row.end()), row.end());
+        for (uint64_t v : row) {
+          s.a.push_back((uint32_t)(v >> 32));
+          if (two) s.b.push_back((uint32_t)v);
+        }
+        s.ptr[a + 1] = (uint32_t)s.a.size();
+      }
+      return s;
+    };
+    o.exr = star(o.exr, false);
+    o.exl = star(o.exl, true);
+  }
   // CR5 per pair: pids of (s, Y) for every strict super-role s of r
   {
     std::vector<std::array<uint32_t, 3>> t;

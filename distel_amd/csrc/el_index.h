@@ -30,8 +30,8 @@ struct HostIndex {
   Csr cidx;       // A -> conj id c              CR2  conjunct index (AxiomLoader.java:931-941, DB3)
   Csr conj;       // c -> operands (sorted)      CR2
   std::vector<uint32_t> conj_b;     // c -> B
-  Csr exr;        // A -> pid                    CR3  (A ⊑ ∃r.B)
-  Csr exl;        // A -> (r, B) sorted (r,B)    CR4  (∃r.A ⊑ B)
+  Csr exr;        // A -> pid of A' ⊑ ∃r.B, A' ∈ {A} ∪ told*(A)          CR3 (over the told closure)
+  Csr exl;        // A -> (r, B) of ∃r.A' ⊑ B, A' ∈ {A} ∪ told*(A), sorted   CR4 half-1 (idem)
   std::vector<uint32_t> fp_ptr;     // Y -> pid range (pairs sorted by (Y, r))
   std::vector<uint32_t> pair_role;  // pid -> r
   std::vector<uint32_t> pair_y;     // pid -> Y

@@ -97,6 +97,32 @@ typedef struct {
   uint32_t* b;
 } csr;
 
+static csr csr_build(uint32_t rows, trip* t, size_t n);
+
+/* rows of src for {A} ∪ toldc(A) per A, as one CSR (src is freed) */
+static csr csr_star(csr* src, const csr* toldc, uint32_t N) {
+  size_t n = 0, m = 0;
+  uint32_t A, j, q;
+  trip* t;
+  csr out;
+  for (A = 0; A < N; ++A) {
+    n += src->ptr[A + 1] - src->ptr[A];
+    for (j = toldc->ptr[A]; j < toldc->ptr[A + 1]; ++j) n += src->ptr[toldc->a[j] + 1] - src->ptr[toldc->a[j]];
+  }
+  t = (trip*)malloc((n + 1) * sizeof(trip));
+  for (A = 0; A < N; ++A) {
+    for (q = src->ptr[A]; q < src->ptr[A + 1]; ++q) t[m++] = (trip){A, src->a[q], src->b[q]};
+    for (j = toldc->ptr[A]; j < toldc->ptr[A + 1]; ++j) {
+      uint32_t B = toldc->a[j];
+      for (q = src->ptr[B]; q < src->ptr[B + 1]; ++q) t[m++] = (trip){A, src->a[q], src->b[q]};
+    }
+  }
+  out = csr_build(N, t, m);
+  free(t);
+  free(src->ptr), free(src->a), free(src->b);
+  return out;
+}
+
 /* rows sorted by (a, b), duplicates removed */
 static csr csr_build(uint32_t rows, trip* t, size_t n) {
   csr c;
@@ -204,7 +230,8 @@ struct elo_ctx {
   /* state */
   uint32_t* bits;
   vec slog_x, slog_a;
-  vec slog_f; /* 1: the fact came from a CR1 told closure, so its own closure is already out */
+  vec slog_f; /* 1: the fact came from a CR1 told closure, so its own closure, links and
+               * propagations are already out; 2: init X ∈ S(X), closure written; 0: neither */
   vec* srow;
   hset links;
   vec llog_x, llog_p;
@@ -458,6 +485,11 @@ static int build_index(elo_ctx* c, const el_axioms* ax) {
     c->role_has_exl[ax->exl_r[i]] = 1;
   }
   c->exl = csr_build(N, t, n);
+  /* CR3 / CR4 half-1 over the told closure (el_index.cpp): row A gathers the rows of every
+   * B ∈ {A} ∪ told*(A), sorted and unique, so a fact emits its closure's links and
+   * propagations in the superstep that emits the closure; closure facts skip both rules */
+  c->exr = csr_star(&c->exr, &c->toldc, N);
+  c->exl = csr_star(&c->exl, &c->toldc, N);
   {
     size_t m = 0, pc = 0;
     trip* u;
@@ -699,7 +731,9 @@ static void expand_s(elo_ctx* c, cands* k, uint32_t mask, uint64_t b, uint64_t e
         }
       }
     }
-    if (mask & M_R3) {
+    /* CR3 / CR4 half-1 over the told closure: a fact that came out of a closure (flag 1) was
+     * covered by the fact that emitted the closure (the exr / exl rows span {A} ∪ told*(A)) */
+    if ((mask & M_R3) && c->slog_f.v[i] != 1) {
       EV(K, EL_EV_ROW);
       for (j = c->exr.ptr[A]; j < c->exr.ptr[A + 1]; ++j) {
         uint32_t pid = c->exr.a[j];
@@ -708,7 +742,7 @@ static void expand_s(elo_ctx* c, cands* k, uint32_t mask, uint64_t b, uint64_t e
         if (!hs_has(&c->links, lkey(pid, X))) emit_l(c, k, K, X, pid);
       }
     }
-    if (mask & M_R4Y) { /* A ∈ S(Y=X) new, ∃r.A ⊑ B => propagation ((r, Y), B) */
+    if ((mask & M_R4Y) && c->slog_f.v[i] != 1) { /* A ∈ S(Y=X) new, ∃r.A ⊑ B => propagation ((r, Y), B) */
       EV(K, EL_EV_ROW);
       for (j = c->exl.ptr[A]; j < c->exl.ptr[A + 1]; ++j) {
         uint32_t r = c->exl.a[j], B = c->exl.b[j], pid;
@@ -1133,7 +1167,7 @@ int elo_init(elo_ctx* c) {
     setbit(c, x, x);
     vpush(&c->slog_x, x);
     vpush(&c->slog_a, x);
-    vpush(&c->slog_f, 1); /* its closure is written right here */
+    vpush(&c->slog_f, 2); /* its closure is written right here; its links / propagations are not */
     vpush(&c->srow[x], x);
     ++init;
     if (two) {
