@@ -33,11 +33,15 @@ def init_from_env(prefer_nccl: bool = True) -> Ranks:
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     has_cuda = torch.cuda.is_available()
+    if has_cuda:  # more ranks than GPUs (a rehearsal on a 1-GPU box) share the cards round-robin
+        local = local % max(1, torch.cuda.device_count())
     dev = torch.device("cuda", local) if has_cuda else torch.device("cpu")
     if world <= 1:
         return Ranks(rank, 1, local, None, dev)
     import torch.distributed as dist
-    backend = "nccl" if (prefer_nccl and has_cuda) else "gloo"
+    # EL_DIST_BACKEND=gloo: the barrier and the two reductions over gloo (RCCL refuses two
+    # ranks on one GPU, which a 1-GPU rehearsal of the N-rank launch needs)
+    backend = os.environ.get("EL_DIST_BACKEND") or ("nccl" if (prefer_nccl and has_cuda) else "gloo")
     if backend == "nccl":
         torch.cuda.set_device(local)
     else:

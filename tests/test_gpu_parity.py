@@ -213,3 +213,15 @@ def test_queue_overflow_exact(wl, oracle_mod, monkeypatch):
     eng, st = _gpu(ax)
     _assert_same(eng, oracle_mod.saturate(ax, 0), events=False, trace=True)
     eng.close()
+
+
+def test_g3_full(oracle_mod):
+    """BASELINE configs[2] size (SNOMED-shaped, 390k concepts after normalization, 136 M derived
+    axioms): closure, links, every per-superstep delta and the per-phase event counts equal
+    the CPU oracle's (≈20 s of oracle time on the GPU box's host)."""
+    ax = generators.workload("g3")
+    eng, st = _gpu(ax)
+    o = oracle_mod.saturate(ax, 0)
+    _assert_same(eng, o)
+    assert st["derived"] == o.stats()["derived"] == 136499458
+    eng.close()
