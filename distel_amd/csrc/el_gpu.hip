@@ -174,7 +174,8 @@ __device__ __forceinline__ uint2 gap_row(const DGap& g, uint32_t r) {
 }
 
 // capacity of a row with n entries after a re-layout (the CPU oracle mirrors it)
-__host__ __device__ constexpr uint32_t gap_cap(uint32_t n) { return 4 * n + 16; }
+constexpr uint32_t GAP_MUL = 8;  // slack factor: a row re-laid out with n entries has room for GAP_MUL·n + 16
+__host__ __device__ constexpr uint32_t gap_cap(uint32_t n) { return GAP_MUL * n + 16; }
 
 struct DState {
   uint32_t* bits;
@@ -3141,7 +3142,7 @@ void el_ctx::gap_rebuild(GapCsr& g, uint32_t n_ovf, uint64_t entries) {
   if (n_ovf > g.ovq_cap) throw std::runtime_error("gapped-CSR overflow queue overrun");
   const uint32_t R = g.rows;
   // Σ_r gap_cap(len[r]) with Σ len = entries: the host sizes the new layout without a readback
-  const uint64_t total = 4 * entries + (uint64_t)gap_cap(0) * R;
+  const uint64_t total = (uint64_t)GAP_MUL * entries + (uint64_t)gap_cap(0) * R;
   if (total > 0xffffffffull) throw ElError{EL_ENOMEM, "gapped CSR beyond 2^32 slots"};
   if (total > g.val2_cap) {
     sync();
@@ -3208,7 +3209,7 @@ void el_ctx::gap_build_from_log(GapCsr& g, const uint32_t* rows, const uint32_t*
     HIPCHK(hipGetLastError());
   }
   launch_gap_scan(g.len, R, g.start);
-  const uint64_t total = 4 * n + (uint64_t)gap_cap(0) * R;
+  const uint64_t total = (uint64_t)GAP_MUL * n + (uint64_t)gap_cap(0) * R;
   if (total > g.val_cap) {
     sync();
     dfree(g.val);
