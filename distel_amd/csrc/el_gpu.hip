@@ -2859,11 +2859,11 @@ bool el_ctx::superstep(uint32_t mask, uint64_t sb, uint64_t se, uint64_t lb, uin
     }
     if (slog_cap > S.cap) S.grow(s_csr_count, slog_cap);
     grow_log(l_count, cl_cap, llog_cap, llog_x, llog_p);
-    if (2 * (l_count + cl_cap) > lhash_cap) rehash_links(next_pow2(4 * (l_count + cl_cap)));
+    if (2 * (l_count + cl_cap) > lhash_cap) rehash_links(next_pow2(2 * (l_count + cl_cap)));
     grow_log(a_count, ca_cap, alog_cap, alog_y, alog_c);
-    if (2 * (a_count + ca_cap) > ahash_cap) rehash_acts(next_pow2(4 * (a_count + ca_cap)));
+    if (2 * (a_count + ca_cap) > ahash_cap) rehash_acts(next_pow2(2 * (a_count + ca_cap)));
     grow_log(p_count, cp_cap, plog_cap, plog_p, plog_b);
-    if (2 * (p_count + cp_cap) > phash_cap) rehash_props(next_pow2(4 * (p_count + cp_cap)));
+    if (2 * (p_count + cp_cap) > phash_cap) rehash_props(next_pow2(2 * (p_count + cp_cap)));
 
     // ---- generation (reads only the state of step t-1; candidate counters are zero here)
     DState st = dstate();
@@ -2985,9 +2985,9 @@ void el_ctx::grow_part(uint64_t new_xcap) {
     cap = c;
   };
   grow_log(p_count, p_count + cp_cap + rb, plog_cap, plog_p, plog_b);
-  if (2 * (p_count + cp_cap + rb) > phash_cap) rehash_props(next_pow2(4 * (p_count + cp_cap + rb)));
+  if (2 * (p_count + cp_cap + rb) > phash_cap) rehash_props(next_pow2(2 * (p_count + cp_cap + rb)));
   grow_log(a_count, a_count + ca_cap + rb, alog_cap, alog_y, alog_c);
-  if (2 * (a_count + ca_cap + rb) > ahash_cap) rehash_acts(next_pow2(4 * (a_count + ca_cap + rb)));
+  if (2 * (a_count + ca_cap + rb) > ahash_cap) rehash_acts(next_pow2(2 * (a_count + ca_cap + rb)));
   grow_log(x_count, x_count + xb, xlog_cap, xlog_x, xlog_p);
 }
 
@@ -3051,7 +3051,7 @@ uint64_t el_ctx::superstep_part(uint32_t mask, uint64_t sb, uint64_t se, uint64_
       }
       if (slog_cap > S.cap) S.grow(s_csr_count, slog_cap);
       grow_log(l_count, cl_cap, llog_cap, llog_x, llog_p);
-      if (2 * (l_count + cl_cap) > lhash_cap) rehash_links(next_pow2(4 * (l_count + cl_cap)));
+      if (2 * (l_count + cl_cap) > lhash_cap) rehash_links(next_pow2(2 * (l_count + cl_cap)));
       grow_part(xcap);
     }
     const uint32_t s0 = (uint32_t)s_count, l0 = (uint32_t)l_count, a0 = (uint32_t)a_count, p0 = (uint32_t)p_count;
