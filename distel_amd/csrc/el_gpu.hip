@@ -116,6 +116,7 @@ struct DIndex {
   const uint4* meta;  // per concept A: {told_ptr, cidx_ptr, exr_ptr, exl_ptr}[A] — one 32 B span for A, A+1
   const uint32_t* init_off;  // N + 1: start of concept X's init facts in an init-ordered log
   uint32_t has_range;
+  uint32_t has_bot;  // some axiom concludes ⊥ (or ∃r.⊥): else ⊥ ∈ S(Y) only for Y = ⊥, no link reaches ⊥
   // row partition (el_config.exchange != NONE): this context owns rows [lo, hi)
   uint32_t lo, hi;
   uint32_t part;               // 1 = partitioned protocol (oracle/partition_model.py)
@@ -817,7 +818,7 @@ __device__ void expand_s(const DIndex& ix, const DState& st, BlockQ& q, uint32_t
         emit_job(st, q, pl > 0, JOB_PRED_S, pb, pl, 0, B, ev);
       });
     }
-    if (act && (mask & M_RBOT) && A == EL_BOTTOM) {  // ⊥ ∈ S(Y=X) new, (X', Y) ∈ R(*)  =>  ⊥ ∈ S(X')
+    if (act && (mask & M_RBOT) && ix.has_bot && A == EL_BOTTOM) {  // ⊥ ∈ S(Y=X) new, (X', Y) ∈ R(*)  =>  ⊥ ∈ S(X')
       ev.v[EL_EV_ROW]++;
       const uint32_t p1 = ix.fp_ptr[X + 1];
       for (uint32_t p = ix.fp_ptr[X]; p < p1; ++p) {
@@ -917,7 +918,7 @@ __device__ void expand_l(const DIndex& ix, const DState& st, BlockQ& q, uint32_t
       });
     }
     if (act) {
-      if ((mask & M_RBOT) && !ix.part) {  // ⊥ ∈ S(Y)  =>  ⊥ ∈ S(X)  (partitioned: via propagations)
+      if ((mask & M_RBOT) && ix.has_bot && !ix.part) {  // ⊥ ∈ S(Y) => ⊥ ∈ S(X)  (partitioned: via propagations)
         ev.v[EL_EV_TEST]++;
         bool nw = false;
         if (test_bit(st.bits, ix.W, Y, EL_BOTTOM)) {
@@ -2452,6 +2453,7 @@ std::string el_ctx::install_index(el::HostIndex&& hnew) {
                      has0(store.dom_c) || has0(store.rng_c);
     need_succ = !h.chf.a.empty();
     need_pred = !h.exl.a.empty() || need_succ || bot;
+    ix.has_bot = bot ? 1u : 0u;
     use_props = !h.exl.a.empty() || (part() && bot);
   }
   // owned rows: the configured range, or the equal split of [0, N)

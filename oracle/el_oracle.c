@@ -244,6 +244,7 @@ struct elo_ctx {
   vec* prow; /* propagations per pid */
   uint64_t s_init;
   int need_pred, need_succ; /* the GPU maintains these CSRs only when they have readers */
+  int has_bot;              /* some axiom concludes ⊥: else the ⊥ rule cannot fire (skipped, as on the GPU) */
   /* slack capacities of the GPU's gapped CSR rows (predecessors, successors, propagations)
    * and this step's entries past them: the GPU re-lays out a CSR after a step with any */
   uint32_t *cap_pr, *cap_sc, *cap_pp;
@@ -590,6 +591,7 @@ int elo_create(elo_ctx** out, const el_axioms* ax, int mode) {
     for (i = 0; i < ax->n_range; ++i) bot |= ax->rng_c[i] == EL_BOTTOM;
     c->need_succ = ax->n_chain > 0;
     c->need_pred = ax->n_ex_lhs > 0 || ax->n_chain > 0 || bot;
+    c->has_bot = bot;
   }
   c->bits = (uint32_t*)calloc((size_t)c->N * c->W + 1, sizeof(uint32_t));
   if (!c->bits) {
@@ -762,7 +764,7 @@ static void expand_s(elo_ctx* c, cands* k, uint32_t mask, uint64_t b, uint64_t e
         }
       }
     }
-    if ((mask & M_RBOT) && A == EL_BOTTOM) {
+    if ((mask & M_RBOT) && c->has_bot && A == EL_BOTTOM) {
       uint32_t p;
       EV(K, EL_EV_ROW);
       for (p = c->fp_ptr[X]; p < c->fp_ptr[X + 1]; ++p) {
@@ -806,7 +808,7 @@ static void expand_l(elo_ctx* c, cands* k, uint32_t mask, uint64_t b, uint64_t e
         if (!bit(c, X, B)) emit_s(c, k, K, X, B);
       }
     }
-    if (mask & M_RBOT) {
+    if ((mask & M_RBOT) && c->has_bot) {
       EV(K, EL_EV_TEST);
       if (bit(c, Y, EL_BOTTOM)) {
         EV(K, EL_EV_TEST);
