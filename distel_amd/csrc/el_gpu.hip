@@ -2193,6 +2193,7 @@ struct el_ctx {
     return e ? (uint32_t)std::max(1ul, strtoul(e, nullptr, 10)) : d;
   }
   uint32_t tune_commit = env_u32("EL_COMMIT_BLOCKS", 1024);
+  uint32_t tune_expand = env_u32("EL_EXPAND_BLOCKS", 1024);
   uint32_t tune_jobs = env_u32("EL_JOBS_BLOCKS", 1024);
   uint32_t tune_scatter = env_u32("EL_SCATTER_BLOCKS", 512);
   bool small_queues = getenv("EL_QUEUE_CAP") != nullptr;
@@ -2888,8 +2889,8 @@ bool el_ctx::superstep(uint32_t mask, uint64_t sb, uint64_t se, uint64_t lb, uin
     // ---- generation (reads only the state of step t-1; candidate counters are zero here)
     DState st = dstate();
     ExpandArgs ea{};
-    ea.gs = se > sb ? grid_for(se - sb) : 0u;
-    ea.gl = le > lb ? grid_for(le - lb) : 0u;
+    ea.gs = se > sb ? grid_for(se - sb, tune_expand) : 0u;
+    ea.gl = le > lb ? grid_for(le - lb, tune_expand) : 0u;
     ea.ga = do_a ? grid_for(hx.N) : 0u;
     ea.gp = do_p ? grid_for(pe - pb) : 0u;
     ea.sb = (uint32_t)sb, ea.se = (uint32_t)se, ea.lb = (uint32_t)lb, ea.le = (uint32_t)le;
@@ -2905,8 +2906,12 @@ bool el_ctx::superstep(uint32_t mask, uint64_t sb, uint64_t se, uint64_t lb, uin
     // ---- commit (counts read on the device); its last block publishes the counters to
     // pinned host memory and zeroes the candidate counters, so the step ends with ONE sync
     CommitArgs ca{};
-    ca.gs = grid_for(cs_cap, tune_commit);
-    ca.gl = grid_for(cl_cap, tune_commit);
+    // commit grids sized from the step's triggers (the candidate counts are only known on the
+    // device; the roles loop grid-stride, so any size is correct): a small step gets a small
+    // launch, whose dispatch and completion protocol cost less than 1024 idle workgroups
+    const uint64_t est = std::max<uint64_t>(2 * ((se - sb) + (le - lb)), 16384);
+    ca.gs = grid_for(std::min<uint64_t>(cs_cap, est), tune_commit);
+    ca.gl = grid_for(std::min<uint64_t>(cl_cap, est), tune_commit);
     ca.ga = hx.rng.a.size() ? grid_for(ca_cap, 64) : 0u;
     ca.gp = hx.exl.a.size() ? grid_for(cp_cap, 256) : 0u;
     ca.cs_cap = (uint32_t)cs_cap, ca.cl_cap = (uint32_t)cl_cap;
@@ -2914,8 +2919,8 @@ bool el_ctx::superstep(uint32_t mask, uint64_t sb, uint64_t se, uint64_t lb, uin
     ca.pub = PubArgs{hc_dev, commit_done, ++commit_seq};
     ca.publish = 1;
     launch(EL_K_COMMIT_T, [&] {  // CR1 told-closure candidates first (see k_commit_told)
-      hipLaunchKernelGGL(k_commit_told, dim3(grid_for(ct_cap, tune_commit)), dim3(BLOCK), 0, stream, ix, st,
-                         (uint32_t)ct_cap);
+      hipLaunchKernelGGL(k_commit_told, dim3(grid_for(std::min<uint64_t>(ct_cap, 8 * est), tune_commit)), dim3(BLOCK),
+                         0, stream, ix, st, (uint32_t)ct_cap);
     });
     if (split_commit) {  // diagnostic: S role alone, then the other roles (rocprof sees both)
       CommitArgs c1 = ca;
