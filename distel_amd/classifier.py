@@ -53,9 +53,9 @@ class GpuAxiomProcessor(AxiomProcessor):
 class ELClassifier:
     """Loads the normalized axioms once (AxiomLoader), then classifies (ELClassifier)."""
 
-    def __init__(self, axioms: Axioms, device: int = 0, profile: bool = False):
+    def __init__(self, axioms: Axioms, device: int = 0, profile: bool = False, compat_chain: bool = False):
         self.axioms = axioms
-        self.engine = Engine(device=device, profile=profile)
+        self.engine = Engine(device=device, profile=profile, compat_chain=compat_chain)
         t0 = time.perf_counter()
         self.engine.load(axioms)
         self.engine.init()

@@ -28,6 +28,8 @@ def _classify(args) -> int:
     ax = owl.load_functional(args.ontology, normalized=args.normalized)
     parse_s = time.perf_counter() - t0
     if args.parts > 1:
+        if args.compat_chain:
+            raise SystemExit("--compat-chain runs on one context (--parts 1)")
         t1 = time.perf_counter()
         engs, sts = engine.classify_partitioned(ax, args.parts, devices=list(range(args.devices)))
         cls_s = time.perf_counter() - t1
@@ -37,7 +39,7 @@ def _classify(args) -> int:
         for e in engs:
             e.close()
     else:
-        eng = engine.Engine(device=args.device)
+        eng = engine.Engine(device=args.device, compat_chain=args.compat_chain)
         t1 = time.perf_counter()
         eng.load(ax)
         load_s = time.perf_counter() - t1
@@ -81,6 +83,8 @@ def main(argv=None) -> int:
     c.add_argument("--out", help="write X|B lines here")
     c.add_argument("--names", action="store_true", help="IRIs instead of DistEL packed ids")
     c.add_argument("--distel-compat", action="store_true", help="add individuals' ⊥ ⊑ a entries (H7)")
+    c.add_argument("--compat-chain", action="store_true",
+                   help="DistEL's CR6 join that ignores s (hazard H2, EL_FLAG_COMPAT_DISTEL_CHAIN)")
     c.add_argument("--device", type=int, default=0)
     c.add_argument("--parts", type=int, default=1, help="row partitions (in-process delta exchange)")
     c.add_argument("--devices", type=int, default=1, help="GPUs the partitions are spread over")

@@ -2096,6 +2096,7 @@ struct LocalExchange : Exchange {
 struct el_ctx {
   int device = 0;
   int profile = 0;
+  uint32_t flags = 0;  // EL_FLAG_* (el_config.flags)
   hipStream_t stream = nullptr;
   std::string err;
   bool loaded = false, inited = false;
@@ -3435,10 +3436,11 @@ int el_create(el_ctx** out, const el_config* cfg) {
   el_ctx* c = new (std::nothrow) el_ctx();
   if (!c) return EL_ENOMEM;
   if (cfg) {
-    if (cfg->flags != 0) {
+    if (cfg->flags & ~EL_FLAGS_KNOWN) {
       delete c;
       return EL_EINVAL;
     }
+    c->flags = cfg->flags;
     c->device = cfg->device;
     c->profile = cfg->profile;
     c->xmode = cfg->exchange;
@@ -3511,7 +3513,7 @@ int el_load(el_ctx* c, const el_axioms* ax) {
     el::AxiomStore store;
     std::string e = store.append(*ax);
     el::HostIndex hx;
-    if (e.empty()) e = el::build_index(store.view(), hx);
+    if (e.empty()) e = el::build_index(store.view(), hx, c->flags);
     if (!e.empty()) return fail(c, EL_EINVAL, e);
     HIPCHK(hipStreamSynchronize(c->stream));
     c->free_state();
@@ -3539,7 +3541,7 @@ int el_add_axioms(el_ctx* c, const el_axioms* inc) {
     el::AxiomStore store = c->store;
     std::string e = store.append(*inc);
     el::HostIndex hx;
-    if (e.empty()) e = el::build_index(store.view(), hx);
+    if (e.empty()) e = el::build_index(store.view(), hx, c->flags);
     if (!e.empty()) return fail(c, EL_EINVAL, e);
     c->sync();
     if (!c->inited) {  // nothing saturated yet: a plain reload

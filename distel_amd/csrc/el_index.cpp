@@ -12,7 +12,9 @@
 #include <algorithm>
 #include <array>
 #include <cstdio>
+#include <map>
 #include <numeric>
+#include <set>
 #include <utility>
 
 namespace el {
@@ -91,7 +93,29 @@ el_axioms AxiomStore::view() const {
   return a;
 }
 
-std::string build_index(const el_axioms& ax, HostIndex& o) {
+void distel_chain_set(const el_axioms& ax, std::vector<uint32_t>& r, std::vector<uint32_t>& s,
+                      std::vector<uint32_t>& t) {
+  // Type5AxiomProcessorBase.java:128-143: for key "Yr" every Z of DB4["Yr"] (any s whose
+  // chain starts with r, RolePairHandler.java:428-443) goes to every t of r's chains
+  std::map<uint32_t, std::pair<std::set<uint32_t>, std::set<uint32_t>>> by_first;
+  for (uint32_t i = 0; i < ax.n_chain; ++i) {
+    by_first[ax.ch_r[i]].first.insert(ax.ch_s[i]);
+    by_first[ax.ch_r[i]].second.insert(ax.ch_t[i]);
+  }
+  r.clear(), s.clear(), t.clear();
+  for (const auto& [rr, st] : by_first)
+    for (uint32_t ss : st.first)
+      for (uint32_t tt : st.second) r.push_back(rr), s.push_back(ss), t.push_back(tt);
+}
+
+std::string build_index(const el_axioms& ax_in, HostIndex& o, uint32_t flags) {
+  el_axioms ax = ax_in;
+  std::vector<uint32_t> xr, xs, xt;
+  if (flags & EL_FLAG_COMPAT_DISTEL_CHAIN) {
+    distel_chain_set(ax_in, xr, xs, xt);
+    ax.n_chain = (uint32_t)xr.size();
+    ax.ch_r = xr.data(), ax.ch_s = xs.data(), ax.ch_t = xt.data();
+  }
   char msg[256];
   const uint32_t N = ax.n_concepts, R = ax.n_roles;
   if (N < 2) return "n_concepts must be >= 2 (⊥ = 0 and ⊤ = 1 are reserved)";

@@ -56,6 +56,12 @@ struct AxiomStore {
 
 // Validates ids and builds the canonical indexes.  Returns "" on success or an
 // error message (the reference throws on unknown concepts, AxiomLoader.java:1343-1354).
-std::string build_index(const el_axioms& ax, HostIndex& out);
+// flags: el_config.flags (EL_FLAG_COMPAT_DISTEL_CHAIN indexes the DistEL chain set).
+std::string build_index(const el_axioms& ax, HostIndex& out, uint32_t flags = 0);
+
+// H2 (EL_FLAG_COMPAT_DISTEL_CHAIN): the chain set DistEL's CR6 effectively applies,
+// {r∘s⊑t : some r∘s⊑t' and some r∘s'⊑t told}, sorted and deduplicated.
+void distel_chain_set(const el_axioms& ax, std::vector<uint32_t>& r, std::vector<uint32_t>& s,
+                      std::vector<uint32_t>& t);
 
 }  // namespace el

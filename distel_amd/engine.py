@@ -20,6 +20,7 @@ LIB_PATH = os.path.join(_HERE, "lib", "libel_gpu.so")
 
 EL_OK, EL_EINVAL, EL_ENOMEM, EL_EHIP, EL_ESTATE, EL_ERANGE = 0, -1, -2, -3, -4, -5
 LAYOUT_X_TO_B, LAYOUT_B_TO_X = 0, 1
+EL_FLAG_COMPAT_DISTEL_CHAIN = 0x1  # el_config.flags: hazard H2 reproduced (include/el_gpu.h)
 
 # work phases (el_kernel); "kernel:role" where several phases share one launch
 KERNEL_NAMES = ["k_expand:s", "k_expand:l", "k_jobs", "k_expand:a", "k_commit:s", "k_commit:l", "k_commit:a",
@@ -227,10 +228,13 @@ def rccl_unique_id() -> bytes:
 class Engine:
     """One GPU saturation context (one DistEL rule cluster), on one device."""
 
-    def __init__(self, device: int = 0, profile: bool = False, partition: Optional[Partition] = None):
+    def __init__(self, device: int = 0, profile: bool = False, partition: Optional[Partition] = None,
+                 compat_chain: bool = False):
+        """compat_chain: EL_FLAG_COMPAT_DISTEL_CHAIN, DistEL's CR6 join that ignores s (hazard H2,
+        Type5AxiomProcessorBase.java:115-154); default the complete EL+ closure."""
         self._lib = load_library()
         self._ctx = C.c_void_p()
-        cfg = _ElConfig(device, 1 if profile else 0, 0)
+        cfg = _ElConfig(device, 1 if profile else 0, EL_FLAG_COMPAT_DISTEL_CHAIN if compat_chain else 0)
         if partition is not None:
             cfg.exchange = partition.exchange
             cfg.part_rank, cfg.part_count = partition.rank, partition.count
@@ -438,9 +442,10 @@ def merge_links(engs: List[Engine]) -> Tuple[np.ndarray, np.ndarray, np.ndarray]
     return x[o], r[o], y[o]
 
 
-def classify(ax: Axioms, device: int = 0, profile: bool = False) -> Tuple[Engine, Stats]:
+def classify(ax: Axioms, device: int = 0, profile: bool = False,
+             compat_chain: bool = False) -> Tuple[Engine, Stats]:
     """Load + init + saturate in one call (ELClassifier.classify() over all rule types)."""
-    eng = Engine(device=device, profile=profile)
+    eng = Engine(device=device, profile=profile, compat_chain=compat_chain)
     eng.load(ax)
     eng.init()
     st = eng.saturate()

@@ -146,10 +146,20 @@ typedef struct el_axioms {
 
 typedef struct el_group el_group;
 
+/* el_config.flags.  EL_FLAG_COMPAT_DISTEL_CHAIN reproduces parity hazard H2 (SURVEY.md
+ * §8.H) deterministically: DistEL's CR6 joins DB1["Yr"] (X with (X,Y) ∈ R(r)) with DB4["Yr"]
+ * (Z with (Y,Z) ∈ R(s) for ANY s second in a chain whose first role is r) and adds (X,Z) to
+ * the t of EVERY chain whose first role is r (Type5AxiomProcessorBase.java:115-154;
+ * RolePairHandler.java:395-443).  That is the complete join over the chain set
+ * {r∘s⊑t : s ∈ second(r), t ∈ third(r)}, which el_load builds in place of the told chains.
+ * Default (0): the correct EL+ join on s. */
+#define EL_FLAG_COMPAT_DISTEL_CHAIN 0x1u
+#define EL_FLAGS_KNOWN (EL_FLAG_COMPAT_DISTEL_CHAIN)
+
 typedef struct el_config {
   int device;            /* HIP device ordinal (one context per GPU / rank) */
   int profile;           /* 1 = record per-kernel HIP-event times (el_kernel_stats) */
-  uint32_t flags;        /* reserved, must be 0 */
+  uint32_t flags;        /* EL_FLAG_* bits; an unknown bit is EL_EINVAL */
   int exchange;          /* EL_XCHG_*; NONE ignores every field below */
   uint32_t part_rank;    /* this context's rank in [0, part_count) */
   uint32_t part_count;   /* ranks in the group */

@@ -12,7 +12,12 @@ BOTTOM, TOP = 0, 1
 DATATYPE = 3
 
 
-def saturate(ax) -> Tuple[Dict[int, Set[int]], Set[Tuple[int, int, int]]]:
+def saturate(ax, distel_chain: bool = False) -> Tuple[Dict[int, Set[int]], Set[Tuple[int, int, int]]]:
+    """distel_chain: CR6 as DistEL runs it (hazard H2), restated literally from the store
+    layout: DB1["Yr"] holds X for (X,Y) in R(r), r first in a chain; DB4["Yr"] holds Z for
+    (Y,Z) in R(s), s second in a chain whose FIRST role is r (RolePairHandler.java:395-443);
+    CR6 adds (X,Z) to the t of every chain whose first role is r, without checking s
+    (Type5AxiomProcessorBase.java:128-143)."""
     n = ax.n_concepts
     kind = [int(k) for k in ax.kind]
     # init: S(X) = {X, ⊤}  (AxiomLoader.java:1237-1245, individuals :1281-1289)
@@ -51,11 +56,19 @@ def saturate(ax) -> Tuple[Dict[int, Set[int]], Set[Tuple[int, int, int]]]:
             for r1, s in subrole:  # CR5  Type4AxiomProcessorBase.java:38-76
                 if r1 == r:
                     R.add((x, s, y))
-            for r1, s, t in chain:  # CR6  Type5AxiomProcessorBase.java:115-154 (s checked)
-                if r1 == r:
-                    for (y2, s2, z) in list(R):
-                        if y2 == y and s2 == s:
-                            R.add((x, t, z))
+            if distel_chain:  # CR6 over the "Yr" keys (H2)
+                seconds = {s for r1, s, _ in chain if r1 == r}
+                thirds = {t for r1, _, t in chain if r1 == r}
+                db4 = {z for (y2, s2, z) in R if y2 == y and s2 in seconds}
+                for t in thirds:
+                    for z in db4:
+                        R.add((x, t, z))
+            else:
+                for r1, s, t in chain:  # CR6  Type5AxiomProcessorBase.java:115-154 (s checked)
+                    if r1 == r:
+                        for (y2, s2, z) in list(R):
+                            if y2 == y and s2 == s:
+                                R.add((x, t, z))
             if BOTTOM in S[y]:  # ⊥  TypeBottomAxiomProcessorBase.java:62-123
                 S[x].add(BOTTOM)
             for r1, d in domain:  # domain  RolePairHandler.java:480-490

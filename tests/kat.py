@@ -51,3 +51,21 @@ def to_sets(fx, fa, lx=None, lr=None, ly=None):
     if lx is not None:
         R = set(zip(lx.tolist(), lr.tolist(), ly.tolist()))
     return S, R
+
+
+def compat_file(name):
+    return os.path.join(GOLDEN, name)
+
+
+def distel_chain_set(ax):
+    """Test-side mirror of el::distel_chain_set (hazard H2): the chain set DistEL's CR6 applies,
+    {r∘s⊑t : s second and t third in some chains whose first role is r}."""
+    import dataclasses
+
+    import numpy as np
+    by = {}
+    for r, s, t in ax.chain.tolist():
+        a, b = by.setdefault(r, (set(), set()))
+        a.add(s), b.add(t)
+    ch = sorted((r, s, t) for r, (ss, tt) in by.items() for s in ss for t in tt)
+    return dataclasses.replace(ax, chain=np.asarray(ch, dtype=np.uint32).reshape(-1, 3))

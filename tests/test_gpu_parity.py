@@ -225,3 +225,45 @@ def test_g3_full(oracle_mod):
     _assert_same(eng, o)
     assert st["derived"] == o.stats()["derived"] == 136499458
     eng.close()
+
+
+def test_h2_compat_gpu(oracle_mod):
+    """EL_FLAG_COMPAT_DISTEL_CHAIN: the H2 KAT, and random ontologies against both the literal
+    DistEL CR6 restatement (naive) and the C oracle over the expanded chain set (bit-exact,
+    events and per-step deltas included); incremental chain axioms re-expand over old ∪ inc."""
+    import naive
+    ax, exp = kat.load_kat(kat.compat_file("compat_h2_two_chains.elax"))
+    eng, _ = engine.classify(ax, device=0, compat_chain=True)
+    kat.check(exp, *kat.to_sets(*eng.facts(), *eng.links()))
+    eng.close()
+    eng = engine.Engine(device=0, compat_chain=True)
+    for seed in range(120):
+        ax = generators.random_small(9100 + seed, n=8 + seed % 30, n_roles=2 + seed % 4)
+        eng.load(ax)
+        eng.init()
+        eng.saturate()
+        _assert_same(eng, oracle_mod.saturate(kat.distel_chain_set(ax), 0))
+        if seed < 40:
+            assert kat.to_sets(*eng.facts(), *eng.links()) == naive.saturate(ax, distel_chain=True), seed
+    eng.close()
+    # increment: the second chain sharing r arrives later; H2 must fire for the old links too
+    import dataclasses
+    full, exp = kat.load_kat(kat.compat_file("compat_h2_two_chains.elax"))
+    base = dataclasses.replace(full, chain=full.chain[:1])
+    eng = engine.Engine(device=0, compat_chain=True)
+    eng.load(base)
+    eng.init()
+    eng.saturate()
+    inc = ir.Axioms.build(full.n_concepts, full.n_roles, kind=full.kind, chain=full.chain[1:])
+    eng.add_axioms(inc)
+    eng.saturate()
+    kat.check(exp, *kat.to_sets(*eng.facts(), *eng.links()))
+    eng.close()
+
+
+def test_flags_unknown_rejected():
+    lib = engine.load_library()
+    import ctypes as C
+    ctx = C.c_void_p()
+    cfg = engine._ElConfig(0, 0, 0x80)
+    assert lib.el_create(C.byref(ctx), C.byref(cfg)) == engine.EL_EINVAL

@@ -100,3 +100,27 @@ def test_closure_digests(oracle_lib):
         ax = generators.workload(name, scale)
         assert ax.digest() == inp, name
         assert _closure_digest(oracle_lib.saturate(ax, 0)) == clo, name
+
+
+def test_h2_compat_kat_python_naive():
+    """The literal DistEL CR6 restatement (naive.saturate(distel_chain=True)) reproduces H2."""
+    ax, exp = kat.load_kat(kat.compat_file("compat_h2_two_chains.elax"))
+    S, R = naive.saturate(ax, distel_chain=True)
+    kat.check(exp, S, R)
+    _, exp0 = kat.load_kat(os.path.join(kat.GOLDEN, "kat_h2_two_chains.elax"))
+    with pytest.raises(AssertionError):  # the complete closure does not hold under H2
+        kat.check(exp0, S, R)
+
+
+def test_h2_compat_equals_expanded_chain_set(oracle_lib):
+    """DistEL's s-blind join over the told chains = the correct join over the expanded chain set
+    (what EL_FLAG_COMPAT_DISTEL_CHAIN indexes), checked on random ontologies; at least some of
+    them differ from the complete closure."""
+    differ = 0
+    for seed in range(150):
+        ax = generators.random_small(9100 + seed, n=8 + seed % 16, n_roles=2 + seed % 3)
+        S, R = naive.saturate(ax, distel_chain=True)
+        o = oracle_lib.saturate(kat.distel_chain_set(ax), 0)
+        assert kat.to_sets(*o.facts(), *o.links()) == (S, R), seed
+        differ += (S, R) != naive.saturate(ax)
+    assert differ > 0
