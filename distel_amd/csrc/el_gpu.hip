@@ -115,6 +115,7 @@ struct DIndex {
   const uint8_t* role_has_exl;
   const uint4* meta;  // per concept A: {told_ptr, cidx_ptr, exr_ptr, exl_ptr}[A] — one 32 B span for A, A+1
   const uint32_t* init_off;  // N + 1: start of concept X's init facts in an init-ordered log
+  const uint32_t* init_row64;  // init_off[N] / 64 + 1: the row holding init slot 64·c
   uint32_t has_range;
   uint32_t has_bot;  // some axiom concludes ⊥ (or ∃r.⊥): else ⊥ ∈ S(Y) only for Y = ⊥, no link reaches ⊥
   // row partition (el_config.exchange != NONE): this context owns rows [lo, hi)
@@ -623,7 +624,7 @@ __global__ void k_fill(FillArgs f) {
 // closure of X — exactly what CR1 derives from the init fact X ∈ S(X) in the first
 // superstep — written without candidates: the init facts of rows [lo, hi) are the
 // contiguous log range [init_off[lo], init_off[hi]) (host prefix sums), so each thread takes
-// one log slot k, finds its row by a binary search over init_off and its fact by the offset
+// one log slot k, finds its row from init_row64 plus a short scan of init_off and its fact by the offset
 // inside the row, and a wave's log stores are coalesced.  Row X's facts: X (closure flag:
 // its closure is written right here), ⊤ for classes and individuals, then told*(X) (flagged)
 // without a second ⊤.
@@ -632,12 +633,11 @@ __global__ void k_init(DIndex ix, DState st, uint32_t lo, uint32_t hi, uint32_t 
   const uint32_t o0 = ix.init_off[lo], n = ix.init_off[hi] - o0;
   const uint32_t stride = gridDim.x * blockDim.x;
   for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < n; k += stride) {
-    uint32_t a = lo, b = hi;  // the row: largest x with init_off[x] - o0 <= k
-    while (b - a > 1) {
-      const uint32_t m = (a + b) >> 1;
-      if (ix.init_off[m] - o0 <= k) a = m;
-      else b = m;
-    }
+    // the row: largest x < hi with init_off[x] <= o0 + k, from the row of the slot's 64-slot
+    // chunk (host table) by a short forward scan whose loads the wave shares
+    const uint32_t K = o0 + k;
+    uint32_t a = max(lo, ix.init_row64[K >> 6]);
+    while (a + 1 < hi && ix.init_off[a + 1] <= K) ++a;
     const uint32_t x = a, j = k - (ix.init_off[x] - o0);
     const bool two = x != EL_TOP && x != EL_BOTTOM && ix.kind[x] != EL_KIND_DATATYPE;
     const uint32_t t0 = ix.told_ptr[x], t1 = ix.told_ptr[x + 1];
@@ -1763,10 +1763,10 @@ __global__ void k_clear_logged(uint32_t* bits_base, uint64_t W, const uint32_t* 
 }
 
 // ---- gapped-CSR layout kernels (rare: initial layout, re-layout after an overflow)
-__global__ void k_gap_init(uint32_t* start, uint32_t* len, uint32_t rows) {
+__global__ void k_gap_init(uint32_t* start, uint32_t* len, uint32_t rows, const uint32_t* __restrict__ start0) {
   const uint32_t stride = gridDim.x * blockDim.x;
   for (uint32_t r = blockIdx.x * blockDim.x + threadIdx.x; r <= rows; r += stride) {
-    start[r] = r * gap_cap(0);
+    start[r] = start0 ? start0[r] : r * gap_cap(0);
     if (r < rows) len[r] = 0;
   }
 }
@@ -1934,12 +1934,27 @@ struct GapCsr {
   uint32_t* ovq = nullptr;
   uint64_t ovq_cap = 0;
   bool live = false;  // maintained for this ontology (it has readers)
-  void alloc(uint32_t n, uint64_t ovq_entries) {
+  uint32_t* start0 = nullptr;  // initial row starts when presized (else r · gap_cap(0))
+  uint64_t total0 = 0;         // slots of the initial layout
+  // cap0: initial row capacities (the first superstep's expected appends, el_ctx::alloc_state),
+  // or null for gap_cap(0) per row
+  void alloc(uint32_t n, uint64_t ovq_entries, const std::vector<uint32_t>* cap0 = nullptr) {
     rows = n;
     start = dalloc<uint32_t>(n + 1);
     start2 = dalloc<uint32_t>(n + 1);
     len = dalloc<uint32_t>(n);
-    val_cap = (uint64_t)gap_cap(0) * n;
+    total0 = (uint64_t)gap_cap(0) * n;
+    if (cap0) {
+      std::vector<uint32_t> s0(n + 1, 0);
+      uint64_t t = 0;
+      for (uint32_t r = 0; r < n; ++r) s0[r] = (uint32_t)t, t += gap_cap((*cap0)[r]);
+      if (t <= 0xffffffffull) {
+        s0[n] = (uint32_t)t;
+        start0 = dupload(s0);
+        total0 = t;
+      }
+    }
+    val_cap = total0;
     val = dalloc<uint32_t>(val_cap);
     live = true;
     set_ovq(ovq_entries);
@@ -1957,7 +1972,8 @@ struct GapCsr {
     dfree(val);
     dfree(val2);
     dfree(ovq);
-    val_cap = val2_cap = ovq_cap = 0;
+    dfree(start0);
+    val_cap = val2_cap = ovq_cap = total0 = 0;
     live = false;
   }
   DGap view(uint32_t* ov_count) const {
@@ -2447,6 +2463,13 @@ std::string el_ctx::install_index(el::HostIndex&& hnew) {
       init_off[x + 1] = init_off[x] + (uint32_t)n;
     }
     d.init_off = up32(init_off);
+    // every row has >= 1 init fact, so a slot's row is at most 63 rows past its chunk's row
+    std::vector<uint32_t> r64(init_off[h.N] / 64 + 1);
+    for (uint32_t x = 0, c = 0; c < r64.size(); ++c) {
+      while (x + 1 < h.N && init_off[x + 1] <= 64ull * c) ++x;
+      r64[c] = x;
+    }
+    d.init_row64 = up32(r64);
   }
   {
     // ⊥ derivable only if some axiom mentions it (as a conclusion or a CR3 filler)
@@ -2612,9 +2635,43 @@ void el_ctx::alloc_state() {
     if (const char* e = getenv("EL_XCHG_CAP")) xcap = std::max<uint64_t>(1, strtoull(e, nullptr, 10));
   }
   // gapped CSRs, only where the rules read them; overflow queues hold a step's appends
-  if (P && need_pred) PR.alloc((uint32_t)P, cl_cap);
-  if (need_succ) SC.alloc((uint32_t)N, part() ? (uint64_t)part_count * xcap : cl_cap);
-  if (use_props) PP.alloc((uint32_t)P, cp_cap + remote_bound());
+  // Row capacities for the first supersteps: every init fact X ∈ S(X) emits the pairs of
+  // exr(X) and CR5 lifts them to their super-role pairs (psup) one step later, so pid p's
+  // predecessor row receives its count of both and X's successor row the chain-second ones;
+  // slack gap_cap() as after a re-layout.  Spares the first steps'
+  // re-layouts (G3 step 0: 25 M links into 16-slot rows, 0.7 ms of moves and overflow
+  // placement).  The oracle sizes its rows the same way (el_oracle.c, elo_create).
+  std::vector<uint32_t> cap_pr, cap_sc;
+  if (!part() && ((P && need_pred) || need_succ)) {
+    cap_pr.assign(P, 0);
+    cap_sc.assign(N, 0);
+    for (uint32_t x = 0; x < N; ++x)
+      for (uint32_t j = hx.exr.ptr[x]; j < hx.exr.ptr[x + 1]; ++j) {
+        const uint32_t p = hx.exr.a[j], r = hx.pair_role[p];
+        ++cap_pr[p];
+        cap_sc[x] += hx.chs.ptr[r + 1] > hx.chs.ptr[r];
+        for (uint32_t k = hx.psup.ptr[p]; k < hx.psup.ptr[p + 1]; ++k) {  // CR5 lifts them next step
+          const uint32_t u = hx.psup.a[k], ru = hx.pair_role[u];
+          ++cap_pr[u];
+          cap_sc[x] += hx.chs.ptr[ru + 1] > hx.chs.ptr[ru];
+        }
+      }
+  }
+  // propagation rows: init fact X (as Y) records ((r, X), B) for every (r, B) of exl(X)
+  std::vector<uint32_t> cap_pp;
+  if (!part() && use_props) {
+    cap_pp.assign(P, 0);
+    for (uint32_t x = 0; x < N; ++x)
+      for (uint32_t j = hx.exl.ptr[x]; j < hx.exl.ptr[x + 1]; ++j)
+        for (uint32_t q = hx.fp_ptr[x]; q < hx.fp_ptr[x + 1]; ++q)
+          if (hx.pair_role[q] == hx.exl.a[j]) {
+            ++cap_pp[q];
+            break;
+          }
+  }
+  if (P && need_pred) PR.alloc((uint32_t)P, cl_cap, cap_pr.empty() ? nullptr : &cap_pr);
+  if (need_succ) SC.alloc((uint32_t)N, part() ? (uint64_t)part_count * xcap : cl_cap, cap_sc.empty() ? nullptr : &cap_sc);
+  if (use_props) PP.alloc((uint32_t)P, cp_cap + remote_bound(), cap_pp.empty() ? nullptr : &cap_pp);
   HIPCHK(hipHostMalloc((void**)&pin_word, sizeof(uint32_t), hipHostMallocDefault));
   ca_cap = 1u << 12;
   cs_x = dalloc<uint32_t>(cs_cap);
@@ -2694,12 +2751,13 @@ void el_ctx::reset_state() {
   HIPCHK(hipGetLastError());
   for (GapCsr* g : {&PR, &SC, &PP}) {
     if (!g->live) continue;
-    if (g->val_cap < (uint64_t)gap_cap(0) * g->rows) {  // (a re-layout may have shrunk nothing: val only grows)
+    if (g->val_cap < g->total0) {  // (a re-layout may have shrunk nothing: val only grows)
       dfree(g->val);
-      g->val_cap = (uint64_t)gap_cap(0) * g->rows;
+      g->val_cap = g->total0;
       g->val = dalloc<uint32_t>(g->val_cap);
     }
-    hipLaunchKernelGGL(k_gap_init, dim3(grid_for(g->rows + 1)), dim3(BLOCK), 0, stream, g->start, g->len, g->rows);
+    hipLaunchKernelGGL(k_gap_init, dim3(grid_for(g->rows + 1)), dim3(BLOCK), 0, stream, g->start, g->len, g->rows,
+                       g->start0);
     HIPCHK(hipGetLastError());
   }
   s_count = l_count = a_count = p_count = s_init = s_csr_count = x_count = 0;

@@ -609,8 +609,33 @@ int elo_create(elo_ctx** out, const el_axioms* ax, int mode) {
   c->cap_sc = (uint32_t*)malloc((c->N ? c->N : 1) * sizeof(uint32_t));
   {
     uint32_t q;
-    for (q = 0; q < (c->P ? c->P : 1); ++q) c->cap_pr[q] = c->cap_pp[q] = GAP_CAP(0);
-    for (q = 0; q < c->N; ++q) c->cap_sc[q] = GAP_CAP(0);
+    uint32_t j;
+    for (q = 0; q < (c->P ? c->P : 1); ++q) c->cap_pr[q] = c->cap_pp[q] = 0;
+    for (q = 0; q < c->N; ++q) c->cap_sc[q] = 0;
+    /* initial row capacities sized for the first supersteps' links (as el_ctx::alloc_state
+     * sizes the GPU's): every init fact X ∈ S(X) emits the pairs of exr(X) and CR5 lifts them
+     * to their super-role pairs psup, so pid p's predecessor row receives its count of both and
+     * X's successor row its chain-second ones; slack as after a re-layout */
+    for (q = 0; q < c->N; ++q)
+      for (j = c->exr.ptr[q]; j < c->exr.ptr[q + 1]; ++j) {
+        uint32_t p = c->exr.a[j], r = c->pair_role[p], k;
+        ++c->cap_pr[p];
+        if (c->chs.ptr[r + 1] > c->chs.ptr[r]) ++c->cap_sc[q];
+        for (k = c->psup.ptr[p]; k < c->psup.ptr[p + 1]; ++k) { /* CR5 lifts them in the next step */
+          uint32_t u = c->psup.a[k], ru = c->pair_role[u];
+          ++c->cap_pr[u];
+          if (c->chs.ptr[ru + 1] > c->chs.ptr[ru]) ++c->cap_sc[q];
+        }
+      }
+    /* propagation rows: init fact X (as Y) records ((r, X), B) for every (r, B) of exl(X) */
+    for (q = 0; q < c->N; ++q)
+      for (j = c->exl.ptr[q]; j < c->exl.ptr[q + 1]; ++j) {
+        uint32_t p;
+        PID_OF(c->exl.a[j], q, p);
+        if (p != NONE) ++c->cap_pp[p];
+      }
+    for (q = 0; q < (c->P ? c->P : 1); ++q) c->cap_pr[q] = GAP_CAP(c->cap_pr[q]), c->cap_pp[q] = GAP_CAP(c->cap_pp[q]);
+    for (q = 0; q < c->N; ++q) c->cap_sc[q] = GAP_CAP(c->cap_sc[q]);
   }
   hs_init(&c->props, 1024);
   hs_init(&c->links, 1024);
@@ -984,6 +1009,9 @@ static void merge_seg_events(elo_ctx* c, uint64_t nrows, uint64_t old_n, uint64_
 static void gap_step_end(elo_ctx* c, const vec* rows, uint32_t R, uint32_t* cap, uint64_t* ov, uint64_t entries) {
   uint32_t r;
   if (!*ov) return;
+  if (getenv("ELO_GAPTRACE")) /* diagnostic: which gapped CSR re-lays out after which step */
+    fprintf(stderr, "step %u relayout rows %u ovf %llu entries %llu\n", c->supersteps, R, (unsigned long long)*ov,
+            (unsigned long long)entries);
   merge_seg_events(c, R, entries - *ov, *ov);
   for (r = 0; r < R; ++r) cap[r] = GAP_CAP(rows[r].n);
   *ov = 0;
