@@ -1771,14 +1771,37 @@ __global__ void k_gap_init(uint32_t* start, uint32_t* len, uint32_t rows, const 
   }
 }
 
-// one wave per row: the in-place entries of row r move to its new slots
+// The in-place entries of every row move to its new slots.  A wave takes 64 rows, one lane
+// loading each row's bounds, and walks their concatenation 64 entries a round
+// (wave_rows): a row's move no longer waits on its own bounds loads, and short rows do not
+// leave lanes idle (one wave per row was latency-bound: G3, 338 k rows, 0.4 ms per re-layout).
 __global__ void k_gap_move(const uint32_t* __restrict__ s_old, const uint32_t* __restrict__ len,
                            const uint32_t* __restrict__ v_old, const uint32_t* __restrict__ s_new,
                            uint32_t* __restrict__ v_new, uint32_t rows) {
   const uint32_t lane = threadIdx.x & 63u, waves = gridDim.x * (blockDim.x >> 6);
-  for (uint32_t r = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); r < rows; r += waves) {
-    const uint32_t b = s_old[r], n = min(len[r], s_old[r + 1] - b), d = s_new[r];
-    for (uint32_t k = lane; k < n; k += 64) v_new[d + k] = v_old[b + k];
+  const uint32_t w = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  // lane i of round k takes row w + waves·(64k + i): rows `waves` apart, so the adjacent hub
+  // rows of one filler (pids sorted by (Y, r)) land in different waves
+  for (uint64_t r0 = w; r0 < rows; r0 += 64ull * waves) {
+    const uint64_t r = r0 + (uint64_t)lane * waves;
+    uint32_t b = 0, n = 0, d = 0;
+    if (r < rows) {
+      b = s_old[r];
+      n = min(len[r], s_old[r + 1] - b);
+      d = s_new[r];
+    }
+    // long rows (hubs) one at a time with the whole wave: independent iterations the
+    // compiler unrolls, several loads in flight
+    const bool big = n > 256;
+    for (unsigned long long m = __ballot(big); m; m &= m - 1) {
+      const int o = __builtin_ctzll(m);
+      const uint32_t bo = __shfl(b, o), no = __shfl(n, o), dO = __shfl(d, o);
+      for (uint32_t k = lane; k < no; k += 64) v_new[dO + k] = v_old[bo + k];
+    }
+    wave_rows(b, big ? b : b + n, [&](bool v, uint32_t own, uint32_t j) {
+      const uint32_t bo = __shfl(b, (int)own), dO = __shfl(d, (int)own);
+      if (v) v_new[dO + (j - bo)] = v_old[j];
+    });
   }
 }
 
@@ -3236,7 +3259,7 @@ void el_ctx::gap_rebuild(GapCsr& g, uint32_t n_ovf, uint64_t entries) {
   }
   launch_gap_scan(g.len, R, g.start2);
   launch(EL_K_SCATTER_OLD, [&] {
-    hipLaunchKernelGGL(k_gap_move, dim3(grid_for((uint64_t)R * 64, 1024)), dim3(BLOCK), 0, stream, g.start, g.len,
+    hipLaunchKernelGGL(k_gap_move, dim3(grid_for((uint64_t)R, 2048)), dim3(BLOCK), 0, stream, g.start, g.len,
                        g.val, g.start2, g.val2, R);
   });
   if (n_ovf)
