@@ -176,8 +176,9 @@ __device__ __forceinline__ uint2 gap_row(const DGap& g, uint32_t r) {
 }
 
 // capacity of a row with n entries after a re-layout (the CPU oracle mirrors it)
-constexpr uint32_t GAP_MUL = 8;  // slack factor: a row re-laid out with n entries has room for GAP_MUL·n + 16
-__host__ __device__ constexpr uint32_t gap_cap(uint32_t n) { return GAP_MUL * n + 16; }
+constexpr uint32_t GAP_MUL = 8;    // slack factor: a row re-laid out with n entries has room for GAP_MUL·n + GAP_BASE
+constexpr uint32_t GAP_BASE = 64;  // (16 left G3 / G5 a late re-layout for a handful of entries)
+__host__ __device__ constexpr uint32_t gap_cap(uint32_t n) { return GAP_MUL * n + GAP_BASE; }
 
 struct DState {
   uint32_t* bits;

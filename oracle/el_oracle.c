@@ -269,7 +269,7 @@ static int setbit(elo_ctx* c, uint32_t x, uint32_t b) { /* returns 1 if newly se
 }
 
 /* gapped-CSR row capacity after a re-layout: gap_cap() in distel_amd/csrc/el_gpu.hip */
-#define GAP_CAP(n) (8u * (uint32_t)(n) + 16u)
+#define GAP_CAP(n) (8u * (uint32_t)(n) + 64u)
 
 #define EV(k, e) (c->ev[(k)][(e)]++)
 #define EVN(k, e, n) (c->ev[(k)][(e)] += (n))
