@@ -905,17 +905,17 @@ __device__ void expand_l(const DIndex& ix, const DState& st, BlockQ& q, uint32_t
         ev.v[EL_EV_ROW]++;
         row = gap_row(st.pp, pid);  // (no propagation CSR without ∃r.A ⊑ B: rows are empty)
       }
+      // No probe of B ∈ S(X) here: a new link's conclusions are nearly all new (G3: 103 M of
+      // 107 M), so the probe was one random line read per conclusion that the commit's
+      // atomicOr repeats anyway; the commit drops the few already present.
       wave_rows(row.x, row.x + row.y, [&](bool v, uint32_t own, uint32_t j) {
         const uint32_t Xo = __shfl(X, (int)own);
         uint32_t B = 0;
-        bool nw = false;
         if (v) {
           B = st.pp.val[j];
           ev.v[EL_EV_ENT]++;
-          ev.v[EL_EV_TEST]++;
-          nw = !test_bit(st.bits, ix.W, Xo, B);
         }
-        emit_s(st, q, nw, Xo, B, ev);
+        emit_s(st, q, v, Xo, B, ev);
       });
     }
     if (act) {

@@ -829,8 +829,7 @@ static void expand_l(elo_ctx* c, cands* k, uint32_t mask, uint64_t b, uint64_t e
       for (q = 0; q < c->prow[pid].n; ++q) {
         uint32_t B = c->prow[pid].v[q];
         EV(K, EL_EV_ENT);
-        EV(K, EL_EV_TEST);
-        if (!bit(c, X, B)) emit_s(c, k, K, X, B);
+        emit_s(c, k, K, X, B); /* unprobed (as on the GPU): the commit drops facts already present */
       }
     }
     if ((mask & M_RBOT) && c->has_bot) {
