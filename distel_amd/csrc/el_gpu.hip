@@ -73,6 +73,8 @@ enum : uint32_t {
   M_RRNG = 1u << 9,  // range
   M_R4P = 1u << 10,  // CR4: new propagations × existing predecessors (per-rule stepping)
   M_R4D = 1u << 11,  // CR4: fused mode — a new propagation fans out to predecessors at once
+  M_LEMPTY = 1u << 12,  // no link committed before this step: link probes would all miss
+  M_PEMPTY = 1u << 13,  // no propagation committed before this step: idem
   M_ALL = M_R1 | M_R2 | M_R3 | M_R4Y | M_R4L | M_R5 | M_R6 | M_RBOT | M_RDOM | M_RRNG | M_R4D
 };
 
@@ -785,8 +787,11 @@ __device__ void expand_s(const DIndex& ix, const DState& st, BlockQ& q, uint32_t
         if (v) {
           pid = ix.exr_pid[j];
           ev.v[EL_EV_ENT]++;
-          ev.v[EL_EV_HASH]++;
-          nw = !hash_contains(st.lhash, st.lmask, link_key(pid, Xo));
+          nw = true;
+          if (!(mask & M_LEMPTY)) {  // (first superstep: 25 M misses spared on G3)
+            ev.v[EL_EV_HASH]++;
+            nw = !hash_contains(st.lhash, st.lmask, link_key(pid, Xo));
+          }
         }
         emit_l(st, q, nw, Xo, pid, ev);
       });
@@ -805,8 +810,11 @@ __device__ void expand_s(const DIndex& ix, const DState& st, BlockQ& q, uint32_t
           ev.v[EL_EV_ENT] += 2;
           pid = pair_lookup(ix, r, Yo, ev);
           if (pid != NONE) {
-            ev.v[EL_EV_HASH]++;
-            fresh = !hash_contains(st.phash, st.pmask, link_key(pid, B));
+            fresh = true;
+            if (!(mask & M_PEMPTY)) {
+              ev.v[EL_EV_HASH]++;
+              fresh = !hash_contains(st.phash, st.pmask, link_key(pid, B));
+            }
             if (fresh && (mask & M_R4D)) {  // fused mode: B reaches today's predecessors now
               ev.v[EL_EV_ROW]++;
               const uint2 row = gap_row(st.pr, pid);
@@ -2978,7 +2986,8 @@ bool el_ctx::superstep(uint32_t mask, uint64_t sb, uint64_t se, uint64_t lb, uin
     ea.gp = do_p ? grid_for(pe - pb) : 0u;
     ea.sb = (uint32_t)sb, ea.se = (uint32_t)se, ea.lb = (uint32_t)lb, ea.le = (uint32_t)le;
     ea.ab = (uint32_t)ab, ea.ae = (uint32_t)ae, ea.pb = (uint32_t)pb, ea.pe = (uint32_t)pe;
-    ea.mask = mask;
+    // an empty link / propagation set (the first superstep): their probes cannot hit
+    ea.mask = mask | (!part() && l_count == 0 ? (uint32_t)M_LEMPTY : 0u) | (!part() && p_count == 0 ? (uint32_t)M_PEMPTY : 0u);
     ea.a_end = (uint32_t)a0;
     launch(EL_K_EXPAND_S, [&] {
       hipLaunchKernelGGL(k_expand, dim3(ea.gs + ea.gl + ea.ga + ea.gp), dim3(BLOCK), 0, stream, ix, st, ea);

@@ -47,6 +47,8 @@ enum {
   M_R5 = 1u << 5, M_R6 = 1u << 6, M_RBOT = 1u << 7, M_RDOM = 1u << 8, M_RRNG = 1u << 9,
   M_R4P = 1u << 10, /* new propagations × existing predecessors (per-rule stepping) */
   M_R4D = 1u << 11, /* fused mode: a new propagation fans out to predecessors at once */
+  M_LEMPTY = 1u << 12, /* no link committed before this step: link probes would all miss */
+  M_PEMPTY = 1u << 13, /* no propagation committed before this step: idem */
   M_ALL = M_R1 | M_R2 | M_R3 | M_R4Y | M_R4L | M_R5 | M_R6 | M_RBOT | M_RDOM | M_RRNG | M_R4D
 };
 /* el_rule -> sub-rules; CR4 is factored through propagations ((r, Y), B) exactly as the
@@ -765,6 +767,10 @@ static void expand_s(elo_ctx* c, cands* k, uint32_t mask, uint64_t b, uint64_t e
       for (j = c->exr.ptr[A]; j < c->exr.ptr[A + 1]; ++j) {
         uint32_t pid = c->exr.a[j];
         EV(K, EL_EV_ENT);
+        if (mask & M_LEMPTY) { /* empty link set: the probe is skipped (as on the GPU) */
+          emit_l(c, k, K, X, pid);
+          continue;
+        }
         EV(K, EL_EV_HASH);
         if (!hs_has(&c->links, lkey(pid, X))) emit_l(c, k, K, X, pid);
       }
@@ -776,8 +782,8 @@ static void expand_s(elo_ctx* c, cands* k, uint32_t mask, uint64_t b, uint64_t e
         EVN(K, EL_EV_ENT, 2);
         pid = pair_lookup(c, K, r, X);
         if (pid != NONE) {
-          EV(K, EL_EV_HASH);
-          if (!hs_has(&c->props, lkey(pid, B))) {
+          if (!(mask & M_PEMPTY)) EV(K, EL_EV_HASH);
+          if ((mask & M_PEMPTY) || !hs_has(&c->props, lkey(pid, B))) {
             EV(K, EL_EV_EMIT);
             vpush(&k->pp, pid);
             vpush(&k->pb, B);
@@ -1023,6 +1029,8 @@ static int superstep(elo_ctx* c, uint32_t mask, uint64_t sb, uint64_t se, uint64
   uint64_t s0 = c->slog_x.n, l0 = c->llog_x.n, a0 = c->alog_y.n, p0 = c->plog_p.n;
   int do_a = (mask & M_RRNG) && ae > ab, do_p = (mask & M_R4P) && pe > pb;
   if (!(se > sb || le > lb || do_a || do_p)) return 0;
+  if (c->llog_x.n == 0) mask |= M_LEMPTY; /* empty sets: their probes are skipped (as on the GPU) */
+  if (c->plog_p.n == 0) mask |= M_PEMPTY;
   memset(&k, 0, sizeof k);
   /* generation: reads only the state of the previous step */
   expand_s(c, &k, mask, sb, se, a0);
