@@ -2770,7 +2770,12 @@ void el_ctx::reset_state() {
     add(bits, matrix_bytes, 0u);
   }
   bits_logged = true;  // from here on every set bit is in the fact log (k_init and k_commit append)
-  add(lhash, lhash_cap * sizeof(unsigned long long), ~0u);
+  // the link set is by far the largest (G3: 2 GB): the runtime's fill reaches a higher write
+  // rate than k_fill's grid-stride loop for it (k_fill: 2.0 ms per G3 classification)
+  if (lhash_cap * sizeof(unsigned long long) >= (64ull << 20))
+    HIPCHK(hipMemsetAsync(lhash, 0xff, lhash_cap * sizeof(unsigned long long), stream));
+  else
+    add(lhash, lhash_cap * sizeof(unsigned long long), ~0u);
   add(ahash, ahash_cap * sizeof(unsigned long long), ~0u);
   add(has_act, hx.N, 0u);
   add(phash, phash_cap * sizeof(unsigned long long), ~0u);
