@@ -20,8 +20,8 @@
 //   commit      k_commit (roles: S, links, activations, propagations) dedups the
 //               candidates against the bit rows / hash sets, appends the new ones
 //               to the logs and publishes the counters to pinned host memory;
-//   merge       per-row delta counts → k_scan_merge (single-pass scan + new row
-//               offsets), k_scatter_old, k_scatter_new rebuild the CSRs.
+//   (re-layout) only when a gapped CSR row overflowed: k_gap_scan, k_gap_move, k_gap_ovf.
+// Result rows (export, copy-back) are built from the logs on demand (el_rows.hip).
 // Generation never writes state, so a step can be re-run after growing a buffer,
 // and the delta of every step is exactly {candidates} \ S_{t-1}: the same sets
 // and the same algorithmic event counts as the CPU oracle (oracle/el_oracle.c).
@@ -41,6 +41,7 @@
 #include <condition_variable>
 #include <memory>
 #include <mutex>
+#include <numeric>
 #include <cstddef>
 #include <cstdio>
 #include <cstdlib>
@@ -51,6 +52,7 @@
 
 #include "el_gpu.h"
 #include "el_index.h"
+#include "el_rows.h"
 
 namespace {
 
@@ -150,7 +152,7 @@ constexpr uint32_t CTR_KEEP = 9;
 struct DCounters {
   EL_COUNTERS(EL_CTR_DEV)
 };
-struct HCounters {  // ticket: k_scan_merge tile dispenser; seq: host copy only
+struct HCounters {  // ticket: k_gap_scan tile dispenser; seq: host copy only
   EL_COUNTERS(EL_CTR_HOST)
 };
 constexpr uint32_t NUM_CTRS = sizeof(HCounters) / 4;
@@ -200,7 +202,6 @@ struct DState {
   uint32_t *plog_p, *plog_b;
   DGap pp;                          // propagations per pid
   uint32_t *cp_p, *cp_b, cp_cap;
-  const uint32_t *s_ptr, *s_val;    // S rows (CSR, current)
   DGap pr;                          // predecessors per pid
   DGap sc;                          // successors per X (chain-second links in partitioned mode)
   uint32_t need_pred, need_succ;  // CSRs with readers: only those get delta counts
@@ -1562,38 +1563,19 @@ __global__ void k_ximport(DIndex ix, DState st, XchgArgs x, PubArgs pub) {
   });
 }
 
-// CSR merges of one superstep, all CSRs at once (segments: S, PR, SC, PP).  The delta
-// counts of every CSR sit in one array; each segment is scanned on its own, so dscan is
-// segment-local.
-struct MergeSeg {
-  const uint32_t *ptr, *row, *val;
-  uint32_t *ptr2, *row2, *val2;
-  const uint32_t *lx, *lv;  // delta: row key / value arrays of the log
-  uint32_t off;             // segment offset in dcnt / dscan
-  uint32_t n1;              // rows + 1
-  uint32_t n_old;           // existing entries
-  uint32_t begin;           // delta = log[begin, *end_ptr)
-  const uint32_t* end_ptr;  // device log counter (the host learns it only after the step)
-  const uint32_t* rank;     // rank of delta entry i among its row's new entries
-  const uint32_t* gap_len;  // non-null: scan gap_cap(gap_len[r]) into ptr2 (gapped-CSR re-layout)
-};
-struct MergeArgs {
-  MergeSeg seg[4];
-  uint32_t nseg;
-  uint32_t max_rows, max_old, max_new;
-};
-
-// Single-pass scan of the delta counts fused with the new row offsets: replaces a library
-// scan (two launches) plus a pointer kernel.  Each segment (one CSR) is scanned on its own,
-// so dscan is segment-local and ptr2 = ptr + dscan.  Tiles are handed out by an atomic
-// ticket, so every predecessor tile of a block is owned by a block that is already running
-// (decoupled look-back cannot wait on an unscheduled block).  Look-back flags carry the
-// launch epoch: stale words from earlier launches never match, so they need no reset.
+// Re-layout scan of a gapped CSR: new row starts = exclusive scan of gap_cap(len[r]).
+// Single pass with decoupled look-back: tiles are handed out by an atomic ticket, so every
+// predecessor tile of a block is owned by a block that is already running (look-back cannot
+// wait on an unscheduled block).  Look-back flags carry the launch epoch: stale words from
+// earlier launches never match, so they need no reset.
 constexpr uint32_t SCAN_ITEMS = 8;
 constexpr uint32_t SCAN_TILE = 256 * SCAN_ITEMS;
 constexpr uint32_t FLAG_AGG = 1, FLAG_INC = 2;
 struct ScanArgs {
-  uint32_t tile0[5];  // first global tile of segment k; tile0[nseg] = total tiles
+  const uint32_t* len;  // rows
+  uint32_t* start_out;  // rows + 1
+  uint32_t n1;          // rows + 1
+  uint32_t tiles;
   uint32_t epoch;
   unsigned long long* flags;
   uint32_t* ticket;
@@ -1603,33 +1585,20 @@ __device__ __forceinline__ unsigned long long flag_word(uint32_t epoch, uint32_t
   return ((unsigned long long)((epoch << 2) | state) << 32) | v;
 }
 
-__global__ void __launch_bounds__(256) k_scan_merge(MergeArgs m, ScanArgs sa, uint32_t* __restrict__ dcnt,
-                                                    uint32_t* __restrict__ dscan) {
+__global__ void __launch_bounds__(256) k_gap_scan(ScanArgs sa) {
   __shared__ uint32_t buf[SCAN_TILE];
   __shared__ uint32_t wtot[4];
   __shared__ uint32_t s_tile, s_excl;
   const uint32_t tid = threadIdx.x, lane = tid & 63u, wv = tid >> 6;
   if (tid == 0) s_tile = atomicAdd(sa.ticket, 1u);
   __syncthreads();
-  const uint32_t t = __builtin_amdgcn_readfirstlane(s_tile), total = sa.tile0[m.nseg];
-  if (t == total - 1 && tid == 0) *sa.ticket = 0;  // every other tile is already taken
-  uint32_t k = 0;
-  while (k + 1 < m.nseg && sa.tile0[k + 1] <= t) ++k;
-  const MergeSeg& g = m.seg[k];
-  if (!g.gap_len && *g.end_ptr == g.begin) return;  // nothing new in this CSR: none of its tiles scans
-  const uint32_t lt = t - sa.tile0[k], r0 = lt * SCAN_TILE;
-  uint32_t* __restrict__ dc = dcnt + g.off;
+  const uint32_t t = __builtin_amdgcn_readfirstlane(s_tile);
+  if (t == sa.tiles - 1 && tid == 0) *sa.ticket = 0;  // every other tile is already taken
+  const uint32_t r0 = t * SCAN_TILE;
 #pragma unroll
   for (uint32_t i = 0; i < SCAN_ITEMS; ++i) {
     const uint32_t idx = r0 + i * 256 + tid;
-    uint32_t v = 0;
-    if (g.gap_len) {
-      if (idx + 1 < g.n1) v = gap_cap(g.gap_len[idx]);  // row capacities of the new layout
-    } else if (idx < g.n1) {
-      v = dc[idx];
-      if (v) dc[idx] = 0;  // consumed: the counts start from zero next step
-    }
-    buf[i * 256 + tid] = v;
+    buf[i * 256 + tid] = idx + 1 < sa.n1 ? gap_cap(sa.len[idx]) : 0u;  // row capacities of the new layout
   }
   __syncthreads();
   uint32_t v[SCAN_ITEMS], run = 0;
@@ -1653,19 +1622,18 @@ __global__ void __launch_bounds__(256) k_scan_merge(MergeArgs m, ScanArgs sa, ui
     if (w < wv) wbase += wtot[w];
     agg += wtot[w];
   }
-  if (wv == 0) {  // look-back over the segment's earlier tiles, 64 at a time
+  if (wv == 0) {  // look-back over the earlier tiles, 64 at a time
     unsigned long long* fl = sa.flags;
     const uint32_t ep = sa.epoch & 0x3fffffffu;
     uint32_t excl = 0;
-    if (lt == 0) {
+    if (t == 0) {
       if (lane == 0) __hip_atomic_store(fl + t, flag_word(ep, FLAG_INC, agg), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     } else {
       if (lane == 0) __hip_atomic_store(fl + t, flag_word(ep, FLAG_AGG, agg), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      const int64_t lo = sa.tile0[k];
       int64_t j = (int64_t)t - 1;
       while (true) {
         const int64_t idx = j - (int64_t)lane;
-        const bool valid = idx >= lo;
+        const bool valid = idx >= 0;
         uint32_t state = valid ? 0u : FLAG_INC, val = 0;
         while (true) {
           if (valid && state == 0) {
@@ -1697,62 +1665,11 @@ __global__ void __launch_bounds__(256) k_scan_merge(MergeArgs m, ScanArgs sa, ui
 #pragma unroll
   for (uint32_t j = 0; j < SCAN_ITEMS; ++j) buf[tid * SCAN_ITEMS + j] = tbase + v[j];
   __syncthreads();
-  uint32_t* __restrict__ ds = dscan + g.off;
 #pragma unroll
   for (uint32_t i = 0; i < SCAN_ITEMS; ++i) {
     const uint32_t idx = r0 + i * 256 + tid;
-    if (idx < g.n1) {
-      const uint32_t d = buf[i * 256 + tid];
-      if (g.gap_len) {
-        g.ptr2[idx] = d;
-      } else {
-        ds[idx] = d;
-        g.ptr2[idx] = g.ptr[idx] + d;
-      }
-    }
+    if (idx < sa.n1) sa.start_out[idx] = buf[i * 256 + tid];
   }
-}
-
-// existing entry j of row x moves by the number of delta entries in rows < x
-// (blockIdx.y selects the segment; blockIdx.x grid-strides over it)
-__global__ void k_scatter_old(MergeArgs m, const uint32_t* __restrict__ dscan) {
-  const MergeSeg g = m.seg[blockIdx.y];
-  if (*g.end_ptr == g.begin) return;
-  const uint32_t stride = gridDim.x * blockDim.x;
-  const uint32_t* __restrict__ ds = dscan + g.off;
-  for (uint32_t j = blockIdx.x * blockDim.x + threadIdx.x; j < g.n_old; j += stride) {
-    const uint32_t x = g.row[j];
-    const uint32_t d = j + ds[x];
-    g.row2[d] = x;
-    g.val2[d] = g.val[j];
-  }
-}
-
-// delta entry i of row x lands after the row's old entries, at its rank among the row's
-// new entries (recorded when its count was taken): no atomics here
-__global__ void k_scatter_new(MergeArgs m, const uint32_t* __restrict__ dscan) {
-  const MergeSeg g = m.seg[blockIdx.y];
-  const uint32_t stride = gridDim.x * blockDim.x, n = *g.end_ptr - g.begin;
-  const uint32_t* __restrict__ ds = dscan + g.off;
-  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
-    const uint32_t x = g.lx[g.begin + i];
-    const uint32_t pos = g.ptr[x + 1] + ds[x] + g.rank[i];
-    g.row2[pos] = x;
-    g.val2[pos] = g.lv[g.begin + i];
-  }
-}
-
-// per-row counts of log[begin, end) with each entry's rank (lazy S-row CSR for export)
-__global__ void k_count_rows(uint32_t* dcnt, uint32_t* rank, const uint32_t* lx, uint32_t begin, uint32_t end) {
-  const uint32_t stride = gridDim.x * blockDim.x;
-  for (uint32_t i = begin + blockIdx.x * blockDim.x + threadIdx.x; i < end; i += stride)
-    rank[i - begin] = atomicAdd(dcnt + lx[i], 1u);
-}
-
-__global__ void k_pack_keys(unsigned long long* out, const uint32_t* hi, const uint32_t* lo, uint32_t n) {
-  const uint32_t stride = gridDim.x * blockDim.x;
-  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
-    out[i] = ((unsigned long long)hi[i] << 32) | lo[i];
 }
 
 __global__ void k_rehash(unsigned long long* t, unsigned long long mask, const uint32_t* kx,
@@ -1857,7 +1774,7 @@ __global__ void k_gap_ovf(const uint32_t* __restrict__ q, uint32_t n, const uint
 // ---------------------------------------------------------------- host side
 
 // Launch that carries a work phase: expand roles run in k_expand (timed as EXPAND_S),
-// commit roles in k_commit (COMMIT_S), the scan and the new row offsets in k_scan_merge.
+// commit roles in k_commit (COMMIT_S), the re-layout scan in k_gap_scan.
 uint32_t kernel_group(int k) {
   switch (k) {
     case EL_K_EXPAND_L:
@@ -1916,46 +1833,6 @@ uint64_t next_pow2(uint64_t v) {
   while (p < v) p <<= 1;
   return p;
 }
-
-// CSR with double buffers and per-row delta counts
-struct DevCsr {
-  uint32_t nrows = 0;
-  uint64_t cap = 0;
-  uint32_t *ptr = nullptr, *row = nullptr, *val = nullptr;
-  uint32_t *ptr2 = nullptr, *row2 = nullptr, *val2 = nullptr;
-  uint32_t *dcnt = nullptr, *dscan = nullptr;
-  void alloc(uint32_t n, uint64_t c, uint32_t* dcnt_view, uint32_t* dscan_view) {
-    nrows = n;
-    cap = c;
-    ptr = dalloc<uint32_t>(n + 1);
-    ptr2 = dalloc<uint32_t>(n + 1);
-    dcnt = dcnt_view;
-    dscan = dscan_view;
-    row = dalloc<uint32_t>(c);
-    val = dalloc<uint32_t>(c);
-    row2 = dalloc<uint32_t>(c);
-    val2 = dalloc<uint32_t>(c);
-  }
-  void grow(uint64_t used, uint64_t c) {
-    dgrow(row, used, c);
-    dgrow(val, used, c);
-    dfree(row2);
-    dfree(val2);
-    row2 = dalloc<uint32_t>(c);
-    val2 = dalloc<uint32_t>(c);
-    cap = c;
-  }
-  void reset(hipStream_t s) { HIPCHK(hipMemsetAsync(ptr, 0, (nrows + 1) * sizeof(uint32_t), s)); }
-  void release() {
-    dfree(ptr);
-    dfree(row);
-    dfree(val);
-    dfree(ptr2);
-    dfree(row2);
-    dfree(val2);
-    dcnt = dscan = nullptr;
-  }
-};
 
 // Gapped CSR (DGap) on the host side: the layout buffers, the overflow queue, scan scratch.
 struct GapCsr {
@@ -2176,12 +2053,29 @@ struct el_ctx {
   uint64_t plog_cap = 0;
   uint32_t *cp_p = nullptr, *cp_b = nullptr;
   uint64_t cp_cap = 0;
-  DevCsr S;            // S rows, built lazily for export (merge kernels)
+  // result rows for export / copy-back (el_rows.h), rebuilt from the logs when they changed
+  struct Rows {
+    uint64_t* ptr = nullptr;  // owned rows + 1
+    uint32_t* val = nullptr;
+    uint64_t cap = 0;
+    uint64_t n = ~0ull;  // entries the rows were built from (~0: stale)
+    void release() {
+      if (ptr) (void)hipFree(ptr);
+      if (val) (void)hipFree(val);
+      ptr = nullptr;
+      val = nullptr;
+      cap = 0;
+      n = ~0ull;
+    }
+  };
+  Rows rs, rl;  // S rows X -> {B}; link rows X -> {q}, q = pair rank in (role, filler) order
+  elrows::Scratch rsc;
+  const uint32_t* pid_rank = nullptr;        // device: pid -> q (an index buffer)
+  std::vector<uint32_t> rank_role, rank_y;   // host: the pair (role, filler) of rank q
+  hipStream_t cstream = nullptr;             // copy-back DMA, beside the row builds
+  hipEvent_t ev_rows[2] = {nullptr, nullptr};
   GapCsr PR, SC, PP;   // predecessors per pid, successors per X, propagations per pid
   uint32_t* pin_word = nullptr;  // pinned scratch for the rare synchronous readbacks
-  uint32_t *dcnt_all = nullptr, *dscan_all = nullptr;
-  uint64_t dcnt_total = 0;
-  uint64_t s_csr_count = 0;   // S-row CSR is built lazily (only export reads it)
   bool need_pred = true;      // predecessor CSR has readers (CR4, ⊥, CR6)
   bool need_succ = true;      // successor CSR has readers (CR6)
   uint32_t *cs_x = nullptr, *cs_a = nullptr, *cl_x = nullptr, *cl_p = nullptr, *ca_y = nullptr,
@@ -2192,7 +2086,7 @@ struct el_ctx {
   DCounters* ctr = nullptr;
   unsigned long long* ev = nullptr;
   unsigned long long hev[EL_NUM_KERNELS][EL_NUM_EVENTS] = {};
-  unsigned long long* scan_flags = nullptr;  // k_scan_merge look-back words (epoch-tagged)
+  unsigned long long* scan_flags = nullptr;  // k_gap_scan look-back words (epoch-tagged)
   uint32_t* commit_done = nullptr;           // k_commit finished-block counters
   uint64_t scan_tiles = 0;
   uint32_t scan_epoch = 0;
@@ -2275,8 +2169,6 @@ struct el_ctx {
     s.cp_p = cp_p;
     s.cp_b = cp_b;
     s.cp_cap = (uint32_t)cp_cap;
-    s.s_ptr = S.ptr;
-    s.s_val = S.val;
     s.pr = PR.view(&ctr->ov_pr);
     s.sc = SC.view(&ctr->ov_sc);
     s.need_pred = need_pred ? 1u : 0u;
@@ -2390,16 +2282,7 @@ struct el_ctx {
   void alloc_state();
   void reset_state();
   void ensure_capacity();
-  struct MergeReq {
-    DevCsr* c;
-    const uint32_t *lx, *lv;
-    uint64_t old_n, begin;
-    const uint32_t* end_ptr;  // device log counter
-    const uint32_t* rank;     // rank of each delta entry in its row (index: log slot - begin)
-  };
-  void launch_merges(const std::vector<MergeReq>& reqs);
-  void finish_merges(const std::vector<MergeReq>& reqs, const std::vector<uint64_t>& ends, bool account);
-  void ensure_s_csr();
+  void ensure_rows(bool facts, bool links);
   void rehash_links(uint64_t cap);
   void rehash_acts(uint64_t cap);
   void rehash_props(uint64_t cap);
@@ -2473,6 +2356,21 @@ std::string el_ctx::install_index(el::HostIndex&& hnew) {
   d.rng_ptr = up32(h.rng.ptr);
   d.rng_c = up32(h.rng.a);
   d.role_has_exl = up8(h.role_has_exl);
+  {  // link export order: pair ids ranked by (role, filler)
+    std::vector<uint32_t> ord(h.P), rank(h.P);
+    std::iota(ord.begin(), ord.end(), 0u);
+    std::sort(ord.begin(), ord.end(), [&](uint32_t u, uint32_t v) {
+      return h.pair_role[u] != h.pair_role[v] ? h.pair_role[u] < h.pair_role[v] : h.pair_y[u] < h.pair_y[v];
+    });
+    rank_role.resize(h.P);
+    rank_y.resize(h.P);
+    for (uint32_t q = 0; q < h.P; ++q) {
+      rank[ord[q]] = q;
+      rank_role[q] = h.pair_role[ord[q]];
+      rank_y[q] = h.pair_y[ord[q]];
+    }
+    pid_rank = up32(rank);
+  }
   {
     std::vector<uint32_t> meta(4 * (size_t)(h.N + 1));
     for (uint32_t a = 0; a <= h.N; ++a) {
@@ -2564,12 +2462,12 @@ void el_ctx::free_state() {
   dfree(plog_b);
   dfree(cp_p);
   dfree(cp_b);
-  S.release();
+  rs.release();
+  rl.release();
+  rsc.release();
   PR.release();
   SC.release();
   PP.release();
-  dfree(dcnt_all);
-  dfree(dscan_all);
   dfree(cs_x);
   dfree(cs_a);
   dfree(cl_x);
@@ -2625,10 +2523,6 @@ void el_ctx::alloc_state() {
   cp_cap = plog_cap;
   cp_p = dalloc<uint32_t>(cp_cap);
   cp_b = dalloc<uint32_t>(cp_cap);
-  dcnt_total = N + 1;  // the S-row CSR (export) is the only merged CSR
-  dcnt_all = dalloc<uint32_t>(dcnt_total);
-  dscan_all = dalloc<uint32_t>(dcnt_total);
-  S.alloc((uint32_t)N, slog_cap, dcnt_all, dscan_all);
   // The first superstep re-triggers every init fact (the told closures included), so the
   // candidate queues start sized for it: bounds from the index, per owned row X over
   // F(X) = {X, ⊤} ∪ told*(X) — CR3 links Σ|exr(A)|, CR2 candidates Σ|cidx(A)|, CR4
@@ -2726,8 +2620,6 @@ void el_ctx::alloc_state() {
       slog_x = dalloc<uint32_t>(slog_cap);
       slog_a = dalloc<uint32_t>(slog_cap);
       slog_f = dalloc<uint8_t>(slog_cap);
-      S.release();
-      S.alloc((uint32_t)N, slog_cap, dcnt_all, dscan_all);
     }
   }
   job_cap = std::max<uint64_t>(1u << 20, 2 * N);
@@ -2742,7 +2634,7 @@ void el_ctx::alloc_state() {
   HIPCHK(hipHostMalloc((void**)&ev_host, EV_TOTAL * sizeof(unsigned long long), hipHostMallocDefault));
   HIPCHK(hipHostGetDevicePointer((void**)&hc_dev, hc_pinned, 0));
   scan_tiles = 0;
-  scan_tiles = (std::max(N, P) + 1 + SCAN_TILE - 1) / SCAN_TILE;  // S rows or a gapped CSR re-layout
+  scan_tiles = (std::max(N, P) + 1 + SCAN_TILE - 1) / SCAN_TILE;  // a gapped CSR re-layout
   scan_flags = dalloc<unsigned long long>(scan_tiles);
   commit_done = dalloc<uint32_t>((DONE_SHARDS + 1) * CTR_STRIDE);
   HIPCHK(hipMemset(scan_flags, 0, scan_tiles * sizeof(unsigned long long)));
@@ -2779,8 +2671,6 @@ void el_ctx::reset_state() {
   add(ahash, ahash_cap * sizeof(unsigned long long), ~0u);
   add(has_act, hx.N, 0u);
   add(phash, phash_cap * sizeof(unsigned long long), ~0u);
-  add(dcnt_all, dcnt_total * sizeof(uint32_t), 0u);
-  add(S.ptr, (S.nrows + 1) * sizeof(uint32_t), 0u);
   add(ctr, sizeof(DCounters), 0u);
   add(commit_done, (DONE_SHARDS + 1) * CTR_STRIDE * sizeof(uint32_t), 0u);
   add(ev, EV_WORDS * sizeof(unsigned long long), 0u);
@@ -2797,7 +2687,8 @@ void el_ctx::reset_state() {
                        g->start0);
     HIPCHK(hipGetLastError());
   }
-  s_count = l_count = a_count = p_count = s_init = s_csr_count = x_count = 0;
+  s_count = l_count = a_count = p_count = s_init = x_count = 0;
+  rs.n = rl.n = ~0ull;  // result rows are stale
   for (int r = 0; r < EL_NUM_RULE_TYPES; ++r) wm_s[r] = wm_l[r] = wm_a[r] = wm_p[r] = 0;
   wm_x = 0;
   memset(launches, 0, sizeof launches);
@@ -2844,102 +2735,29 @@ void el_ctx::rehash_props(uint64_t cap) {
     });
 }
 
-// Rebuild every CSR with new entries: one launch each of k_scan_merge / k_scatter_old /
-// k_scatter_new over all segments.  The delta
-// sizes are read on the device (a segment without new entries skips itself), so the
-// merges are enqueued in the same superstep without a host round trip.
-void el_ctx::launch_merges(const std::vector<MergeReq>& reqs) {
-  if (reqs.empty()) return;
-  MergeArgs m{};
-  m.nseg = (uint32_t)reqs.size();
-  for (uint32_t k = 0; k < m.nseg; ++k) {
-    const MergeReq& r = reqs[k];
-    MergeSeg& g = m.seg[k];
-    g.ptr = r.c->ptr;
-    g.row = r.c->row;
-    g.val = r.c->val;
-    g.ptr2 = r.c->ptr2;
-    g.row2 = r.c->row2;
-    g.val2 = r.c->val2;
-    g.lx = r.lx;
-    g.lv = r.lv;
-    g.off = (uint32_t)(r.c->dcnt - dcnt_all);
-    g.n1 = r.c->nrows + 1;
-    g.n_old = (uint32_t)r.old_n;
-    g.begin = (uint32_t)r.begin;
-    g.end_ptr = r.end_ptr;
-    g.rank = r.rank;
-    m.max_rows = std::max(m.max_rows, g.n1);
-    m.max_old = std::max(m.max_old, g.n_old);
-  }
-  ScanArgs sa{};
-  uint32_t tiles = 0;
-  for (uint32_t k = 0; k < m.nseg; ++k) {
-    sa.tile0[k] = tiles;
-    tiles += (m.seg[k].n1 + SCAN_TILE - 1) / SCAN_TILE;
-  }
-  sa.tile0[m.nseg] = tiles;
-  if (tiles > scan_tiles) throw std::runtime_error("scan tile overflow");
-  if (++scan_epoch >= (1u << 30)) {  // epoch field is 30 bits: restart from clean flags
-    HIPCHK(hipMemsetAsync(scan_flags, 0, scan_tiles * sizeof(unsigned long long), stream));
-    scan_epoch = 1;
-  }
-  sa.epoch = scan_epoch;
-  sa.flags = scan_flags;
-  sa.ticket = &ctr->ticket;
-  launch(EL_K_SCAN, [&] {
-    hipLaunchKernelGGL(k_scan_merge, dim3(tiles), dim3(256), 0, stream, m, sa, dcnt_all, dscan_all);
-  });
-  if (m.max_old)
-    launch(EL_K_SCATTER_OLD, [&] {
-      hipLaunchKernelGGL(k_scatter_old, dim3(grid_for(m.max_old, tune_scatter), m.nseg), dim3(BLOCK), 0, stream, m,
-                         dscan_all);
-    });
-  launch(EL_K_SCATTER_NEW, [&] {
-    hipLaunchKernelGGL(k_scatter_new, dim3(tune_scatter, m.nseg), dim3(BLOCK), 0, stream, m, (const uint32_t*)dscan_all);
-  });
-}
-
-// After the step's sync: account the merges that did work and swap their buffers.
-void el_ctx::finish_merges(const std::vector<MergeReq>& reqs, const std::vector<uint64_t>& ends, bool account) {
-  for (size_t k = 0; k < reqs.size(); ++k) {
-    const MergeReq& r = reqs[k];
-    const uint64_t nn = ends[k] - r.begin;
-    if (!nn) continue;
-    if (account) {
-      const uint64_t n1 = r.c->nrows + 1, old_n = r.old_n;
-      host_ev[EL_K_SCAN][EL_EV_ENT] += 3ull * n1;       // read + zero dcnt, write dscan
-      host_ev[EL_K_MERGE_PTR][EL_EV_ENT] += 2ull * n1;  // read ptr, write ptr2
-      host_ev[EL_K_SCATTER_OLD][EL_EV_TRIG] += old_n;   // read (row, val)
-      host_ev[EL_K_SCATTER_OLD][EL_EV_ENT] += old_n;    // read dscan[row]
-      host_ev[EL_K_SCATTER_OLD][EL_EV_EMIT] += old_n;   // write (row2, val2)
-      host_ev[EL_K_SCATTER_NEW][EL_EV_TRIG] += nn;      // read log pair
-      host_ev[EL_K_SCATTER_NEW][EL_EV_ENT] += 3 * nn;   // read rank, ptr[x + 1], dscan[x]
-      host_ev[EL_K_SCATTER_NEW][EL_EV_EMIT] += nn;      // write (row2, val2)
+// Result rows from the logs (el_rows.hip), enqueued on the engine stream: S rows X -> {B}
+// ascending (long rows read off the bit matrix), link rows X -> {q} ascending, q = the
+// link's pair rank in (role, filler) order.  Rows stay valid until the logs change.
+void el_ctx::ensure_rows(bool facts, bool links) {
+  const uint32_t R = hi - lo;
+  auto fit = [&](Rows& r, uint64_t n) {
+    if (!r.ptr) r.ptr = dalloc<uint64_t>((uint64_t)R + 1);
+    if (n > r.cap || !r.val) {
+      dfree(r.val);
+      r.cap = n + n / 8 + 1024;
+      r.val = dalloc<uint32_t>(r.cap);
     }
-    std::swap(r.c->ptr, r.c->ptr2);
-    std::swap(r.c->row, r.c->row2);
-    std::swap(r.c->val, r.c->val2);
+  };
+  if (facts && rs.n != s_count) {
+    fit(rs, s_count);
+    elrows::build(stream, rsc, slog_x, slog_a, s_count, lo, R, nullptr, rs.ptr, rs.val, dstate().bits, W);
+    rs.n = s_count;
   }
-}
-
-// Bring the S-row CSR up to date with the fact log (export path, not counted as saturation).
-void el_ctx::ensure_s_csr() {
-  if (s_csr_count == s_count) return;
-  sync();  // the saturation's last merges may still be running
-  uint32_t* rank = dalloc<uint32_t>(s_count - s_csr_count);
-  hipLaunchKernelGGL(k_count_rows, dim3(grid_for(s_count - s_csr_count)), dim3(BLOCK), 0, stream, S.dcnt, rank,
-                     slog_x, (uint32_t)s_csr_count, (uint32_t)s_count);
-  HIPCHK(hipGetLastError());
-  std::vector<MergeReq> reqs{{&S, slog_x, slog_a, s_csr_count, s_csr_count, &ctr->s_log, rank}};
-  uint64_t saved_launch[EL_NUM_KERNELS];
-  memcpy(saved_launch, launches, sizeof launches);
-  launch_merges(reqs);
-  sync();
-  memcpy(launches, saved_launch, sizeof launches);  // export work is not saturation work
-  finish_merges(reqs, {s_count}, false);
-  dfree(rank);
-  s_csr_count = s_count;
+  if (links && rl.n != l_count) {
+    fit(rl, l_count);
+    elrows::build(stream, rsc, llog_x, llog_p, l_count, lo, R, pid_rank, rl.ptr, rl.val, nullptr, 0);
+    rl.n = l_count;
+  }
 }
 
 // One Jacobi superstep over the given trigger ranges; one host sync.  Returns true if
@@ -2957,7 +2775,7 @@ bool el_ctx::superstep(uint32_t mask, uint64_t sb, uint64_t se, uint64_t lb, uin
   for (int attempt = 0;; ++attempt) {
     // ---- capacities: every candidate could be new.  Growth copies device arrays outside
     // the stream, so the previous step's kernels must have finished first.
-    const bool grow = s_count + cs_cap + ct_cap > slog_cap || slog_cap > S.cap || l_count + cl_cap > llog_cap ||
+    const bool grow = s_count + cs_cap + ct_cap > slog_cap || l_count + cl_cap > llog_cap ||
                       2 * (l_count + cl_cap) > lhash_cap || a_count + ca_cap > alog_cap ||
                       2 * (a_count + ca_cap) > ahash_cap || p_count + cp_cap > plog_cap ||
                       2 * (p_count + cp_cap) > phash_cap;
@@ -2974,7 +2792,6 @@ bool el_ctx::superstep(uint32_t mask, uint64_t sb, uint64_t se, uint64_t lb, uin
       grow_log(s_count, cs_cap + ct_cap, slog_cap, slog_x, slog_a);
       if (slog_cap != old_cap) dgrow(slog_f, s_count, slog_cap);
     }
-    if (slog_cap > S.cap) S.grow(s_csr_count, slog_cap);
     grow_log(l_count, cl_cap, llog_cap, llog_x, llog_p);
     if (2 * (l_count + cl_cap) > lhash_cap) rehash_links(next_pow2(2 * (l_count + cl_cap)));
     grow_log(a_count, ca_cap, alog_cap, alog_y, alog_c);
@@ -3153,7 +2970,7 @@ uint64_t el_ctx::superstep_part(uint32_t mask, uint64_t sb, uint64_t se, uint64_
   for (int attempt = 0;; ++attempt) {
     // ---- capacities for the local candidates (as in superstep) and the remote imports
     const uint64_t rb = remote_bound();
-    const bool grow = s_count + cs_cap + ct_cap > slog_cap || slog_cap > S.cap || l_count + cl_cap > llog_cap ||
+    const bool grow = s_count + cs_cap + ct_cap > slog_cap || l_count + cl_cap > llog_cap ||
                       2 * (l_count + cl_cap) > lhash_cap || a_count + ca_cap + rb > alog_cap || 2 * (a_count + ca_cap + rb) > ahash_cap ||
                       p_count + cp_cap + rb > plog_cap || 2 * (p_count + cp_cap + rb) > phash_cap ||
                       x_count + part_count * xcap > xlog_cap;
@@ -3171,8 +2988,7 @@ uint64_t el_ctx::superstep_part(uint32_t mask, uint64_t sb, uint64_t se, uint64_
         grow_log(s_count, cs_cap + ct_cap, slog_cap, slog_x, slog_a);
         if (slog_cap != old_cap) dgrow(slog_f, s_count, slog_cap);
       }
-      if (slog_cap > S.cap) S.grow(s_csr_count, slog_cap);
-      grow_log(l_count, cl_cap, llog_cap, llog_x, llog_p);
+        grow_log(l_count, cl_cap, llog_cap, llog_x, llog_p);
       if (2 * (l_count + cl_cap) > lhash_cap) rehash_links(next_pow2(2 * (l_count + cl_cap)));
       grow_part(xcap);
     }
@@ -3295,19 +3111,14 @@ void el_ctx::gap_rebuild(GapCsr& g, uint32_t n_ovf, uint64_t entries) {
   host_ev[EL_K_SCATTER_NEW][EL_EV_EMIT] += n_ovf;
 }
 
-// new row starts = exclusive scan of gap_cap(len[r]): the single-pass look-back scan of
-// k_scan_merge in its gapped mode
+// new row starts = exclusive scan of gap_cap(len[r]) (k_gap_scan)
 void el_ctx::launch_gap_scan(const uint32_t* len, uint32_t R, uint32_t* start_out) {
-  MergeArgs m{};
-  m.nseg = 1;
-  m.seg[0].ptr2 = start_out;
-  m.seg[0].n1 = R + 1;
-  m.seg[0].gap_len = len;
   ScanArgs sa{};
-  const uint32_t tiles = (R + 1 + SCAN_TILE - 1) / SCAN_TILE;
-  if (tiles > scan_tiles) throw std::runtime_error("scan tile overflow");
-  sa.tile0[0] = 0;
-  sa.tile0[1] = tiles;
+  sa.len = len;
+  sa.start_out = start_out;
+  sa.n1 = R + 1;
+  sa.tiles = (R + 1 + SCAN_TILE - 1) / SCAN_TILE;
+  if (sa.tiles > scan_tiles) throw std::runtime_error("scan tile overflow");
   if (++scan_epoch >= (1u << 30)) {
     HIPCHK(hipMemsetAsync(scan_flags, 0, scan_tiles * sizeof(unsigned long long), stream));
     scan_epoch = 1;
@@ -3315,9 +3126,7 @@ void el_ctx::launch_gap_scan(const uint32_t* len, uint32_t R, uint32_t* start_ou
   sa.epoch = scan_epoch;
   sa.flags = scan_flags;
   sa.ticket = &ctr->ticket;
-  launch(EL_K_SCAN, [&] {
-    hipLaunchKernelGGL(k_scan_merge, dim3(tiles), dim3(256), 0, stream, m, sa, dcnt_all, dscan_all);
-  });
+  launch(EL_K_SCAN, [&] { hipLaunchKernelGGL(k_gap_scan, dim3(sa.tiles), dim3(256), 0, stream, sa); });
 }
 
 // A gapped CSR laid out for, and filled with, the n logged entries (rows[i], vals[i]).
@@ -3358,7 +3167,6 @@ void el_ctx::init_rows(uint32_t a, uint32_t b) {
     dgrow(slog_a, s_count, c);
     dgrow(slog_f, s_count, c);
     slog_cap = c;
-    if (slog_cap > S.cap) S.grow(s_csr_count, slog_cap);
   }
   DState st = dstate();
   launch(EL_K_INIT, [&] {
@@ -3389,17 +3197,9 @@ void el_ctx::migrate_state(uint32_t N0, const std::vector<uint32_t>& pmap) {
     bits = nb;
     has_act = ha;
     W = W1;
-    S.release();
-    dfree(dcnt_all);
-    dfree(dscan_all);
-    dcnt_total = N + 1;
-    dcnt_all = dalloc<uint32_t>(dcnt_total);
-    dscan_all = dalloc<uint32_t>(dcnt_total);
-    HIPCHK(hipMemsetAsync(dcnt_all, 0, dcnt_total * sizeof(uint32_t), stream));
-    S.alloc((uint32_t)N, slog_cap, dcnt_all, dscan_all);
   }
-  HIPCHK(hipMemsetAsync(S.ptr, 0, (N + 1) * sizeof(uint32_t), stream));
-  s_csr_count = 0;  // the export CSR is rebuilt from the log on demand
+  rs.release();  // result rows: more rows, remapped pair ids — rebuilt on demand
+  rl.release();
   dfree(scan_flags);
   scan_tiles = (std::max(N, P) + 1 + SCAN_TILE - 1) / SCAN_TILE;
   scan_flags = dalloc<unsigned long long>(scan_tiles);
@@ -3565,6 +3365,8 @@ int el_create(el_ctx** out, const el_config* cfg) {
   }
   int rc = guarded(c, [&] {
     HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+    HIPCHK(hipStreamCreateWithFlags(&c->cstream, hipStreamNonBlocking));
+    for (hipEvent_t& e : c->ev_rows) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     if (c->xmode == EL_XCHG_LOCAL) c->xchg.reset(new LocalExchange(cfg->group, (int)c->part_rank));
     if (c->xmode == EL_XCHG_RCCL)  // collective: every rank of the group calls el_create
       c->xchg.reset(new RcclExchange((int)c->part_rank, (int)c->part_count, cfg->rccl_id));
@@ -3572,6 +3374,9 @@ int el_create(el_ctx** out, const el_config* cfg) {
   });
   if (rc != EL_OK) {
     if (c->stream) (void)hipStreamDestroy(c->stream);
+    if (c->cstream) (void)hipStreamDestroy(c->cstream);
+    for (hipEvent_t e : c->ev_rows)
+      if (e) (void)hipEventDestroy(e);
     delete c;
     return rc;
   }
@@ -3674,7 +3479,6 @@ int el_init(el_ctx* c) {
   return guarded(c, [&] {
     c->reset_state();
     c->init_rows(c->lo, c->hi);
-    c->s_csr_count = 0;
     c->inited = true;
     c->stats_stale = true;
     return EL_OK;
@@ -3814,41 +3618,25 @@ int el_get_subsumers(el_ctx* c, uint32_t x, uint32_t* out, size_t cap, size_t* n
   if (x >= c->hx.N) return fail(c, EL_EINVAL, "concept id out of range");
   if (x < c->lo || x >= c->hi) return fail(c, EL_EINVAL, "row not owned by this partition");
   return guarded(c, [&] {
+    c->ensure_rows(true, false);
     c->sync();
-    c->ensure_s_csr();
-    uint32_t p[2];
-    HIPCHK(hipMemcpy(p, c->S.ptr + x, 2 * sizeof(uint32_t), hipMemcpyDeviceToHost));
+    uint64_t p[2];
+    HIPCHK(hipMemcpy(p, c->rs.ptr + (x - c->lo), sizeof p, hipMemcpyDeviceToHost));
     *n = p[1] - p[0];
     if (cap < *n) return EL_ERANGE;
-    if (*n) {
-      HIPCHK(hipMemcpy(out, c->S.val + p[0], *n * sizeof(uint32_t), hipMemcpyDeviceToHost));
-      std::sort(out, out + *n);
-    }
+    if (*n) HIPCHK(hipMemcpy(out, c->rs.val + p[0], *n * sizeof(uint32_t), hipMemcpyDeviceToHost));
     return EL_OK;
   });
 }
 
-// Copy the S CSR to the host with every row sorted (device segmented radix sort).
-static void copy_sorted_rows(el_ctx* c, std::vector<uint32_t>& ptr, uint32_t* vals) {
-  c->ensure_s_csr();
-  const uint32_t N = c->hx.N;
-  const uint64_t n = c->s_count;
-  ptr.resize(N + 1);
-  HIPCHK(hipMemcpy(ptr.data(), c->S.ptr, ptr.size() * 4, hipMemcpyDeviceToHost));
-  if (!n) return;
-  uint32_t* sorted = dalloc<uint32_t>(n);
-  size_t tb = 0;
-  HIPCHK(hipcub::DeviceSegmentedRadixSort::SortKeys(nullptr, tb, c->S.val, sorted, (int)n, (int)N,
-                                                    c->S.ptr, c->S.ptr + 1, 0, 32, c->stream));
-  void* tmp = nullptr;
-  HIPCHK(hipMalloc(&tmp, tb ? tb : 1));
-  HIPCHK(hipcub::DeviceSegmentedRadixSort::SortKeys(tmp, tb, c->S.val, sorted, (int)n, (int)N, c->S.ptr,
-                                                    c->S.ptr + 1, 0, 32, c->stream));
-  HIPCHK(hipStreamSynchronize(c->stream));
-  HIPCHK(hipMemcpy(vals, sorted, n * 4, hipMemcpyDeviceToHost));
-  (void)hipFree(tmp);
-  dfree(sorted);
+namespace {
+// host copy of result rows: ptr (rows + 1) and, when vals is given, the values
+void read_rows(el_ctx* c, const el_ctx::Rows& r, std::vector<uint64_t>& ptr, uint32_t* vals, uint64_t n) {
+  ptr.resize((size_t)(c->hi - c->lo) + 1);
+  HIPCHK(hipMemcpy(ptr.data(), r.ptr, ptr.size() * sizeof(uint64_t), hipMemcpyDeviceToHost));
+  if (vals && n) HIPCHK(hipMemcpy(vals, r.val, n * sizeof(uint32_t), hipMemcpyDeviceToHost));
 }
+}  // namespace
 
 int el_copy_facts(el_ctx* c, uint32_t* x, uint32_t* a, size_t cap, size_t* n) {
   if (!c || !n) return EL_EINVAL;
@@ -3858,16 +3646,17 @@ int el_copy_facts(el_ctx* c, uint32_t* x, uint32_t* a, size_t cap, size_t* n) {
     *n = c->s_count;
     if (cap < *n) return EL_ERANGE;
     if (!*n) return EL_OK;
-    std::vector<uint32_t> ptr;
-    copy_sorted_rows(c, ptr, a);
-    for (uint32_t r = 0; r < c->hx.N; ++r)
-      for (uint32_t j = ptr[r]; j < ptr[r + 1]; ++j) x[j] = r;
+    c->ensure_rows(true, false);
+    c->sync();
+    std::vector<uint64_t> ptr;
+    read_rows(c, c->rs, ptr, a, *n);
+    for (uint32_t r = 0; r + 1 < ptr.size(); ++r)
+      for (uint64_t j = ptr[r]; j < ptr[r + 1]; ++j) x[j] = c->lo + r;
     return EL_OK;
   });
 }
 
-// Links sorted by (x, r, y): device radix sort of 64-bit (x, pid) keys, then each x's
-// short run is reordered from pid order ((y, r)) to (r, y) on the host.
+// Links sorted by (x, r, y): each link row holds pair ranks in (role, filler) order.
 int el_copy_links(el_ctx* c, uint32_t* x, uint32_t* r, uint32_t* y, size_t cap, size_t* n) {
   if (!c || !n) return EL_EINVAL;
   if (!c->inited) return fail(c, EL_ESTATE, "no state");
@@ -3876,55 +3665,107 @@ int el_copy_links(el_ctx* c, uint32_t* x, uint32_t* r, uint32_t* y, size_t cap, 
     *n = c->l_count;
     if (cap < *n) return EL_ERANGE;
     if (!*n) return EL_OK;
-    const uint64_t m = *n;
-    unsigned long long* keys = dalloc<unsigned long long>(m);
-    unsigned long long* out = dalloc<unsigned long long>(m);
-    // pack on the device: key = x << 32 | pid
-    hipLaunchKernelGGL(k_pack_keys, dim3(grid_for(m)), dim3(BLOCK), 0, c->stream, keys, c->llog_x, c->llog_p,
-                       (uint32_t)m);
-    HIPCHK(hipGetLastError());
-    size_t tb = 0;
-    HIPCHK(hipcub::DeviceRadixSort::SortKeys(nullptr, tb, keys, out, (int)m, 0, 64, c->stream));
-    void* tmp = nullptr;
-    HIPCHK(hipMalloc(&tmp, tb ? tb : 1));
-    HIPCHK(hipcub::DeviceRadixSort::SortKeys(tmp, tb, keys, out, (int)m, 0, 64, c->stream));
-    HIPCHK(hipStreamSynchronize(c->stream));
-    std::vector<unsigned long long> hs(m);
-    HIPCHK(hipMemcpy(hs.data(), out, m * 8, hipMemcpyDeviceToHost));
-    (void)hipFree(tmp);
-    dfree(keys);
-    dfree(out);
-    uint64_t s0 = 0;
-    while (s0 < m) {
-      uint64_t e = s0;
-      const uint32_t xx = (uint32_t)(hs[s0] >> 32);
-      while (e < m && (uint32_t)(hs[e] >> 32) == xx) ++e;
-      // pids are ordered by (y, r); order this x's run by (r, y)
-      std::sort(hs.begin() + s0, hs.begin() + e, [&](unsigned long long u, unsigned long long v) {
-        const uint32_t pu = (uint32_t)u, pv = (uint32_t)v;
-        const uint32_t ru = c->hx.pair_role[pu], rv = c->hx.pair_role[pv];
-        return ru != rv ? ru < rv : c->hx.pair_y[pu] < c->hx.pair_y[pv];
-      });
-      for (uint64_t k = s0; k < e; ++k) {
-        const uint32_t p = (uint32_t)hs[k];
-        x[k] = xx;
-        r[k] = c->hx.pair_role[p];
-        y[k] = c->hx.pair_y[p];
+    c->ensure_rows(false, true);
+    c->sync();
+    std::vector<uint64_t> ptr;
+    std::vector<uint32_t> q(*n);
+    read_rows(c, c->rl, ptr, q.data(), *n);
+    for (uint32_t row = 0; row + 1 < ptr.size(); ++row)
+      for (uint64_t j = ptr[row]; j < ptr[row + 1]; ++j) {
+        x[j] = c->lo + row;
+        r[j] = c->rank_role[q[j]];
+        y[j] = c->rank_y[q[j]];
       }
-      s0 = e;
-    }
     return EL_OK;
   });
+}
+
+int el_result_info(el_ctx* c, el_result* res) {
+  if (!c || !res) return EL_EINVAL;
+  if (!c->inited) return fail(c, EL_ESTATE, "no state");
+  return guarded(c, [&] {
+    c->sync();
+    res->row_lo = c->lo;
+    res->row_hi = c->hi;
+    res->n_facts = c->s_count;
+    res->n_links = c->l_count;
+    res->n_pairs = c->hx.P;
+    return EL_OK;
+  });
+}
+
+// Result copy-back: the S rows are built and their DMA starts on the copy stream while the
+// link rows are built on the engine stream.  Buffers from el_host_alloc (pinned) are written
+// by the DMA engines directly; pageable buffers are staged by the runtime.
+int el_copy_result(el_ctx* c, el_result* res) {
+  if (!c || !res) return EL_EINVAL;
+  if (!c->inited) return fail(c, EL_ESTATE, "no state");
+  return guarded(c, [&] {
+    c->sync();  // counts of the last superstep
+    const uint64_t R1 = (uint64_t)(c->hi - c->lo) + 1;
+    res->row_lo = c->lo;
+    res->row_hi = c->hi;
+    res->n_facts = c->s_count;
+    res->n_links = c->l_count;
+    res->n_pairs = c->hx.P;
+    if ((res->s_val && res->s_cap < c->s_count) || (res->l_pair && res->l_cap < c->l_count))
+      return fail(c, EL_ERANGE, "result buffer too small (el_result_info gives the sizes)");
+    const bool want_s = res->s_ptr || res->s_val, want_l = res->l_ptr || res->l_pair;
+    if (want_s) {
+      c->ensure_rows(true, false);
+      HIPCHK(hipEventRecord(c->ev_rows[0], c->stream));
+      HIPCHK(hipStreamWaitEvent(c->cstream, c->ev_rows[0], 0));
+      if (res->s_ptr)
+        HIPCHK(hipMemcpyAsync(res->s_ptr, c->rs.ptr, R1 * sizeof(uint64_t), hipMemcpyDeviceToHost, c->cstream));
+      if (res->s_val && c->s_count)
+        HIPCHK(hipMemcpyAsync(res->s_val, c->rs.val, c->s_count * sizeof(uint32_t), hipMemcpyDeviceToHost,
+                              c->cstream));
+    }
+    if (want_l) {
+      c->ensure_rows(false, true);
+      HIPCHK(hipEventRecord(c->ev_rows[1], c->stream));
+      HIPCHK(hipStreamWaitEvent(c->cstream, c->ev_rows[1], 0));
+      if (res->l_ptr)
+        HIPCHK(hipMemcpyAsync(res->l_ptr, c->rl.ptr, R1 * sizeof(uint64_t), hipMemcpyDeviceToHost, c->cstream));
+      if (res->l_pair && c->l_count)
+        HIPCHK(hipMemcpyAsync(res->l_pair, c->rl.val, c->l_count * sizeof(uint32_t), hipMemcpyDeviceToHost,
+                              c->cstream));
+    }
+    HIPCHK(hipStreamSynchronize(c->cstream));
+    return EL_OK;
+  });
+}
+
+int el_pair_table(el_ctx* c, uint32_t* role, uint32_t* filler, size_t cap, size_t* n) {
+  if (!c || !n) return EL_EINVAL;
+  if (!c->loaded) return fail(c, EL_ESTATE, "no ontology loaded");
+  *n = c->rank_role.size();
+  if (cap < *n) return EL_ERANGE;
+  if (role) std::copy(c->rank_role.begin(), c->rank_role.end(), role);
+  if (filler) std::copy(c->rank_y.begin(), c->rank_y.end(), filler);
+  return EL_OK;
+}
+
+void* el_host_alloc(size_t bytes) {
+  void* p = nullptr;
+  if (hipHostMalloc(&p, bytes ? bytes : 1, hipHostMallocPortable) != hipSuccess) return nullptr;
+  return p;
+}
+
+void el_host_free(void* p) {
+  if (p) (void)hipHostFree(p);
 }
 
 int el_export_result(el_ctx* c, int layout, el_sink sink, void* user) {
   if (!c || !sink || (layout != EL_LAYOUT_X_TO_B && layout != EL_LAYOUT_B_TO_X)) return EL_EINVAL;
   if (!c->inited) return fail(c, EL_ESTATE, "no state");
   return guarded(c, [&] {
+    c->ensure_rows(true, false);
     c->sync();
-    const uint32_t N = c->hx.N;
-    std::vector<uint32_t> ptr, val(c->s_count);
-    copy_sorted_rows(c, ptr, val.data());
+    const uint32_t N = c->hx.N, lo = c->lo, hi = c->hi;
+    std::vector<uint64_t> ptr;
+    std::vector<uint32_t> val(c->s_count);
+    read_rows(c, c->rs, ptr, val.data(), c->s_count);
     // result node rows: classes and individuals only (⊥ and datatypes have no key)
     auto exported = [&](uint32_t x) {
       return x != EL_BOTTOM && c->hx.kind[x] != EL_KIND_DATATYPE;
@@ -3939,27 +3780,27 @@ int el_export_result(el_ctx* c, int layout, el_sink sink, void* user) {
       return rc;
     };
     if (layout == EL_LAYOUT_X_TO_B) {
-      for (uint32_t x = 0; x < N; ++x) {
+      for (uint32_t x = lo; x < hi; ++x) {
         if (!exported(x)) continue;
-        for (uint32_t j = ptr[x]; j < ptr[x + 1]; ++j) {
+        for (uint64_t j = ptr[x - lo]; j < ptr[x - lo + 1]; ++j) {
           ks.push_back(x);
           vs.push_back(val[j]);
           if (ks.size() >= batch && flush()) return fail(c, EL_EINVAL, "sink aborted");
         }
       }
     } else {
-      std::vector<uint32_t> cnt(N + 1, 0);
-      for (uint32_t x = 0; x < N; ++x)
+      std::vector<uint64_t> cnt(N + 1, 0);
+      for (uint32_t x = lo; x < hi; ++x)
         if (exported(x))
-          for (uint32_t j = ptr[x]; j < ptr[x + 1]; ++j) cnt[val[j] + 1]++;
+          for (uint64_t j = ptr[x - lo]; j < ptr[x - lo + 1]; ++j) cnt[val[j] + 1]++;
       for (uint32_t b = 0; b < N; ++b) cnt[b + 1] += cnt[b];
       std::vector<uint32_t> mem(cnt[N]);
-      std::vector<uint32_t> cur(cnt.begin(), cnt.end() - 1);
-      for (uint32_t x = 0; x < N; ++x)
+      std::vector<uint64_t> cur(cnt.begin(), cnt.end() - 1);
+      for (uint32_t x = lo; x < hi; ++x)
         if (exported(x))
-          for (uint32_t j = ptr[x]; j < ptr[x + 1]; ++j) mem[cur[val[j]]++] = x;
+          for (uint64_t j = ptr[x - lo]; j < ptr[x - lo + 1]; ++j) mem[cur[val[j]]++] = x;
       for (uint32_t b = 0; b < N; ++b)
-        for (uint32_t j = cnt[b]; j < cnt[b + 1]; ++j) {
+        for (uint64_t j = cnt[b]; j < cnt[b + 1]; ++j) {
           ks.push_back(b);
           vs.push_back(mem[j]);
           if (ks.size() >= batch && flush()) return fail(c, EL_EINVAL, "sink aborted");
@@ -3981,9 +3822,13 @@ void el_destroy(el_ctx* c) {
     (void)hipEventDestroy(pe.b);
   }
   for (auto e : c->event_pool) (void)hipEventDestroy(e);
+  if (c->cstream) (void)hipStreamSynchronize(c->cstream);
   c->free_state();
   c->free_index();
   if (c->stream) (void)hipStreamDestroy(c->stream);
+  if (c->cstream) (void)hipStreamDestroy(c->cstream);
+  for (hipEvent_t e : c->ev_rows)
+    if (e) (void)hipEventDestroy(e);
   delete c;
 }
 

@@ -29,7 +29,7 @@ KERNEL_NAMES = ["k_expand:s", "k_expand:l", "k_jobs", "k_expand:a", "k_commit:s"
 EVENT_NAMES = ["trig", "row", "ent", "test", "hash", "emit", "job", "rmw"]
 EVENT_BYTES = [8, 8, 4, 4, 8, 8, 16, 8]
 NUM_KERNELS = len(KERNEL_NAMES)
-ABI_VERSION = 3  # include/el_gpu.h EL_ABI_VERSION
+ABI_VERSION = 4  # include/el_gpu.h EL_ABI_VERSION
 XCHG_NONE, XCHG_LOCAL, XCHG_RCCL = 0, 1, 2
 NUM_EVENTS = len(EVENT_NAMES)
 
@@ -87,13 +87,20 @@ class _ElKernelStat(C.Structure):
                 ("ms", C.c_double), ("group", C.c_uint32)]
 
 
+class _ElResult(C.Structure):
+    _fields_ = [("row_lo", C.c_uint32), ("row_hi", C.c_uint32), ("n_facts", C.c_uint64), ("n_links", C.c_uint64),
+                ("n_pairs", C.c_uint32), ("s_ptr", C.POINTER(C.c_uint64)), ("s_val", _u32p), ("s_cap", C.c_uint64),
+                ("l_ptr", C.POINTER(C.c_uint64)), ("l_pair", _u32p), ("l_cap", C.c_uint64)]
+
+
 _SINK = C.CFUNCTYPE(C.c_int, C.c_void_p, _u32p, _u32p, C.c_size_t)
 
 EXPORTED_SYMBOLS = [
     "el_abi_version", "el_device_count", "el_create", "el_load", "el_init", "el_step", "el_saturate",
     "el_get_stats", "el_kernel_stats", "el_superstep_trace", "el_get_subsumers", "el_copy_facts",
     "el_copy_links", "el_export_result", "el_last_error", "el_destroy", "el_group_create", "el_group_destroy",
-    "el_rccl_unique_id", "el_add_axioms",
+    "el_rccl_unique_id", "el_add_axioms", "el_result_info", "el_copy_result", "el_pair_table", "el_host_alloc",
+    "el_host_free",
 ]
 
 _lib: Optional[C.CDLL] = None
@@ -127,6 +134,13 @@ def load_library(path: Optional[str] = None) -> C.CDLL:
     lib.el_copy_facts.argtypes = [P, _u32p, _u32p, C.c_size_t, C.POINTER(C.c_size_t)]
     lib.el_copy_links.argtypes = [P, _u32p, _u32p, _u32p, C.c_size_t, C.POINTER(C.c_size_t)]
     lib.el_export_result.argtypes = [P, C.c_int, _SINK, C.c_void_p]
+    lib.el_result_info.argtypes = [P, C.POINTER(_ElResult)]
+    lib.el_copy_result.argtypes = [P, C.POINTER(_ElResult)]
+    lib.el_pair_table.argtypes = [P, _u32p, _u32p, C.c_size_t, C.POINTER(C.c_size_t)]
+    lib.el_host_alloc.argtypes = [C.c_size_t]
+    lib.el_host_alloc.restype = C.c_void_p
+    lib.el_host_free.argtypes = [C.c_void_p]
+    lib.el_host_free.restype = None
     lib.el_last_error.argtypes = [P]
     lib.el_last_error.restype = C.c_char_p
     lib.el_destroy.argtypes = [P]
@@ -179,6 +193,52 @@ class AxiomsView:
         s.n_domain, s.dom_r, s.dom_c = len(ax.domain), k(col(ax.domain, 0)), k(col(ax.domain, 1))
         s.n_range, s.rng_r, s.rng_c = len(ax.range), k(col(ax.range, 0)), k(col(ax.range, 1))
         self.struct = s
+
+
+def pinned_array(n: int, dtype) -> np.ndarray:
+    """numpy array over page-locked host memory (el_host_alloc), freed with the array."""
+    import weakref
+    lib = load_library()
+    dt = np.dtype(dtype)
+    nbytes = max(1, int(n)) * dt.itemsize
+    p = lib.el_host_alloc(nbytes)
+    if not p:
+        raise ElError(EL_ENOMEM, f"el_host_alloc({nbytes}) failed")
+    raw = (C.c_uint8 * nbytes).from_address(p)
+    arr = np.frombuffer(raw, dtype=np.uint8, count=nbytes).view(dt)[:int(n)]
+    weakref.finalize(raw, lib.el_host_free, p)
+    return arr
+
+
+class Result:
+    """Result copy-back (el_copy_result): CSR rows over [row_lo, row_hi).
+    S(x) = s_val[s_ptr[x - row_lo]:s_ptr[x - row_lo + 1]] (ascending);
+    links of x = pair ids l_pair[l_ptr[..]:l_ptr[..]] (ascending), pair q = (pair_role[q], pair_y[q])."""
+
+    def __init__(self):
+        self.row_lo = self.row_hi = 0
+        self.n_facts = self.n_links = self.n_pairs = 0
+        self.s_ptr = self.s_val = self.l_ptr = self.l_pair = None
+
+    def _fit(self, rows: int, n_facts: int, n_links: int, pinned: bool) -> None:
+        alloc = pinned_array if pinned else (lambda n, dt: np.empty(n, dt))
+        if self.s_ptr is None or self.s_ptr.size != rows + 1:
+            self.s_ptr = alloc(rows + 1, np.uint64)
+            self.l_ptr = alloc(rows + 1, np.uint64)
+        if self.s_val is None or self.s_val.size < n_facts:
+            self.s_val = alloc(n_facts + n_facts // 8, np.uint32)
+        if self.l_pair is None or self.l_pair.size < n_links:
+            self.l_pair = alloc(n_links + n_links // 8, np.uint32)
+
+    def facts(self) -> Tuple[np.ndarray, np.ndarray]:
+        """(x, a) pairs sorted by (x, a)."""
+        rows = np.arange(self.row_lo, self.row_hi, dtype=np.uint32)
+        cnt = np.diff(self.s_ptr.astype(np.int64))
+        return np.repeat(rows, cnt), self.s_val[:self.n_facts].copy()
+
+    def subsumers(self, x: int) -> np.ndarray:
+        i = x - self.row_lo
+        return self.s_val[int(self.s_ptr[i]):int(self.s_ptr[i + 1])]
 
 
 class Stats(dict):
@@ -361,6 +421,43 @@ class Engine:
         self._check(self._lib.el_copy_links(self._ctx, _ptr(x), _ptr(r), _ptr(y), x.size, C.byref(n)),
                     "el_copy_links")
         return x, r, y
+
+    def result_info(self) -> _ElResult:
+        r = _ElResult()
+        self._check(self._lib.el_result_info(self._ctx, C.byref(r)), "el_result_info")
+        return r
+
+    def copy_result(self, out: Optional[Result] = None, pinned: bool = True, facts: bool = True,
+                    links: bool = True) -> Result:
+        """Result copy-back into ``out`` (reused across calls; page-locked buffers by default)."""
+        info = self.result_info()
+        out = out or Result()
+        out._fit(info.row_hi - info.row_lo, info.n_facts if facts else 0, info.n_links if links else 0, pinned)
+        r = _ElResult()
+        if facts:
+            r.s_ptr = out.s_ptr.ctypes.data_as(C.POINTER(C.c_uint64))
+            r.s_val = out.s_val.ctypes.data_as(_u32p)
+            r.s_cap = out.s_val.size
+        if links:
+            r.l_ptr = out.l_ptr.ctypes.data_as(C.POINTER(C.c_uint64))
+            r.l_pair = out.l_pair.ctypes.data_as(_u32p)
+            r.l_cap = out.l_pair.size
+        self._check(self._lib.el_copy_result(self._ctx, C.byref(r)), "el_copy_result")
+        out.row_lo, out.row_hi, out.n_facts, out.n_links, out.n_pairs = (r.row_lo, r.row_hi, r.n_facts, r.n_links,
+                                                                         r.n_pairs)
+        return out
+
+    def pair_table(self) -> Tuple[np.ndarray, np.ndarray]:
+        """pair q -> (role, filler), ascending in (role, filler)."""
+        n = C.c_size_t(0)
+        rc = self._lib.el_pair_table(self._ctx, None, None, 0, C.byref(n))
+        if rc not in (EL_OK, EL_ERANGE):
+            self._check(rc, "el_pair_table")
+        role = np.zeros(n.value, np.uint32)
+        filler = np.zeros(n.value, np.uint32)
+        self._check(self._lib.el_pair_table(self._ctx, _ptr(role), _ptr(filler), n.value, C.byref(n)),
+                    "el_pair_table")
+        return role, filler
 
     def export_result(self, layout: int = LAYOUT_X_TO_B) -> Tuple[np.ndarray, np.ndarray]:
         """Stream the result node through the C sink; returns (keys, values)."""

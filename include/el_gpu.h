@@ -14,8 +14,8 @@
  *     ELClassifier.classify() switch (ELClassifier.java:74-111)
  *   whole classify-all.sh run + CommunicationHandler     el_saturate()
  *     termination (CommunicationHandler.java:49-84)
- *   result node DB0 B->{X} / ResultRearranger DB1         el_export_result(), el_get_subsumers()
- *     X->{B} (ResultRearranger.java:57-105)
+ *   result node DB0 B->{X} / ResultRearranger DB1         el_copy_result() (copy-back, CSR),
+ *     X->{B} (ResultRearranger.java:57-105)                el_export_result(), el_get_subsumers()
  *   AxiomCounter totals (AxiomCounter.java:168-216)      el_stats
  *
  * Conventions
@@ -42,7 +42,7 @@
 extern "C" {
 #endif
 
-#define EL_ABI_VERSION 3
+#define EL_ABI_VERSION 4
 
 /* return codes */
 #define EL_OK        0
@@ -257,6 +257,41 @@ int el_get_stats(el_ctx* ctx, el_stats* stats);
 int el_kernel_stats(el_ctx* ctx, el_kernel_stat* out, int n);
 /* per-superstep delta sizes of the last el_saturate (|ΔS|, |Δlink|, |Δact|) */
 int el_superstep_trace(el_ctx* ctx, uint64_t* ds, uint64_t* dl, uint64_t* da, size_t cap, size_t* n);
+
+/* ---- results --------------------------------------------------------------------------
+ * Result copy-back (the metric runs from IR-in-HBM to fixpoint PLUS this
+ * copy).  The result node in its rearranged form X -> {B} (ResultRearranger DB1,
+ * ResultRearranger.java:57-105) and the role links X -> {(r, Y)} (the T3_2 DB1 "Yr" -> {X}
+ * keys, RolePairHandler.java:374-376, counted by AxiomCounter.java:193-215), as CSR rows over
+ * this context's rows [row_lo, row_hi):
+ *   S(X)   = s_val[s_ptr[X - row_lo] .. s_ptr[X - row_lo + 1]), ascending
+ *   links  = l_pair[l_ptr[X - row_lo] .. l_ptr[X - row_lo + 1]), ascending pair ids q; pair q is
+ *            (role, filler) = el_pair_table()[q], so each row is in (role, filler) order.
+ * Every row is present (S(X) includes X itself and ⊤; ⊥ / datatype rows are the caller's to
+ * skip, as ResultRearranger does).  Buffers are caller-owned; a NULL pointer skips that array.
+ * Buffers from el_host_alloc are page-locked: the DMA engines write them directly while the
+ * next rows are still being built on the device. */
+typedef struct el_result {
+  uint32_t row_lo, row_hi;  /* out: rows of this context (whole ontology: 0, n_concepts) */
+  uint64_t n_facts;         /* out: Σ_X |S(X)| over the rows */
+  uint64_t n_links;         /* out: links (X, r, Y) with X in the rows */
+  uint32_t n_pairs;         /* out: entries of el_pair_table */
+  uint64_t* s_ptr;          /* in: row_hi - row_lo + 1 entries, or NULL */
+  uint32_t* s_val;          /* in: s_cap entries (>= n_facts), or NULL */
+  uint64_t s_cap;
+  uint64_t* l_ptr;          /* in: row_hi - row_lo + 1 entries, or NULL */
+  uint32_t* l_pair;         /* in: l_cap entries (>= n_links), or NULL */
+  uint64_t l_cap;
+} el_result;
+
+int el_result_info(el_ctx* ctx, el_result* res);   /* the out fields only */
+int el_copy_result(el_ctx* ctx, el_result* res);   /* EL_ERANGE if a buffer is too small */
+/* pair q -> (role, filler), q ascending = (role, filler) ascending */
+int el_pair_table(el_ctx* ctx, uint32_t* role, uint32_t* filler, size_t cap, size_t* n);
+/* page-locked host memory for result buffers (NULL on failure); a JNI host wraps it in a
+ * direct ByteBuffer (NewDirectByteBuffer) */
+void* el_host_alloc(size_t bytes);
+void el_host_free(void* p);
 
 int el_get_subsumers(el_ctx* ctx, uint32_t x, uint32_t* out, size_t cap, size_t* n);
 /* all S facts (x[i], a[i]) meaning a ∈ S(x), grouped by x (rows in id order) */

@@ -13,7 +13,7 @@ HEADER = os.path.join(ROOT, "include", "el_gpu.h")
 
 def _declared():
     text = open(HEADER).read()
-    return sorted(set(re.findall(r"^\s*(?:int|void|const char\*)\s+(el_\w+)\s*\(", text, re.M)))
+    return sorted(set(re.findall(r"^\s*(?:int|void\*?|const char\*)\s*(el_\w+)\s*\(", text, re.M)))
 
 
 @pytest.fixture(scope="module")
@@ -40,7 +40,7 @@ def test_exports_every_symbol(lib):
 
 def test_abi_version(lib):
     from distel_amd import engine
-    assert lib.el_abi_version() == engine.ABI_VERSION == 3
+    assert lib.el_abi_version() == engine.ABI_VERSION == 4
 
 
 def test_config_struct_layout():

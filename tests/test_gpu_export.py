@@ -1,0 +1,144 @@
+"""GPU result export and copy-back against the CPU oracle.
+
+The result node X -> {B} (ResultRearranger DB1, ResultRearranger.java:57-105) and the role
+links come back through el_copy_result (CSR rows built on the device, el_rows.hip),
+el_export_result (B_TO_X = result node DB0, X_TO_B = DB1), el_get_subsumers and the
+el_copy_facts / el_copy_links triples.  Every path is compared with the oracle's closure —
+bit-exact, rows ascending — including rows on each of the row-sort paths (≤ 64 entries:
+register sort; ≤ 4096: LDS sort; longer: bit-matrix read-out for S rows, global sort for link
+rows).
+"""
+import os
+
+import numpy as np
+import pytest
+
+import kat
+from distel_amd import engine, generators, ir
+
+pytestmark = pytest.mark.gpu
+
+
+def _oracle_rows(o, n):
+    ox, oa = o.facts()
+    ptr = np.zeros(n + 1, np.uint64)
+    np.add.at(ptr, ox.astype(np.int64) + 1, 1)
+    return np.cumsum(ptr).astype(np.uint64), oa
+
+
+def _check_result(eng, o, ax, pinned=True):
+    res = eng.copy_result(pinned=pinned)
+    st = o.stats()
+    assert (res.row_lo, res.row_hi) == (0, ax.n_concepts)
+    assert res.n_facts == st["s_facts"] and res.n_links == st["links"]
+    ptr, oa = _oracle_rows(o, ax.n_concepts)
+    assert np.array_equal(res.s_ptr, ptr)
+    assert np.array_equal(res.s_val[:res.n_facts], oa)
+    # links: pair q -> (role, filler); rows ascending in q = ascending in (role, filler)
+    role, filler = eng.pair_table()
+    assert res.n_pairs == role.size
+    key = role.astype(np.uint64) << np.uint64(32) | filler.astype(np.uint64)
+    assert np.all(np.diff(key.astype(np.int64)) > 0)
+    lx, lr, ly = o.links()
+    lptr = np.zeros(ax.n_concepts + 1, np.uint64)
+    np.add.at(lptr, lx.astype(np.int64) + 1, 1)
+    assert np.array_equal(res.l_ptr, np.cumsum(lptr).astype(np.uint64))
+    q = res.l_pair[:res.n_links]
+    assert np.array_equal(role[q], lr) and np.array_equal(filler[q], ly)
+    return res
+
+
+def test_copy_result_g2(oracle_lib):
+    ax = generators.workload("g2")
+    eng, _ = engine.classify(ax, device=0)
+    o = oracle_lib.saturate(ax, 0)
+    _check_result(eng, o, ax, pinned=True)
+    _check_result(eng, o, ax, pinned=False)  # pageable buffers: staged by the runtime
+    # a second classification into the same (reused) buffers
+    res = engine.Result()
+    eng.init()
+    eng.saturate()
+    eng.copy_result(res)
+    eng.init()
+    eng.saturate()
+    eng.copy_result(res)
+    x, a = res.facts()
+    ox, oa = o.facts()
+    assert np.array_equal(x, ox) and np.array_equal(a, oa)
+    eng.close()
+
+
+@pytest.mark.parametrize("path", kat.kat_files(), ids=lambda p: os.path.basename(p))
+def test_copy_result_kat(path, oracle_lib):
+    ax, _ = kat.load_kat(path)
+    eng, _ = engine.classify(ax, device=0)
+    _check_result(eng, oracle_lib.saturate(ax, 0), ax)
+    eng.close()
+
+
+def _long_rows_ontology():
+    """One concept with 5,000 told subsumers (a long S row: bit-matrix read-out), one with
+    6,000 existentials (a long link row: global sort), one with 300 of each (LDS sort)."""
+    n = 2 + 3 + 6000
+    big_s, big_l, mid = 2, 3, 4
+    fill = list(range(5, n))
+    rng = np.random.default_rng(3)
+    sub = [(big_s, int(b)) for b in rng.permutation(fill)[:5000]]
+    sub += [(mid, int(b)) for b in rng.permutation(fill)[:300]]
+    ex = [(big_l, int(rng.integers(0, 3)), int(b)) for b in rng.permutation(fill)[:6000]]
+    ex += [(mid, int(rng.integers(0, 3)), int(b)) for b in rng.permutation(fill)[:300]]
+    return ir.Axioms.build(n, 3, sub=sub, ex_rhs=ex)
+
+
+def test_copy_result_long_rows(oracle_lib):
+    ax = _long_rows_ontology()
+    eng, _ = engine.classify(ax, device=0)
+    o = oracle_lib.saturate(ax, 0)
+    res = _check_result(eng, o, ax)
+    assert int(res.s_ptr[3] - res.s_ptr[2]) > 4096 and int(res.l_ptr[4] - res.l_ptr[3]) > 4096
+    eng.close()
+
+
+def test_export_and_subsumers_g2(oracle_lib):
+    """el_export_result (both layouts) and el_get_subsumers against the oracle, after the
+    result node's filter (no ⊥ row, no datatype rows; ResultRearranger.java:57-105)."""
+    ax = generators.workload("g2", scale=0.3)
+    eng, _ = engine.classify(ax, device=0)
+    o = oracle_lib.saturate(ax, 0)
+    ox, oa = o.facts()
+    keep = (ox != 0) & (ax.kind[ox] != 3)
+    k, v = eng.export_result(engine.LAYOUT_X_TO_B)
+    assert np.array_equal(k, ox[keep]) and np.array_equal(v, oa[keep])
+    kb, vb = eng.export_result(engine.LAYOUT_B_TO_X)
+    o2 = np.lexsort((ox[keep], oa[keep]))
+    assert np.array_equal(kb, oa[keep][o2]) and np.array_equal(vb, ox[keep][o2])
+    rng = np.random.default_rng(5)
+    for x in rng.integers(0, ax.n_concepts, 200).tolist() + [0, 1, ax.n_concepts - 1]:
+        assert np.array_equal(eng.subsumers(x), oa[ox == x])
+    gx, ga = eng.facts()
+    assert np.array_equal(gx, ox) and np.array_equal(ga, oa)
+    for g, c in zip(eng.links(), o.links()):
+        assert np.array_equal(g, c)
+    eng.close()
+
+
+def test_copy_result_small_buffers():
+    ax = generators.workload("g1", scale=0.05)
+    eng, st = engine.classify(ax, device=0)
+    import ctypes as C
+    r = engine._ElResult()
+    small = np.zeros(4, np.uint32)
+    r.s_val = small.ctypes.data_as(C.POINTER(C.c_uint32))
+    r.s_cap = small.size
+    assert eng._lib.el_copy_result(eng._ctx, C.byref(r)) == engine.EL_ERANGE
+    assert r.n_facts == st["s_facts"]
+    eng.close()
+
+
+def test_copy_result_empty():
+    ax = ir.Axioms.build(2, 0)
+    eng, _ = engine.classify(ax, device=0)
+    res = eng.copy_result()
+    assert res.n_facts == 2 and res.n_links == 0
+    assert res.s_ptr.tolist() == [0, 1, 2] and res.s_val[:2].tolist() == [0, 1]
+    eng.close()
