@@ -2069,7 +2069,7 @@ struct el_ctx {
     }
   };
   Rows rs, rl;  // S rows X -> {B}; link rows X -> {q}, q = pair rank in (role, filler) order
-  elrows::Scratch rsc;
+  elrows::Scratch rsc, rsc_l;  // row-build scratch (S rows, link rows: built concurrently)
   const uint32_t* pid_rank = nullptr;        // device: pid -> q (an index buffer)
   std::vector<uint32_t> rank_role, rank_y;   // host: the pair (role, filler) of rank q
   hipStream_t cstream = nullptr;             // copy-back DMA, beside the row builds
@@ -2283,6 +2283,13 @@ struct el_ctx {
   void reset_state();
   void ensure_capacity();
   void ensure_rows(bool facts, bool links);
+  // half: 0 = whole build, 1 = the part that reads the state, 2 = the rest (el_rows.h);
+  // clear: the S-row build zeroes the bit matrix as it writes (a releasing copy-back)
+  void build_rows(bool facts, hipStream_t s, uint64_t* ptr, uint32_t* dst, int half = 0, bool clear = false);
+  hipStream_t rstream = nullptr;  // state reset behind a releasing copy-back
+  hipEvent_t ev_reset = nullptr;
+  bool pre_reset = false;         // the device part of the next reset_state is already enqueued
+  void reset_device(hipStream_t s, bool matrix_clear = false);
   void rehash_links(uint64_t cap);
   void rehash_acts(uint64_t cap);
   void rehash_props(uint64_t cap);
@@ -2444,6 +2451,8 @@ void el_ctx::free_index() {
 }
 
 void el_ctx::free_state() {
+  if (rstream) (void)hipStreamSynchronize(rstream);  // a reset behind a releasing copy-back
+  pre_reset = false;
   dfree(bits);
   dfree(slog_x);
   dfree(slog_a);
@@ -2465,6 +2474,7 @@ void el_ctx::free_state() {
   rs.release();
   rl.release();
   rsc.release();
+  rsc_l.release();
   PR.release();
   SC.release();
   PP.release();
@@ -2650,18 +2660,21 @@ void el_ctx::alloc_state() {
   }
 }
 
-void el_ctx::reset_state() {
+// The device part of reset_state on stream s: clear the bit matrix (by the fact log), the
+// sets, counters and gapped rows.  Reads only the logs and counts of the finished state.
+void el_ctx::reset_device(hipStream_t stream, bool matrix_clear) {
   FillArgs f{};
   auto add = [&](void* p, uint64_t bytes, uint32_t pattern) { f.seg[f.n++] = FillSeg{p, bytes, pattern}; };
   const uint64_t matrix_bytes = (uint64_t)(hi - lo) * W * sizeof(uint32_t);
-  if (bits_logged && s_count * 64 < matrix_bytes) {  // one 64-B line per logged fact vs. the whole matrix
+  if (matrix_clear) {
+    // the releasing copy-back's S-row sorts zero the matrix as they write the rows
+  } else if (bits_logged && s_count * 64 < matrix_bytes) {  // one 64-B line per logged fact vs. the whole matrix
     hipLaunchKernelGGL(k_clear_logged, dim3(grid_for(s_count)), dim3(BLOCK), 0, stream, dstate().bits, W, slog_x,
                        slog_a, (uint32_t)s_count);
     HIPCHK(hipGetLastError());
   } else {
     add(bits, matrix_bytes, 0u);
   }
-  bits_logged = true;  // from here on every set bit is in the fact log (k_init and k_commit append)
   // the link set is by far the largest (G3: 2 GB): the runtime's fill reaches a higher write
   // rate than k_fill's grid-stride loop for it (k_fill: 2.0 ms per G3 classification)
   if (lhash_cap * sizeof(unsigned long long) >= (64ull << 20))
@@ -2687,6 +2700,16 @@ void el_ctx::reset_state() {
                        g->start0);
     HIPCHK(hipGetLastError());
   }
+}
+
+void el_ctx::reset_state() {
+  if (pre_reset) {  // done behind the copy-back that released the state (el_copy_result)
+    HIPCHK(hipStreamWaitEvent(stream, ev_reset, 0));
+    pre_reset = false;
+  } else {
+    reset_device(stream);
+  }
+  bits_logged = true;  // from here on every set bit is in the fact log (k_init and k_commit append)
   s_count = l_count = a_count = p_count = s_init = x_count = 0;
   rs.n = rl.n = ~0ull;  // result rows are stale
   for (int r = 0; r < EL_NUM_RULE_TYPES; ++r) wm_s[r] = wm_l[r] = wm_a[r] = wm_p[r] = 0;
@@ -2735,9 +2758,25 @@ void el_ctx::rehash_props(uint64_t cap) {
     });
 }
 
-// Result rows from the logs (el_rows.hip), enqueued on the engine stream: S rows X -> {B}
-// ascending (long rows read off the bit matrix), link rows X -> {q} ascending, q = the
-// link's pair rank in (role, filler) order.  Rows stay valid until the logs change.
+// Result rows from the logs (el_rows.hip): S rows X -> {B} ascending (long rows read off the
+// bit matrix), link rows X -> {q} ascending, q = the link's pair rank in (role, filler) order.
+// dst: device memory or mapped page-locked host memory (the copy-back writes the sorted rows
+// straight over PCIe).  Enqueued on s.
+void el_ctx::build_rows(bool facts, hipStream_t s, uint64_t* ptr, uint32_t* dst, int half, bool clear) {
+  const uint32_t R = hi - lo;
+  elrows::Scratch& sc = facts ? rsc : rsc_l;
+  clear = clear && facts;
+  if (half != 2) {
+    if (facts)
+      elrows::build_prep(s, sc, slog_x, slog_a, s_count, lo, R, nullptr, ptr, dst, dstate().bits, W, clear);
+    else
+      elrows::build_prep(s, sc, llog_x, llog_p, l_count, lo, R, pid_rank, ptr, dst, nullptr, 0, false);
+  }
+  if (half != 1) elrows::build_sort(s, sc, ptr, dst, clear ? elrows::Clear{dstate().bits, W, lo} : elrows::Clear{});
+}
+
+// Device-resident result rows (el_get_subsumers, el_copy_facts / links, el_export_result),
+// kept until the logs change.
 void el_ctx::ensure_rows(bool facts, bool links) {
   const uint32_t R = hi - lo;
   auto fit = [&](Rows& r, uint64_t n) {
@@ -2750,12 +2789,12 @@ void el_ctx::ensure_rows(bool facts, bool links) {
   };
   if (facts && rs.n != s_count) {
     fit(rs, s_count);
-    elrows::build(stream, rsc, slog_x, slog_a, s_count, lo, R, nullptr, rs.ptr, rs.val, dstate().bits, W);
+    build_rows(true, stream, rs.ptr, rs.val);
     rs.n = s_count;
   }
   if (links && rl.n != l_count) {
     fit(rl, l_count);
-    elrows::build(stream, rsc, llog_x, llog_p, l_count, lo, R, pid_rank, rl.ptr, rl.val, nullptr, 0);
+    build_rows(false, stream, rl.ptr, rl.val);
     rl.n = l_count;
   }
 }
@@ -3366,7 +3405,9 @@ int el_create(el_ctx** out, const el_config* cfg) {
   int rc = guarded(c, [&] {
     HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
     HIPCHK(hipStreamCreateWithFlags(&c->cstream, hipStreamNonBlocking));
+    HIPCHK(hipStreamCreateWithFlags(&c->rstream, hipStreamNonBlocking));
     for (hipEvent_t& e : c->ev_rows) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    HIPCHK(hipEventCreateWithFlags(&c->ev_reset, hipEventDisableTiming));
     if (c->xmode == EL_XCHG_LOCAL) c->xchg.reset(new LocalExchange(cfg->group, (int)c->part_rank));
     if (c->xmode == EL_XCHG_RCCL)  // collective: every rank of the group calls el_create
       c->xchg.reset(new RcclExchange((int)c->part_rank, (int)c->part_count, cfg->rccl_id));
@@ -3375,8 +3416,10 @@ int el_create(el_ctx** out, const el_config* cfg) {
   if (rc != EL_OK) {
     if (c->stream) (void)hipStreamDestroy(c->stream);
     if (c->cstream) (void)hipStreamDestroy(c->cstream);
+    if (c->rstream) (void)hipStreamDestroy(c->rstream);
     for (hipEvent_t e : c->ev_rows)
       if (e) (void)hipEventDestroy(e);
+    if (c->ev_reset) (void)hipEventDestroy(c->ev_reset);
     delete c;
     return rc;
   }
@@ -3694,12 +3737,29 @@ int el_result_info(el_ctx* c, el_result* res) {
   });
 }
 
-// Result copy-back: the S rows are built and their DMA starts on the copy stream while the
-// link rows are built on the engine stream.  Buffers from el_host_alloc (pinned) are written
-// by the DMA engines directly; pageable buffers are staged by the runtime.
+namespace {
+// device address of page-locked host memory (el_host_alloc / hipHostMalloc / registered), or null
+uint32_t* mapped_for_device(void* h) {
+  hipPointerAttribute_t a{};
+  if (!h || hipPointerGetAttributes(&a, h) != hipSuccess) {
+    (void)hipGetLastError();  // pageable memory: not an error of ours
+    return nullptr;
+  }
+  return a.type == hipMemoryTypeHost && a.devicePointer ? (uint32_t*)a.devicePointer : nullptr;
+}
+}  // namespace
+
+// Result copy-back.  Into page-locked buffers the row sorts write the sorted rows straight over
+// PCIe: the S rows on the engine stream and the link rows on the copy stream at the same time,
+// each row offset array by DMA behind its rows.  Rows already resident on the device (an earlier
+// export) and pageable buffers go by DMA from the device rows.  EL_RESULT_RELEASE: once the
+// row builds have read the state (their prep halves), the next el_init's reset runs on a third
+// stream while the sorted rows still stream over PCIe; the context then has no state until
+// that el_init.
 int el_copy_result(el_ctx* c, el_result* res) {
   if (!c || !res) return EL_EINVAL;
   if (!c->inited) return fail(c, EL_ESTATE, "no state");
+  if (res->flags & ~EL_RESULT_FLAGS_KNOWN) return fail(c, EL_EINVAL, "unknown el_result flags");
   return guarded(c, [&] {
     c->sync();  // counts of the last superstep
     const uint64_t R1 = (uint64_t)(c->hi - c->lo) + 1;
@@ -3710,28 +3770,65 @@ int el_copy_result(el_ctx* c, el_result* res) {
     res->n_pairs = c->hx.P;
     if ((res->s_val && res->s_cap < c->s_count) || (res->l_pair && res->l_cap < c->l_count))
       return fail(c, EL_ERANGE, "result buffer too small (el_result_info gives the sizes)");
-    const bool want_s = res->s_ptr || res->s_val, want_l = res->l_ptr || res->l_pair;
-    if (want_s) {
-      c->ensure_rows(true, false);
+    const bool release = (res->flags & EL_RESULT_RELEASE) != 0;
+    struct Part {
+      bool facts;
+      uint64_t* ptr_out;
+      uint32_t* val_out;
+      el_ctx::Rows* rows;
+      uint64_t n;
+      hipStream_t s;
+      uint32_t* direct;
+    };
+    Part parts[2] = {{false, res->l_ptr, res->l_pair, &c->rl, c->l_count, c->cstream, nullptr},
+                     {true, res->s_ptr, res->s_val, &c->rs, c->s_count, c->stream, nullptr}};
+    // the copy stream starts behind the saturation
+    HIPCHK(hipEventRecord(c->ev_rows[1], c->stream));
+    HIPCHK(hipStreamWaitEvent(c->cstream, c->ev_rows[1], 0));
+    // 1. everything that reads the state
+    for (Part& p : parts) {
+      if (!p.ptr_out && !p.val_out) continue;
+      el_ctx::Rows& r = *p.rows;
+      p.direct = r.n == p.n || !p.n ? nullptr : mapped_for_device(p.val_out);
+      if (p.direct) {  // sorted rows straight into the caller's page-locked buffer
+        if (!r.ptr) r.ptr = dalloc<uint64_t>(R1);
+        r.n = ~0ull;  // r.ptr is reused; the device rows are not built
+        c->build_rows(p.facts, p.s, r.ptr, p.direct, 1, release);
+      } else {
+        p.direct = nullptr;
+        c->ensure_rows(p.facts, !p.facts);  // engine stream
+      }
+    }
+    if (release) {  // the next classification's reset, beside the rest of the copy-back
+      HIPCHK(hipEventRecord(c->ev_rows[0], c->stream));
+      HIPCHK(hipEventRecord(c->ev_rows[1], c->cstream));
+      HIPCHK(hipStreamWaitEvent(c->rstream, c->ev_rows[0], 0));
+      HIPCHK(hipStreamWaitEvent(c->rstream, c->ev_rows[1], 0));
+      c->reset_device(c->rstream, parts[1].direct != nullptr);  // the S-row sorts clear the matrix
+      HIPCHK(hipEventRecord(c->ev_reset, c->rstream));
+    }
+    // 2. the sorts into the caller's buffers, the device rows by DMA
+    for (Part& p : parts) {
+      if (!p.ptr_out && !p.val_out) continue;
+      el_ctx::Rows& r = *p.rows;
+      if (p.direct) {
+        c->build_rows(p.facts, p.s, r.ptr, p.direct, 2, release);
+        if (p.ptr_out) HIPCHK(hipMemcpyAsync(p.ptr_out, r.ptr, R1 * sizeof(uint64_t), hipMemcpyDeviceToHost, p.s));
+        continue;
+      }
       HIPCHK(hipEventRecord(c->ev_rows[0], c->stream));
       HIPCHK(hipStreamWaitEvent(c->cstream, c->ev_rows[0], 0));
-      if (res->s_ptr)
-        HIPCHK(hipMemcpyAsync(res->s_ptr, c->rs.ptr, R1 * sizeof(uint64_t), hipMemcpyDeviceToHost, c->cstream));
-      if (res->s_val && c->s_count)
-        HIPCHK(hipMemcpyAsync(res->s_val, c->rs.val, c->s_count * sizeof(uint32_t), hipMemcpyDeviceToHost,
-                              c->cstream));
-    }
-    if (want_l) {
-      c->ensure_rows(false, true);
-      HIPCHK(hipEventRecord(c->ev_rows[1], c->stream));
-      HIPCHK(hipStreamWaitEvent(c->cstream, c->ev_rows[1], 0));
-      if (res->l_ptr)
-        HIPCHK(hipMemcpyAsync(res->l_ptr, c->rl.ptr, R1 * sizeof(uint64_t), hipMemcpyDeviceToHost, c->cstream));
-      if (res->l_pair && c->l_count)
-        HIPCHK(hipMemcpyAsync(res->l_pair, c->rl.val, c->l_count * sizeof(uint32_t), hipMemcpyDeviceToHost,
-                              c->cstream));
+      if (p.ptr_out) HIPCHK(hipMemcpyAsync(p.ptr_out, r.ptr, R1 * sizeof(uint64_t), hipMemcpyDeviceToHost, c->cstream));
+      if (p.val_out && p.n)
+        HIPCHK(hipMemcpyAsync(p.val_out, r.val, p.n * sizeof(uint32_t), hipMemcpyDeviceToHost, c->cstream));
     }
     HIPCHK(hipStreamSynchronize(c->cstream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    if (release) {  // the reset may still run: el_init waits for it, free_state too
+      c->pre_reset = true;
+      c->inited = false;  // no state until el_init
+      c->rs.n = c->rl.n = ~0ull;
+    }
     return EL_OK;
   });
 }
@@ -3823,12 +3920,15 @@ void el_destroy(el_ctx* c) {
   }
   for (auto e : c->event_pool) (void)hipEventDestroy(e);
   if (c->cstream) (void)hipStreamSynchronize(c->cstream);
+  if (c->rstream) (void)hipStreamSynchronize(c->rstream);
   c->free_state();
   c->free_index();
   if (c->stream) (void)hipStreamDestroy(c->stream);
   if (c->cstream) (void)hipStreamDestroy(c->cstream);
+  if (c->rstream) (void)hipStreamDestroy(c->rstream);
   for (hipEvent_t e : c->ev_rows)
     if (e) (void)hipEventDestroy(e);
+  if (c->ev_reset) (void)hipEventDestroy(c->ev_reset);
   delete c;
 }
 

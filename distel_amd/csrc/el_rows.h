@@ -8,12 +8,17 @@
 //
 //   k_rows_count    per-row counts + each entry's rank in its row (one atomic per run of equal
 //                   rows in a wave: the log holds whole told closures back to back)
-//   scan            uint64 row offsets (library scan)
-//   k_rows_scatter  entry -> ptr[row] + rank (optionally through a value -> key map)
-//   k_rows_small    rows of <= 64 entries: one register bitonic sort per row (a wave)
-//   k_rows_lds      rows of <= 4096 entries: LDS bitonic sort, one workgroup per row
-//   k_rows_bits     longer rows with a bit matrix: the row's set bits in order (no sort)
-//   k_rows_global   longer rows without one: bitonic sort in global memory, one workgroup per row
+//   scan            uint64 row offsets (k_rows_tiles, k_rows_tile_scan, k_rows_offsets; the
+//                   last also lists the rows longer than 64 entries)
+//   k_rows_scatter  entry -> tmp[ptr[row] + rank] (optionally through a value -> key map)
+//   k_rows_small    rows of <= 64 entries: register bitonic sort per row (a wave) -> dst
+//   k_rows_lds      rows of <= 4096 entries: LDS bitonic sort, one workgroup per row -> dst
+//   k_rows_bits     longer rows with a bit matrix: the row's set bits in order (no sort) -> dst
+//   k_rows_global   longer rows without one: bitonic sort in place in tmp, then -> dst
+//
+// dst may be device memory or page-locked host memory mapped for the device: the sort
+// kernels then write the sorted rows straight over PCIe (the copy-back is fused with the sort,
+// no device staging copy and no separate DMA).
 #pragma once
 
 #include <hip/hip_runtime.h>
@@ -22,25 +27,49 @@
 
 namespace elrows {
 
+// A bit matrix to clear while the rows are written (the caller releases its state): row x at
+// bits + x·W, rows r of the build at x = r + lo.  bits = nullptr: nothing to clear.
+struct Clear {
+  uint32_t* bits = nullptr;
+  uint64_t W = 0;
+  uint32_t lo = 0;
+  __device__ void bit(uint32_t r, uint32_t v) const;
+};
+
 struct Scratch {
   uint32_t* rank = nullptr;  // per log entry
   uint64_t rank_cap = 0;
+  uint32_t* tmp = nullptr;  // scattered (unsorted) rows, per log entry
+  uint64_t tmp_cap = 0;
   uint32_t* cnt = nullptr;  // rows + 1
   uint64_t cnt_cap = 0;
   uint32_t* lists = nullptr;  // medium rows [0, rows), long rows [rows, 2 rows)
   uint64_t list_cap = 0;
   uint32_t* nlist = nullptr;  // two counters, 256 B apart
-  void* cub = nullptr;
-  size_t cub_bytes = 0;
+  uint64_t* tile = nullptr;  // scan tile sums
+  uint64_t tile_cap = 0;
+  uint64_t n = 0;      // the prepared build (build_prep -> build_sort)
+  uint32_t R = 0;
+  bool bits = false;
   void release();
 };
 
 // Rows [row_lo, row_lo + R) of the log entries (rows[i], vals[i]), i < n (every rows[i] in
-// range).  ptr: R + 1 offsets; out: n values, keymap ? keymap[v] : v, ascending in each row.
+// range).  ptr (device): R + 1 offsets; dst: n values, keymap ? keymap[v] : v, ascending in
+// each row (device memory, or host memory the device can write).
 // bits (optional): virtual base of a bit matrix holding exactly the log's entries, row x at
 // bits + x * W (values are column ids); long rows are then read from it instead of sorted.
 // Everything is enqueued on `s`; nothing is read back.  Throws std::runtime_error on a HIP error.
 void build(hipStream_t s, Scratch& sc, const uint32_t* rows, const uint32_t* vals, uint64_t n, uint32_t row_lo,
-           uint32_t R, const uint32_t* keymap, uint64_t* ptr, uint32_t* out, const uint32_t* bits, uint64_t W);
+           uint32_t R, const uint32_t* keymap, uint64_t* ptr, uint32_t* dst, uint32_t* bits, uint64_t W);
+
+// build() in two halves: build_prep reads the log (and the bit matrix for the long rows);
+// build_sort reads only the scratch, so the log's owner may reuse its state once the prep's
+// work has completed on s.  clear (prep) / cl (sort): zero the matrix bits of the written
+// entries as they go, leaving the matrix empty (the caller is done with it).
+void build_prep(hipStream_t s, Scratch& sc, const uint32_t* rows, const uint32_t* vals, uint64_t n, uint32_t row_lo,
+                uint32_t R, const uint32_t* keymap, uint64_t* ptr, uint32_t* dst, uint32_t* bits, uint64_t W,
+                bool clear);
+void build_sort(hipStream_t s, Scratch& sc, const uint64_t* ptr, uint32_t* dst, Clear cl);
 
 }  // namespace elrows

@@ -1,12 +1,12 @@
 // el_rows.hip — row-sorted CSR of an append-only (row, value) log (see el_rows.h).
 //
-// Integer gather/scatter work, HBM-bound: the log is read twice (count, scatter), the CSR
-// written once and re-read once by the row sorts.  Row sorts run in registers (≤ 64 entries,
-// one wave) or LDS (≤ 4096 entries, one workgroup); the few longer rows are read off the
-// bit matrix in column order when there is one.
+// Integer gather/scatter work, HBM-bound on the device side: the log is read twice (count,
+// scatter), the unsorted rows written once and re-read once by the row sorts, which write the
+// sorted rows to dst (device memory, or page-locked host memory over PCIe).  Row sorts run in
+// registers (≤ 64 entries, one wave; ≤ 4096 entries, one workgroup with the cross-wave stages
+// through LDS); the few longer rows are read off the bit matrix in column order when there is
+// one.
 #include "el_rows.h"
-
-#include <hipcub/hipcub.hpp>
 
 #include <stdexcept>
 #include <string>
@@ -16,7 +16,7 @@ namespace {
 
 constexpr uint32_t BLOCK = 256;
 constexpr uint32_t SMALL = 64;      // register sort: one row per wave
-constexpr uint32_t LDS_MAX = 4096;  // LDS sort: one row per workgroup (16 KB)
+constexpr uint32_t LDS_MAX = 4096;  // workgroup sort: 16 values per lane, 16 KB of LDS
 constexpr uint32_t NONE = 0xffffffffu;
 
 #define RCHK(expr)                                                                                  \
@@ -30,7 +30,7 @@ void ensure(T*& p, uint64_t& cap, uint64_t n) {
   if (n <= cap && p) return;
   if (p) (void)hipFree(p);
   p = nullptr;
-  cap = n + n / 4 + 1024;
+  cap = n + n / 8 + 1024;
   RCHK(hipMalloc((void**)&p, cap * sizeof(T)));
 }
 
@@ -71,20 +71,132 @@ __global__ void __launch_bounds__(BLOCK) k_rows_scatter(const uint32_t* __restri
                                                         const uint64_t* __restrict__ ptr,
                                                         const uint32_t* __restrict__ rank,
                                                         const uint32_t* __restrict__ keymap,
-                                                        uint32_t* __restrict__ out) {
+                                                        uint32_t* __restrict__ tmp) {
   const uint64_t stride = (uint64_t)gridDim.x * BLOCK;
   for (uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; i < n; i += stride) {
     const uint32_t v = vals[i];
-    out[ptr[rows[i] - lo] + rank[i]] = keymap ? keymap[v] : v;
+    tmp[ptr[rows[i] - lo] + rank[i]] = keymap ? keymap[v] : v;
   }
 }
 
-// Rows of <= 64 entries sorted in registers (bitonic network over the wave, shuffles only);
-// longer rows are listed for k_rows_lds (<= LDS_MAX) or the long-row kernels.  A wave looks
-// at 64 rows at once, so a list append is one atomic per wave.
+// Workgroup barrier for LDS hand-offs only: waits for this wave's LDS operations, not for its
+// global stores (__syncthreads would also drain the row's PCIe stores into a host buffer
+// before the next row could start).
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+}  // namespace
+
+// Bit matrix the sorts clear as they write (EL_RESULT_RELEASE): row x at bits + x·W.
+__device__ void Clear::bit(uint32_t r, uint32_t v) const {
+  if (bits) bits[(uint64_t)(r + lo) * W + (v >> 5)] = 0u;
+}
+
+namespace {
+
+// bitonic compare-exchange of a lane's value with the lane j away (j < 64) in stage k, where
+// e is the element's index in the padded row
+__device__ __forceinline__ uint32_t bitonic_xor(uint32_t v, uint32_t e, uint32_t k, uint32_t j) {
+  const uint32_t u = __shfl_xor(v, (int)j);
+  const bool up = (e & k) == 0, lower = (e & j) == 0;
+  return (lower == up) ? min(v, u) : max(v, u);
+}
+
+// Row offsets: exclusive scan of the row counts (uint32) into uint64 offsets, in tiles of
+// SCAN_TILE rows: tile sums, one block scans them, then each tile scans itself and lists its
+// rows longer than 64 entries for k_rows_lds (<= LDS_MAX) or the long-row kernels (one global
+// atomic per tile and list).
+constexpr uint32_t SCAN_PER = 16, SCAN_TILE = BLOCK * SCAN_PER;
+
+__device__ __forceinline__ uint64_t block_excl_scan(uint64_t v, uint64_t* wsum, uint64_t* total) {
+  const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+  uint64_t inc = v;
+#pragma unroll
+  for (uint32_t o = 1; o < 64; o <<= 1) {
+    const uint64_t y = __shfl_up(inc, o);
+    if (lane >= o) inc += y;
+  }
+  if (lane == 63) wsum[wv] = inc;
+  __syncthreads();
+  uint64_t before = 0, all = 0;
+#pragma unroll
+  for (uint32_t k = 0; k < BLOCK / 64; ++k) {
+    before += k < wv ? wsum[k] : 0u;
+    all += wsum[k];
+  }
+  __syncthreads();
+  if (total) *total = all;
+  return before + inc - v;
+}
+
+__global__ void __launch_bounds__(BLOCK) k_rows_tiles(const uint32_t* __restrict__ cnt, uint32_t n1,
+                                                      uint64_t* __restrict__ tile_sum) {
+  __shared__ uint64_t wsum[BLOCK / 64];
+  const uint32_t base = blockIdx.x * SCAN_TILE + threadIdx.x * SCAN_PER;
+  uint64_t t = 0;
+#pragma unroll
+  for (uint32_t j = 0; j < SCAN_PER; ++j) t += base + j < n1 ? cnt[base + j] : 0u;
+  uint64_t all = 0;
+  block_excl_scan(t, wsum, &all);
+  if (threadIdx.x == 0) tile_sum[blockIdx.x] = all;
+}
+
+__global__ void __launch_bounds__(BLOCK) k_rows_tile_scan(uint64_t* __restrict__ tile_sum, uint32_t ntiles) {
+  __shared__ uint64_t wsum[BLOCK / 64];
+  uint64_t carry = 0;
+  for (uint32_t b = 0; b < ntiles; b += BLOCK) {
+    const uint32_t i = b + threadIdx.x;
+    const uint64_t v = i < ntiles ? tile_sum[i] : 0;
+    uint64_t all = 0;
+    const uint64_t ex = block_excl_scan(v, wsum, &all);
+    if (i < ntiles) tile_sum[i] = carry + ex;
+    carry += all;
+  }
+}
+
+__global__ void __launch_bounds__(BLOCK) k_rows_offsets(const uint32_t* __restrict__ cnt, uint32_t R,
+                                                        const uint64_t* __restrict__ tile_pre,
+                                                        uint64_t* __restrict__ ptr, uint32_t* __restrict__ lists,
+                                                        uint32_t* __restrict__ nlist) {
+  __shared__ uint64_t wsum[BLOCK / 64];
+  __shared__ uint32_t lmid[SCAN_TILE], lbig[64];
+  __shared__ uint32_t nmid, nbig, gmid, gbig;
+  if (threadIdx.x == 0) nmid = nbig = 0;
+  const uint32_t base = blockIdx.x * SCAN_TILE + threadIdx.x * SCAN_PER;
+  uint32_t c[SCAN_PER];
+  uint64_t t = 0;
+#pragma unroll
+  for (uint32_t j = 0; j < SCAN_PER; ++j) {
+    c[j] = base + j < R ? cnt[base + j] : 0u;  // row R (the end offset) counts nothing
+    t += c[j];
+  }
+  uint64_t run = tile_pre[blockIdx.x] + block_excl_scan(t, wsum, nullptr);  // (its barriers order the LDS init)
+#pragma unroll
+  for (uint32_t j = 0; j < SCAN_PER; ++j) {
+    const uint32_t r = base + j;
+    if (r <= R) ptr[r] = run;
+    run += c[j];
+    if (c[j] > SMALL && c[j] <= LDS_MAX) lmid[atomicAdd(&nmid, 1u)] = r;
+    if (c[j] > LDS_MAX) {
+      const uint32_t k = atomicAdd(&nbig, 1u);
+      if (k < 64) lbig[k] = r;
+      else lists[R + atomicAdd(nlist + 64, 1u)] = r;  // (a tile with > 64 long rows)
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    gmid = nmid ? atomicAdd(nlist, nmid) : 0u;
+    gbig = nbig ? atomicAdd(nlist + 64, min(nbig, 64u)) : 0u;
+  }
+  __syncthreads();
+  for (uint32_t i = threadIdx.x; i < nmid; i += BLOCK) lists[gmid + i] = lmid[i];
+  for (uint32_t i = threadIdx.x; i < min(nbig, 64u); i += BLOCK) lists[R + gbig + i] = lbig[i];
+}
+
+// Rows of 1..64 entries, sorted in registers (bitonic network over the wave, shuffles only),
+// written to dst: a wave sorts the short rows among 64 consecutive rows one after the other.
 __global__ void __launch_bounds__(BLOCK) k_rows_small(const uint64_t* __restrict__ ptr, uint32_t R,
-                                                      uint32_t* __restrict__ out, uint32_t* __restrict__ lists,
-                                                      uint32_t* __restrict__ nlist) {
+                                                      const uint32_t* __restrict__ tmp, uint32_t* __restrict__ dst,
+                                                      Clear cl) {
   const uint32_t lane = __lane_id();
   const uint32_t waves = gridDim.x * (BLOCK / 64);
   for (uint32_t g = blockIdx.x * (BLOCK / 64) + (threadIdx.x >> 6); (uint64_t)g * 64 < R; g += waves) {
@@ -94,88 +206,116 @@ __global__ void __launch_bounds__(BLOCK) k_rows_small(const uint64_t* __restrict
       b = ptr[r];
       len = ptr[r + 1] - b;
     }
+    if (len == 1) {
+      const uint32_t v = tmp[b];
+      dst[b] = v;
+      cl.bit(r, v);
+    }
     const unsigned long long small = __ballot(len > 1 && len <= SMALL);
-    const unsigned long long mid = __ballot(len > SMALL && len <= LDS_MAX);
-    const unsigned long long big = __ballot(len > LDS_MAX);
-    if (mid) {
-      uint32_t at = 0;
-      if (lane == 0) at = atomicAdd(nlist, (uint32_t)__popcll(mid));
-      at = __shfl(at, 0);
-      if (mid >> lane & 1) lists[at + __popcll(mid & ((1ull << lane) - 1))] = r;
-    }
-    if (big) {
-      uint32_t at = 0;
-      if (lane == 0) at = atomicAdd(nlist + 64, (uint32_t)__popcll(big));
-      at = __shfl(at, 0);
-      if (big >> lane & 1) lists[R + at + __popcll(big & ((1ull << lane) - 1))] = r;
-    }
     for (unsigned long long m = small; m; m &= m - 1) {
       const int src = __ffsll((long long)m) - 1;
       const uint64_t rb = __shfl(b, src);
       const uint32_t rl = (uint32_t)__shfl(len, src);
-      uint32_t v = lane < rl ? out[rb + lane] : NONE;
+      uint32_t v = lane < rl ? tmp[rb + lane] : NONE;
 #pragma unroll
       for (uint32_t k = 2; k <= 64; k <<= 1) {
 #pragma unroll
-        for (uint32_t j = k >> 1; j > 0; j >>= 1) {
-          const uint32_t u = __shfl_xor(v, (int)j);
-          const bool up = (lane & k) == 0, lower = (lane & j) == 0;
-          v = (lower == up) ? min(v, u) : max(v, u);
-        }
+        for (uint32_t j = k >> 1; j > 0; j >>= 1) v = bitonic_xor(v, lane, k, j);
       }
-      if (lane < rl) out[rb + lane] = v;
+      if (lane < rl) {
+        dst[rb + lane] = v;
+        cl.bit(g * 64 + (uint32_t)src, v);
+      }
     }
   }
 }
 
-// One workgroup per listed row of 65..4096 entries: bitonic sort in LDS, padded to a power of two.
-__global__ void __launch_bounds__(BLOCK) k_rows_lds(const uint64_t* __restrict__ ptr, uint32_t* __restrict__ out,
-                                                    const uint32_t* __restrict__ lists,
-                                                    const uint32_t* __restrict__ nlist) {
+// One row of 65..4096 entries padded to P = 256·E: lane l of wave w holds the elements
+// e = (w + 4i)·64 + l, i < E.  Network stages whose partner is within 64 elements run on
+// registers with shuffles; the others (j >= 64) exchange through LDS (two barriers).
+template <uint32_t E>
+__device__ __forceinline__ void sort_row(const uint32_t* __restrict__ src, uint32_t* __restrict__ dst, uint32_t len,
+                                         uint32_t* s, const Clear& cl, uint32_t r) {
+  const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
+  constexpr uint32_t P = 256 * E;
+  uint32_t v[E];
+#pragma unroll
+  for (uint32_t i = 0; i < E; ++i) {
+    const uint32_t e = (w + 4 * i) * 64 + lane;
+    v[i] = e < len ? src[e] : NONE;
+  }
+#pragma unroll
+  for (uint32_t k = 2; k <= P; k <<= 1) {
+#pragma unroll
+    for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+      if (j >= 64) {
+        lds_barrier();
+#pragma unroll
+        for (uint32_t i = 0; i < E; ++i) s[(w + 4 * i) * 64 + lane] = v[i];
+        lds_barrier();
+#pragma unroll
+        for (uint32_t i = 0; i < E; ++i) {
+          const uint32_t e = (w + 4 * i) * 64 + lane, p = e ^ j;
+          const uint32_t u = s[p];
+          const bool up = (e & k) == 0, lower = e < p;
+          v[i] = (lower == up) ? min(v[i], u) : max(v[i], u);
+        }
+      } else {
+#pragma unroll
+        for (uint32_t i = 0; i < E; ++i) v[i] = bitonic_xor(v[i], (w + 4 * i) * 64 + lane, k, j);
+      }
+    }
+  }
+#pragma unroll
+  for (uint32_t i = 0; i < E; ++i) {
+    const uint32_t e = (w + 4 * i) * 64 + lane;
+    if (e < len) {
+      dst[e] = v[i];
+      cl.bit(r, v[i]);
+    }
+  }
+}
+
+__global__ void __launch_bounds__(BLOCK) k_rows_lds(const uint64_t* __restrict__ ptr, const uint32_t* __restrict__ tmp,
+                                                    uint32_t* __restrict__ dst, const uint32_t* __restrict__ lists,
+                                                    const uint32_t* __restrict__ nlist, Clear cl) {
   __shared__ uint32_t s[LDS_MAX];
-  const uint32_t nrows = *nlist, tid = threadIdx.x;
+  const uint32_t nrows = *nlist;
   for (uint32_t q = blockIdx.x; q < nrows; q += gridDim.x) {
     const uint32_t r = lists[q];
     const uint64_t b = ptr[r];
     const uint32_t len = (uint32_t)(ptr[r + 1] - b);
-    uint32_t P = 128;
-    while (P < len) P <<= 1;
-    for (uint32_t i = tid; i < P; i += BLOCK) s[i] = i < len ? out[b + i] : NONE;
-    __syncthreads();
-    for (uint32_t k = 2; k <= P; k <<= 1) {
-      for (uint32_t j = k >> 1; j > 0; j >>= 1) {
-        for (uint32_t t = tid; t < P / 2; t += BLOCK) {
-          const uint32_t i = 2 * t - (t & (j - 1)), p = i + j;
-          const uint32_t a = s[i], c = s[p];
-          if ((a > c) == ((i & k) == 0)) {
-            s[i] = c;
-            s[p] = a;
-          }
-        }
-        __syncthreads();
-      }
-    }
-    for (uint32_t i = tid; i < len; i += BLOCK) out[b + i] = s[i];
-    __syncthreads();
+    if (len <= 256)
+      sort_row<1>(tmp + b, dst + b, len, s, cl, r);
+    else if (len <= 512)
+      sort_row<2>(tmp + b, dst + b, len, s, cl, r);
+    else if (len <= 1024)
+      sort_row<4>(tmp + b, dst + b, len, s, cl, r);
+    else if (len <= 2048)
+      sort_row<8>(tmp + b, dst + b, len, s, cl, r);
+    else
+      sort_row<16>(tmp + b, dst + b, len, s, cl, r);
+    lds_barrier();  // s is reused by the next row
   }
 }
 
 // Long rows with a bit matrix: the row's set bits are its entries, already in column order.
 // One workgroup per row: popcounts of 256 words, block scan, then each lane writes its
 // word's columns.
-__global__ void __launch_bounds__(BLOCK) k_rows_bits(const uint64_t* __restrict__ ptr, uint32_t* __restrict__ out,
+__global__ void __launch_bounds__(BLOCK) k_rows_bits(const uint64_t* __restrict__ ptr, uint32_t* __restrict__ dst,
                                                      const uint32_t* __restrict__ lists,
                                                      const uint32_t* __restrict__ nlist, uint32_t R, uint32_t lo,
-                                                     const uint32_t* __restrict__ bits, uint64_t W) {
+                                                     uint32_t* __restrict__ bits, uint64_t W, bool clear) {
   __shared__ uint32_t wsum[BLOCK / 64];
   const uint32_t nrows = nlist[64], tid = threadIdx.x, lane = __lane_id(), wv = tid >> 6;
   for (uint32_t q = blockIdx.x; q < nrows; q += gridDim.x) {
     const uint32_t r = lists[R + q];
-    const uint32_t* __restrict__ row = bits + (uint64_t)(r + lo) * W;
+    uint32_t* __restrict__ row = bits + (uint64_t)(r + lo) * W;
     uint64_t at = ptr[r];
     for (uint64_t w0 = 0; w0 < W; w0 += BLOCK) {
       const uint64_t w = w0 + tid;
       uint32_t word = w < W ? row[w] : 0u;
+      if (clear && word) row[w] = 0u;
       const uint32_t c = (uint32_t)__popc(word);
       uint32_t inc = c;
 #pragma unroll
@@ -194,7 +334,7 @@ __global__ void __launch_bounds__(BLOCK) k_rows_bits(const uint64_t* __restrict_
       uint64_t o = at + before + inc - c;
       while (word) {
         const uint32_t bit = (uint32_t)__ffs(word) - 1;
-        out[o++] = (uint32_t)(w * 32 + bit);
+        dst[o++] = (uint32_t)(w * 32 + bit);
         word &= word - 1;
       }
       at += total;
@@ -203,19 +343,19 @@ __global__ void __launch_bounds__(BLOCK) k_rows_bits(const uint64_t* __restrict_
   }
 }
 
-// Long rows without a bit matrix: bitonic sort in place in global memory, one workgroup per
-// row.  The network only ever puts the smaller value at the lower index (the first merge step
-// of each stage compares mirrored positions), so positions past the row act as +inf and are
-// never touched.
-__global__ void __launch_bounds__(BLOCK) k_rows_global(const uint64_t* __restrict__ ptr, uint32_t* out,
-                                                       const uint32_t* __restrict__ lists,
+// Long rows without a bit matrix: bitonic sort in place in tmp, one workgroup per row, then
+// the row to dst.  The network only ever puts the smaller value at the lower index (the first
+// merge step of each stage compares mirrored positions), so positions past the row act as
+// +inf and are never touched.
+__global__ void __launch_bounds__(BLOCK) k_rows_global(const uint64_t* __restrict__ ptr, uint32_t* tmp,
+                                                       uint32_t* __restrict__ dst, const uint32_t* __restrict__ lists,
                                                        const uint32_t* __restrict__ nlist, uint32_t R) {
   const uint32_t nrows = nlist[64], tid = threadIdx.x;
   for (uint32_t q = blockIdx.x; q < nrows; q += gridDim.x) {
     const uint32_t r = lists[R + q];
     const uint64_t b = ptr[r];
     const uint64_t len = ptr[r + 1] - b;
-    uint32_t* v = out + b;
+    uint32_t* v = tmp + b;
     uint64_t P = 1;
     while (P < len) P <<= 1;
     for (uint64_t k = 2; k <= P; k <<= 1) {
@@ -240,27 +380,26 @@ __global__ void __launch_bounds__(BLOCK) k_rows_global(const uint64_t* __restric
         __syncthreads();
       }
     }
+    for (uint64_t i = tid; i < len; i += BLOCK) dst[b + i] = v[i];
+    __syncthreads();
   }
 }
-
-struct Widen {
-  __host__ __device__ uint64_t operator()(uint32_t v) const { return v; }
-};
 
 }  // namespace
 
 void Scratch::release() {
-  for (void* p : {(void*)rank, (void*)cnt, (void*)lists, (void*)nlist, cub})
+  for (void* p : {(void*)rank, (void*)tmp, (void*)cnt, (void*)lists, (void*)nlist, (void*)tile})
     if (p) (void)hipFree(p);
-  rank = cnt = lists = nlist = nullptr;
-  cub = nullptr;
-  rank_cap = cnt_cap = list_cap = 0;
-  cub_bytes = 0;
+  rank = tmp = cnt = lists = nlist = nullptr;
+  tile = nullptr;
+  rank_cap = tmp_cap = cnt_cap = list_cap = tile_cap = 0;
 }
 
-void build(hipStream_t s, Scratch& sc, const uint32_t* rows, const uint32_t* vals, uint64_t n, uint32_t row_lo,
-           uint32_t R, const uint32_t* keymap, uint64_t* ptr, uint32_t* out, const uint32_t* bits, uint64_t W) {
+void build_prep(hipStream_t s, Scratch& sc, const uint32_t* rows, const uint32_t* vals, uint64_t n, uint32_t row_lo,
+                uint32_t R, const uint32_t* keymap, uint64_t* ptr, uint32_t* dst, uint32_t* bits, uint64_t W,
+                bool clear) {
   ensure(sc.rank, sc.rank_cap, n);
+  ensure(sc.tmp, sc.tmp_cap, n);
   ensure(sc.cnt, sc.cnt_cap, (uint64_t)R + 1);
   ensure(sc.lists, sc.list_cap, 2 * (uint64_t)R + 2);
   if (!sc.nlist) RCHK(hipMalloc((void**)&sc.nlist, 128 * sizeof(uint32_t)));
@@ -270,30 +409,46 @@ void build(hipStream_t s, Scratch& sc, const uint32_t* rows, const uint32_t* val
     hipLaunchKernelGGL(k_rows_count, dim3(grid(n, 2048)), dim3(BLOCK), 0, s, rows, n, row_lo, sc.cnt, sc.rank);
     RCHK(hipGetLastError());
   }
-  hipcub::TransformInputIterator<uint64_t, Widen, const uint32_t*> in(sc.cnt, Widen{});
-  size_t bytes = 0;
-  RCHK(hipcub::DeviceScan::ExclusiveSum(nullptr, bytes, in, ptr, (int)(R + 1), s));
-  if (bytes > sc.cub_bytes) {
-    if (sc.cub) (void)hipFree(sc.cub);
-    sc.cub = nullptr;
-    sc.cub_bytes = bytes;
-    RCHK(hipMalloc(&sc.cub, bytes));
-  }
-  RCHK(hipcub::DeviceScan::ExclusiveSum(sc.cub, bytes, in, ptr, (int)(R + 1), s));
+  const uint32_t tiles = (uint32_t)(((uint64_t)R + 1 + SCAN_TILE - 1) / SCAN_TILE);
+  ensure(sc.tile, sc.tile_cap, tiles);
+  hipLaunchKernelGGL(k_rows_tiles, dim3(tiles), dim3(BLOCK), 0, s, sc.cnt, R + 1, sc.tile);
+  RCHK(hipGetLastError());
+  hipLaunchKernelGGL(k_rows_tile_scan, dim3(1), dim3(BLOCK), 0, s, sc.tile, tiles);
+  RCHK(hipGetLastError());
+  hipLaunchKernelGGL(k_rows_offsets, dim3(tiles), dim3(BLOCK), 0, s, sc.cnt, R, sc.tile, ptr, sc.lists, sc.nlist);
+  RCHK(hipGetLastError());
+  sc.n = n;
+  sc.R = R;
+  sc.bits = bits != nullptr;
   if (!n) return;
   hipLaunchKernelGGL(k_rows_scatter, dim3(grid(n, 2048)), dim3(BLOCK), 0, s, rows, vals, n, row_lo, ptr, sc.rank,
-                     keymap, out);
+                     keymap, sc.tmp);
   RCHK(hipGetLastError());
-  hipLaunchKernelGGL(k_rows_small, dim3(grid(((uint64_t)R + 63) / 64 * 64, 2048)), dim3(BLOCK), 0, s, ptr, R, out,
-                     sc.lists, sc.nlist);
+  if (bits) {
+    hipLaunchKernelGGL(k_rows_bits, dim3(512), dim3(BLOCK), 0, s, ptr, dst, sc.lists, sc.nlist, R, row_lo, bits, W,
+                       clear);
+    RCHK(hipGetLastError());
+  }
+}
+
+void build_sort(hipStream_t s, Scratch& sc, const uint64_t* ptr, uint32_t* dst, Clear cl) {
+  if (!sc.n) return;
+  const uint32_t R = sc.R;
+  hipLaunchKernelGGL(k_rows_small, dim3(grid(((uint64_t)R + 63) / 64 * 64, 2048)), dim3(BLOCK), 0, s, ptr, R, sc.tmp,
+                     dst, cl);
   RCHK(hipGetLastError());
-  hipLaunchKernelGGL(k_rows_lds, dim3(2048), dim3(BLOCK), 0, s, ptr, out, sc.lists, sc.nlist);
+  hipLaunchKernelGGL(k_rows_lds, dim3(1024), dim3(BLOCK), 0, s, ptr, sc.tmp, dst, sc.lists, sc.nlist, cl);
   RCHK(hipGetLastError());
-  if (bits)
-    hipLaunchKernelGGL(k_rows_bits, dim3(512), dim3(BLOCK), 0, s, ptr, out, sc.lists, sc.nlist, R, row_lo, bits, W);
-  else
-    hipLaunchKernelGGL(k_rows_global, dim3(512), dim3(BLOCK), 0, s, ptr, out, sc.lists, sc.nlist, R);
-  RCHK(hipGetLastError());
+  if (!sc.bits) {
+    hipLaunchKernelGGL(k_rows_global, dim3(512), dim3(BLOCK), 0, s, ptr, sc.tmp, dst, sc.lists, sc.nlist, R);
+    RCHK(hipGetLastError());
+  }
+}
+
+void build(hipStream_t s, Scratch& sc, const uint32_t* rows, const uint32_t* vals, uint64_t n, uint32_t row_lo,
+           uint32_t R, const uint32_t* keymap, uint64_t* ptr, uint32_t* dst, uint32_t* bits, uint64_t W) {
+  build_prep(s, sc, rows, vals, n, row_lo, R, keymap, ptr, dst, bits, W, false);
+  build_sort(s, sc, ptr, dst, Clear{});
 }
 
 }  // namespace elrows

@@ -21,6 +21,7 @@ LIB_PATH = os.path.join(_HERE, "lib", "libel_gpu.so")
 EL_OK, EL_EINVAL, EL_ENOMEM, EL_EHIP, EL_ESTATE, EL_ERANGE = 0, -1, -2, -3, -4, -5
 LAYOUT_X_TO_B, LAYOUT_B_TO_X = 0, 1
 EL_FLAG_COMPAT_DISTEL_CHAIN = 0x1  # el_config.flags: hazard H2 reproduced (include/el_gpu.h)
+EL_RESULT_RELEASE = 0x1  # el_result.flags: the state is released behind the copy-back
 
 # work phases (el_kernel); "kernel:role" where several phases share one launch
 KERNEL_NAMES = ["k_expand:s", "k_expand:l", "k_jobs", "k_expand:a", "k_commit:s", "k_commit:l", "k_commit:a",
@@ -89,7 +90,7 @@ class _ElKernelStat(C.Structure):
 
 class _ElResult(C.Structure):
     _fields_ = [("row_lo", C.c_uint32), ("row_hi", C.c_uint32), ("n_facts", C.c_uint64), ("n_links", C.c_uint64),
-                ("n_pairs", C.c_uint32), ("s_ptr", C.POINTER(C.c_uint64)), ("s_val", _u32p), ("s_cap", C.c_uint64),
+                ("n_pairs", C.c_uint32), ("flags", C.c_uint32), ("s_ptr", C.POINTER(C.c_uint64)), ("s_val", _u32p), ("s_cap", C.c_uint64),
                 ("l_ptr", C.POINTER(C.c_uint64)), ("l_pair", _u32p), ("l_cap", C.c_uint64)]
 
 
@@ -428,12 +429,15 @@ class Engine:
         return r
 
     def copy_result(self, out: Optional[Result] = None, pinned: bool = True, facts: bool = True,
-                    links: bool = True) -> Result:
-        """Result copy-back into ``out`` (reused across calls; page-locked buffers by default)."""
+                    links: bool = True, release: bool = False) -> Result:
+        """Result copy-back into ``out`` (reused across calls; page-locked buffers by default).
+        release: EL_RESULT_RELEASE — the next init()'s reset runs behind the copy-back; the engine
+        has no state until init()."""
         info = self.result_info()
         out = out or Result()
         out._fit(info.row_hi - info.row_lo, info.n_facts if facts else 0, info.n_links if links else 0, pinned)
         r = _ElResult()
+        r.flags = EL_RESULT_RELEASE if release else 0
         if facts:
             r.s_ptr = out.s_ptr.ctypes.data_as(C.POINTER(C.c_uint64))
             r.s_val = out.s_val.ctypes.data_as(_u32p)

@@ -269,13 +269,19 @@ int el_superstep_trace(el_ctx* ctx, uint64_t* ds, uint64_t* dl, uint64_t* da, si
  *            (role, filler) = el_pair_table()[q], so each row is in (role, filler) order.
  * Every row is present (S(X) includes X itself and ⊤; ⊥ / datatype rows are the caller's to
  * skip, as ResultRearranger does).  Buffers are caller-owned; a NULL pointer skips that array.
- * Buffers from el_host_alloc are page-locked: the DMA engines write them directly while the
- * next rows are still being built on the device. */
+ * Buffers from el_host_alloc are page-locked: the row sorts write the sorted rows into them
+ * straight over PCIe (no device staging copy).
+ * flags: EL_RESULT_RELEASE = the caller is done with this classification: once the state has
+ * been read, the next el_init's reset runs beside the rest of the copy-back, and the context
+ * has no state (EL_ESTATE) until el_init. */
+#define EL_RESULT_RELEASE 0x1u
+#define EL_RESULT_FLAGS_KNOWN (EL_RESULT_RELEASE)
 typedef struct el_result {
   uint32_t row_lo, row_hi;  /* out: rows of this context (whole ontology: 0, n_concepts) */
   uint64_t n_facts;         /* out: Σ_X |S(X)| over the rows */
   uint64_t n_links;         /* out: links (X, r, Y) with X in the rows */
   uint32_t n_pairs;         /* out: entries of el_pair_table */
+  uint32_t flags;           /* in: EL_RESULT_* */
   uint64_t* s_ptr;          /* in: row_hi - row_lo + 1 entries, or NULL */
   uint32_t* s_val;          /* in: s_cap entries (>= n_facts), or NULL */
   uint64_t s_cap;

@@ -142,3 +142,28 @@ def test_copy_result_empty():
     assert res.n_facts == 2 and res.n_links == 0
     assert res.s_ptr.tolist() == [0, 1, 2] and res.s_val[:2].tolist() == [0, 1]
     eng.close()
+
+
+def test_copy_result_release(oracle_lib):
+    """EL_RESULT_RELEASE: the copy is the closure, the engine then has no state until init(),
+    and the reset done behind the copy-back leaves a clean start (same closure again)."""
+    ax = generators.workload("g1", scale=0.3)
+    o = oracle_lib.saturate(ax, 0)
+    eng = engine.Engine(device=0)
+    eng.load(ax)
+    res = engine.Result()
+    for _ in range(3):
+        eng.init()
+        eng.saturate()
+        eng.copy_result(res, release=True)
+        x, a = res.facts()
+        ox, oa = o.facts()
+        assert np.array_equal(x, ox) and np.array_equal(a, oa)
+        with pytest.raises(engine.ElError):
+            eng.subsumers(2)
+        with pytest.raises(engine.ElError):
+            eng.saturate()
+    eng.init()
+    eng.saturate()
+    _check_result(eng, o, ax)
+    eng.close()
