@@ -46,7 +46,8 @@ WORKLOAD_DESC = {
     "g2": "G2 NCI-like synthetic (70k classes, 60 roles, tree-like, no chains) — BASELINE configs[1]",
     "g3": "G3 SNOMED-shaped synthetic (300k classes, 60 roles, 0.3N definitions, 2 chains + 3 transitive) "
           "— BASELINE configs[2]",
-    "g5": "G5 role-heavy synthetic (100k classes, 200 roles, depth-20 chains, hub fillers)",
+    "g3x": "G3X = G3 + 1% sibling disjointness (⊥), domains on 8 roles, ranges on 3",
+    "g5": "G5 role-heavy synthetic (100k classes, 200 roles, depth-20 chains, hub fillers) — BASELINE configs[4]",
 }
 
 

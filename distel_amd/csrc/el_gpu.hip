@@ -2081,6 +2081,7 @@ struct el_ctx {
   uint32_t *cs_x = nullptr, *cs_a = nullptr, *cl_x = nullptr, *cl_p = nullptr, *ca_y = nullptr,
            *ca_c = nullptr;
   uint64_t cs_cap = 0, cl_cap = 0, ca_cap = 0;
+  uint32_t max_rng = 0;  // most ranges of one role: activation candidates per new link
   uint4* jobs = nullptr;
   uint64_t job_cap = 0;
   DCounters* ctr = nullptr;
@@ -2609,7 +2610,12 @@ void el_ctx::alloc_state() {
   if (need_succ) SC.alloc((uint32_t)N, part() ? (uint64_t)part_count * xcap : cl_cap, cap_sc.empty() ? nullptr : &cap_sc);
   if (use_props) PP.alloc((uint32_t)P, cp_cap + remote_bound(), cap_pp.empty() ? nullptr : &cap_pp);
   HIPCHK(hipHostMalloc((void**)&pin_word, sizeof(uint32_t), hipHostMallocDefault));
+  // range activation candidates: a new link (X, r, Y) emits one (Y, C) per C ∈ rng(r), so a
+  // step's links bound them; an undersized queue would re-run a whole generation
   ca_cap = 1u << 12;
+  max_rng = 0;
+  for (uint32_t r = 0; r < hx.R && !hx.rng.a.empty(); ++r) max_rng = std::max(max_rng, hx.rng.ptr[r + 1] - hx.rng.ptr[r]);
+  ca_cap = std::max<uint64_t>(ca_cap, next_pow2(cl_cap * max_rng));
   cs_x = dalloc<uint32_t>(cs_cap);
   cs_a = dalloc<uint32_t>(cs_cap);
   // the first superstep emits the whole told closure of every concept (its init fact X ∈ S(X))
@@ -2926,9 +2932,18 @@ bool el_ctx::superstep(uint32_t mask, uint64_t sb, uint64_t se, uint64_t lb, uin
     regrow2(hc.cand_l, cl_cap, cl_x, cl_p);
     regrow2(hc.cand_a, ca_cap, ca_y, ca_c);
     regrow2(hc.cand_p, cp_cap, cp_p, cp_b);
+    if (max_rng && cl_cap * max_rng > ca_cap)  // activation candidates follow the link queue
+      regrow2((uint32_t)std::min<uint64_t>(cl_cap * max_rng / 2, 0xffffffffu), ca_cap, ca_y, ca_c);
     PR.set_ovq(cl_cap);  // overflow queues hold one step's appends
     SC.set_ovq(part() ? (uint64_t)part_count * xcap : cl_cap);
     PP.set_ovq(cp_cap + remote_bound());
+    // fan-out jobs: about one per trigger at most (G5 step 1: 4.4 M new links -> 1.7 M jobs)
+    if (const uint64_t want = std::min<uint64_t>(next_trig, 1ull << 26); want > job_cap && !small_queues) {
+      sync();
+      job_cap = next_pow2(want);
+      dfree(jobs);
+      jobs = dalloc<uint4>(job_cap);
+    }
     if (2ull * hc.jobs > job_cap) {
       sync();
       overflow |= hc.jobs > job_cap;
@@ -2937,6 +2952,7 @@ bool el_ctx::superstep(uint32_t mask, uint64_t sb, uint64_t se, uint64_t lb, uin
       jobs = dalloc<uint4>(job_cap);
     }
     if (!overflow) break;
+    if (trace_cands) fprintf(stderr, "step re-run after a queue overflow (attempt %d)\n", attempt + 1);
   }
   return s_count > s0 || l_count > l0 || a_count > a0 || p_count > p0;
 }

@@ -103,9 +103,13 @@ def shaped(seed: int, n: int, n_roles: int, depth: int, mean_parents: float, ex_
            zipf_s: float = 1.1, transitive: Sequence[int] = (), subroles: Sequence[Tuple[int, int]] = (),
            chains: Sequence[Tuple[int, int, int]] = (), domains: Sequence[Tuple[int, int]] = (),
            role_weights: Optional[Sequence[float]] = None, lift: int = 1, growth: float = 1.45,
-           hubs: int = 0, hub_frac: float = 0.0) -> Axioms:
+           hubs: int = 0, hub_frac: float = 0.0, ranges: Sequence[Tuple[int, int]] = (),
+           disjoint_frac: float = 0.0, disjoint_mid: int = 0) -> Axioms:
     """Generic shaped generator; ids: 0 ⊥, 1 ⊤, 2..n+1 taxonomy classes, then fresh
-    definition classes F.  ``domains`` are (role, local class index)."""
+    definition classes F.  ``domains`` / ``ranges`` are (role, local class index).
+    ``disjoint_frac``·n disjointness axioms A ⊓ B ⊑ ⊥ between neighbouring classes of one
+    level (siblings, as DisjointClasses usually are), drawn from the two deepest levels, plus
+    ``disjoint_mid`` such pairs four levels up (classes that are fillers: ⊥ crosses links)."""
     rng = np.random.default_rng(seed)
     m = n
     child, parent, level, b = _taxonomy(rng, m, depth, mean_parents, growth)
@@ -155,6 +159,17 @@ def shaped(seed: int, n: int, n_roles: int, depth: int, mean_parents: float, ex_
     conj_ptr = np.arange(0, 2 * nd + 1, 2)
     conj_b = da + base
     N = base + m + nd
+    conj_ptr = conj_ptr.astype(np.int64)
+    if disjoint_frac > 0:
+        deep = np.nonzero((level >= depth - 2) & (np.arange(m) + 1 < m))[0]  # the two deepest levels
+        deep = deep[level[np.minimum(deep + 1, m - 1)] == level[deep]]  # B = A + 1 on the same level
+        da_ = rng.choice(deep, size=min(int(disjoint_frac * m), deep.size), replace=False)
+        mid = np.nonzero((level == depth - 4) & (np.arange(m) + 1 < m))[0]
+        mid = mid[level[np.minimum(mid + 1, m - 1)] == level[mid]]
+        da_ = np.concatenate([da_, rng.choice(mid, size=min(disjoint_mid, mid.size), replace=False)])
+        conj_ops = np.concatenate([conj_ops, np.stack([da_ + base, da_ + 1 + base], 1).reshape(-1)])
+        conj_ptr = np.concatenate([conj_ptr, conj_ptr[-1] + 2 * np.arange(1, da_.size + 1)])
+        conj_b = np.concatenate([conj_b, np.zeros(da_.size, dtype=np.int64)])
     ax = Axioms(
         n_concepts=int(N), n_roles=int(n_roles), kind=np.zeros(N, dtype=np.uint8),
         sub=np.ascontiguousarray(np.concatenate(sub).astype(np.uint32)),
@@ -164,7 +179,7 @@ def shaped(seed: int, n: int, n_roles: int, depth: int, mean_parents: float, ex_
         subrole=np.asarray(list(subroles), dtype=np.uint32).reshape(-1, 2),
         chain=np.asarray([(t, t, t) for t in transitive] + list(chains), dtype=np.uint32).reshape(-1, 3),
         domain=np.asarray([(rr, c + base) for rr, c in domains], dtype=np.uint32).reshape(-1, 2),
-        range=np.zeros((0, 2), dtype=np.uint32))
+        range=np.asarray([(rr, c + base) for rr, c in ranges], dtype=np.uint32).reshape(-1, 2))
     ax.validate()
     return ax
 
@@ -195,6 +210,18 @@ def g3_snomed(seed: int = 0x5C7, n: int = 300_000) -> Axioms:
                   growth=1.4)
 
 
+def g3_bottom_domain_range(seed: int = 0x5C7, n: int = 300_000) -> Axioms:
+    """G3 with the rules G3 never trips: 1 % disjointness axioms A ⊓ B ⊑ ⊥ between sibling
+    classes (⊥, TypeBottomAxiomProcessorBase.java:62-123), domains on 8 roles and ranges on 3
+    (RolePairHandler.java:456-491; ranges with DistEL's semantics, hazard H1)."""
+    sub = [(10 + i, 50 + i) for i in range(10)]
+    domains = [(r, 1 + r % 7) for r in (0, 3, 5, 8, 12, 20, 33, 44)]
+    ranges = [(r, 2 + r % 5) for r in (6, 17, 25)]
+    return shaped(seed, n, n_roles=60, depth=24, mean_parents=1.7, ex_frac=0.8, def_frac=0.3, zipf_s=1.1,
+                  transitive=[57, 58, 59], subroles=sub, chains=[(20, 57, 20), (21, 58, 21)], lift=2,
+                  growth=1.4, domains=domains, ranges=ranges, disjoint_frac=0.01, disjoint_mid=30)
+
+
 def g4_snomed_x(copies: int = 8, seed: int = 0x5C7, n: int = 300_000) -> Axioms:
     """G4: ``copies`` disjoint copies of G3 (OntologyMultiplier semantics)."""
     return replicate(g3_snomed(seed, n), copies)
@@ -214,6 +241,7 @@ WORKLOADS = {
     "g1": g1_go,
     "g2": g2_nci,
     "g3": g3_snomed,
+    "g3x": g3_bottom_domain_range,
     "g5": g5_role_heavy,
 }
 
@@ -223,7 +251,7 @@ def workload(name: str, scale: float = 1.0) -> Axioms:
     if name == "g4":
         return g4_snomed_x(n=int(300_000 * scale))
     fn = WORKLOADS[name]
-    default_n = {"g1": 20_000, "g2": 70_000, "g3": 300_000, "g5": 100_000}[name]
+    default_n = {"g1": 20_000, "g2": 70_000, "g3": 300_000, "g3x": 300_000, "g5": 100_000}[name]
     return fn(n=max(64, int(default_n * scale)))
 
 
