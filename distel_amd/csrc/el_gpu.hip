@@ -124,6 +124,9 @@ struct DIndex {
   uint32_t has_bot;  // some axiom concludes ⊥ (or ∃r.⊥): else ⊥ ∈ S(Y) only for Y = ⊥, no link reaches ⊥
   // row partition (el_config.exchange != NONE): this context owns rows [lo, hi)
   uint32_t lo, hi;
+  // bit-row columns: ⊥, ⊤, then the concepts [c_lo, c_hi) — every concept an owned row can
+  // hold (el_ctx::column_window; the whole ontology: 2, N, i.e. column = concept id)
+  uint32_t c_lo, c_hi;
   uint32_t part;               // 1 = partitioned protocol (oracle/partition_model.py)
   const uint8_t* role_chs;     // r -> r is the second role of some chain (its links are exchanged)
 };
@@ -353,8 +356,14 @@ __device__ __forceinline__ void gap_append(const DGap& g, uint32_t row, uint32_t
   }
 }
 
-__device__ __forceinline__ bool test_bit(const uint32_t* bits, uint64_t W, uint32_t x, uint32_t b) {
-  return (bits[(uint64_t)x * W + (b >> 5)] >> (b & 31u)) & 1u;
+// bit-row column of concept a, NONE when no owned row can hold a (outside the window)
+__device__ __forceinline__ uint32_t col_of(const DIndex& ix, uint32_t a) {
+  return a < 2u ? a : (a >= ix.c_lo && a < ix.c_hi ? a - ix.c_lo + 2u : NONE);
+}
+
+__device__ __forceinline__ bool test_bit(const DIndex& ix, const uint32_t* bits, uint32_t x, uint32_t b) {
+  const uint32_t c = col_of(ix, b);
+  return c != NONE && ((bits[(uint64_t)x * ix.W + (c >> 5)] >> (c & 31u)) & 1u);
 }
 
 __device__ __forceinline__ unsigned long long mix64(unsigned long long k) {
@@ -665,8 +674,10 @@ __global__ void k_init(DIndex ix, DState st, uint32_t lo, uint32_t hi, uint32_t 
       v = ix.told_b[t0 + c];
       ev.v[EL_EV_ENT]++;
     }
-    __hip_atomic_fetch_or(st.bits + (uint64_t)x * ix.W + (v >> 5), 1u << (v & 31u), __ATOMIC_RELAXED,
-                          __HIP_MEMORY_SCOPE_AGENT);
+    const uint32_t c = col_of(ix, v);  // (the told closure lies inside the window)
+    if (c != NONE)
+      __hip_atomic_fetch_or(st.bits + (uint64_t)x * ix.W + (c >> 5), 1u << (c & 31u), __ATOMIC_RELAXED,
+                            __HIP_MEMORY_SCOPE_AGENT);
     st.slog_x[base + k] = x;
     st.slog_a[base + k] = v;
     st.slog_f[base + k] = f;
@@ -742,7 +753,7 @@ __device__ void expand_s(const DIndex& ix, const DState& st, BlockQ& q, uint32_t
           B = ix.told_b[j];
           ev.v[EL_EV_ENT]++;
           ev.v[EL_EV_TEST]++;
-          nw = !test_bit(st.bits, ix.W, Xo, B);
+          nw = !test_bit(ix, st.bits, Xo, B);
         }
         emit_t(st, q, nw, Xo, B, ev);
       });
@@ -760,7 +771,7 @@ __device__ void expand_s(const DIndex& ix, const DState& st, BlockQ& q, uint32_t
           ev.v[EL_EV_ENT]++;
           if (op == A) continue;
           ev.v[EL_EV_TEST]++;
-          if (!test_bit(st.bits, ix.W, X, op)) {
+          if (!test_bit(ix, st.bits, X, op)) {
             ok = false;
             break;
           }
@@ -770,7 +781,7 @@ __device__ void expand_s(const DIndex& ix, const DState& st, BlockQ& q, uint32_t
         if (ok) {
           ev.v[EL_EV_ENT]++;
           ev.v[EL_EV_TEST]++;
-          nw = !test_bit(st.bits, ix.W, X, B);
+          nw = !test_bit(ix, st.bits, X, B);
         }
         emit_s(st, q, nw, X, B, ev);
       }
@@ -852,7 +863,7 @@ __device__ void expand_s(const DIndex& ix, const DState& st, BlockQ& q, uint32_t
           bool nw = false;
           if (hit) {
             ev.v[EL_EV_TEST]++;
-            nw = !test_bit(st.bits, ix.W, X, C);
+            nw = !test_bit(ix, st.bits, X, C);
           }
           emit_s(st, q, nw, X, C, ev);
         }
@@ -931,9 +942,9 @@ __device__ void expand_l(const DIndex& ix, const DState& st, BlockQ& q, uint32_t
       if ((mask & M_RBOT) && ix.has_bot && !ix.part) {  // ⊥ ∈ S(Y) => ⊥ ∈ S(X)  (partitioned: via propagations)
         ev.v[EL_EV_TEST]++;
         bool nw = false;
-        if (test_bit(st.bits, ix.W, Y, EL_BOTTOM)) {
+        if (test_bit(ix, st.bits, Y, EL_BOTTOM)) {
           ev.v[EL_EV_TEST]++;
-          nw = !test_bit(st.bits, ix.W, X, EL_BOTTOM);
+          nw = !test_bit(ix, st.bits, X, EL_BOTTOM);
         }
         emit_s(st, q, nw, X, EL_BOTTOM, ev);
       }
@@ -974,7 +985,7 @@ __device__ void expand_l(const DIndex& ix, const DState& st, BlockQ& q, uint32_t
           bool nw = false;
           if (ok) {
             ev.v[EL_EV_TEST]++;
-            nw = !test_bit(st.bits, ix.W, X, D);
+            nw = !test_bit(ix, st.bits, X, D);
           }
           emit_s(st, q, nw, X, D, ev);
         }
@@ -1039,7 +1050,7 @@ __global__ void k_jobs(DIndex ix, DState st) {
           xp = st.pr.val[k];
           ev.v[EL_EV_ENT]++;
           ev.v[EL_EV_TEST]++;
-          nw = !test_bit(st.bits, ix.W, xp, b);
+          nw = !test_bit(ix, st.bits, xp, b);
         }
         emit_s(st, q, nw, xp, b, ev);
       } else if (t == JOB_PRED_L) {  // preds(pq) × {pid_t}
@@ -1098,9 +1109,9 @@ __device__ void expand_a(const DIndex& ix, const DState& st, BlockQ& q, uint32_t
         const uint32_t Y = st.alog_y[k], C = st.alog_c[k];
         ev.v[EL_EV_TEST]++;
         bool nw = false;
-        if (test_bit(st.bits, ix.W, x, Y)) {
+        if (test_bit(ix, st.bits, x, Y)) {
           ev.v[EL_EV_TEST]++;
-          nw = !test_bit(st.bits, ix.W, x, C);
+          nw = !test_bit(ix, st.bits, x, C);
         }
         emit_s(st, q, nw, x, C, ev);
       }
@@ -1139,8 +1150,9 @@ __device__ void commit_s(const DIndex& ix, const DState& st, CommitLds& sm, uint
       a = qa[i];
       ev.v[EL_EV_TRIG]++;
       ev.v[EL_EV_RMW]++;
-      const uint32_t m = 1u << (a & 31u);
-      const uint32_t old = atomicOr(st.bits + (uint64_t)x * ix.W + (a >> 5), m);
+      const uint32_t c = col_of(ix, a);  // (every candidate of an owned row lies inside the window)
+      const uint32_t m = 1u << (c & 31u);
+      const uint32_t old = c != NONE ? atomicOr(st.bits + (uint64_t)x * ix.W + (c >> 5), m) : m;
       nw = (old & m) == 0;
       if (nw) ev.v[EL_EV_EMIT]++;
     }
@@ -1681,11 +1693,13 @@ __global__ void k_rehash(unsigned long long* t, unsigned long long mask, const u
 
 // el_init after a classification: only the words the fact log names can be non-zero, and
 // when the log is small next to the matrix, clearing those words beats streaming it all
-__global__ void k_clear_logged(uint32_t* bits_base, uint64_t W, const uint32_t* __restrict__ lx,
+__global__ void k_clear_logged(DIndex ix, uint32_t* bits_base, const uint32_t* __restrict__ lx,
                                const uint32_t* __restrict__ la, uint32_t n) {
   const uint32_t stride = gridDim.x * blockDim.x;
-  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
-    bits_base[(uint64_t)lx[i] * W + (la[i] >> 5)] = 0u;
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    const uint32_t c = col_of(ix, la[i]);
+    if (c != NONE) bits_base[(uint64_t)lx[i] * ix.W + (c >> 5)] = 0u;
+  }
 }
 
 // ---- gapped-CSR layout kernels (rare: initial layout, re-layout after an overflow)
@@ -2309,6 +2323,7 @@ struct el_ctx {
                           const uint8_t* keep = nullptr);
   void launch_gap_scan(const uint32_t* len, uint32_t R, uint32_t* start_out);
   std::string install_index(el::HostIndex&& h);
+  void column_window();
   void migrate_state(uint32_t N0, const std::vector<uint32_t>& pmap);
   void init_rows(uint32_t a, uint32_t b);
   el::AxiomStore store;  // the loaded axioms (increments append to them)
@@ -2334,7 +2349,6 @@ std::string el_ctx::install_index(el::HostIndex&& hnew) {
   d.N = h.N;
   d.R = h.R;
   d.P = h.P;
-  d.W = (h.N + 31) / 32;
   d.kind = up8(h.kind);
   d.told_ptr = up32(h.told.ptr);
   d.told_b = up32(h.told.a);
@@ -2442,8 +2456,71 @@ std::string el_ctx::install_index(el::HostIndex&& hnew) {
   }
   d.lo = lo;
   d.hi = hi;
+  column_window();
   d.part = part() ? 1u : 0u;
   return "";
+}
+
+// Bit-row columns of this context (SURVEY.md §7 "hard parts": columns compacted per
+// partition).  A whole-ontology context keeps column = concept id.  A partition keeps ⊥, ⊤
+// and the id window spanning every concept an owned row can ever hold: the closure of the
+// owned rows under the ways a concept enters S(X) — told supers (CR1), conjunctions with an
+// operand in it (CR2), the fillers of its existentials (CR4 reads S(Y) of a filler Y), the B
+// of ∃r.A ⊑ B for A in it (CR4), the domains and ranges of every role its links can carry
+// (CR3, CR5 supers, CR6 results), and the ranges of every role a link into it can carry
+// (DistEL's range rule puts them into each S(X) that holds the link's target).  For OntologyMultiplier copies aligned with the partition
+// (G4) the window is the rank's own copy: 8 × 19 GB for SNOMED×8 instead of 8 × 152 GB.
+void el_ctx::column_window() {
+  const el::HostIndex& h = hx;
+  uint32_t c_lo = 2, c_hi = std::max<uint32_t>(h.N, 2);
+  if (part()) {
+    std::vector<uint8_t> seen(h.N, 0), role_seen(h.R + 1, 0);
+    std::vector<uint32_t> st, rst;
+    auto add = [&](uint32_t a) {
+      if (!seen[a]) seen[a] = 1, st.push_back(a);
+    };
+    auto add_role = [&](uint32_t r) {
+      if (!role_seen[r]) role_seen[r] = 1, rst.push_back(r);
+    };
+    for (uint32_t x = lo; x < hi; ++x) add(x);
+    add(EL_BOTTOM);
+    add(EL_TOP);
+    while (!st.empty() || !rst.empty()) {
+      if (!st.empty()) {
+        const uint32_t a = st.back();
+        st.pop_back();
+        for (uint32_t j = h.told.ptr[a]; j < h.told.ptr[a + 1]; ++j) add(h.told.a[j]);
+        for (uint32_t j = h.cidx.ptr[a]; j < h.cidx.ptr[a + 1]; ++j) add(h.conj_b[h.cidx.a[j]]);
+        for (uint32_t j = h.exr.ptr[a]; j < h.exr.ptr[a + 1]; ++j) {
+          const uint32_t p = h.exr.a[j];
+          add(h.pair_y[p]);
+          add_role(h.pair_role[p]);
+          for (uint32_t k = h.psup.ptr[p]; k < h.psup.ptr[p + 1]; ++k) add_role(h.pair_role[h.psup.a[k]]);
+        }
+        for (uint32_t j = h.exl.ptr[a]; j < h.exl.ptr[a + 1]; ++j) add(h.exl.b[j]);
+        // range (DistEL, H1): a link into a — made on any rank — puts rng(r) into every S(X)
+        // holding a
+        for (uint32_t q = h.fp_ptr[a]; q < h.fp_ptr[a + 1]; ++q) {
+          const uint32_t r = h.pair_role[q];
+          for (uint32_t j = h.rng.ptr[r]; j < h.rng.ptr[r + 1]; ++j) add(h.rng.a[j]);
+        }
+        continue;
+      }
+      const uint32_t r = rst.back();
+      rst.pop_back();
+      for (uint32_t j = h.chf.ptr[r]; j < h.chf.ptr[r + 1]; ++j) add_role(h.chf.b[j]);
+      for (uint32_t j = h.chs.ptr[r]; j < h.chs.ptr[r + 1]; ++j) add_role(h.chs.b[j]);
+      for (uint32_t j = h.dom.ptr[r]; j < h.dom.ptr[r + 1]; ++j) add(h.dom.a[j]);
+      for (uint32_t j = h.rng.ptr[r]; j < h.rng.ptr[r + 1]; ++j) add(h.rng.a[j]);
+    }
+    c_lo = h.N, c_hi = 2;
+    for (uint32_t a = 2; a < h.N; ++a)
+      if (seen[a]) c_lo = std::min(c_lo, a), c_hi = a + 1;
+    if (c_hi <= c_lo) c_lo = c_hi = 2;
+  }
+  ix.c_lo = c_lo;
+  ix.c_hi = c_hi;
+  ix.W = (2 + (c_hi - c_lo) + 31) / 32;
 }
 
 void el_ctx::free_index() {
@@ -2508,7 +2585,7 @@ void el_ctx::free_state() {
 
 void el_ctx::alloc_state() {
   const uint64_t N = hx.N, P = hx.P;
-  W = (N + 31) / 32;
+  W = ix.W;  // bit-row words: ⊥, ⊤ and the column window
   bits = dalloc<uint32_t>((uint64_t)(hi - lo) * W);  // owned rows only
   bits_logged = false;
   slog_cap = std::max<uint64_t>(1u << 20, 8 * N);
@@ -2675,7 +2752,7 @@ void el_ctx::reset_device(hipStream_t stream, bool matrix_clear) {
   if (matrix_clear) {
     // the releasing copy-back's S-row sorts zero the matrix as they write the rows
   } else if (bits_logged && s_count * 64 < matrix_bytes) {  // one 64-B line per logged fact vs. the whole matrix
-    hipLaunchKernelGGL(k_clear_logged, dim3(grid_for(s_count)), dim3(BLOCK), 0, stream, dstate().bits, W, slog_x,
+    hipLaunchKernelGGL(k_clear_logged, dim3(grid_for(s_count)), dim3(BLOCK), 0, stream, ix, dstate().bits, slog_x,
                        slog_a, (uint32_t)s_count);
     HIPCHK(hipGetLastError());
   } else {
@@ -2774,11 +2851,13 @@ void el_ctx::build_rows(bool facts, hipStream_t s, uint64_t* ptr, uint32_t* dst,
   clear = clear && facts;
   if (half != 2) {
     if (facts)
-      elrows::build_prep(s, sc, slog_x, slog_a, s_count, lo, R, nullptr, ptr, dst, dstate().bits, W, clear);
+      elrows::build_prep(s, sc, slog_x, slog_a, s_count, lo, R, nullptr, ptr, dst,
+                         elrows::Clear{dstate().bits, W, lo, ix.c_lo, ix.c_hi}, clear);
     else
-      elrows::build_prep(s, sc, llog_x, llog_p, l_count, lo, R, pid_rank, ptr, dst, nullptr, 0, false);
+      elrows::build_prep(s, sc, llog_x, llog_p, l_count, lo, R, pid_rank, ptr, dst, elrows::Clear{}, false);
   }
-  if (half != 1) elrows::build_sort(s, sc, ptr, dst, clear ? elrows::Clear{dstate().bits, W, lo} : elrows::Clear{});
+  if (half != 1)
+    elrows::build_sort(s, sc, ptr, dst, clear ? elrows::Clear{dstate().bits, W, lo, ix.c_lo, ix.c_hi} : elrows::Clear{});
 }
 
 // Device-resident result rows (el_get_subsumers, el_copy_facts / links, el_export_result),

@@ -27,12 +27,15 @@
 
 namespace elrows {
 
-// A bit matrix to clear while the rows are written (the caller releases its state): row x at
-// bits + x·W, rows r of the build at x = r + lo.  bits = nullptr: nothing to clear.
+// The S bit matrix: row x at bits + x·W, rows r of the build at x = r + lo; columns ⊥, ⊤,
+// then the concepts [c_lo, c_hi) (column c >= 2 is concept c + c_lo - 2).  Read by the
+// long-row read-out; cleared as the rows are written when the caller releases its state.
+// bits = nullptr: no matrix.
 struct Clear {
   uint32_t* bits = nullptr;
   uint64_t W = 0;
   uint32_t lo = 0;
+  uint32_t c_lo = 2, c_hi = 0xffffffffu;
   __device__ void bit(uint32_t r, uint32_t v) const;
 };
 
@@ -57,19 +60,18 @@ struct Scratch {
 // Rows [row_lo, row_lo + R) of the log entries (rows[i], vals[i]), i < n (every rows[i] in
 // range).  ptr (device): R + 1 offsets; dst: n values, keymap ? keymap[v] : v, ascending in
 // each row (device memory, or host memory the device can write).
-// bits (optional): virtual base of a bit matrix holding exactly the log's entries, row x at
-// bits + x * W (values are column ids); long rows are then read from it instead of sorted.
+// matrix (optional): a bit matrix holding exactly the log's entries (values are concept ids);
+// long rows are then read from it instead of sorted.
 // Everything is enqueued on `s`; nothing is read back.  Throws std::runtime_error on a HIP error.
 void build(hipStream_t s, Scratch& sc, const uint32_t* rows, const uint32_t* vals, uint64_t n, uint32_t row_lo,
-           uint32_t R, const uint32_t* keymap, uint64_t* ptr, uint32_t* dst, uint32_t* bits, uint64_t W);
+           uint32_t R, const uint32_t* keymap, uint64_t* ptr, uint32_t* dst, Clear matrix);
 
 // build() in two halves: build_prep reads the log (and the bit matrix for the long rows);
 // build_sort reads only the scratch, so the log's owner may reuse its state once the prep's
 // work has completed on s.  clear (prep) / cl (sort): zero the matrix bits of the written
 // entries as they go, leaving the matrix empty (the caller is done with it).
 void build_prep(hipStream_t s, Scratch& sc, const uint32_t* rows, const uint32_t* vals, uint64_t n, uint32_t row_lo,
-                uint32_t R, const uint32_t* keymap, uint64_t* ptr, uint32_t* dst, uint32_t* bits, uint64_t W,
-                bool clear);
+                uint32_t R, const uint32_t* keymap, uint64_t* ptr, uint32_t* dst, Clear matrix, bool clear);
 void build_sort(hipStream_t s, Scratch& sc, const uint64_t* ptr, uint32_t* dst, Clear cl);
 
 }  // namespace elrows

@@ -88,7 +88,9 @@ __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(
 
 // Bit matrix the sorts clear as they write (EL_RESULT_RELEASE): row x at bits + x·W.
 __device__ void Clear::bit(uint32_t r, uint32_t v) const {
-  if (bits) bits[(uint64_t)(r + lo) * W + (v >> 5)] = 0u;
+  if (!bits) return;
+  const uint32_t c = v < 2u ? v : v - c_lo + 2u;  // (every value of a row lies in the window)
+  bits[(uint64_t)(r + lo) * W + (c >> 5)] = 0u;
 }
 
 namespace {
@@ -304,13 +306,14 @@ __global__ void __launch_bounds__(BLOCK) k_rows_lds(const uint64_t* __restrict__
 // word's columns.
 __global__ void __launch_bounds__(BLOCK) k_rows_bits(const uint64_t* __restrict__ ptr, uint32_t* __restrict__ dst,
                                                      const uint32_t* __restrict__ lists,
-                                                     const uint32_t* __restrict__ nlist, uint32_t R, uint32_t lo,
-                                                     uint32_t* __restrict__ bits, uint64_t W, bool clear) {
+                                                     const uint32_t* __restrict__ nlist, uint32_t R, Clear m,
+                                                     bool clear) {
   __shared__ uint32_t wsum[BLOCK / 64];
   const uint32_t nrows = nlist[64], tid = threadIdx.x, lane = __lane_id(), wv = tid >> 6;
   for (uint32_t q = blockIdx.x; q < nrows; q += gridDim.x) {
     const uint32_t r = lists[R + q];
-    uint32_t* __restrict__ row = bits + (uint64_t)(r + lo) * W;
+    const uint64_t W = m.W;
+    uint32_t* __restrict__ row = m.bits + (uint64_t)(r + m.lo) * W;
     uint64_t at = ptr[r];
     for (uint64_t w0 = 0; w0 < W; w0 += BLOCK) {
       const uint64_t w = w0 + tid;
@@ -334,7 +337,8 @@ __global__ void __launch_bounds__(BLOCK) k_rows_bits(const uint64_t* __restrict_
       uint64_t o = at + before + inc - c;
       while (word) {
         const uint32_t bit = (uint32_t)__ffs(word) - 1;
-        dst[o++] = (uint32_t)(w * 32 + bit);
+        const uint32_t c = (uint32_t)(w * 32 + bit);
+        dst[o++] = c < 2u ? c : c + m.c_lo - 2u;  // column -> concept
         word &= word - 1;
       }
       at += total;
@@ -396,8 +400,7 @@ void Scratch::release() {
 }
 
 void build_prep(hipStream_t s, Scratch& sc, const uint32_t* rows, const uint32_t* vals, uint64_t n, uint32_t row_lo,
-                uint32_t R, const uint32_t* keymap, uint64_t* ptr, uint32_t* dst, uint32_t* bits, uint64_t W,
-                bool clear) {
+                uint32_t R, const uint32_t* keymap, uint64_t* ptr, uint32_t* dst, Clear matrix, bool clear) {
   ensure(sc.rank, sc.rank_cap, n);
   ensure(sc.tmp, sc.tmp_cap, n);
   ensure(sc.cnt, sc.cnt_cap, (uint64_t)R + 1);
@@ -419,14 +422,13 @@ void build_prep(hipStream_t s, Scratch& sc, const uint32_t* rows, const uint32_t
   RCHK(hipGetLastError());
   sc.n = n;
   sc.R = R;
-  sc.bits = bits != nullptr;
+  sc.bits = matrix.bits != nullptr;
   if (!n) return;
   hipLaunchKernelGGL(k_rows_scatter, dim3(grid(n, 2048)), dim3(BLOCK), 0, s, rows, vals, n, row_lo, ptr, sc.rank,
                      keymap, sc.tmp);
   RCHK(hipGetLastError());
-  if (bits) {
-    hipLaunchKernelGGL(k_rows_bits, dim3(512), dim3(BLOCK), 0, s, ptr, dst, sc.lists, sc.nlist, R, row_lo, bits, W,
-                       clear);
+  if (matrix.bits) {
+    hipLaunchKernelGGL(k_rows_bits, dim3(512), dim3(BLOCK), 0, s, ptr, dst, sc.lists, sc.nlist, R, matrix, clear);
     RCHK(hipGetLastError());
   }
 }
@@ -446,8 +448,8 @@ void build_sort(hipStream_t s, Scratch& sc, const uint64_t* ptr, uint32_t* dst, 
 }
 
 void build(hipStream_t s, Scratch& sc, const uint32_t* rows, const uint32_t* vals, uint64_t n, uint32_t row_lo,
-           uint32_t R, const uint32_t* keymap, uint64_t* ptr, uint32_t* dst, uint32_t* bits, uint64_t W) {
-  build_prep(s, sc, rows, vals, n, row_lo, R, keymap, ptr, dst, bits, W, false);
+           uint32_t R, const uint32_t* keymap, uint64_t* ptr, uint32_t* dst, Clear matrix) {
+  build_prep(s, sc, rows, vals, n, row_lo, R, keymap, ptr, dst, matrix, false);
   build_sort(s, sc, ptr, dst, Clear{});
 }
 

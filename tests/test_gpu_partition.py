@@ -123,3 +123,22 @@ def test_rccl_single_rank(oracle_lib):
     st = eng.saturate()
     _assert_oracle([eng], ax, oracle_lib)
     eng.close()
+
+
+@pytest.mark.parametrize("name", ["g3", "g3x"])
+def test_g4_shape_eight_partitions(name, oracle_lib):
+    """configs[3] in miniature: OntologyMultiplier ×8 of G3 (2 %) — and of G3X, whose ⊥ /
+    domain / range facts cross the exchange — on 8 partitions aligned with the copies (rank i
+    owns copy i; ⊥ and ⊤ on rank 0), each with its compacted column window, exchanging deltas
+    every superstep: the union of the partitions is bit-exactly the oracle's closure of the
+    whole ×8 ontology, in lock-step supersteps."""
+    base = generators.workload(name, scale=0.02)
+    k = 8
+    ax = ir.replicate(base, k)
+    bounds = [ir.copy_slice(base, k, i) for i in range(k)]
+    bounds[0] = (0, bounds[0][1])
+    engs, st = engine.classify_partitioned(ax, k, rows=bounds)
+    o = _assert_oracle(engs, ax, oracle_lib)
+    assert sum(s["derived"] for s in st) == o.stats()["derived"]
+    assert len({s["supersteps"] for s in st}) == 1
+    _close(engs)
