@@ -68,22 +68,27 @@ class _stdout_to_stderr:
 
 def pmc_traffic(workload: str, kernel: str):
     """HBM bytes per launch of `kernel` from the committed PMC summary of this workload
-    (profiles/pmc/r01_pmc_<workload>.json, written by scripts/pmc_summary.py from separate
+    (profiles/pmc/rNN_pmc_<workload>.json, written by scripts/pmc_summary.py from separate
     rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes, gfx950-corrected as MI355X_MICROARCH.md
     prescribes).  Used only when the summary was taken on this exact kernel source; else None."""
+    import glob
     import hashlib
-    path = os.path.join(ROOT, "profiles", "pmc", f"r01_pmc_{workload}.json")
     try:
-        with open(path) as f:
-            pmc = json.load(f)
         with open(os.path.join(ROOT, "distel_amd", "csrc", "el_gpu.hip"), "rb") as f:
             digest = hashlib.sha256(f.read()).hexdigest()
-    except (OSError, ValueError):
+    except OSError:
         return None
-    if pmc.get("source_sha256") != digest:
-        return None
-    k = pmc.get("kernels", {}).get(kernel)
-    return None if not k or k.get("hbm_bytes_per_dispatch") is None else int(k["hbm_bytes_per_dispatch"])
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "pmc", f"r*_pmc_{workload}.json")), reverse=True):
+        try:
+            with open(path) as f:
+                pmc = json.load(f)
+        except (OSError, ValueError):
+            continue
+        if pmc.get("source_sha256") != digest:
+            continue
+        k = pmc.get("kernels", {}).get(kernel)
+        return None if not k or k.get("hbm_bytes_per_dispatch") is None else int(k["hbm_bytes_per_dispatch"])
+    return None
 
 
 def parse():

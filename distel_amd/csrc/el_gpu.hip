@@ -200,6 +200,8 @@ struct DState {
   unsigned long long amask;
   uint32_t *alog_y, *alog_c;
   uint8_t* has_act;
+  const uint64_t* act_ptr;  // activations by Y: log indices, ascending (rebuilt between supersteps)
+  const uint32_t* act_k;
   unsigned long long* phash;  // CR4 propagations (pid, B)
   unsigned long long pmask;
   uint32_t *plog_p, *plog_b;
@@ -855,17 +857,16 @@ __device__ void expand_s(const DIndex& ix, const DState& st, BlockQ& q, uint32_t
     }
     if (act && (mask & M_RRNG) && ix.has_range) {  // Y=A ∈ S(X) new, active range (Y, C)  =>  C ∈ S(X)
       ev.v[EL_EV_ENT]++;
-      if (st.has_act[A]) {
-        for (uint32_t k = 0; k < a_end; ++k) {
+      if (st.has_act[A]) {  // A's activations: its row of the activation index
+        ev.v[EL_EV_ROW]++;
+        const uint64_t e = st.act_ptr[A + 1];
+        for (uint64_t j = st.act_ptr[A]; j < e; ++j) {
+          const uint32_t k = st.act_k[j];
+          if (k >= a_end) break;
           ev.v[EL_EV_ENT] += 2;
-          const bool hit = st.alog_y[k] == A;
           const uint32_t C = st.alog_c[k];
-          bool nw = false;
-          if (hit) {
-            ev.v[EL_EV_TEST]++;
-            nw = !test_bit(ix, st.bits, X, C);
-          }
-          emit_s(st, q, nw, X, C, ev);
+          ev.v[EL_EV_TEST]++;
+          emit_s(st, q, !test_bit(ix, st.bits, X, C), X, C, ev);
         }
       }
     }
@@ -1097,23 +1098,31 @@ __global__ void k_jobs(DIndex ix, DState st) {
 }
 
 // Range activations (Y, C) = act log[a_begin, a_end): every X with Y ∈ S(X) gets C
-// (ScriptsCollection.insertClassAssertions1 :45-62 copies result[Y] into result[C]).
+// (ScriptsCollection.insertClassAssertions1 :45-62 copies result[Y] into result[C]).  The
+// X's holding Y are found in the fact log (one coalesced pass over the facts known at t-1,
+// each fact (X, Y) meeting the new activations of Y through the activation index), not by
+// sweeping column Y of the bit matrix (one random line per row and activation).
 __device__ void expand_a(const DIndex& ix, const DState& st, BlockQ& q, uint32_t bid, uint32_t nb,
-                         uint32_t a_begin, uint32_t a_end) {
+                         uint32_t s_end, uint32_t a_begin, uint32_t a_end) {
   Ev ev;
-  if (bid == 0 && threadIdx.x == 0) ev.v[EL_EV_TRIG] += a_end - a_begin;
-  for (uint32_t base = ix.lo + bid * blockDim.x; base < ix.hi; base += nb * blockDim.x) {
-    const uint32_t x = base + threadIdx.x;
-    if (x < ix.hi) {
-      for (uint32_t k = a_begin; k < a_end; ++k) {
-        const uint32_t Y = st.alog_y[k], C = st.alog_c[k];
-        ev.v[EL_EV_TEST]++;
-        bool nw = false;
-        if (test_bit(ix, st.bits, x, Y)) {
+  for (uint32_t base = bid * blockDim.x; base < s_end; base += nb * blockDim.x) {
+    const uint32_t i = base + threadIdx.x;
+    if (i < s_end) {
+      const uint32_t x = st.slog_x[i], Y = st.slog_a[i];
+      ev.v[EL_EV_TRIG]++;
+      ev.v[EL_EV_ENT]++;
+      if (st.has_act[Y]) {
+        ev.v[EL_EV_ROW]++;
+        const uint64_t b = st.act_ptr[Y];
+        for (uint64_t j = st.act_ptr[Y + 1]; j > b; --j) {  // the newest activations are last
+          const uint32_t k = st.act_k[j - 1];
+          if (k < a_begin) break;
+          if (k >= a_end) continue;
+          ev.v[EL_EV_ENT] += 2;
+          const uint32_t C = st.alog_c[k];
           ev.v[EL_EV_TEST]++;
-          nw = !test_bit(ix, st.bits, x, C);
+          emit_s(st, q, !test_bit(ix, st.bits, x, C), x, C, ev);
         }
-        emit_s(st, q, nw, x, C, ev);
       }
     }
     q_maybe_flush(q, st);
@@ -1339,7 +1348,7 @@ __global__ void k_expand(DIndex ix, DState st, ExpandArgs a) {
   }
   b -= a.gl;
   if (b < a.ga) {
-    expand_a(ix, st, q, b, a.ga, a.ab, a.ae);
+    expand_a(ix, st, q, b, a.ga, a.se, a.ab, a.ae);
     return;
   }
   b -= a.ga;
@@ -2061,6 +2070,12 @@ struct el_ctx {
   uint32_t *alog_y = nullptr, *alog_c = nullptr;
   uint64_t alog_cap = 0;
   uint8_t* has_act = nullptr;
+  // activation index: log indices of the activations (Y, C) by Y, ascending (el_rows build)
+  uint64_t* act_ptr = nullptr;  // N + 1
+  uint32_t* act_k = nullptr;
+  uint64_t act_k_cap = 0, act_n = ~0ull;  // entries indexed (~0: rebuild)
+  elrows::Scratch asc;
+  void refresh_acts();
   unsigned long long* phash = nullptr;
   uint64_t phash_cap = 0;
   uint32_t *plog_p = nullptr, *plog_b = nullptr;
@@ -2176,6 +2191,8 @@ struct el_ctx {
     s.alog_y = alog_y;
     s.alog_c = alog_c;
     s.has_act = has_act;
+    s.act_ptr = act_ptr;
+    s.act_k = act_k;
     s.phash = phash;
     s.pmask = phash_cap - 1;
     s.plog_p = plog_p;
@@ -2553,6 +2570,11 @@ void el_ctx::free_state() {
   rl.release();
   rsc.release();
   rsc_l.release();
+  asc.release();
+  dfree(act_ptr);
+  dfree(act_k);
+  act_k_cap = 0;
+  act_n = ~0ull;
   PR.release();
   SC.release();
   PP.release();
@@ -2795,6 +2817,7 @@ void el_ctx::reset_state() {
   bits_logged = true;  // from here on every set bit is in the fact log (k_init and k_commit append)
   s_count = l_count = a_count = p_count = s_init = x_count = 0;
   rs.n = rl.n = ~0ull;  // result rows are stale
+  act_n = ~0ull;
   for (int r = 0; r < EL_NUM_RULE_TYPES; ++r) wm_s[r] = wm_l[r] = wm_a[r] = wm_p[r] = 0;
   wm_x = 0;
   memset(launches, 0, sizeof launches);
@@ -2839,6 +2862,20 @@ void el_ctx::rehash_props(uint64_t cap) {
       hipLaunchKernelGGL(k_rehash, dim3(grid_for(p_count)), dim3(BLOCK), 0, stream, phash, cap - 1,
                          plog_b, plog_p, (uint32_t)p_count);
     });
+}
+
+// The activation index (expand_s / expand_a read it): the activation log's entries by Y.
+// Rebuilt before a generation whenever activations were added (a few supersteps at most).
+void el_ctx::refresh_acts() {
+  if (hx.rng.a.empty() || act_n == a_count) return;
+  if (!act_ptr) act_ptr = dalloc<uint64_t>((uint64_t)hx.N + 1);
+  if (a_count > act_k_cap || !act_k) {
+    dfree(act_k);
+    act_k_cap = std::max<uint64_t>(alog_cap, a_count);
+    act_k = dalloc<uint32_t>(act_k_cap);
+  }
+  elrows::build(stream, asc, alog_y, nullptr, a_count, 0, hx.N, nullptr, act_ptr, act_k, elrows::Clear{});
+  act_n = a_count;
 }
 
 // Result rows from the logs (el_rows.hip): S rows X -> {B} ascending (long rows read off the
@@ -2924,11 +2961,12 @@ bool el_ctx::superstep(uint32_t mask, uint64_t sb, uint64_t se, uint64_t lb, uin
     if (2 * (p_count + cp_cap) > phash_cap) rehash_props(next_pow2(2 * (p_count + cp_cap)));
 
     // ---- generation (reads only the state of step t-1; candidate counters are zero here)
+    refresh_acts();
     DState st = dstate();
     ExpandArgs ea{};
     ea.gs = se > sb ? grid_for(se - sb, tune_expand) : 0u;
     ea.gl = le > lb ? grid_for(le - lb, tune_expand) : 0u;
-    ea.ga = do_a ? grid_for(hx.N) : 0u;
+    ea.ga = do_a ? grid_for(se) : 0u;  // the facts known at t-1 meet the new activations
     ea.gp = do_p ? grid_for(pe - pb) : 0u;
     ea.sb = (uint32_t)sb, ea.se = (uint32_t)se, ea.lb = (uint32_t)lb, ea.le = (uint32_t)le;
     ea.ab = (uint32_t)ab, ea.ae = (uint32_t)ae, ea.pb = (uint32_t)pb, ea.pe = (uint32_t)pe;
@@ -3129,13 +3167,14 @@ uint64_t el_ctx::superstep_part(uint32_t mask, uint64_t sb, uint64_t se, uint64_
     const uint32_t s0 = (uint32_t)s_count, l0 = (uint32_t)l_count, a0 = (uint32_t)a_count, p0 = (uint32_t)p_count;
 
     // ---- generation + local commit (no publish: the import publishes for the step)
+    refresh_acts();
     DState st = dstate();
     ExpandArgs ea{};
     const bool do_a = (mask & M_RRNG) && ae > ab;
     const bool do_p = (mask & M_R4P) && pe > pb;
     ea.gs = se > sb ? grid_for(se - sb) : 0u;
     ea.gl = le > lb ? grid_for(le - lb) : 0u;
-    ea.ga = do_a ? grid_for(hi - lo) : 0u;
+    ea.ga = do_a ? grid_for(se) : 0u;
     ea.gp = do_p ? grid_for(pe - pb) : 0u;
     ea.gx = ((mask & M_R6) && xe > xb) ? grid_for(xe - xb) : 0u;
     ea.sb = (uint32_t)sb, ea.se = (uint32_t)se, ea.lb = (uint32_t)lb, ea.le = (uint32_t)le;
@@ -3334,6 +3373,8 @@ void el_ctx::migrate_state(uint32_t N0, const std::vector<uint32_t>& pmap) {
   }
   rs.release();  // result rows: more rows, remapped pair ids — rebuilt on demand
   rl.release();
+  dfree(act_ptr);  // the activation index covers the grown concept space
+  act_n = ~0ull;
   dfree(scan_flags);
   scan_tiles = (std::max(N, P) + 1 + SCAN_TILE - 1) / SCAN_TILE;
   scan_flags = dalloc<unsigned long long>(scan_tiles);

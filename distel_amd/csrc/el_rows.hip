@@ -74,7 +74,7 @@ __global__ void __launch_bounds__(BLOCK) k_rows_scatter(const uint32_t* __restri
                                                         uint32_t* __restrict__ tmp) {
   const uint64_t stride = (uint64_t)gridDim.x * BLOCK;
   for (uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; i < n; i += stride) {
-    const uint32_t v = vals[i];
+    const uint32_t v = vals ? vals[i] : (uint32_t)i;  // no values: the entry's log index
     tmp[ptr[rows[i] - lo] + rank[i]] = keymap ? keymap[v] : v;
   }
 }

@@ -241,6 +241,7 @@ struct elo_ctx {
   hset acts;
   vec alog_y, alog_c;
   uint8_t* has_act;
+  vec* actrow; /* activation log indices by Y, ascending (the GPU's activation index) */
   hset props; /* CR4 propagations (pid, B) */
   vec plog_p, plog_b;
   vec* prow; /* propagations per pid */
@@ -605,6 +606,7 @@ int elo_create(elo_ctx** out, const el_axioms* ax, int mode) {
   c->pred = (vec*)calloc(c->P ? c->P : 1, sizeof(vec));
   c->succ = (vec*)calloc(c->N, sizeof(vec));
   c->has_act = (uint8_t*)calloc(c->N, 1);
+  c->actrow = (vec*)calloc(c->N, sizeof(vec));
   c->prow = (vec*)calloc(c->P ? c->P : 1, sizeof(vec));
   c->cap_pr = (uint32_t*)malloc((c->P ? c->P : 1) * sizeof(uint32_t));
   c->cap_pp = (uint32_t*)malloc((c->P ? c->P : 1) * sizeof(uint32_t));
@@ -805,15 +807,16 @@ static void expand_s(elo_ctx* c, cands* k, uint32_t mask, uint64_t b, uint64_t e
     }
     if ((mask & M_RRNG) && c->rng.ptr[c->R] > 0) {
       EV(K, EL_EV_ENT);
-      if (c->has_act[A]) {
-        uint64_t q;
-        for (q = 0; q < a_end; ++q) {
+      if (c->has_act[A]) { /* A's row of the activation index */
+        uint64_t j;
+        EV(K, EL_EV_ROW);
+        for (j = 0; j < c->actrow[A].n; ++j) {
+          uint32_t q = c->actrow[A].v[j], C;
+          if (q >= a_end) break;
           EVN(K, EL_EV_ENT, 2);
-          if (c->alog_y.v[q] == A) {
-            uint32_t C = c->alog_c.v[q];
-            EV(K, EL_EV_TEST);
-            if (!bit(c, X, C)) emit_s(c, k, K, X, C);
-          }
+          C = c->alog_c.v[q];
+          EV(K, EL_EV_TEST);
+          if (!bit(c, X, C)) emit_s(c, k, K, X, C);
         }
       }
     }
@@ -956,20 +959,29 @@ static void run_jobs(elo_ctx* c, cands* k) {
   }
 }
 
-static void expand_a(elo_ctx* c, cands* k, uint64_t ab, uint64_t ae) {
+/* New activations (Y, C) = act log[ab, ae) meet every fact (X, Y) known at t-1 (the fact log
+ * [0, s_end)) through Y's row of the activation index (newest last) */
+static void expand_a(elo_ctx* c, cands* k, uint64_t s_end, uint64_t ab, uint64_t ae) {
   const int K = EL_K_EXPAND_A;
-  uint32_t x;
-  uint64_t q;
-  EVN(K, EL_EV_TRIG, ae - ab);
-  for (x = 0; x < c->N; ++x)
-    for (q = ab; q < ae; ++q) {
-      uint32_t Y = c->alog_y.v[q], C = c->alog_c.v[q];
-      EV(K, EL_EV_TEST);
-      if (bit(c, x, Y)) {
+  uint64_t i;
+  for (i = 0; i < s_end; ++i) {
+    uint32_t x = c->slog_x.v[i], Y = c->slog_a.v[i];
+    EV(K, EL_EV_TRIG);
+    EV(K, EL_EV_ENT);
+    if (c->has_act[Y]) {
+      uint64_t j;
+      EV(K, EL_EV_ROW);
+      for (j = c->actrow[Y].n; j > 0; --j) {
+        uint32_t q = c->actrow[Y].v[j - 1], C;
+        if (q < ab) break;
+        if (q >= ae) continue;
+        EVN(K, EL_EV_ENT, 2);
+        C = c->alog_c.v[q];
         EV(K, EL_EV_TEST);
         if (!bit(c, x, C)) emit_s(c, k, K, x, C);
       }
     }
+  }
 }
 
 static void expand_p(elo_ctx* c, cands* k, uint64_t pb, uint64_t pe) {
@@ -1035,7 +1047,7 @@ static int superstep(elo_ctx* c, uint32_t mask, uint64_t sb, uint64_t se, uint64
   /* generation: reads only the state of the previous step */
   expand_s(c, &k, mask, sb, se, a0);
   expand_l(c, &k, mask, lb, le);
-  if (do_a) expand_a(c, &k, ab, ae);
+  if (do_a) expand_a(c, &k, se, ab, ae);
   if (do_p) expand_p(c, &k, pb, pe);
   run_jobs(c, &k);
   if (k.sx.n + k.s1x.n + k.lx.n + k.ay.n + k.pp.n == 0) {
@@ -1091,6 +1103,7 @@ static int superstep(elo_ctx* c, uint32_t mask, uint64_t sb, uint64_t se, uint64
     EV(EL_K_COMMIT_A, EL_EV_HASH);
     if (hs_add(&c->acts, lkey(cc, y))) {
       EV(EL_K_COMMIT_A, EL_EV_EMIT);
+      vpush(&c->actrow[y], (uint32_t)c->alog_y.n);
       vpush(&c->alog_y, y);
       vpush(&c->alog_c, cc);
       c->has_act[y] = 1;
@@ -1412,6 +1425,9 @@ void elo_destroy(elo_ctx* c) {
   if (c->prow)
     for (i = 0; i < c->P; ++i) free(c->prow[i].v);
   free(c->prow), free(c->props.t), free(c->plog_p.v), free(c->plog_b.v);
+  if (c->actrow)
+    for (uint32_t y = 0; y < c->N; ++y) free(c->actrow[y].v);
+  free(c->actrow);
   free(c->srow), free(c->succ), free(c->pred), free(c->has_act);
   free(c->cap_pr), free(c->cap_sc), free(c->cap_pp);
   free(c->slog_x.v), free(c->slog_a.v), free(c->slog_f.v), free(c->llog_x.v), free(c->llog_p.v);
