@@ -2344,6 +2344,13 @@ struct el_ctx {
   void migrate_state(uint32_t N0, const std::vector<uint32_t>& pmap);
   void init_rows(uint32_t a, uint32_t b);
   el::AxiomStore store;  // the loaded axioms (increments append to them)
+  // ELK range fillers (el_index.h elk_ranges): concepts [n_user, N) are internal; the result
+  // rows cover the caller's concepts [lo, uhi()) only
+  uint32_t n_user = 0;
+  std::vector<uint32_t> fresh_b, fresh_r;
+  uint32_t uhi() const { return std::max(lo, std::min(hi, n_user)); }
+  uint64_t user_count(bool facts);  // facts / links of the result rows (= the log's without fresh rows)
+  uint64_t uc_s_n = ~0ull, uc_s = 0, uc_l_n = ~0ull, uc_l = 0;
   std::vector<uint32_t> init_off;  // host copy of DIndex::init_off
 };
 
@@ -2458,7 +2465,7 @@ std::string el_ctx::install_index(el::HostIndex&& hnew) {
     } else {
       if (cfg_hi > h.N) return "partition rows beyond n_concepts";
       lo = cfg_lo;
-      hi = cfg_hi;
+      hi = cfg_hi == n_user ? h.N : cfg_hi;  // the last rank also owns the ELK range fillers
     }
   } else {
     lo = 0;
@@ -2878,12 +2885,42 @@ void el_ctx::refresh_acts() {
   act_n = a_count;
 }
 
+// entries of a log whose row is below `limit` (the caller's rows when ELK range fillers exist)
+__global__ void k_count_below(const uint32_t* __restrict__ rows, uint64_t n, uint32_t limit,
+                              unsigned long long* __restrict__ out) {
+  unsigned long long c = 0;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+    c += rows[i] < limit;
+  c = wave_sum_u64(c);
+  if (__lane_id() == 0 && c) atomicAdd(out, c);
+}
+
+uint64_t el_ctx::user_count(bool facts) {
+  const uint64_t n = facts ? s_count : l_count;
+  if (uhi() == hi) return n;
+  uint64_t& key = facts ? uc_s_n : uc_l_n;
+  uint64_t& val = facts ? uc_s : uc_l;
+  if (key == n) return val;
+  unsigned long long* d = dalloc<unsigned long long>(1);
+  HIPCHK(hipMemsetAsync(d, 0, sizeof *d, stream));
+  if (n)
+    hipLaunchKernelGGL(k_count_below, dim3(grid_for(n)), dim3(BLOCK), 0, stream, facts ? slog_x : llog_x, n, uhi(), d);
+  HIPCHK(hipGetLastError());
+  unsigned long long h = 0;
+  HIPCHK(hipMemcpyAsync(&h, d, sizeof h, hipMemcpyDeviceToHost, stream));
+  HIPCHK(hipStreamSynchronize(stream));
+  dfree(d);
+  key = n;
+  val = h;
+  return h;
+}
+
 // Result rows from the logs (el_rows.hip): S rows X -> {B} ascending (long rows read off the
 // bit matrix), link rows X -> {q} ascending, q = the link's pair rank in (role, filler) order.
 // dst: device memory or mapped page-locked host memory (the copy-back writes the sorted rows
 // straight over PCIe).  Enqueued on s.
 void el_ctx::build_rows(bool facts, hipStream_t s, uint64_t* ptr, uint32_t* dst, int half, bool clear) {
-  const uint32_t R = hi - lo;
+  const uint32_t R = uhi() - lo;
   elrows::Scratch& sc = facts ? rsc : rsc_l;
   clear = clear && facts;
   if (half != 2) {
@@ -2900,7 +2937,7 @@ void el_ctx::build_rows(bool facts, hipStream_t s, uint64_t* ptr, uint32_t* dst,
 // Device-resident result rows (el_get_subsumers, el_copy_facts / links, el_export_result),
 // kept until the logs change.
 void el_ctx::ensure_rows(bool facts, bool links) {
-  const uint32_t R = hi - lo;
+  const uint32_t R = uhi() - lo;
   auto fit = [&](Rows& r, uint64_t n) {
     if (!r.ptr) r.ptr = dalloc<uint64_t>((uint64_t)R + 1);
     if (n > r.cap || !r.val) {
@@ -3590,14 +3627,24 @@ int el_rccl_unique_id(uint8_t out[128]) {
 int el_load(el_ctx* c, const el_axioms* ax) {
   if (!c || !ax) return EL_EINVAL;
   return guarded(c, [&] {
-    el::AxiomStore store;
+    el::AxiomStore store, eff;
+    std::vector<uint32_t> fb, fr;
     std::string e = store.append(*ax);
     el::HostIndex hx;
-    if (e.empty()) e = el::build_index(store.view(), hx, c->flags);
+    if (e.empty()) {
+      if (c->flags & EL_FLAG_COMPAT_DISTEL_RANGE)
+        eff = store;
+      else
+        el::elk_ranges(store, eff, fb, fr);  // H1: ELK's reading of ranges (the default)
+      e = el::build_index(eff.view(), hx, c->flags);
+    }
     if (!e.empty()) return fail(c, EL_EINVAL, e);
     HIPCHK(hipStreamSynchronize(c->stream));
     c->free_state();
     c->free_index();
+    c->n_user = store.N;
+    c->fresh_b = std::move(fb);
+    c->fresh_r = std::move(fr);
     c->store = std::move(store);
     e = c->install_index(std::move(hx));
     if (!e.empty()) return fail(c, EL_EINVAL, e);
@@ -3617,6 +3664,9 @@ int el_add_axioms(el_ctx* c, const el_axioms* inc) {
   if (!c || !inc) return EL_EINVAL;
   if (!c->loaded) return fail(c, EL_ESTATE, "el_add_axioms before el_load");
   if (c->part()) return fail(c, EL_ESTATE, "increments need a whole-ontology context");
+  if (!(c->flags & EL_FLAG_COMPAT_DISTEL_RANGE) && (!c->store.rng_r.empty() || inc->n_range))
+    return fail(c, EL_EINVAL, "increments with range axioms need EL_FLAG_COMPAT_DISTEL_RANGE "
+                              "(ELK range fillers are numbered after the concepts)");
   return guarded(c, [&] {
     el::AxiomStore store = c->store;
     std::string e = store.append(*inc);
@@ -3627,6 +3677,7 @@ int el_add_axioms(el_ctx* c, const el_axioms* inc) {
     if (!c->inited) {  // nothing saturated yet: a plain reload
       c->free_state();
       c->free_index();
+      c->n_user = store.N;
       c->store = std::move(store);
       e = c->install_index(std::move(hx));
       if (!e.empty()) return fail(c, EL_EINVAL, e);
@@ -3644,6 +3695,7 @@ int el_add_axioms(el_ctx* c, const el_axioms* inc) {
     }
     const uint32_t N0 = c->hx.N;
     c->free_index();
+    c->n_user = store.N;
     c->store = std::move(store);
     e = c->install_index(std::move(hx));
     if (!e.empty()) return fail(c, EL_EINVAL, e);
@@ -3794,8 +3846,8 @@ int el_superstep_trace(el_ctx* c, uint64_t* ds, uint64_t* dl, uint64_t* da, size
 int el_get_subsumers(el_ctx* c, uint32_t x, uint32_t* out, size_t cap, size_t* n) {
   if (!c || !n) return EL_EINVAL;
   if (!c->inited) return fail(c, EL_ESTATE, "no state");
-  if (x >= c->hx.N) return fail(c, EL_EINVAL, "concept id out of range");
-  if (x < c->lo || x >= c->hi) return fail(c, EL_EINVAL, "row not owned by this partition");
+  if (x >= c->n_user) return fail(c, EL_EINVAL, "concept id out of range");
+  if (x < c->lo || x >= c->uhi()) return fail(c, EL_EINVAL, "row not owned by this partition");
   return guarded(c, [&] {
     c->ensure_rows(true, false);
     c->sync();
@@ -3811,7 +3863,7 @@ int el_get_subsumers(el_ctx* c, uint32_t x, uint32_t* out, size_t cap, size_t* n
 namespace {
 // host copy of result rows: ptr (rows + 1) and, when vals is given, the values
 void read_rows(el_ctx* c, const el_ctx::Rows& r, std::vector<uint64_t>& ptr, uint32_t* vals, uint64_t n) {
-  ptr.resize((size_t)(c->hi - c->lo) + 1);
+  ptr.resize((size_t)(c->uhi() - c->lo) + 1);
   HIPCHK(hipMemcpy(ptr.data(), r.ptr, ptr.size() * sizeof(uint64_t), hipMemcpyDeviceToHost));
   if (vals && n) HIPCHK(hipMemcpy(vals, r.val, n * sizeof(uint32_t), hipMemcpyDeviceToHost));
 }
@@ -3822,7 +3874,7 @@ int el_copy_facts(el_ctx* c, uint32_t* x, uint32_t* a, size_t cap, size_t* n) {
   if (!c->inited) return fail(c, EL_ESTATE, "no state");
   return guarded(c, [&] {
     c->sync();
-    *n = c->s_count;
+    *n = c->user_count(true);
     if (cap < *n) return EL_ERANGE;
     if (!*n) return EL_OK;
     c->ensure_rows(true, false);
@@ -3841,7 +3893,7 @@ int el_copy_links(el_ctx* c, uint32_t* x, uint32_t* r, uint32_t* y, size_t cap, 
   if (!c->inited) return fail(c, EL_ESTATE, "no state");
   return guarded(c, [&] {
     c->sync();
-    *n = c->l_count;
+    *n = c->user_count(false);
     if (cap < *n) return EL_ERANGE;
     if (!*n) return EL_OK;
     c->ensure_rows(false, true);
@@ -3865,9 +3917,9 @@ int el_result_info(el_ctx* c, el_result* res) {
   return guarded(c, [&] {
     c->sync();
     res->row_lo = c->lo;
-    res->row_hi = c->hi;
-    res->n_facts = c->s_count;
-    res->n_links = c->l_count;
+    res->row_hi = c->uhi();
+    res->n_facts = c->user_count(true);
+    res->n_links = c->user_count(false);
     res->n_pairs = c->hx.P;
     return EL_OK;
   });
@@ -3898,15 +3950,18 @@ int el_copy_result(el_ctx* c, el_result* res) {
   if (res->flags & ~EL_RESULT_FLAGS_KNOWN) return fail(c, EL_EINVAL, "unknown el_result flags");
   return guarded(c, [&] {
     c->sync();  // counts of the last superstep
-    const uint64_t R1 = (uint64_t)(c->hi - c->lo) + 1;
+    const uint64_t R1 = (uint64_t)(c->uhi() - c->lo) + 1;
+    const uint64_t nf = c->user_count(true), nl = c->user_count(false);
     res->row_lo = c->lo;
-    res->row_hi = c->hi;
-    res->n_facts = c->s_count;
-    res->n_links = c->l_count;
+    res->row_hi = c->uhi();
+    res->n_facts = nf;
+    res->n_links = nl;
     res->n_pairs = c->hx.P;
-    if ((res->s_val && res->s_cap < c->s_count) || (res->l_pair && res->l_cap < c->l_count))
+    if ((res->s_val && res->s_cap < nf) || (res->l_pair && res->l_cap < nl))
       return fail(c, EL_ERANGE, "result buffer too small (el_result_info gives the sizes)");
     const bool release = (res->flags & EL_RESULT_RELEASE) != 0;
+    // the S-row sorts clear the bit matrix only when they write every row (no ELK range fillers)
+    const bool fuse_clear = release && c->uhi() == c->hi;
     struct Part {
       bool facts;
       uint64_t* ptr_out;
@@ -3916,8 +3971,8 @@ int el_copy_result(el_ctx* c, el_result* res) {
       hipStream_t s;
       uint32_t* direct;
     };
-    Part parts[2] = {{false, res->l_ptr, res->l_pair, &c->rl, c->l_count, c->cstream, nullptr},
-                     {true, res->s_ptr, res->s_val, &c->rs, c->s_count, c->stream, nullptr}};
+    Part parts[2] = {{false, res->l_ptr, res->l_pair, &c->rl, nl, c->cstream, nullptr},
+                     {true, res->s_ptr, res->s_val, &c->rs, nf, c->stream, nullptr}};
     // the copy stream starts behind the saturation
     HIPCHK(hipEventRecord(c->ev_rows[1], c->stream));
     HIPCHK(hipStreamWaitEvent(c->cstream, c->ev_rows[1], 0));
@@ -3925,11 +3980,12 @@ int el_copy_result(el_ctx* c, el_result* res) {
     for (Part& p : parts) {
       if (!p.ptr_out && !p.val_out) continue;
       el_ctx::Rows& r = *p.rows;
-      p.direct = r.n == p.n || !p.n ? nullptr : mapped_for_device(p.val_out);
+      const uint64_t logged = p.facts ? c->s_count : c->l_count;  // Rows::n counts log entries
+      p.direct = r.n == logged || !p.n ? nullptr : mapped_for_device(p.val_out);
       if (p.direct) {  // sorted rows straight into the caller's page-locked buffer
         if (!r.ptr) r.ptr = dalloc<uint64_t>(R1);
         r.n = ~0ull;  // r.ptr is reused; the device rows are not built
-        c->build_rows(p.facts, p.s, r.ptr, p.direct, 1, release);
+        c->build_rows(p.facts, p.s, r.ptr, p.direct, 1, fuse_clear);
       } else {
         p.direct = nullptr;
         c->ensure_rows(p.facts, !p.facts);  // engine stream
@@ -3940,7 +3996,7 @@ int el_copy_result(el_ctx* c, el_result* res) {
       HIPCHK(hipEventRecord(c->ev_rows[1], c->cstream));
       HIPCHK(hipStreamWaitEvent(c->rstream, c->ev_rows[0], 0));
       HIPCHK(hipStreamWaitEvent(c->rstream, c->ev_rows[1], 0));
-      c->reset_device(c->rstream, parts[1].direct != nullptr);  // the S-row sorts clear the matrix
+      c->reset_device(c->rstream, fuse_clear && parts[1].direct != nullptr);  // the S-row sorts clear the matrix
       HIPCHK(hipEventRecord(c->ev_reset, c->rstream));
     }
     // 2. the sorts into the caller's buffers, the device rows by DMA
@@ -3948,7 +4004,7 @@ int el_copy_result(el_ctx* c, el_result* res) {
       if (!p.ptr_out && !p.val_out) continue;
       el_ctx::Rows& r = *p.rows;
       if (p.direct) {
-        c->build_rows(p.facts, p.s, r.ptr, p.direct, 2, release);
+        c->build_rows(p.facts, p.s, r.ptr, p.direct, 2, fuse_clear);
         if (p.ptr_out) HIPCHK(hipMemcpyAsync(p.ptr_out, r.ptr, R1 * sizeof(uint64_t), hipMemcpyDeviceToHost, p.s));
         continue;
       }
@@ -3979,6 +4035,16 @@ int el_pair_table(el_ctx* c, uint32_t* role, uint32_t* filler, size_t cap, size_
   return EL_OK;
 }
 
+int el_fresh_fillers(el_ctx* c, uint32_t* filler, uint32_t* role, size_t cap, size_t* n) {
+  if (!c || !n) return EL_EINVAL;
+  if (!c->loaded) return fail(c, EL_ESTATE, "no ontology loaded");
+  *n = c->fresh_b.size();
+  if (cap < *n) return EL_ERANGE;
+  if (filler) std::copy(c->fresh_b.begin(), c->fresh_b.end(), filler);
+  if (role) std::copy(c->fresh_r.begin(), c->fresh_r.end(), role);
+  return EL_OK;
+}
+
 void* el_host_alloc(size_t bytes) {
   void* p = nullptr;
   if (hipHostMalloc(&p, bytes ? bytes : 1, hipHostMallocPortable) != hipSuccess) return nullptr;
@@ -3995,10 +4061,10 @@ int el_export_result(el_ctx* c, int layout, el_sink sink, void* user) {
   return guarded(c, [&] {
     c->ensure_rows(true, false);
     c->sync();
-    const uint32_t N = c->hx.N, lo = c->lo, hi = c->hi;
+    const uint32_t N = c->n_user, lo = c->lo, hi = c->uhi();
     std::vector<uint64_t> ptr;
-    std::vector<uint32_t> val(c->s_count);
-    read_rows(c, c->rs, ptr, val.data(), c->s_count);
+    std::vector<uint32_t> val(c->user_count(true));
+    read_rows(c, c->rs, ptr, val.data(), val.size());
     // result node rows: classes and individuals only (⊥ and datatypes have no key)
     auto exported = [&](uint32_t x) {
       return x != EL_BOTTOM && c->hx.kind[x] != EL_KIND_DATATYPE;

@@ -93,6 +93,63 @@ el_axioms AxiomStore::view() const {
   return a;
 }
 
+void elk_ranges(const AxiomStore& in, AxiomStore& out, std::vector<uint32_t>& fresh_b,
+                std::vector<uint32_t>& fresh_r) {
+  out = in;
+  fresh_b.clear();
+  fresh_r.clear();
+  if (in.rng_r.empty()) return;
+  // ranges*(r): the ranges of every s with r ⊑* s
+  std::vector<std::vector<uint32_t>> sup(in.R), rng(in.R);
+  for (size_t i = 0; i < in.sr_r.size(); ++i) sup[in.sr_r[i]].push_back(in.sr_s[i]);
+  for (size_t i = 0; i < in.rng_r.size(); ++i) rng[in.rng_r[i]].push_back(in.rng_c[i]);
+  std::vector<std::vector<uint32_t>> rstar(in.R);
+  for (uint32_t r = 0; r < in.R; ++r) {
+    std::vector<uint8_t> seen(in.R, 0);
+    std::vector<uint32_t> st{r};
+    seen[r] = 1;
+    std::set<uint32_t> cs;
+    while (!st.empty()) {
+      const uint32_t q = st.back();
+      st.pop_back();
+      cs.insert(rng[q].begin(), rng[q].end());
+      for (uint32_t s2 : sup[q])
+        if (!seen[s2]) seen[s2] = 1, st.push_back(s2);
+    }
+    rstar[r].assign(cs.begin(), cs.end());
+  }
+  std::map<std::pair<uint32_t, uint32_t>, uint32_t> fresh;  // (B, r) -> F
+  std::set<std::pair<uint32_t, uint32_t>> ind_sub;          // individual b ⊑ C
+  for (size_t i = 0; i < in.exr_a.size(); ++i) {
+    const uint32_t r = in.exr_r[i], b = in.exr_b[i];
+    if (rstar[r].empty()) continue;
+    const uint8_t k = b < in.kind.size() ? in.kind[b] : (uint8_t)EL_KIND_CLASS;
+    if (k == EL_KIND_DATATYPE) continue;
+    if (k == EL_KIND_INDIVIDUAL) {
+      for (uint32_t c : rstar[r]) ind_sub.insert({b, c});
+      continue;
+    }
+    auto it = fresh.find({b, r});
+    uint32_t f;
+    if (it == fresh.end()) {
+      f = in.N + (uint32_t)fresh_b.size();
+      fresh.emplace(std::make_pair(b, r), f);
+      fresh_b.push_back(b);
+      fresh_r.push_back(r);
+      out.sub_a.push_back(f), out.sub_b.push_back(b);
+      for (uint32_t c : rstar[r]) out.sub_a.push_back(f), out.sub_b.push_back(c);
+    } else {
+      f = it->second;
+    }
+    out.exr_b[i] = f;
+  }
+  for (const auto& [b, c] : ind_sub) out.sub_a.push_back(b), out.sub_b.push_back(c);
+  out.N = in.N + (uint32_t)fresh_b.size();
+  out.kind.resize(out.N, EL_KIND_CLASS);
+  out.rng_r.clear();
+  out.rng_c.clear();
+}
+
 void distel_chain_set(const el_axioms& ax, std::vector<uint32_t>& r, std::vector<uint32_t>& s,
                       std::vector<uint32_t>& t) {
   // Type5AxiomProcessorBase.java:128-143: for key "Yr" every Z of DB4["Yr"] (any s whose

@@ -59,6 +59,17 @@ struct AxiomStore {
 // flags: el_config.flags (EL_FLAG_COMPAT_DISTEL_CHAIN indexes the DistEL chain set).
 std::string build_index(const el_axioms& ax, HostIndex& out, uint32_t flags = 0);
 
+// H1, the default: ranges read the ELK way, as the normalizer eliminates
+// them (Normalizer.java:122-137, 455-497).  Every CR3 axiom A ⊑ ∃r.B whose role has ranges
+// ranges*(r) (the ranges of r and of its super-roles) and whose filler is a class gets the
+// fresh filler F = n_concepts + i standing for B ⊓ ranges*(r) — one per (B, r), numbered in
+// first-occurrence order — with told F ⊑ B and F ⊑ C for C ∈ ranges*(r); an individual filler
+// b gets b ⊑ C (it is an r-successor); a datatype filler is left alone.  The range axioms are
+// consumed.  fresh_b / fresh_r describe the fresh fillers.  (Exact for ontologies within
+// EL++'s restriction that a role inclusion r1∘…∘rk ⊑ s implies ranges(s) ⊆ ranges(rk).)
+void elk_ranges(const AxiomStore& in, AxiomStore& out, std::vector<uint32_t>& fresh_b,
+                std::vector<uint32_t>& fresh_r);
+
 // H2 (EL_FLAG_COMPAT_DISTEL_CHAIN): the chain set DistEL's CR6 effectively applies,
 // {r∘s⊑t : some r∘s⊑t' and some r∘s'⊑t told}, sorted and deduplicated.
 void distel_chain_set(const el_axioms& ax, std::vector<uint32_t>& r, std::vector<uint32_t>& s,

@@ -57,8 +57,8 @@ struct Scratch {
   void release();
 };
 
-// Rows [row_lo, row_lo + R) of the log entries (rows[i], vals[i]), i < n (every rows[i] in
-// range).  ptr (device): R + 1 offsets; dst: n values, keymap ? keymap[v] : v, ascending in
+// Rows [row_lo, row_lo + R) of the log entries (rows[i], vals[i]), i < n (entries of other
+// rows are left out).  ptr (device): R + 1 offsets; dst: n values, keymap ? keymap[v] : v, ascending in
 // each row (device memory, or host memory the device can write).  vals = nullptr: the value
 // of entry i is i (rows of log indices).
 // matrix (optional): a bit matrix holding exactly the log's entries (values are concept ids);

@@ -41,41 +41,46 @@ uint32_t grid(uint64_t n, uint32_t cap) {
 
 // Per-row counts and ranks.  A wave's 64 consecutive log entries are cut into runs of equal
 // rows (the log holds each told closure, each CR4 fan-out of one X, back to back): the run
-// head takes the run's slots with one atomic and its lanes take consecutive ranks.
+// head takes the run's slots with one atomic and its lanes take consecutive ranks.  Entries
+// of rows outside [lo, lo + R) are skipped (they end runs).
 __global__ void __launch_bounds__(BLOCK) k_rows_count(const uint32_t* __restrict__ rows, uint64_t n, uint32_t lo,
-                                                      uint32_t* __restrict__ cnt, uint32_t* __restrict__ rank) {
+                                                      uint32_t R, uint32_t* __restrict__ cnt,
+                                                      uint32_t* __restrict__ rank) {
   const uint32_t lane = __lane_id();
   const uint64_t stride = (uint64_t)gridDim.x * BLOCK;
   for (uint64_t i0 = (uint64_t)blockIdx.x * BLOCK + (threadIdx.x & ~63u); i0 < n; i0 += stride) {  // wave-uniform
     const uint64_t i = i0 + lane;
-    const bool ok = i < n;
-    const uint32_t x = ok ? rows[i] - lo : NONE;
+    uint32_t x = i < n ? rows[i] - lo : NONE;
+    const bool ok = x < R;
+    if (!ok) x = NONE;
     const uint32_t px = __shfl_up(x, 1);
     const bool head = ok && (lane == 0 || px != x);
     const unsigned long long hm = __ballot(head);
-    const uint32_t nvalid = (uint32_t)__popcll(__ballot(ok));  // valid lanes are a prefix
-    // this lane's run: head h = last head at or below the lane, end = next head or nvalid
+    const unsigned long long bm = __ballot(head || !ok);  // a run ends at the next head or skipped entry
+    // this lane's run: head h = last head at or below the lane, end = next break above it
     const unsigned long long le = lane == 63 ? ~0ull : ((1ull << (lane + 1)) - 1);
     const uint32_t h = 63u - (uint32_t)__clzll(hm & le);
-    const unsigned long long above = hm & ~le;
-    const uint32_t end = above ? (uint32_t)__ffsll((long long)above) - 1 : nvalid;
+    const unsigned long long above = bm & ~le;
+    const uint32_t end = above ? (uint32_t)__ffsll((long long)above) - 1 : 64u;
     uint32_t base = 0;
     if (head) base = atomicAdd(cnt + x, end - lane);
-    base = __shfl(base, (int)h);
+    base = __shfl(base, (int)(h & 63u));
     if (ok) rank[i] = base + (lane - h);
   }
 }
 
 __global__ void __launch_bounds__(BLOCK) k_rows_scatter(const uint32_t* __restrict__ rows,
                                                         const uint32_t* __restrict__ vals, uint64_t n, uint32_t lo,
-                                                        const uint64_t* __restrict__ ptr,
+                                                        uint32_t R, const uint64_t* __restrict__ ptr,
                                                         const uint32_t* __restrict__ rank,
                                                         const uint32_t* __restrict__ keymap,
                                                         uint32_t* __restrict__ tmp) {
   const uint64_t stride = (uint64_t)gridDim.x * BLOCK;
   for (uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x; i < n; i += stride) {
+    const uint32_t x = rows[i] - lo;
+    if (x >= R) continue;
     const uint32_t v = vals ? vals[i] : (uint32_t)i;  // no values: the entry's log index
-    tmp[ptr[rows[i] - lo] + rank[i]] = keymap ? keymap[v] : v;
+    tmp[ptr[x] + rank[i]] = keymap ? keymap[v] : v;
   }
 }
 
@@ -409,7 +414,7 @@ void build_prep(hipStream_t s, Scratch& sc, const uint32_t* rows, const uint32_t
   RCHK(hipMemsetAsync(sc.cnt, 0, ((uint64_t)R + 1) * sizeof(uint32_t), s));
   RCHK(hipMemsetAsync(sc.nlist, 0, 128 * sizeof(uint32_t), s));
   if (n) {
-    hipLaunchKernelGGL(k_rows_count, dim3(grid(n, 2048)), dim3(BLOCK), 0, s, rows, n, row_lo, sc.cnt, sc.rank);
+    hipLaunchKernelGGL(k_rows_count, dim3(grid(n, 2048)), dim3(BLOCK), 0, s, rows, n, row_lo, R, sc.cnt, sc.rank);
     RCHK(hipGetLastError());
   }
   const uint32_t tiles = (uint32_t)(((uint64_t)R + 1 + SCAN_TILE - 1) / SCAN_TILE);
@@ -424,7 +429,7 @@ void build_prep(hipStream_t s, Scratch& sc, const uint32_t* rows, const uint32_t
   sc.R = R;
   sc.bits = matrix.bits != nullptr;
   if (!n) return;
-  hipLaunchKernelGGL(k_rows_scatter, dim3(grid(n, 2048)), dim3(BLOCK), 0, s, rows, vals, n, row_lo, ptr, sc.rank,
+  hipLaunchKernelGGL(k_rows_scatter, dim3(grid(n, 2048)), dim3(BLOCK), 0, s, rows, vals, n, row_lo, R, ptr, sc.rank,
                      keymap, sc.tmp);
   RCHK(hipGetLastError());
   if (matrix.bits) {

@@ -21,6 +21,7 @@ LIB_PATH = os.path.join(_HERE, "lib", "libel_gpu.so")
 EL_OK, EL_EINVAL, EL_ENOMEM, EL_EHIP, EL_ESTATE, EL_ERANGE = 0, -1, -2, -3, -4, -5
 LAYOUT_X_TO_B, LAYOUT_B_TO_X = 0, 1
 EL_FLAG_COMPAT_DISTEL_CHAIN = 0x1  # el_config.flags: hazard H2 reproduced (include/el_gpu.h)
+EL_FLAG_COMPAT_DISTEL_RANGE = 0x2  # el_config.flags: DistEL's range reading (H1); default ELK's
 EL_RESULT_RELEASE = 0x1  # el_result.flags: the state is released behind the copy-back
 
 # work phases (el_kernel); "kernel:role" where several phases share one launch
@@ -101,7 +102,7 @@ EXPORTED_SYMBOLS = [
     "el_get_stats", "el_kernel_stats", "el_superstep_trace", "el_get_subsumers", "el_copy_facts",
     "el_copy_links", "el_export_result", "el_last_error", "el_destroy", "el_group_create", "el_group_destroy",
     "el_rccl_unique_id", "el_add_axioms", "el_result_info", "el_copy_result", "el_pair_table", "el_host_alloc",
-    "el_host_free",
+    "el_host_free", "el_fresh_fillers",
 ]
 
 _lib: Optional[C.CDLL] = None
@@ -142,6 +143,7 @@ def load_library(path: Optional[str] = None) -> C.CDLL:
     lib.el_host_alloc.restype = C.c_void_p
     lib.el_host_free.argtypes = [C.c_void_p]
     lib.el_host_free.restype = None
+    lib.el_fresh_fillers.argtypes = [P, _u32p, _u32p, C.c_size_t, C.POINTER(C.c_size_t)]
     lib.el_last_error.argtypes = [P]
     lib.el_last_error.restype = C.c_char_p
     lib.el_destroy.argtypes = [P]
@@ -290,12 +292,15 @@ class Engine:
     """One GPU saturation context (one DistEL rule cluster), on one device."""
 
     def __init__(self, device: int = 0, profile: bool = False, partition: Optional[Partition] = None,
-                 compat_chain: bool = False):
+                 compat_chain: bool = False, compat_range: bool = False):
         """compat_chain: EL_FLAG_COMPAT_DISTEL_CHAIN, DistEL's CR6 join that ignores s (hazard H2,
-        Type5AxiomProcessorBase.java:115-154); default the complete EL+ closure."""
+        Type5AxiomProcessorBase.java:115-154); default the complete EL+ closure.
+        compat_range: EL_FLAG_COMPAT_DISTEL_RANGE, DistEL's range rule (hazard H1,
+        RolePairHandler.java:471-479); default ELK's reading of ranges."""
         self._lib = load_library()
         self._ctx = C.c_void_p()
-        cfg = _ElConfig(device, 1 if profile else 0, EL_FLAG_COMPAT_DISTEL_CHAIN if compat_chain else 0)
+        flags = (EL_FLAG_COMPAT_DISTEL_CHAIN if compat_chain else 0) | (EL_FLAG_COMPAT_DISTEL_RANGE if compat_range else 0)
+        cfg = _ElConfig(device, 1 if profile else 0, flags)
         if partition is not None:
             cfg.exchange = partition.exchange
             cfg.part_rank, cfg.part_count = partition.rank, partition.count
@@ -451,6 +456,17 @@ class Engine:
                                                                          r.n_pairs)
         return out
 
+    def fresh_fillers(self) -> Tuple[np.ndarray, np.ndarray]:
+        """ELK range fillers: concept n_concepts + i = filler[i] ⊓ ranges*(role[i])."""
+        n = C.c_size_t(0)
+        rc = self._lib.el_fresh_fillers(self._ctx, None, None, 0, C.byref(n))
+        if rc not in (EL_OK, EL_ERANGE):
+            self._check(rc, "el_fresh_fillers")
+        b = np.zeros(n.value, np.uint32)
+        r = np.zeros(n.value, np.uint32)
+        self._check(self._lib.el_fresh_fillers(self._ctx, _ptr(b), _ptr(r), n.value, C.byref(n)), "el_fresh_fillers")
+        return b, r
+
     def pair_table(self) -> Tuple[np.ndarray, np.ndarray]:
         """pair q -> (role, filler), ascending in (role, filler)."""
         n = C.c_size_t(0)
@@ -495,14 +511,15 @@ def merge_axioms(a: Axioms, b: Axioms) -> Axioms:
 
 
 def classify_partitioned(ax: Axioms, parts: int, devices: Optional[List[int]] = None,
-                         rows: Optional[List[Tuple[int, int]]] = None) -> Tuple[List[Engine], List[Stats]]:
+                         rows: Optional[List[Tuple[int, int]]] = None,
+                         compat_range: bool = False) -> Tuple[List[Engine], List[Stats]]:
     """Row-partitioned classification in ONE process: ``parts`` engines (one per thread,
     on ``devices`` round-robin, default all on device 0) exchanging their deltas through an
     in-process group (EL_XCHG_LOCAL).  The union of the engines' rows is the closure."""
     import threading
     devices = devices or [0]
     group = LocalGroup(parts)
-    engs = [Engine(device=devices[q % len(devices)],
+    engs = [Engine(device=devices[q % len(devices)], compat_range=compat_range,
                    partition=Partition(q, parts, XCHG_LOCAL, group=group, rows=rows[q] if rows else (0, 0)))
             for q in range(parts)]
     engs[0]._group = group  # keep the group alive as long as the engines
@@ -544,9 +561,9 @@ def merge_links(engs: List[Engine]) -> Tuple[np.ndarray, np.ndarray, np.ndarray]
 
 
 def classify(ax: Axioms, device: int = 0, profile: bool = False,
-             compat_chain: bool = False) -> Tuple[Engine, Stats]:
+             compat_chain: bool = False, compat_range: bool = False) -> Tuple[Engine, Stats]:
     """Load + init + saturate in one call (ELClassifier.classify() over all rule types)."""
-    eng = Engine(device=device, profile=profile, compat_chain=compat_chain)
+    eng = Engine(device=device, profile=profile, compat_chain=compat_chain, compat_range=compat_range)
     eng.load(ax)
     eng.init()
     st = eng.saturate()

@@ -359,6 +359,62 @@ def replicate(ax: Axioms, copies: int) -> Axioms:
                   concept_names=names, role_names=rnames)
 
 
+def elk_ranges(ax: Axioms) -> Tuple[Axioms, List[int], List[int]]:
+    """ELK's reading of range axioms (hazard H1 default; the engine's el::elk_ranges, which this
+    mirrors for the test oracles): every A ⊑ ∃r.B whose role has ranges ranges*(r) (of r and
+    its super-roles) and whose filler is a class points at a fresh concept F = n + i standing
+    for B ⊓ ranges*(r), one per (B, r) in first-occurrence order, with F ⊑ B and F ⊑ C; an
+    individual filler b gets b ⊑ C; datatype fillers are untouched; the range axioms are
+    consumed (the normalizer's range elimination, Normalizer.java:122-137, 455-497).
+    Returns (axioms, fresh fillers B, fresh roles r)."""
+    if not len(ax.range):
+        return ax, [], []
+    sup: Dict[int, List[int]] = {}
+    for r, s in ax.subrole.tolist():
+        sup.setdefault(r, []).append(s)
+    rng: Dict[int, List[int]] = {}
+    for r, c in ax.range.tolist():
+        rng.setdefault(r, []).append(c)
+    rstar: Dict[int, List[int]] = {}
+    for r in range(ax.n_roles):
+        seen, st, cs = {r}, [r], set()
+        while st:
+            q = st.pop()
+            cs.update(rng.get(q, ()))
+            for s in sup.get(q, ()):
+                if s not in seen:
+                    seen.add(s)
+                    st.append(s)
+        rstar[r] = sorted(cs)
+    fresh: Dict[Tuple[int, int], int] = {}
+    fb: List[int] = []
+    fr: List[int] = []
+    sub = ax.sub.tolist()
+    ind = set()
+    ex = ax.ex_rhs.copy()
+    for i, (a, r, b) in enumerate(ax.ex_rhs.tolist()):
+        if not rstar[r] or ax.kind[b] == KIND_DATATYPE:
+            continue
+        if ax.kind[b] == KIND_INDIVIDUAL:
+            ind.update((b, c) for c in rstar[r])
+            continue
+        f = fresh.get((b, r))
+        if f is None:
+            f = fresh[(b, r)] = ax.n_concepts + len(fb)
+            fb.append(b)
+            fr.append(r)
+            sub.append((f, b))
+            sub.extend((f, c) for c in rstar[r])
+        ex[i, 2] = f
+    sub.extend(sorted(ind))
+    n = ax.n_concepts + len(fb)
+    kind = np.zeros(n, dtype=np.uint8)
+    kind[:ax.n_concepts] = ax.kind
+    out = dataclasses.replace(ax, n_concepts=n, kind=kind, sub=_arr(sub, 2), ex_rhs=ex,
+                              range=np.zeros((0, 2), dtype=U32), concept_names=None)
+    return out, fb, fr
+
+
 def copy_slice(ax: Axioms, copies: int, index: int) -> Tuple[int, int]:
     """Concept-id range [lo, hi) owned by copy ``index`` of ``replicate(ax, copies)``."""
     m = ax.n_concepts - 2

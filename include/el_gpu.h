@@ -154,7 +154,17 @@ typedef struct el_group el_group;
  * {r∘s⊑t : s ∈ second(r), t ∈ third(r)}, which el_load builds in place of the told chains.
  * Default (0): the correct EL+ join on s. */
 #define EL_FLAG_COMPAT_DISTEL_CHAIN 0x1u
-#define EL_FLAGS_KNOWN (EL_FLAG_COMPAT_DISTEL_CHAIN)
+/* Range axioms (parity hazard H1).  Default: ELK's reading, as the
+ * normalizer's range elimination gives it (Normalizer.java:122-137, 455-497): a CR3 axiom
+ * A ⊑ ∃r.B whose role has ranges ranges*(r) (of r and its super-roles) points its links at a
+ * fresh internal filler F = B ⊓ ranges*(r) (ids n_concepts, n_concepts + 1, …; see
+ * el_fresh_fillers); an individual filler b gets b ⊑ C; datatype fillers are untouched.  The
+ * result rows cover the caller's concepts only; link fillers may be fresh ids.
+ * EL_FLAG_COMPAT_DISTEL_RANGE: DistEL's reading instead (RolePairHandler.java:471-479, K10
+ * ScriptsCollection.java:45-62): a link into Y activates Y ⊑ C, and C joins every S(X)
+ * holding Y. */
+#define EL_FLAG_COMPAT_DISTEL_RANGE 0x2u
+#define EL_FLAGS_KNOWN (EL_FLAG_COMPAT_DISTEL_CHAIN | EL_FLAG_COMPAT_DISTEL_RANGE)
 
 typedef struct el_config {
   int device;            /* HIP device ordinal (one context per GPU / rank) */
@@ -294,6 +304,9 @@ int el_result_info(el_ctx* ctx, el_result* res);   /* the out fields only */
 int el_copy_result(el_ctx* ctx, el_result* res);   /* EL_ERANGE if a buffer is too small */
 /* pair q -> (role, filler), q ascending = (role, filler) ascending */
 int el_pair_table(el_ctx* ctx, uint32_t* role, uint32_t* filler, size_t cap, size_t* n);
+/* ELK range fillers (default range reading): fresh concept n_concepts + i stands for
+ * filler[i] ⊓ ranges*(role[i]); *n = their number (0 without range axioms) */
+int el_fresh_fillers(el_ctx* ctx, uint32_t* filler, uint32_t* role, size_t cap, size_t* n);
 /* page-locked host memory for result buffers (NULL on failure); a JNI host wraps it in a
  * direct ByteBuffer (NewDirectByteBuffer) */
 void* el_host_alloc(size_t bytes);

@@ -12,12 +12,20 @@ BOTTOM, TOP = 0, 1
 DATATYPE = 3
 
 
-def saturate(ax, distel_chain: bool = False) -> Tuple[Dict[int, Set[int]], Set[Tuple[int, int, int]]]:
+def saturate(ax, distel_chain: bool = False,
+             distel_range: bool = False) -> Tuple[Dict[int, Set[int]], Set[Tuple[int, int, int]]]:
     """distel_chain: CR6 as DistEL runs it (hazard H2), restated literally from the store
     layout: DB1["Yr"] holds X for (X,Y) in R(r), r first in a chain; DB4["Yr"] holds Z for
     (Y,Z) in R(s), s second in a chain whose FIRST role is r (RolePairHandler.java:395-443);
     CR6 adds (X,Z) to the t of every chain whose first role is r, without checking s
     (Type5AxiomProcessorBase.java:128-143)."""
+    if not distel_range and len(ax.range):
+        # ranges read ELK's way: normalize them away first (distel_amd.ir.elk_ranges); the
+        # fresh fillers' rows are internal
+        from distel_amd import ir
+        n_user = ax.n_concepts
+        S, R = saturate(ir.elk_ranges(ax)[0], distel_chain, True)
+        return {x: v for x, v in S.items() if x < n_user}, {t for t in R if t[0] < n_user}
     n = ax.n_concepts
     kind = [int(k) for k in ax.kind]
     # init: S(X) = {X, ⊤}  (AxiomLoader.java:1237-1245, individuals :1281-1289)
@@ -74,7 +82,7 @@ def saturate(ax, distel_chain: bool = False) -> Tuple[Dict[int, Set[int]], Set[T
             for r1, d in domain:  # domain  RolePairHandler.java:480-490
                 if r1 == r and x != TOP and kind[x] != DATATYPE:
                     S[x].add(d)
-            for r1, c in rng:  # range (H1 closure)  RolePairHandler.java:471-479
+            for r1, c in rng:  # range, DistEL's reading (H1, closed)  RolePairHandler.java:471-479
                 if r1 == r and y != TOP and kind[y] != DATATYPE:
                     for z in range(n):
                         if y in S[z]:

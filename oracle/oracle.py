@@ -64,12 +64,22 @@ def _load():
 
 
 class Oracle:
-    """mode 0 = semi-naive Jacobi supersteps (GPU-identical deltas/events), 1 = naive fixpoint."""
+    """mode 0 = semi-naive Jacobi supersteps (GPU-identical deltas/events), 1 = naive fixpoint.
 
-    def __init__(self, ax, mode: int = 0):
+    Range axioms are read the way the engine reads them: ELK-style by default (the ontology is
+    first put through distel_amd.ir.elk_ranges, the mirror of the engine's el::elk_ranges, and
+    facts() / links() cover the given concepts' rows), DistEL's way (hazard H1, el_oracle.c's
+    range rule) with compat_range=True.  stats(), trace() and events() are the whole closure's,
+    like the engine's el_stats."""
+
+    def __init__(self, ax, mode: int = 0, compat_range: bool = False):
         from distel_amd.engine import AxiomsView
+        from distel_amd import ir
         self.lib = _load()
         self.ctx = C.c_void_p()
+        self.n_user = ax.n_concepts
+        if not compat_range:
+            ax, _, _ = ir.elk_ranges(ax)
         self._view = AxiomsView(ax)
         rc = self.lib.elo_create(C.byref(self.ctx), C.byref(self._view.struct), mode)
         if rc != 0:
@@ -118,7 +128,8 @@ class Oracle:
         a = np.zeros(n, np.uint32)
         p = lambda v: v.ctypes.data_as(C.POINTER(C.c_uint32))
         self.lib.elo_copy_facts(self.ctx, p(x), p(a), n)
-        return x, a
+        keep = x < self.n_user  # (ELK range fillers are internal rows)
+        return x[keep], a[keep]
 
     def links(self):
         n = int(self.lib.elo_num_links(self.ctx))
@@ -126,6 +137,7 @@ class Oracle:
         p = lambda v: v.ctypes.data_as(C.POINTER(C.c_uint32))
         self.lib.elo_copy_links(self.ctx, p(x), p(r), p(y), n)
         order = np.lexsort((y, r, x))
+        order = order[x[order] < self.n_user]
         return x[order], r[order], y[order]
 
     def trace(self):
@@ -141,8 +153,8 @@ class Oracle:
         return ev.reshape(NUM_KERNELS, NUM_EVENTS)
 
 
-def saturate(ax, mode: int = 0) -> Oracle:
-    o = Oracle(ax, mode)
+def saturate(ax, mode: int = 0, compat_range: bool = False) -> Oracle:
+    o = Oracle(ax, mode, compat_range)
     o.init()
     o.saturate()
     return o

@@ -193,8 +193,15 @@ def run(rank: Rank, allgather: Callable[[dict], List[dict]], max_steps: int = 10
     raise RuntimeError("no fixpoint")
 
 
-def saturate_inprocess(ax, parts: int):
-    """All ranks in one process, in lock-step.  Returns (S, R, supersteps) as plain sets."""
+def saturate_inprocess(ax, parts: int, compat_range: bool = True):
+    """All ranks in one process, in lock-step.  Returns (S, R, supersteps) as plain sets.
+    The model's range rule is DistEL's (compat_range); compat_range=False reads ranges ELK's
+    way, as the engine does by default: the ontology goes through distel_amd.ir.elk_ranges and
+    the fresh fillers' rows are left out."""
+    n_user = ax.n_concepts
+    if not compat_range:
+        from distel_amd import ir
+        ax = ir.elk_ranges(ax)[0]
     rs = [Rank(ax, lo, hi) for lo, hi in ranges(ax.n_concepts, parts)]
     t = 0
     while True:
@@ -209,4 +216,6 @@ def saturate_inprocess(ax, parts: int):
     for r in rs:
         S.update(r.S)
         R |= r.links
+    S = {x: v for x, v in S.items() if x < n_user}
+    R = {l for l in R if l[0] < n_user}
     return S, R, t

@@ -23,7 +23,8 @@
  *                                  from A ⊑ ∃r.B goes to the filler B ⊓ ranges(r) instead, i.e.
  *                                  the link target is the normalizer's fresh X_{B,r} with
  *                                  X ⊑ B, X ⊑ C for C ∈ ranges*(r) (Normalizer.java:122-137,
- *                                  455-497); see wl_saturate.
+ *                                  455-497); an individual filler b is an instance of each C;
+ *                                  see wl_saturate.
  *   init S(X) = {X, ⊤}             AxiomLoader.java:1237-1245, 1281-1289
  */
 #include <stdint.h>
@@ -297,8 +298,11 @@ int wl_saturate(const el_axioms* ax, int distel_range, wl_result** out) {
     vec fkey_b = {0}, fkey_r = {0};
     for (uint32_t i = 0; i < ax->n_ex_rhs; ++i) {
       const uint32_t r = ax->exr_r[i], b = ax->exr_b[i];
-      if (w->rng_ptr[r + 1] == w->rng_ptr[r]) {
-        exr_b2[i] = b;
+      const uint8_t kb = ax->concept_kind ? ax->concept_kind[b] : EL_KIND_CLASS;
+      exr_b2[i] = b;
+      if (w->rng_ptr[r + 1] == w->rng_ptr[r] || kb == EL_KIND_DATATYPE) continue;
+      if (kb == EL_KIND_INDIVIDUAL) {  /* an r-successor individual is in every range of r */
+        for (uint32_t j = w->rng_ptr[r]; j < w->rng_ptr[r + 1]; ++j) vpush(&sa, b), vpush(&sb, w->rng_all[j]);
         continue;
       }
       uint32_t f = UINT32_MAX;
@@ -388,25 +392,9 @@ int wl_saturate(const el_axioms* ax, int distel_range, wl_result** out) {
     w->srow[x].n = keep;
     qsort(w->srow[x].a, w->srow[x].n, sizeof(uint32_t), cmp_u32);
     w->n_facts += keep;
-    /* links (r, y) of x: a fresh filler F_{B,r} reports as (r, B) */
-    for (uint64_t j = 0; j < w->out[x].n; j += 2) {
-      uint32_t y = w->out[x].a[j + 1];
-      if (y >= w->N_out) {
-        /* the fresh filler's first told super is B */
-        y = w->subA.val[w->subA.ptr[y]];
-        w->out[x].a[j + 1] = y;
-      }
-    }
+    /* links (r, y) of x, sorted (a fresh filler F keeps its id, as the engine reports it) */
     qsort(w->out[x].a, w->out[x].n / 2, 2 * sizeof(uint32_t), cmp_pair);
-    uint64_t m = 0;
-    for (uint64_t j = 0; j < w->out[x].n; j += 2)
-      if (!m || w->out[x].a[m - 2] != w->out[x].a[j] || w->out[x].a[m - 1] != w->out[x].a[j + 1]) {
-        w->out[x].a[m] = w->out[x].a[j];
-        w->out[x].a[m + 1] = w->out[x].a[j + 1];
-        m += 2;
-      }
-    w->out[x].n = m;
-    w->n_links += m / 2;
+    w->n_links += w->out[x].n / 2;
   }
   return w->oom ? -1 : 0;
 }

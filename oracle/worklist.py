@@ -61,9 +61,10 @@ class Closure:
         return h.hexdigest()
 
 
-def saturate(ax, distel_range: bool = True) -> Closure:
-    """The closure of ax by worklist completion.  distel_range: DistEL's range semantics (K10,
-    hazard H1); False: ELK's (ranges folded into fresh existential fillers)."""
+def saturate(ax, distel_range: bool = False) -> Closure:
+    """The closure of ax by worklist completion.  Ranges are read ELK's way (folded into fresh
+    existential fillers, as the engine's default), DistEL's way (K10, hazard H1) with
+    distel_range=True."""
     from distel_amd.engine import AxiomsView
     lib = _load()
     view = AxiomsView(ax)

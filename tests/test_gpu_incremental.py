@@ -1,7 +1,9 @@
 """GPU: incremental classification.  An ontology split into a base
 and increments, classified base-first with el_add_axioms in between, must reach exactly the
 closure the CPU oracle computes from scratch on the union (size-independent property: the
-least fixpoint does not depend on the order axioms arrive in)."""
+least fixpoint does not depend on the order axioms arrive in).  The random ontologies carry
+range axioms, so these runs read ranges DistEL's way (EL_FLAG_COMPAT_DISTEL_RANGE): increments
+are refused with ELK range fillers (test_increment_rejects_elk_ranges)."""
 import numpy as np
 import pytest
 
@@ -39,14 +41,14 @@ def _split(ax: Axioms, parts: int, seed: int, grow: bool):
 
 
 def _check(ax, pieces, oracle_lib):
-    eng = engine.Engine(device=0)
+    eng = engine.Engine(device=0, compat_range=True)
     eng.load(pieces[0])
     eng.init()
     eng.saturate()
     for inc in pieces[1:]:
         eng.add_axioms(inc)
         st = eng.saturate()
-    o = oracle_lib.saturate(ax, 0)
+    o = oracle_lib.saturate(ax, 0, compat_range=True)
     gx, ga = eng.facts()
     ox, oa = o.facts()
     assert np.array_equal(gx, ox) and np.array_equal(ga, oa), "S(X) differs from the from-scratch closure"
@@ -72,12 +74,12 @@ def test_increments_workloads(name, scale, oracle_lib):
 def test_increment_before_init(oracle_lib):
     ax = generators.random_small(5, n=30, n_roles=3)
     a, b = _split(ax, 2, 5, grow=True)
-    eng = engine.Engine(device=0)
+    eng = engine.Engine(device=0, compat_range=True)
     eng.load(a)
     eng.add_axioms(b)  # nothing saturated yet: a plain reload of old ∪ inc
     eng.init()
     eng.saturate()
-    o = oracle_lib.saturate(ax, 0)
+    o = oracle_lib.saturate(ax, 0, compat_range=True)
     assert np.array_equal(np.stack(eng.facts()), np.stack(o.facts()))
     eng.close()
 
@@ -89,5 +91,21 @@ def test_increment_rejects_shrink():
     small = Axioms.build(10, ax.n_roles, kind=ax.kind[:10])
     with pytest.raises(engine.ElError) as e:
         eng.add_axioms(small)
+    assert e.value.code == engine.EL_EINVAL
+    eng.close()
+
+
+def test_increment_rejects_elk_ranges():
+    """ELK range fillers are numbered after the caller's concepts, which an increment may
+    extend: with range axioms, increments need the DistEL range reading."""
+    ax = generators.random_small(6, n=30, n_roles=3)
+    assert len(ax.range)
+    a, b = _split(ax, 2, 6, grow=False)
+    eng = engine.Engine(device=0)
+    eng.load(a)
+    eng.init()
+    eng.saturate()
+    with pytest.raises(engine.ElError) as e:
+        eng.add_axioms(b)
     assert e.value.code == engine.EL_EINVAL
     eng.close()

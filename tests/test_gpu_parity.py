@@ -50,6 +50,32 @@ def test_kat_gpu(path, oracle_mod):
     eng.close()
 
 
+def test_range_readings_gpu(oracle_mod):
+    """Hazard H1 both ways: ELK's reading (default) on the ELK range KATs and random
+    ontologies with ranges is covered by test_kat_gpu / test_fuzz_gpu; DistEL's reading
+    (EL_FLAG_COMPAT_DISTEL_RANGE, RolePairHandler.java:471-479) on its KAT and on random
+    ontologies, bit-exact with the oracle's DistEL range rule (events and deltas included)."""
+    ax, exp = kat.load_kat(kat.compat_file("compat_range_distel.elax"))
+    eng, _ = engine.classify(ax, device=0, compat_range=True)
+    kat.check(exp, *kat.to_sets(*eng.facts(), *eng.links()))
+    _assert_same(eng, oracle_mod.saturate(ax, 0, compat_range=True))
+    eng.close()
+    eng = engine.Engine(device=0, compat_range=True)
+    for seed in range(150):
+        ax = generators.random_small(7700 + seed, n=8 + seed % 50, n_roles=1 + seed % 5)
+        eng.load(ax)
+        eng.init()
+        eng.saturate()
+        _assert_same(eng, oracle_mod.saturate(ax, 0, compat_range=True))
+    eng.close()
+    # ELK's reading: the fresh fillers are reported, and every one is B ⊓ ranges*(r)
+    ax, _ = kat.load_kat(os.path.join(kat.GOLDEN, "kat_range.elax"))
+    eng, _ = engine.classify(ax, device=0)
+    b, r = eng.fresh_fillers()
+    assert b.size == 1 and eng.copy_result().row_hi == ax.n_concepts
+    eng.close()
+
+
 def test_fuzz_gpu(oracle_mod):
     eng = engine.Engine(device=0)
     for seed in range(300):

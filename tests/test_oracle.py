@@ -102,6 +102,28 @@ def test_closure_digests(oracle_lib):
         assert _closure_digest(oracle_lib.saturate(ax, 0)) == clo, name
 
 
+def test_range_compat_kat(oracle_lib):
+    """Hazard H1, DistEL's reading (compat_range): the KAT, the C oracle and the literal Python
+    restatement agree, and differ from the ELK reading (the default) on it."""
+    ax, exp = kat.load_kat(kat.compat_file("compat_range_distel.elax"))
+    kat.check(exp, *naive.saturate(ax, distel_range=True))
+    o = oracle_lib.saturate(ax, 0, compat_range=True)
+    kat.check(exp, *kat.to_sets(*o.facts(), *o.links()))
+    assert naive.saturate(ax) != naive.saturate(ax, distel_range=True)
+
+
+def test_range_readings_random(oracle_lib):
+    import worklist
+    for seed in range(300):
+        ax = generators.random_small(4400 + seed, n=8 + seed % 40, n_roles=1 + seed % 4)
+        for compat in (False, True):
+            o = oracle_lib.saturate(ax, 0, compat_range=compat)
+            S, R = naive.saturate(ax, distel_range=compat)
+            assert (S, R) == kat.to_sets(*o.facts(), *o.links()), (seed, compat)
+            w = worklist.saturate(ax, distel_range=compat)
+            assert _same(w, o), (seed, compat)
+
+
 def test_h2_compat_kat_python_naive():
     """The literal DistEL CR6 restatement (naive.saturate(distel_chain=True)) reproduces H2."""
     ax, exp = kat.load_kat(kat.compat_file("compat_h2_two_chains.elax"))

@@ -21,14 +21,14 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 def test_kat_partition_model(path):
     ax, exp = kat.load_kat(path)
     for parts in (1, 2, 3):
-        S, R, _ = pm.saturate_inprocess(ax, min(parts, ax.n_concepts))
+        S, R, _ = pm.saturate_inprocess(ax, min(parts, ax.n_concepts), compat_range=False)
         kat.check(exp, S, R)
 
 
 def test_partition_model_equals_naive():
     for seed in range(200):
         ax = generators.random_small(seed, n=6 + seed % 34, n_roles=1 + seed % 4)
-        S0, R0 = naive.saturate(ax)
+        S0, R0 = naive.saturate(ax, distel_range=True)  # the model's own (DistEL) range rule
         for parts in (2, 3, 5):
             S, R, _ = pm.saturate_inprocess(ax, min(parts, ax.n_concepts))
             assert S == S0 and R == R0, (seed, parts)
@@ -79,7 +79,7 @@ def test_partition_model_gloo_two_ranks():
         assert p.exitcode == 0
     for i, seed in enumerate(seeds):
         ax = generators.random_small(seed, n=30, n_roles=3)
-        S0, R0 = naive.saturate(ax)
+        S0, R0 = naive.saturate(ax, distel_range=True)
         S, R = {}, set()
         steps = set()
         for rank in range(world):
