@@ -99,13 +99,12 @@ def test_increment_rejects_elk_ranges():
     """ELK range fillers are numbered after the caller's concepts, which an increment may
     extend: with range axioms, increments need the DistEL range reading."""
     ax = generators.random_small(6, n=30, n_roles=3)
-    assert len(ax.range)
-    a, b = _split(ax, 2, 6, grow=False)
+    inc = Axioms.build(ax.n_concepts, ax.n_roles, kind=ax.kind, range=[(0, 5)])
     eng = engine.Engine(device=0)
-    eng.load(a)
+    eng.load(ax)
     eng.init()
     eng.saturate()
     with pytest.raises(engine.ElError) as e:
-        eng.add_axioms(b)
+        eng.add_axioms(inc)
     assert e.value.code == engine.EL_EINVAL
     eng.close()

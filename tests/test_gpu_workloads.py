@@ -3,8 +3,9 @@ per-superstep deltas and per-phase event counts).
 
 * G3X = G3 + 1 % sibling disjointness (A ⊓ B ⊑ ⊥), domains on 8 roles and ranges on 3: the
   ⊥ rule (TypeBottomAxiomProcessorBase.java:62-123, incl. ⊥ crossing links), domain and range
-  (RolePairHandler.java:456-491, DistEL's range semantics) at SNOMED scale, where G1–G5 never
-  trip them.
+  (RolePairHandler.java:456-491) at SNOMED scale, where G1–G5 never trip them — ranges both
+  ways: DistEL's reading (EL_FLAG_COMPAT_DISTEL_RANGE: range activations) and ELK's (the
+  default: fresh range fillers).
 * G5 (BASELINE configs[4], role-heavy) at full size: depth-20 chains, 50 transitive roles and
   hub fillers — the heaviest reference rule, T3_2 (ShardInfo.properties:9,
   Type3_2AxiomProcessorBase.java:67-96), over predecessor lists of up to ~39 k entries.
@@ -30,8 +31,8 @@ def _same(eng, o):
 
 def test_g3x_bottom_domain_range_full(oracle_lib):
     ax = generators.workload("g3x")
-    eng, st = engine.classify(ax, device=0)
-    o = oracle_lib.saturate(ax, 0)
+    eng, st = engine.classify(ax, device=0, compat_range=True)
+    o = oracle_lib.saturate(ax, 0, compat_range=True)
     _same(eng, o)
     assert st["derived"] == o.stats()["derived"]
     # the rules this workload exists for did fire
@@ -49,6 +50,19 @@ def test_g3x_bottom_domain_range_full(oracle_lib):
         have = np.zeros(ax.n_concepts, bool)
         have[x[a == d]] = True
         assert subj.size and have[subj].all()
+    eng.close()
+
+
+def test_g3x_elk_ranges_full(oracle_lib):
+    """G3X with ranges read ELK's way (the default): fresh fillers B ⊓ ranges*(r) for the
+    range roles' existentials; the caller's rows bit-exact with the oracle's."""
+    ax = generators.workload("g3x")
+    eng, st = engine.classify(ax, device=0)
+    o = oracle_lib.saturate(ax, 0)
+    _same(eng, o)
+    fb, fr = eng.fresh_fillers()
+    assert fb.size > 100 and set(fr.tolist()) <= {r for r, _ in ax.range.tolist()}
+    assert st["activations"] == 0
     eng.close()
 
 
