@@ -84,7 +84,11 @@ enum : uint32_t {
 const uint32_t kRuleMask[EL_NUM_RULE_TYPES] = {
     M_R1, M_R2, M_R3 | M_RDOM | M_RRNG, M_R4Y, M_R4L | M_R4P, M_R5, M_R6, M_RBOT};
 
-enum : uint32_t { JOB_PRED_S = 0, JOB_PRED_L = 1, JOB_R6A = 3 };
+// JOB_PRED_U: JOB_PRED_S without the B ∈ S(x) probe, for the first superstep over the base
+// links (M_LEMPTY): S(x) holds only the told closure then, so nearly every conclusion of the
+// fan-out is new (G3: 96 M candidates) and the probe was one random read each that the
+// commit's atomicOr repeats anyway
+enum : uint32_t { JOB_PRED_S = 0, JOB_PRED_L = 1, JOB_PRED_U = 2, JOB_R6A = 3 };
 
 struct ElError {
   int code;
@@ -128,6 +132,8 @@ struct DIndex {
   // hold (el_ctx::column_window; the whole ontology: 2, N, i.e. column = concept id)
   uint32_t c_lo, c_hi;
   uint32_t part;               // 1 = partitioned protocol (oracle/partition_model.py)
+  uint32_t base;               // 1 = the base links {(X, p) : p ∈ exr(X)} are in the link log and
+                               // rows but not in the link set (el_ctx::install_base)
   const uint8_t* role_chs;     // r -> r is the second role of some chain (its links are exchanged)
 };
 
@@ -402,6 +408,36 @@ __device__ __forceinline__ bool hash_insert(unsigned long long* t, unsigned long
     if (prev == key) return false;
     h = (h + 1) & mask;
   }
+}
+
+// Base links: the links every init fact X ∈ S(X) implies by CR3 over its told closure,
+// {(X, p) : p ∈ exr(X)} (G3: 25 M of 33 M links).  el_saturate writes them into the link log
+// and the predecessor / successor rows before the first superstep, with coalesced stores,
+// instead of deriving them as 25 M candidates that the commit would hash one by one; the
+// set of them is exr itself, so membership is a binary search of the row exr(X) (sorted).
+__device__ __forceinline__ bool base_has(const DIndex& ix, uint32_t x, uint32_t pid, Ev& ev) {
+  ev.v[EL_EV_ROW]++;
+  uint32_t lo = ix.exr_ptr[x], hi = ix.exr_ptr[x + 1];
+  while (lo < hi) {
+    const uint32_t mid = (lo + hi) >> 1;
+    ev.v[EL_EV_ENT]++;
+    const uint32_t v = ix.exr_pid[mid];
+    if (v == pid) return true;
+    if (v < pid)
+      lo = mid + 1;
+    else
+      hi = mid;
+  }
+  return false;
+}
+
+// (x, pid) known at t-1: a base link, or in the link set (lempty: the set is empty, no probe)
+__device__ __forceinline__ bool link_known(const DIndex& ix, const DState& st, uint32_t x, uint32_t pid,
+                                           bool lempty, Ev& ev) {
+  if (ix.base && base_has(ix, x, pid, ev)) return true;
+  if (lempty) return false;
+  ev.v[EL_EV_HASH]++;
+  return hash_contains(st.lhash, st.lmask, link_key(pid, x));
 }
 
 // (role, filler) -> pid by a scan of the filler's pair range (sorted by role)
@@ -792,7 +828,8 @@ __device__ void expand_s(const DIndex& ix, const DState& st, BlockQ& q, uint32_t
     // {A} ∪ told*(A)): the facts of a closure were covered by the fact that emitted it
     const bool star = act && f != 1;
     {  // A ∈ S(X), A ⊑ ∃r.B  =>  (X, B) ∈ R(r)
-      const bool on = star && (mask & M_R3);
+      // (an init fact's own links are the base links, already in place)
+      const bool on = star && (mask & M_R3) && !(ix.base && f == 2);
       if (on) ev.v[EL_EV_ROW]++;
       wave_rows(on ? m0.z : 0u, on ? m1.z : 0u, [&](bool v, uint32_t own, uint32_t j) {
         const uint32_t Xo = __shfl(X, (int)own);
@@ -801,11 +838,7 @@ __device__ void expand_s(const DIndex& ix, const DState& st, BlockQ& q, uint32_t
         if (v) {
           pid = ix.exr_pid[j];
           ev.v[EL_EV_ENT]++;
-          nw = true;
-          if (!(mask & M_LEMPTY)) {  // (first superstep: 25 M misses spared on G3)
-            ev.v[EL_EV_HASH]++;
-            nw = !hash_contains(st.lhash, st.lmask, link_key(pid, Xo));
-          }
+          nw = !link_known(ix, st, Xo, pid, mask & M_LEMPTY, ev);
         }
         emit_l(st, q, nw, Xo, pid, ev);
       });
@@ -838,7 +871,7 @@ __device__ void expand_s(const DIndex& ix, const DState& st, BlockQ& q, uint32_t
           }
         }
         emit_p(st, fresh, pid, B, ev);
-        emit_job(st, q, pl > 0, JOB_PRED_S, pb, pl, 0, B, ev);
+        emit_job(st, q, pl > 0, (mask & M_LEMPTY) ? JOB_PRED_U : JOB_PRED_S, pb, pl, 0, B, ev);
       });
     }
     if (act && (mask & M_RBOT) && ix.has_bot && A == EL_BOTTOM) {  // ⊥ ∈ S(Y=X) new, (X', Y) ∈ R(*)  =>  ⊥ ∈ S(X')
@@ -852,7 +885,7 @@ __device__ void expand_s(const DIndex& ix, const DState& st, BlockQ& q, uint32_t
         }
         ev.v[EL_EV_ROW]++;
         const uint2 row = gap_row(st.pr, p);
-        emit_job(st, q, row.y > 0, JOB_PRED_S, row.x, row.y, 0, EL_BOTTOM, ev);
+        emit_job(st, q, row.y > 0, (mask & M_LEMPTY) ? JOB_PRED_U : JOB_PRED_S, row.x, row.y, 0, EL_BOTTOM, ev);
       }
     }
     if (act && (mask & M_RRNG) && ix.has_range) {  // Y=A ∈ S(X) new, active range (Y, C)  =>  C ∈ S(X)
@@ -955,8 +988,7 @@ __device__ void expand_l(const DIndex& ix, const DState& st, BlockQ& q, uint32_t
         for (uint32_t j = ix.psup_ptr[pid]; j < q1; ++j) {
           const uint32_t sp = ix.psup_pid[j];
           ev.v[EL_EV_ENT]++;
-          ev.v[EL_EV_HASH]++;
-          emit_l(st, q, !hash_contains(st.lhash, st.lmask, link_key(sp, X)), X, sp, ev);
+          emit_l(st, q, !link_known(ix, st, X, sp, mask & M_LEMPTY, ev), X, sp, ev);
         }
       }
       if (mask & M_R6) {  // r ∘ s ⊑ t
@@ -1021,7 +1053,8 @@ __device__ void expand_l(const DIndex& ix, const DState& st, BlockQ& q, uint32_t
 //  JOB_PRED_S  preds(pid) × {B}         (CR4 half-1, ⊥)
 //  JOB_PRED_L  preds(pq)  × {pid_t}     (CR6, r second)
 //  JOB_R6A     succ(Y)    × chains of r (CR6, r first)
-__global__ void k_jobs(DIndex ix, DState st) {
+__global__ void k_jobs(DIndex ix, DState st, uint32_t mask) {
+  const bool lempty = mask & M_LEMPTY;
   __shared__ BlockQ q;
   q_init(q);
   Ev ev;
@@ -1044,14 +1077,17 @@ __global__ void k_jobs(DIndex ix, DState st) {
     const uint32_t type = jb.y >> 28;
     wave_rows(jb.x, jb.x + len, [&](bool v, uint32_t own, uint32_t k) {
       const uint32_t t = __shfl(type, (int)own), a = __shfl(jb.z, (int)own), b = __shfl(jb.w, (int)own);
-      if (t == JOB_PRED_S) {  // preds(pid) × {B}
+      if (t == JOB_PRED_S || t == JOB_PRED_U) {  // preds(pid) × {B}
         uint32_t xp = 0;
         bool nw = false;
         if (v) {
           xp = st.pr.val[k];
           ev.v[EL_EV_ENT]++;
-          ev.v[EL_EV_TEST]++;
-          nw = !test_bit(ix, st.bits, xp, b);
+          nw = true;
+          if (t == JOB_PRED_S) {
+            ev.v[EL_EV_TEST]++;
+            nw = !test_bit(ix, st.bits, xp, b);
+          }
         }
         emit_s(st, q, nw, xp, b, ev);
       } else if (t == JOB_PRED_L) {  // preds(pq) × {pid_t}
@@ -1060,8 +1096,7 @@ __global__ void k_jobs(DIndex ix, DState st) {
         if (v) {
           xp = st.pr.val[k];
           ev.v[EL_EV_ENT]++;
-          ev.v[EL_EV_HASH]++;
-          nw = !hash_contains(st.lhash, st.lmask, link_key(a, xp));
+          nw = !link_known(ix, st, xp, a, lempty, ev);
         }
         emit_l(st, q, nw, xp, a, ev);
       } else {  // JOB_R6A: succ(Y) × chains of r
@@ -1084,8 +1119,7 @@ __global__ void k_jobs(DIndex ix, DState st) {
           uint32_t pt = NONE;
           if (s == s2) {
             pt = pair_lookup(ix, tt, Z, ev);
-            ev.v[EL_EV_HASH]++;
-            nw = !hash_contains(st.lhash, st.lmask, link_key(pt, X));
+            nw = !link_known(ix, st, X, pt, lempty, ev);
           }
           emit_l(st, q, nw, X, pt, ev);
         }
@@ -1754,6 +1788,49 @@ __global__ void k_gap_move(const uint32_t* __restrict__ s_old, const uint32_t* _
   }
 }
 
+// ---- base links (el_ctx::install_base): CSR rows written out whole, one entry per thread.
+// A block takes 256 consecutive entries; two lanes find the rows of its first and last entry
+// (binary searches of ptr), then each entry's row is searched within that span only — a hub
+// row (a filler with 10^5 predecessors) spreads over many blocks instead of one wave.
+// out_row != null: flat (row, value) pairs at the entry's index (the link log from exr);
+// else: the entry at its row's slot of a gapped CSR just laid out (predecessor rows from exrT,
+// successor rows from exrC), whose lengths k_gap_len sets.
+__device__ __forceinline__ uint32_t csr_row_of(const uint32_t* __restrict__ ptr, uint32_t lo, uint32_t hi, uint32_t j) {
+  // the largest r in [lo, hi] with ptr[r] <= j (ptr[lo] <= j)
+  while (lo < hi) {
+    const uint32_t mid = (lo + hi + 1) >> 1;
+    if (ptr[mid] <= j)
+      lo = mid;
+    else
+      hi = mid - 1;
+  }
+  return lo;
+}
+__global__ void __launch_bounds__(256) k_csr_scatter(const uint32_t* __restrict__ ptr, const uint32_t* __restrict__ a,
+                                                     uint32_t rows, uint32_t n, uint32_t* __restrict__ out_row,
+                                                     uint32_t* __restrict__ out_val, const uint32_t* __restrict__ start,
+                                                     uint32_t* __restrict__ val) {
+  __shared__ uint32_t span[2];
+  for (uint32_t base = blockIdx.x * 256u; base < n; base += gridDim.x * 256u) {
+    if (threadIdx.x < 2) span[threadIdx.x] = csr_row_of(ptr, 0, rows - 1, threadIdx.x ? min(base + 255u, n - 1) : base);
+    __syncthreads();
+    const uint32_t j = base + threadIdx.x;
+    if (j < n) {
+      const uint32_t r = csr_row_of(ptr, span[0], span[1], j), v = a[j];
+      if (out_row) {
+        out_row[j] = r;
+        out_val[j] = v;
+      } else {
+        val[start[r] + (j - ptr[r])] = v;
+      }
+    }
+    __syncthreads();
+  }
+}
+__global__ void k_gap_len(const uint32_t* __restrict__ ptr, uint32_t rows, uint32_t* __restrict__ len) {
+  for (uint32_t r = blockIdx.x * blockDim.x + threadIdx.x; r < rows; r += gridDim.x * blockDim.x) len[r] = ptr[r + 1] - ptr[r];
+}
+
 // rows[i] -> map[rows[i]] (pair ids after an increment re-numbered the pair universe)
 __global__ void k_remap(uint32_t* __restrict__ v, uint64_t n, const uint32_t* __restrict__ map) {
   const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
@@ -2103,6 +2180,8 @@ struct el_ctx {
   std::vector<uint32_t> rank_role, rank_y;   // host: the pair (role, filler) of rank q
   hipStream_t cstream = nullptr;             // copy-back DMA, beside the row builds
   hipEvent_t ev_rows[2] = {nullptr, nullptr};
+  // base links by predecessor (exrT: pid -> X) and by successor (exrC: X -> chain-second pid)
+  const uint32_t *exrT_ptr = nullptr, *exrT_x = nullptr, *exrC_ptr = nullptr, *exrC_p = nullptr;
   GapCsr PR, SC, PP;   // predecessors per pid, successors per X, propagations per pid
   uint32_t* pin_word = nullptr;  // pinned scratch for the rare synchronous readbacks
   bool need_pred = true;      // predecessor CSR has readers (CR4, ⊥, CR6)
@@ -2132,6 +2211,9 @@ struct el_ctx {
   unsigned long long* ev_host = nullptr;  // pinned copy of ev_sum
   bool events_queued = false;
   uint64_t s_count = 0, l_count = 0, a_count = 0, p_count = 0, s_init = 0;
+  uint64_t l_base = 0;  // base links at the head of the link log (ix.base; install_base)
+  bool fresh = false;   // el_init ran and no superstep since: el_saturate installs the base links
+  void install_base();
   uint64_t wm_s[EL_NUM_RULE_TYPES] = {}, wm_l[EL_NUM_RULE_TYPES] = {}, wm_a[EL_NUM_RULE_TYPES] = {},
            wm_p[EL_NUM_RULE_TYPES] = {}, wm_x = 0;
   el_stats last{};
@@ -2402,6 +2484,10 @@ std::string el_ctx::install_index(el::HostIndex&& hnew) {
   d.rng_ptr = up32(h.rng.ptr);
   d.rng_c = up32(h.rng.a);
   d.role_has_exl = up8(h.role_has_exl);
+  exrT_ptr = up32(h.exrT.ptr);
+  exrT_x = up32(h.exrT.a);
+  exrC_ptr = up32(h.exrC.ptr);
+  exrC_p = up32(h.exrC.a);
   {  // link export order: pair ids ranked by (role, filler)
     std::vector<uint32_t> ord(h.P), rank(h.P);
     std::iota(ord.begin(), ord.end(), 0u);
@@ -2823,6 +2909,8 @@ void el_ctx::reset_state() {
   }
   bits_logged = true;  // from here on every set bit is in the fact log (k_init and k_commit append)
   s_count = l_count = a_count = p_count = s_init = x_count = 0;
+  l_base = 0;
+  ix.base = 0;
   rs.n = rl.n = ~0ull;  // result rows are stale
   act_n = ~0ull;
   for (int r = 0; r < EL_NUM_RULE_TYPES; ++r) wm_s[r] = wm_l[r] = wm_a[r] = wm_p[r] = 0;
@@ -2840,10 +2928,10 @@ void el_ctx::rehash_links(uint64_t cap) {
   lhash_cap = cap;
   lhash = dalloc<unsigned long long>(cap);
   HIPCHK(hipMemsetAsync(lhash, 0xff, cap * sizeof(unsigned long long), stream));
-  if (l_count)
+  if (l_count > l_base)  // the base links stay out of the set
     launch(EL_K_REHASH, [&] {
-      hipLaunchKernelGGL(k_rehash, dim3(grid_for(l_count)), dim3(BLOCK), 0, stream, lhash, cap - 1,
-                         llog_x, llog_p, (uint32_t)l_count);
+      hipLaunchKernelGGL(k_rehash, dim3(grid_for(l_count - l_base)), dim3(BLOCK), 0, stream, lhash, cap - 1,
+                         llog_x + l_base, llog_p + l_base, (uint32_t)(l_count - l_base));
     });
 }
 
@@ -2974,7 +3062,7 @@ bool el_ctx::superstep(uint32_t mask, uint64_t sb, uint64_t se, uint64_t lb, uin
     // ---- capacities: every candidate could be new.  Growth copies device arrays outside
     // the stream, so the previous step's kernels must have finished first.
     const bool grow = s_count + cs_cap + ct_cap > slog_cap || l_count + cl_cap > llog_cap ||
-                      2 * (l_count + cl_cap) > lhash_cap || a_count + ca_cap > alog_cap ||
+                      2 * (l_count - l_base + cl_cap) > lhash_cap || a_count + ca_cap > alog_cap ||
                       2 * (a_count + ca_cap) > ahash_cap || p_count + cp_cap > plog_cap ||
                       2 * (p_count + cp_cap) > phash_cap;
     if (grow) sync();
@@ -2991,7 +3079,7 @@ bool el_ctx::superstep(uint32_t mask, uint64_t sb, uint64_t se, uint64_t lb, uin
       if (slog_cap != old_cap) dgrow(slog_f, s_count, slog_cap);
     }
     grow_log(l_count, cl_cap, llog_cap, llog_x, llog_p);
-    if (2 * (l_count + cl_cap) > lhash_cap) rehash_links(next_pow2(2 * (l_count + cl_cap)));
+    if (2 * (l_count - l_base + cl_cap) > lhash_cap) rehash_links(next_pow2(2 * (l_count - l_base + cl_cap)));
     grow_log(a_count, ca_cap, alog_cap, alog_y, alog_c);
     if (2 * (a_count + ca_cap) > ahash_cap) rehash_acts(next_pow2(2 * (a_count + ca_cap)));
     grow_log(p_count, cp_cap, plog_cap, plog_p, plog_b);
@@ -3008,13 +3096,14 @@ bool el_ctx::superstep(uint32_t mask, uint64_t sb, uint64_t se, uint64_t lb, uin
     ea.sb = (uint32_t)sb, ea.se = (uint32_t)se, ea.lb = (uint32_t)lb, ea.le = (uint32_t)le;
     ea.ab = (uint32_t)ab, ea.ae = (uint32_t)ae, ea.pb = (uint32_t)pb, ea.pe = (uint32_t)pe;
     // an empty link / propagation set (the first superstep): their probes cannot hit
-    ea.mask = mask | (!part() && l_count == 0 ? (uint32_t)M_LEMPTY : 0u) | (!part() && p_count == 0 ? (uint32_t)M_PEMPTY : 0u);
+    ea.mask = mask | (!part() && l_count == l_base ? (uint32_t)M_LEMPTY : 0u) |
+              (!part() && p_count == 0 ? (uint32_t)M_PEMPTY : 0u);
     ea.a_end = (uint32_t)a0;
     launch(EL_K_EXPAND_S, [&] {
       hipLaunchKernelGGL(k_expand, dim3(ea.gs + ea.gl + ea.ga + ea.gp), dim3(BLOCK), 0, stream, ix, st, ea);
     });
     launch(EL_K_JOBS, [&] {
-      hipLaunchKernelGGL(k_jobs, dim3(tune_jobs), dim3(BLOCK), 0, stream, ix, st);
+      hipLaunchKernelGGL(k_jobs, dim3(tune_jobs), dim3(BLOCK), 0, stream, ix, st, ea.mask);
     });
     // ---- commit (counts read on the device); its last block publishes the counters to
     // pinned host memory and zeroes the candidate counters, so the step ends with ONE sync
@@ -3180,7 +3269,7 @@ uint64_t el_ctx::superstep_part(uint32_t mask, uint64_t sb, uint64_t se, uint64_
     // ---- capacities for the local candidates (as in superstep) and the remote imports
     const uint64_t rb = remote_bound();
     const bool grow = s_count + cs_cap + ct_cap > slog_cap || l_count + cl_cap > llog_cap ||
-                      2 * (l_count + cl_cap) > lhash_cap || a_count + ca_cap + rb > alog_cap || 2 * (a_count + ca_cap + rb) > ahash_cap ||
+                      2 * (l_count - l_base + cl_cap) > lhash_cap || a_count + ca_cap + rb > alog_cap || 2 * (a_count + ca_cap + rb) > ahash_cap ||
                       p_count + cp_cap + rb > plog_cap || 2 * (p_count + cp_cap + rb) > phash_cap ||
                       x_count + part_count * xcap > xlog_cap;
     if (grow) {
@@ -3198,7 +3287,7 @@ uint64_t el_ctx::superstep_part(uint32_t mask, uint64_t sb, uint64_t se, uint64_
         if (slog_cap != old_cap) dgrow(slog_f, s_count, slog_cap);
       }
         grow_log(l_count, cl_cap, llog_cap, llog_x, llog_p);
-      if (2 * (l_count + cl_cap) > lhash_cap) rehash_links(next_pow2(2 * (l_count + cl_cap)));
+      if (2 * (l_count - l_base + cl_cap) > lhash_cap) rehash_links(next_pow2(2 * (l_count - l_base + cl_cap)));
       grow_part(xcap);
     }
     const uint32_t s0 = (uint32_t)s_count, l0 = (uint32_t)l_count, a0 = (uint32_t)a_count, p0 = (uint32_t)p_count;
@@ -3222,7 +3311,7 @@ uint64_t el_ctx::superstep_part(uint32_t mask, uint64_t sb, uint64_t se, uint64_
     const uint32_t eg = ea.gs + ea.gl + ea.ga + ea.gp + ea.gx;
     if (eg) {
       launch(EL_K_EXPAND_S, [&] { hipLaunchKernelGGL(k_expand, dim3(eg), dim3(BLOCK), 0, stream, ix, st, ea); });
-      launch(EL_K_JOBS, [&] { hipLaunchKernelGGL(k_jobs, dim3(tune_jobs), dim3(BLOCK), 0, stream, ix, st); });
+      launch(EL_K_JOBS, [&] { hipLaunchKernelGGL(k_jobs, dim3(tune_jobs), dim3(BLOCK), 0, stream, ix, st, mask); });
     }
     CommitArgs ca{};
     ca.gs = grid_for(cs_cap, tune_commit);
@@ -3390,6 +3479,65 @@ void el_ctx::init_rows(uint32_t a, uint32_t b) {
   s_init += two;
 }
 
+// The base links {(X, p) : p ∈ exr(X)} — what CR3 derives from the init facts X ∈ S(X) in the
+// first superstep — written before it: the link log gets exr in X order, the predecessor rows
+// exrT, the successor rows exrC (rows laid out for them by alloc_state: row capacities count
+// them), and the link set stays without them (link_known: a binary search of exr(X)).  The
+// first superstep then expands the base links, which the second did before; its queues start
+// at what the second got.  The CPU oracle installs the same links (el_oracle.c, base_links).
+void el_ctx::install_base() {
+  const uint64_t nb = hx.exr.a.size();
+  if (nb == 0 || l_count != 0 || (PR.live && !PR.start0) || (SC.live && !SC.start0)) return;
+  const uint64_t trig = s_count + nb;
+  if (!small_queues) {
+    if (const uint64_t want = std::min<uint64_t>(4 * trig, 1ull << 28); want > cs_cap) {
+      sync();
+      cs_cap = next_pow2(want);
+      dfree(cs_x);
+      dfree(cs_a);
+      cs_x = dalloc<uint32_t>(cs_cap);
+      cs_a = dalloc<uint32_t>(cs_cap);
+    }
+    if (const uint64_t want = std::min<uint64_t>(trig, 1ull << 26); want > job_cap) {
+      sync();
+      job_cap = next_pow2(want);
+      dfree(jobs);
+      jobs = dalloc<uint4>(job_cap);
+    }
+  }
+  if (nb + cl_cap > llog_cap) {
+    sync();
+    llog_cap = next_pow2(nb + cl_cap + (nb + cl_cap) / 2);
+    dgrow(llog_x, 0, llog_cap);
+    dgrow(llog_p, 0, llog_cap);
+  }
+  const uint32_t N = hx.N, P = hx.P, nc = (uint32_t)hx.exrC.a.size();
+  auto grid = [](uint64_t n) { return (uint32_t)std::min<uint64_t>(8192, std::max<uint64_t>(1, (n + 255) / 256)); };
+  launch(EL_K_INIT, [&] {
+    hipLaunchKernelGGL(k_csr_scatter, dim3(grid(nb)), dim3(256), 0, stream, ix.exr_ptr, ix.exr_pid, N, (uint32_t)nb,
+                       llog_x, llog_p, nullptr, nullptr);
+  });
+  if (PR.live)
+    launch(EL_K_INIT, [&] {
+      hipLaunchKernelGGL(k_gap_len, dim3(grid(P)), dim3(256), 0, stream, exrT_ptr, P, PR.len);
+      hipLaunchKernelGGL(k_csr_scatter, dim3(grid(nb)), dim3(256), 0, stream, exrT_ptr, exrT_x, P, (uint32_t)nb,
+                         nullptr, nullptr, PR.start, PR.val);
+    });
+  if (SC.live && nc)
+    launch(EL_K_INIT, [&] {
+      hipLaunchKernelGGL(k_gap_len, dim3(grid(N)), dim3(256), 0, stream, exrC_ptr, N, SC.len);
+      hipLaunchKernelGGL(k_csr_scatter, dim3(grid(nc)), dim3(256), 0, stream, exrC_ptr, exrC_p, N, nc, nullptr,
+                         nullptr, SC.start, SC.val);
+    });
+  hipLaunchKernelGGL(k_set_u32, dim3(1), dim3(1), 0, stream, &ctr->l_log, (uint32_t)nb);
+  HIPCHK(hipGetLastError());
+  l_count = l_base = nb;
+  ix.base = 1;
+  // the log entries read and written, the rows' entries
+  host_ev[EL_K_INIT][EL_EV_ENT] += nb + (PR.live ? nb : 0) + (SC.live ? hx.exrC.a.size() : 0);
+  host_ev[EL_K_INIT][EL_EV_EMIT] += nb;
+}
+
 // Carry a saturated state over to indexes rebuilt for old ∪ increment (el_add_axioms).
 void el_ctx::migrate_state(uint32_t N0, const std::vector<uint32_t>& pmap) {
   const uint64_t N = hx.N, P = hx.P, W0 = W, W1 = (N + 31) / 32;
@@ -3426,6 +3574,9 @@ void el_ctx::migrate_state(uint32_t N0, const std::vector<uint32_t>& pmap) {
     sync();
     dfree(dmap);
   }
+  l_base = 0;  // every link goes into the set: the base links of the old index are plain links now
+  ix.base = 0;
+  fresh = false;
   rehash_links(lhash_cap);
   rehash_props(phash_cap);
   // predecessor / successor / propagation rows for the new pair and concept spaces
@@ -3710,6 +3861,7 @@ int el_init(el_ctx* c) {
   return guarded(c, [&] {
     c->reset_state();
     c->init_rows(c->lo, c->hi);
+    c->fresh = true;
     c->inited = true;
     c->stats_stale = true;
     return EL_OK;
@@ -3722,6 +3874,7 @@ int el_step(el_ctx* c, el_rule rule, int* changed) {
   if (c->part()) return fail(c, EL_ESTATE, "el_step needs a whole-ontology context (use el_saturate)");
   return guarded(c, [&] {
     const int r = (int)rule;
+    c->fresh = false;  // per-rule stepping derives every link (DistEL's granularity)
     const uint64_t se = c->s_count, le = c->l_count, ae = c->a_count, pe = c->p_count;
     bool ch = c->superstep(kRuleMask[r], c->wm_s[r], se, c->wm_l[r], le, c->wm_a[r], ae, c->wm_p[r], pe);
     c->wm_s[r] = se;
@@ -3739,6 +3892,8 @@ int el_saturate(el_ctx* c, el_stats* stats) {
   if (!c->inited) return fail(c, EL_ESTATE, "el_saturate before el_init");
   return guarded(c, [&] {
     auto t0 = std::chrono::steady_clock::now();
+    if (c->fresh && !c->part()) c->install_base();
+    c->fresh = false;
     // all rule types share one frontier: start at the oldest watermark
     uint64_t sb = c->s_count, lb = c->l_count, ab = c->a_count, pb = c->p_count;
     for (int r = 0; r < EL_NUM_RULE_TYPES; ++r) {

@@ -400,6 +400,27 @@ std::string build_index(const el_axioms& ax_in, HostIndex& o, uint32_t flags) {
     o.dom = make_csr(R, d, false);
     o.rng = make_csr(R, g, false);
   }
+  // Base links: the links of the told closure, {(X, p) : p ∈ exr(X)} — the first superstep
+  // would derive all of them from the init facts X ∈ S(X).  el_init writes them directly:
+  // the link log in X order (exr itself), the predecessor rows from exrT (pid -> X, the
+  // transpose), the successor rows from exrC (X -> its chain-second pids).
+  {
+    o.exrT.ptr.assign(o.P + 1, 0);
+    for (uint32_t p : o.exr.a) o.exrT.ptr[p + 1]++;
+    for (uint32_t p = 0; p < o.P; ++p) o.exrT.ptr[p + 1] += o.exrT.ptr[p];
+    o.exrT.a.resize(o.exr.a.size());
+    std::vector<uint32_t> fill(o.exrT.ptr.begin(), o.exrT.ptr.end() - 1);
+    for (uint32_t x = 0; x < N; ++x)  // X ascending: every transposed row is sorted
+      for (uint32_t j = o.exr.ptr[x]; j < o.exr.ptr[x + 1]; ++j) o.exrT.a[fill[o.exr.a[j]]++] = x;
+    std::vector<uint8_t> second(R, 0);  // roles second in an indexed chain (the rows CR6 reads)
+    for (uint32_t r = 0; r < R; ++r) second[r] = o.chs.ptr[r + 1] > o.chs.ptr[r];
+    o.exrC.ptr.assign(N + 1, 0);
+    for (uint32_t x = 0; x < N; ++x) {
+      for (uint32_t j = o.exr.ptr[x]; j < o.exr.ptr[x + 1]; ++j)
+        if (second[o.pair_role[o.exr.a[j]]]) o.exrC.a.push_back(o.exr.a[j]);
+      o.exrC.ptr[x + 1] = (uint32_t)o.exrC.a.size();
+    }
+  }
 #undef CHECK
   return "";
 }

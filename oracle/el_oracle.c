@@ -246,6 +246,10 @@ struct elo_ctx {
   vec plog_p, plog_b;
   vec* prow; /* propagations per pid */
   uint64_t s_init;
+  /* base links {(X, p) : p ∈ exr(X)} installed by elo_saturate before its first superstep
+   * (el_ctx::install_base): the head of the link log, not in the link set */
+  int base, fresh;
+  uint64_t l_base;
   int need_pred, need_succ; /* the GPU maintains these CSRs only when they have readers */
   int has_bot;              /* some axiom concludes ⊥: else the ⊥ rule cannot fire (skipped, as on the GPU) */
   /* slack capacities of the GPU's gapped CSR rows (predecessors, successors, propagations)
@@ -697,7 +701,7 @@ static void emit_job(elo_ctx* c, cands* k, int kern, uint32_t type, uint32_t b, 
   }
 }
 
-enum { JOB_PRED_S = 0, JOB_PRED_L = 1, JOB_R6A = 3 };
+enum { JOB_PRED_S = 0, JOB_PRED_L = 1, JOB_PRED_U = 2, JOB_R6A = 3 }; /* U: unprobed (first superstep) */
 
 /* scan of the filler's pair range (sorted by role): one row lookup + entries read */
 static uint32_t pair_lookup(elo_ctx* c, int kern, uint32_t r, uint32_t y) {
@@ -709,6 +713,31 @@ static uint32_t pair_lookup(elo_ctx* c, int kern, uint32_t r, uint32_t y) {
     if (c->pair_role[p] > r) return NONE;
   }
   return NONE;
+}
+
+/* (x, pid) is a base link: binary search of exr(x) (base_has on the GPU, same probe sequence) */
+static int base_has(elo_ctx* c, int kern, uint32_t x, uint32_t pid) {
+  uint32_t lo = c->exr.ptr[x], hi = c->exr.ptr[x + 1];
+  EV(kern, EL_EV_ROW);
+  while (lo < hi) {
+    uint32_t mid = (lo + hi) >> 1, v;
+    EV(kern, EL_EV_ENT);
+    v = c->exr.a[mid];
+    if (v == pid) return 1;
+    if (v < pid)
+      lo = mid + 1;
+    else
+      hi = mid;
+  }
+  return 0;
+}
+
+/* (x, pid) known at t-1: a base link, or in the link set (lempty: the set is empty, no probe) */
+static int link_known(elo_ctx* c, int kern, uint32_t x, uint32_t pid, int lempty) {
+  if (c->base && base_has(c, kern, x, pid)) return 1;
+  if (lempty) return 0;
+  EV(kern, EL_EV_HASH);
+  return hs_has(&c->links, lkey(pid, x));
 }
 
 /* predecessor / succ / S-row "CSR" views: begin offset is irrelevant on the CPU, the
@@ -764,17 +793,13 @@ static void expand_s(elo_ctx* c, cands* k, uint32_t mask, uint64_t b, uint64_t e
     }
     /* CR3 / CR4 half-1 over the told closure: a fact that came out of a closure (flag 1) was
      * covered by the fact that emitted the closure (the exr / exl rows span {A} ∪ told*(A)) */
-    if ((mask & M_R3) && c->slog_f.v[i] != 1) {
+    /* (an init fact's own links are the base links, already in place) */
+    if ((mask & M_R3) && c->slog_f.v[i] != 1 && !(c->base && c->slog_f.v[i] == 2)) {
       EV(K, EL_EV_ROW);
       for (j = c->exr.ptr[A]; j < c->exr.ptr[A + 1]; ++j) {
         uint32_t pid = c->exr.a[j];
         EV(K, EL_EV_ENT);
-        if (mask & M_LEMPTY) { /* empty link set: the probe is skipped (as on the GPU) */
-          emit_l(c, k, K, X, pid);
-          continue;
-        }
-        EV(K, EL_EV_HASH);
-        if (!hs_has(&c->links, lkey(pid, X))) emit_l(c, k, K, X, pid);
+        if (!link_known(c, K, X, pid, (mask & M_LEMPTY) != 0)) emit_l(c, k, K, X, pid);
       }
     }
     if ((mask & M_R4Y) && c->slog_f.v[i] != 1) { /* A ∈ S(Y=X) new, ∃r.A ⊑ B => propagation ((r, Y), B) */
@@ -791,7 +816,8 @@ static void expand_s(elo_ctx* c, cands* k, uint32_t mask, uint64_t b, uint64_t e
             vpush(&k->pb, B);
             if (mask & M_R4D) {
               EV(K, EL_EV_ROW);
-              if (c->pred[pid].n) emit_job(c, k, K, JOB_PRED_S, pid, (uint32_t)c->pred[pid].n, 0, B);
+              if (c->pred[pid].n)
+                emit_job(c, k, K, (mask & M_LEMPTY) ? JOB_PRED_U : JOB_PRED_S, pid, (uint32_t)c->pred[pid].n, 0, B);
             }
           }
         }
@@ -802,7 +828,8 @@ static void expand_s(elo_ctx* c, cands* k, uint32_t mask, uint64_t b, uint64_t e
       EV(K, EL_EV_ROW);
       for (p = c->fp_ptr[X]; p < c->fp_ptr[X + 1]; ++p) {
         EV(K, EL_EV_ROW);
-        if (c->pred[p].n) emit_job(c, k, K, JOB_PRED_S, p, (uint32_t)c->pred[p].n, 0, EL_BOTTOM);
+        if (c->pred[p].n)
+          emit_job(c, k, K, (mask & M_LEMPTY) ? JOB_PRED_U : JOB_PRED_S, p, (uint32_t)c->pred[p].n, 0, EL_BOTTOM);
       }
     }
     if ((mask & M_RRNG) && c->rng.ptr[c->R] > 0) {
@@ -853,8 +880,7 @@ static void expand_l(elo_ctx* c, cands* k, uint32_t mask, uint64_t b, uint64_t e
       for (j = c->psup.ptr[pid]; j < c->psup.ptr[pid + 1]; ++j) {
         uint32_t q = c->psup.a[j];
         EV(K, EL_EV_ENT);
-        EV(K, EL_EV_HASH);
-        if (!hs_has(&c->links, lkey(q, X))) emit_l(c, k, K, X, q);
+        if (!link_known(c, K, X, q, (mask & M_LEMPTY) != 0)) emit_l(c, k, K, X, q);
       }
     }
     if (mask & M_R6) {
@@ -916,7 +942,7 @@ static void expand_l(elo_ctx* c, cands* k, uint32_t mask, uint64_t b, uint64_t e
   }
 }
 
-static void run_jobs(elo_ctx* c, cands* k) {
+static void run_jobs(elo_ctx* c, cands* k, int lempty) {
   const int K = EL_K_JOBS;
   size_t j;
   uint32_t q, e;
@@ -924,10 +950,14 @@ static void run_jobs(elo_ctx* c, cands* k) {
     uint32_t type = k->jt.v[j], owner = k->jb.v[j], o0 = k->jo.v[j], len = k->jl.v[j], a = k->ja.v[j],
              b = k->jbb.v[j];
     EV(K, EL_EV_JOB);
-    if (type == JOB_PRED_S) {
+    if (type == JOB_PRED_S || type == JOB_PRED_U) {
       for (q = 0; q < len; ++q) {
         uint32_t xp = c->pred[owner].v[o0 + q];
         EV(K, EL_EV_ENT);
+        if (type == JOB_PRED_U) {
+          emit_s(c, k, K, xp, b);
+          continue;
+        }
         EV(K, EL_EV_TEST);
         if (!bit(c, xp, b)) emit_s(c, k, K, xp, b);
       }
@@ -935,8 +965,7 @@ static void run_jobs(elo_ctx* c, cands* k) {
       for (q = 0; q < len; ++q) {
         uint32_t xp = c->pred[owner].v[o0 + q];
         EV(K, EL_EV_ENT);
-        EV(K, EL_EV_HASH);
-        if (!hs_has(&c->links, lkey(a, xp))) emit_l(c, k, K, xp, a);
+        if (!link_known(c, K, xp, a, lempty)) emit_l(c, k, K, xp, a);
       }
     } else { /* JOB_R6A */
       uint32_t X = a, r = b;
@@ -950,8 +979,7 @@ static void run_jobs(elo_ctx* c, cands* k) {
           EVN(K, EL_EV_ENT, 2);
           if (s == s2) {
             uint32_t pt = pair_lookup(c, K, t, Z);
-            EV(K, EL_EV_HASH);
-            if (!hs_has(&c->links, lkey(pt, X))) emit_l(c, k, K, X, pt);
+            if (!link_known(c, K, X, pt, lempty)) emit_l(c, k, K, X, pt);
           }
         }
       }
@@ -1041,7 +1069,7 @@ static int superstep(elo_ctx* c, uint32_t mask, uint64_t sb, uint64_t se, uint64
   uint64_t s0 = c->slog_x.n, l0 = c->llog_x.n, a0 = c->alog_y.n, p0 = c->plog_p.n;
   int do_a = (mask & M_RRNG) && ae > ab, do_p = (mask & M_R4P) && pe > pb;
   if (!(se > sb || le > lb || do_a || do_p)) return 0;
-  if (c->llog_x.n == 0) mask |= M_LEMPTY; /* empty sets: their probes are skipped (as on the GPU) */
+  if (c->llog_x.n == c->l_base) mask |= M_LEMPTY; /* empty sets: their probes are skipped (as on the GPU) */
   if (c->plog_p.n == 0) mask |= M_PEMPTY;
   memset(&k, 0, sizeof k);
   /* generation: reads only the state of the previous step */
@@ -1049,7 +1077,7 @@ static int superstep(elo_ctx* c, uint32_t mask, uint64_t sb, uint64_t se, uint64
   expand_l(c, &k, mask, lb, le);
   if (do_a) expand_a(c, &k, se, ab, ae);
   if (do_p) expand_p(c, &k, pb, pe);
-  run_jobs(c, &k);
+  run_jobs(c, &k, (mask & M_LEMPTY) != 0);
   if (k.sx.n + k.s1x.n + k.lx.n + k.ay.n + k.pp.n == 0) {
     cands_free(&k);
     return 0;
@@ -1244,12 +1272,40 @@ int elo_init(elo_ctx* c) {
     }
   }
   c->s_init = init;
+  c->base = 0;
+  c->l_base = 0;
+  c->fresh = 1;
   return EL_OK;
+}
+
+/* the base links (el_ctx::install_base): exr in X order into the link log, each X into the
+ * predecessor row of its pids (so rows hold ascending X, as exrT), chain-second pids into the
+ * successor row of X (exrC); events of the coalesced writes as the GPU host counts them */
+static void base_links(elo_ctx* c) {
+  uint32_t x, j;
+  uint64_t nb = c->exr.ptr[c->N], nc = 0;
+  if (nb == 0 || c->llog_x.n != 0) return;
+  for (x = 0; x < c->N; ++x)
+    for (j = c->exr.ptr[x]; j < c->exr.ptr[x + 1]; ++j) {
+      uint32_t p = c->exr.a[j], r = c->pair_role[p];
+      vpush(&c->llog_x, x);
+      vpush(&c->llog_p, p);
+      vpush(&c->pred[p], x);
+      if (c->need_succ && c->chs.ptr[r + 1] > c->chs.ptr[r]) {
+        vpush(&c->succ[x], p);
+        ++nc;
+      }
+    }
+  EVN(EL_K_INIT, EL_EV_ENT, nb + (c->need_pred ? nb : 0) + nc);
+  EVN(EL_K_INIT, EL_EV_EMIT, nb);
+  c->l_base = nb;
+  c->base = 1;
 }
 
 int elo_step(elo_ctx* c, int rule, int* changed) {
   uint64_t se, le, ae, pe;
   if (!c || !changed || rule < 0 || rule >= EL_NUM_RULE_TYPES || c->mode != 0) return EL_EINVAL;
+  c->fresh = 0; /* per-rule stepping derives every link */
   se = c->slog_x.n, le = c->llog_x.n, ae = c->alog_y.n, pe = c->plog_p.n;
   *changed = superstep(c, rule_mask[rule], c->wm_s[rule], se, c->wm_l[rule], le, c->wm_a[rule], ae,
                        c->wm_p[rule], pe);
@@ -1265,6 +1321,8 @@ int elo_saturate(elo_ctx* c) {
   int r;
   if (!c) return EL_EINVAL;
   if (c->mode == 1) return naive_saturate(c);
+  if (c->fresh) base_links(c);
+  c->fresh = 0;
   sb = c->slog_x.n, lb = c->llog_x.n, ab = c->alog_y.n;
   for (r = 0; r < EL_NUM_RULE_TYPES; ++r) {
     if (c->wm_s[r] < sb) sb = c->wm_s[r];

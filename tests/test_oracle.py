@@ -66,8 +66,29 @@ def test_trace_sums(oracle_lib):
     ds, dl, da = o.trace()
     st = o.stats()
     assert int(ds.sum()) == st["s_facts"] and int(dl.sum()) == st["links"]
-    # the first superstep's triggers: the init facts and the told closures written with them
-    assert ds[0] >= st["s_init"] and dl[0] == 0
+    # the first superstep's triggers: the init facts and the told closures written with them,
+    # and the base links {(X, p) : p ∈ exr(X)} installed before it
+    assert ds[0] >= st["s_init"] and dl[0] == _base_links(ax) > 0
+
+
+def _base_links(ax):
+    """|{(X, (r, B)) : A ⊑ ∃r.B told, A ∈ {X} ∪ told*(X)}| by a plain graph search."""
+    up = {}
+    for a, b in ax.sub.tolist():
+        up.setdefault(a, set()).add(b)
+    ex = {}
+    for a, r, b in ax.ex_rhs.tolist():
+        ex.setdefault(a, set()).add((r, b))
+    n = 0
+    for x in range(ax.n_concepts):
+        seen, st = {x}, [x]
+        while st:
+            for b in up.get(st.pop(), ()):
+                if b not in seen:
+                    seen.add(b)
+                    st.append(b)
+        n += len(set().union(*(ex.get(a, set()) for a in seen)))
+    return n
 
 
 def test_generators_deterministic():
