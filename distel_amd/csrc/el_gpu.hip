@@ -2207,6 +2207,7 @@ struct el_ctx {
   uint32_t commit_seq = 0;         // k_commit launches so far (published with the counters)
   bool stats_stale = false;        // el_init ran without a sync: `last` is filled on demand
   bool split_commit = getenv("EL_SPLIT_COMMIT") != nullptr;  // diagnostic only
+  bool split_expand = getenv("EL_SPLIT_EXPAND") != nullptr;  // diagnostic: one k_expand launch per role
   unsigned long long* ev_sum = nullptr;   // k_ev_reduce output
   unsigned long long* ev_host = nullptr;  // pinned copy of ev_sum
   bool events_queued = false;
@@ -2400,8 +2401,11 @@ struct el_ctx {
   // half: 0 = whole build, 1 = the part that reads the state, 2 = the rest (el_rows.h);
   // clear: the S-row build zeroes the bit matrix as it writes (a releasing copy-back)
   void build_rows(bool facts, hipStream_t s, uint64_t* ptr, uint32_t* dst, int half = 0, bool clear = false);
-  hipStream_t rstream = nullptr;  // state reset behind a releasing copy-back
+  hipStream_t rstream = nullptr;  // state reset behind a releasing copy-back; the base links' set fill
   hipEvent_t ev_reset = nullptr;
+  hipEvent_t ev_base[2] = {nullptr, nullptr};  // base links logged (stream) / in the link set (rstream)
+  bool base_filling = false;                   // the set fill runs beside the first superstep
+  void join_base();
   bool pre_reset = false;         // the device part of the next reset_state is already enqueued
   void reset_device(hipStream_t s, bool matrix_clear = false);
   void rehash_links(uint64_t cap);
@@ -2909,6 +2913,8 @@ void el_ctx::reset_state() {
   }
   bits_logged = true;  // from here on every set bit is in the fact log (k_init and k_commit append)
   s_count = l_count = a_count = p_count = s_init = x_count = 0;
+  if (base_filling) HIPCHK(hipStreamWaitEvent(stream, ev_base[1], 0));  // (an interrupted saturation)
+  base_filling = false;
   l_base = 0;
   ix.base = 0;
   rs.n = rl.n = ~0ull;  // result rows are stale
@@ -2924,6 +2930,7 @@ void el_ctx::reset_state() {
 }
 
 void el_ctx::rehash_links(uint64_t cap) {
+  if (base_filling) HIPCHK(hipEventSynchronize(ev_base[1]));  // (not while the set fill writes it)
   dfree(lhash);
   lhash_cap = cap;
   lhash = dalloc<unsigned long long>(cap);
@@ -3099,9 +3106,29 @@ bool el_ctx::superstep(uint32_t mask, uint64_t sb, uint64_t se, uint64_t lb, uin
     ea.mask = mask | (!part() && l_count == l_base ? (uint32_t)M_LEMPTY : 0u) |
               (!part() && p_count == 0 ? (uint32_t)M_PEMPTY : 0u);
     ea.a_end = (uint32_t)a0;
-    launch(EL_K_EXPAND_S, [&] {
-      hipLaunchKernelGGL(k_expand, dim3(ea.gs + ea.gl + ea.ga + ea.gp), dim3(BLOCK), 0, stream, ix, st, ea);
-    });
+    if (split_expand) {  // the roles are independent: run them one launch each (rocprof sees each)
+      const uint32_t g[4] = {ea.gs, ea.gl, ea.ga, ea.gp};
+      // EL_SPLIT_EXPAND=2: the S role once more per rule group (CR1, CR2, CR3, CR4, the rest)
+      const bool by_rule = getenv("EL_SPLIT_EXPAND")[0] == '2';
+      const uint32_t keep = M_LEMPTY | M_PEMPTY;
+      const uint32_t groups[5] = {M_R1, M_R2, M_R3, M_R4Y | M_R4D, ~(M_R1 | M_R2 | M_R3 | M_R4Y | M_R4D)};
+      for (int r = 0; r < 4; ++r) {
+        if (!g[r]) continue;
+        for (int k = 0; k < (r == 0 && by_rule ? 5 : 1); ++k) {
+          ExpandArgs e1 = ea;
+          e1.gs = r == 0 ? ea.gs : 0u;
+          e1.gl = r == 1 ? ea.gl : 0u;
+          e1.ga = r == 2 ? ea.ga : 0u;
+          e1.gp = r == 3 ? ea.gp : 0u;
+          if (r == 0 && by_rule) e1.mask = (ea.mask & groups[k]) | (ea.mask & keep);
+          hipLaunchKernelGGL(k_expand, dim3(g[r]), dim3(BLOCK), 0, stream, ix, st, e1);
+        }
+      }
+    } else {
+      launch(EL_K_EXPAND_S, [&] {
+        hipLaunchKernelGGL(k_expand, dim3(ea.gs + ea.gl + ea.ga + ea.gp), dim3(BLOCK), 0, stream, ix, st, ea);
+      });
+    }
     launch(EL_K_JOBS, [&] {
       hipLaunchKernelGGL(k_jobs, dim3(tune_jobs), dim3(BLOCK), 0, stream, ix, st, ea.mask);
     });
@@ -3511,6 +3538,9 @@ void el_ctx::install_base() {
     dgrow(llog_x, 0, llog_cap);
     dgrow(llog_p, 0, llog_cap);
   }
+  // the link set takes the base links during the first superstep: room for them and the
+  // second superstep's candidates now (an empty set: no re-insertion)
+  if (2 * (nb + cl_cap) > lhash_cap) rehash_links(next_pow2(2 * (nb + cl_cap)));
   const uint32_t N = hx.N, P = hx.P, nc = (uint32_t)hx.exrC.a.size();
   auto grid = [](uint64_t n) { return (uint32_t)std::min<uint64_t>(8192, std::max<uint64_t>(1, (n + 255) / 256)); };
   launch(EL_K_INIT, [&] {
@@ -3531,11 +3561,33 @@ void el_ctx::install_base() {
     });
   hipLaunchKernelGGL(k_set_u32, dim3(1), dim3(1), 0, stream, &ctr->l_log, (uint32_t)nb);
   HIPCHK(hipGetLastError());
+  // The link set gets the base links beside the first superstep (a second stream; that
+  // superstep finds them by binary search and inserts only other links, and concurrent
+  // inserts of distinct keys are safe); the second superstep waits for it (join_base) and
+  // from then on membership is one probe of the set, as for every other link.
+  HIPCHK(hipEventRecord(ev_base[0], stream));
+  HIPCHK(hipStreamWaitEvent(rstream, ev_base[0], 0));
+  hipLaunchKernelGGL(k_rehash, dim3(grid_for(nb, 2048)), dim3(BLOCK), 0, rstream, lhash, lhash_cap - 1, llog_x, llog_p,
+                     (uint32_t)nb);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipEventRecord(ev_base[1], rstream));
+  base_filling = true;
   l_count = l_base = nb;
   ix.base = 1;
   // the log entries read and written, the rows' entries
   host_ev[EL_K_INIT][EL_EV_ENT] += nb + (PR.live ? nb : 0) + (SC.live ? hx.exrC.a.size() : 0);
   host_ev[EL_K_INIT][EL_EV_EMIT] += nb;
+}
+
+// After the first superstep: the link set holds the base links (k_rehash on rstream), so
+// later supersteps probe the set alone (ix.base off).  The oracle's base_join mirrors it.
+void el_ctx::join_base() {
+  if (!base_filling) return;
+  HIPCHK(hipStreamWaitEvent(stream, ev_base[1], 0));
+  base_filling = false;
+  host_ev[EL_K_REHASH][EL_EV_HASH] += l_base;
+  l_base = 0;
+  ix.base = 0;
 }
 
 // Carry a saturated state over to indexes rebuilt for old ∪ increment (el_add_axioms).
@@ -3574,6 +3626,7 @@ void el_ctx::migrate_state(uint32_t N0, const std::vector<uint32_t>& pmap) {
     sync();
     dfree(dmap);
   }
+  join_base();
   l_base = 0;  // every link goes into the set: the base links of the old index are plain links now
   ix.base = 0;
   fresh = false;
@@ -3732,6 +3785,7 @@ int el_create(el_ctx** out, const el_config* cfg) {
     HIPCHK(hipStreamCreateWithFlags(&c->rstream, hipStreamNonBlocking));
     for (hipEvent_t& e : c->ev_rows) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     HIPCHK(hipEventCreateWithFlags(&c->ev_reset, hipEventDisableTiming));
+    for (hipEvent_t& e : c->ev_base) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     if (c->xmode == EL_XCHG_LOCAL) c->xchg.reset(new LocalExchange(cfg->group, (int)c->part_rank));
     if (c->xmode == EL_XCHG_RCCL)  // collective: every rank of the group calls el_create
       c->xchg.reset(new RcclExchange((int)c->part_rank, (int)c->part_count, cfg->rccl_id));
@@ -3744,6 +3798,8 @@ int el_create(el_ctx** out, const el_config* cfg) {
     for (hipEvent_t e : c->ev_rows)
       if (e) (void)hipEventDestroy(e);
     if (c->ev_reset) (void)hipEventDestroy(c->ev_reset);
+    for (hipEvent_t e : c->ev_base)
+      if (e) (void)hipEventDestroy(e);
     delete c;
     return rc;
   }
@@ -3932,6 +3988,7 @@ int el_saturate(el_ctx* c, el_stats* stats) {
       c->tr_l.push_back(le - lb);
       c->tr_a.push_back(ae - ab);
       c->superstep(pb < pe ? (M_ALL | M_R4P) : M_ALL, sb, se, lb, le, ab, ae, pb, pe);
+      c->join_base();
       sb = se;
       lb = le;
       ab = ae;
@@ -4286,6 +4343,8 @@ void el_destroy(el_ctx* c) {
   for (hipEvent_t e : c->ev_rows)
     if (e) (void)hipEventDestroy(e);
   if (c->ev_reset) (void)hipEventDestroy(c->ev_reset);
+  for (hipEvent_t e : c->ev_base)
+    if (e) (void)hipEventDestroy(e);
   delete c;
 }
 

@@ -1302,6 +1302,17 @@ static void base_links(elo_ctx* c) {
   c->base = 1;
 }
 
+/* after the first superstep the link set holds the base links (the GPU fills it beside that
+ * superstep, EL_K_REHASH): later probes go to the set alone */
+static void base_join(elo_ctx* c) {
+  uint64_t i;
+  if (!c->base) return;
+  for (i = 0; i < c->l_base; ++i) hs_add(&c->links, lkey(c->llog_p.v[i], c->llog_x.v[i]));
+  EVN(EL_K_REHASH, EL_EV_HASH, c->l_base);
+  c->base = 0;
+  c->l_base = 0;
+}
+
 int elo_step(elo_ctx* c, int rule, int* changed) {
   uint64_t se, le, ae, pe;
   if (!c || !changed || rule < 0 || rule >= EL_NUM_RULE_TYPES || c->mode != 0) return EL_EINVAL;
@@ -1342,6 +1353,7 @@ int elo_saturate(elo_ctx* c) {
     vpush(&c->tr_a, (uint32_t)(ae - ab));
     c->supersteps++;
     superstep(c, pb < pe ? (M_ALL | M_R4P) : M_ALL, sb, se, lb, le, ab, ae, pb, pe);
+    base_join(c);
     sb = se, lb = le, ab = ae;
     pb = pe = c->plog_p.n;
   }

@@ -29,6 +29,33 @@ def _same(eng, o):
     assert np.array_equal(eng.events(), o.events())
 
 
+def _digests():
+    import os
+    rows = []
+    for line in open(os.path.join(os.path.dirname(__file__), "golden", "closure_digests.txt")):
+        if line.strip() and not line.startswith("#"):
+            name, scale, d_in, d_out = line.split()
+            rows.append((name, float(scale), d_in, d_out))
+    return rows
+
+
+@pytest.mark.parametrize("case", _digests(), ids=lambda c: f"{c[0]}x{c[1]}")
+def test_closure_digest_gpu(case):
+    """The GPU closure of every pinned workload — G3 at full size (the bench configuration)
+    included — hashes to the digest the semi-naive oracle and the independent worklist
+    saturator both produced (tests/golden/pin_report.txt)."""
+    import hashlib
+    name, scale, d_in, d_out = case
+    ax = generators.workload(name, scale)
+    assert ax.digest() == d_in, "generator output changed"
+    eng, _ = engine.classify(ax, device=0)
+    h = hashlib.sha256()
+    for a in eng.facts() + eng.links():
+        h.update(np.ascontiguousarray(a, dtype=np.uint32).tobytes())
+    eng.close()
+    assert h.hexdigest() == d_out
+
+
 def test_g3x_bottom_domain_range_full(oracle_lib):
     ax = generators.workload("g3x")
     eng, st = engine.classify(ax, device=0, compat_range=True)
