@@ -762,12 +762,14 @@ __device__ __forceinline__ void wave_rows(uint32_t b, uint32_t e, F&& f) {
 //  ⊥    TypeBottomAxiomProcessorBase.java:62-123  range RolePairHandler.java:471-479 + K10
 // The index rows of CR1, CR3 and CR4 half-1 (told closure, its links, its propagations) are
 // walked wave-cooperatively (wave_rows); the short CR2 rows per lane.
+// tpw: triggers per wave (lanes [0, tpw) take one each) — see wave_triggers.
 __device__ void expand_s(const DIndex& ix, const DState& st, BlockQ& q, uint32_t bid, uint32_t nb,
-                         uint32_t begin, uint32_t end, uint32_t mask, uint32_t a_end) {
+                         uint32_t begin, uint32_t end, uint32_t mask, uint32_t a_end, uint32_t tpw) {
   Ev ev;
-  for (uint32_t base = begin + bid * blockDim.x; base < end; base += nb * blockDim.x) {
-    const uint32_t i = base + threadIdx.x;
-    const bool act = i < end;
+  const uint32_t w0 = bid * (blockDim.x >> 6) + (threadIdx.x >> 6), nw = nb * (blockDim.x >> 6);
+  for (uint32_t base = begin + w0 * tpw; base < end; base += nw * tpw) {  // (wave-uniform)
+    const uint32_t i = base + lane_id();
+    const bool act = lane_id() < tpw && i < end;
     uint32_t X = 0, A = 0, f = 1;
     uint4 m0 = make_uint4(0, 0, 0, 0), m1 = m0;
     if (act) {
@@ -937,11 +939,12 @@ __device__ __forceinline__ void r6_second(const DIndex& ix, const DState& st, Bl
 //  CR6  Type5AxiomProcessorBase.java:115-154           ⊥   RolePairHandler.java:358-372
 //  domain/range RolePairHandler.java:456-491
 __device__ void expand_l(const DIndex& ix, const DState& st, BlockQ& q, uint32_t bid, uint32_t nb,
-                         uint32_t begin, uint32_t end, uint32_t mask) {
+                         uint32_t begin, uint32_t end, uint32_t mask, uint32_t tpw) {
   Ev ev;
-  for (uint32_t base = begin + bid * blockDim.x; base < end; base += nb * blockDim.x) {
-    const uint32_t i = base + threadIdx.x;
-    const bool act = i < end;
+  const uint32_t w0 = bid * (blockDim.x >> 6) + (threadIdx.x >> 6), nw = nb * (blockDim.x >> 6);
+  for (uint32_t base = begin + w0 * tpw; base < end; base += nw * tpw) {  // (wave-uniform)
+    const uint32_t i = base + lane_id();
+    const bool act = lane_id() < tpw && i < end;
     uint32_t X = 0, pid = 0, r = 0, Y = 0;
     if (act) {
       X = st.llog_x[i];
@@ -1065,11 +1068,13 @@ __global__ void k_jobs(DIndex ix, DState st, uint32_t mask) {
   // 64 job records per wave, one per lane, their lists walked wave-cooperatively: most
   // records are short (a fresh propagation meets a few predecessors), and one wave per
   // record left most lanes idle (G5 step 1: 1.6 M records, 0.85 ms)
-  for (uint32_t base = (blockIdx.x * wpb + (threadIdx.x >> 6)) * 64; base < njobs; base += nwaves * 64) {
+  // (a step with few jobs spreads them over every wave, as wave_triggers does for triggers)
+  const uint32_t tpw = min(64u, max(1u, (njobs + nwaves - 1) / nwaves));
+  for (uint32_t base = (blockIdx.x * wpb + (threadIdx.x >> 6)) * tpw; base < njobs; base += nwaves * tpw) {
     const uint32_t j = base + lane;
     uint4 jb = make_uint4(0u, 0u, 0u, 0u);
     uint32_t len = 0;
-    if (j < njobs) {
+    if (lane < tpw && j < njobs) {
       jb = st.jobs[j];
       len = jb.y & 0x0fffffffu;
       ev.v[EL_EV_JOB]++;
@@ -1346,6 +1351,7 @@ __device__ void commit_p(const DIndex& ix, const DState& st, uint32_t bid, uint3
 // read only state t-1 and append to disjoint candidate queues, so they run side by side.
 struct ExpandArgs {
   uint32_t gs, gl, ga, gp, gx;
+  uint32_t ts, tl;  // triggers per wave of the S and link roles (wave_triggers)
   uint32_t sb, se, lb, le, ab, ae, pb, pe, xb, xe;
   uint32_t mask, a_end;
 };
@@ -1372,12 +1378,12 @@ __global__ void k_expand(DIndex ix, DState st, ExpandArgs a) {
   q_init(q);
   uint32_t b = blockIdx.x;
   if (b < a.gs) {
-    expand_s(ix, st, q, b, a.gs, a.sb, a.se, a.mask, a.a_end);
+    expand_s(ix, st, q, b, a.gs, a.sb, a.se, a.mask, a.a_end, a.ts);
     return;
   }
   b -= a.gs;
   if (b < a.gl) {
-    expand_l(ix, st, q, b, a.gl, a.lb, a.le, a.mask);
+    expand_l(ix, st, q, b, a.gl, a.lb, a.le, a.mask, a.tl);
     return;
   }
   b -= a.gl;
@@ -1932,6 +1938,19 @@ uint64_t next_pow2(uint64_t v) {
   uint64_t p = 1;
   while (p < v) p <<= 1;
   return p;
+}
+
+// Triggers per wave and grid of an expand role with n triggers: a small step's triggers
+// spread over up to maxb·4 waves, T = ceil(n / waves) each (64, a lane per trigger, once n
+// fills them).  Each wave walks its triggers' index rows 64 entries a round with a dependent
+// random read per round (a link-set probe, a bit test), so a step of 10 k triggers on 40
+// blocks of 64-trigger waves took ~65 rounds of latency (G3's late supersteps: 60–100 µs of
+// CR3 each); at 3 triggers per wave on 834 blocks it takes a few.
+static void wave_triggers(uint64_t n, uint32_t maxb, uint32_t& grid, uint32_t& tpw) {
+  const uint64_t waves = (uint64_t)maxb * (BLOCK / 64);
+  tpw = (uint32_t)std::min<uint64_t>(64, std::max<uint64_t>(1, (n + waves - 1) / waves));
+  const uint64_t per_block = (uint64_t)tpw * (BLOCK / 64);
+  grid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(maxb, (n + per_block - 1) / per_block));
 }
 
 // Gapped CSR (DGap) on the host side: the layout buffers, the overflow queue, scan scratch.
@@ -3096,8 +3115,8 @@ bool el_ctx::superstep(uint32_t mask, uint64_t sb, uint64_t se, uint64_t lb, uin
     refresh_acts();
     DState st = dstate();
     ExpandArgs ea{};
-    ea.gs = se > sb ? grid_for(se - sb, tune_expand) : 0u;
-    ea.gl = le > lb ? grid_for(le - lb, tune_expand) : 0u;
+    if (se > sb) wave_triggers(se - sb, tune_expand, ea.gs, ea.ts);
+    if (le > lb) wave_triggers(le - lb, tune_expand, ea.gl, ea.tl);
     ea.ga = do_a ? grid_for(se) : 0u;  // the facts known at t-1 meet the new activations
     ea.gp = do_p ? grid_for(pe - pb) : 0u;
     ea.sb = (uint32_t)sb, ea.se = (uint32_t)se, ea.lb = (uint32_t)lb, ea.le = (uint32_t)le;
@@ -3325,8 +3344,8 @@ uint64_t el_ctx::superstep_part(uint32_t mask, uint64_t sb, uint64_t se, uint64_
     ExpandArgs ea{};
     const bool do_a = (mask & M_RRNG) && ae > ab;
     const bool do_p = (mask & M_R4P) && pe > pb;
-    ea.gs = se > sb ? grid_for(se - sb) : 0u;
-    ea.gl = le > lb ? grid_for(le - lb) : 0u;
+    if (se > sb) wave_triggers(se - sb, 1024, ea.gs, ea.ts);
+    if (le > lb) wave_triggers(le - lb, 1024, ea.gl, ea.tl);
     ea.ga = do_a ? grid_for(se) : 0u;
     ea.gp = do_p ? grid_for(pe - pb) : 0u;
     ea.gx = ((mask & M_R6) && xe > xb) ? grid_for(xe - xb) : 0u;
