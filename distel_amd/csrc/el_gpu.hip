@@ -222,6 +222,7 @@ struct DState {
   uint32_t *xlog_x, *xlog_p;
   uint32_t *xs_x, *xs_p;
   uint32_t *cs_x, *cs_a, cs_cap;
+  uint32_t cs_chunk;  // S-queue reservation per wave (wq_publish_s; 0: one atomic per publish)
   uint32_t *ct_x, *ct_a, ct_cap;  // CR1 told-closure candidates
   uint32_t *cl_x, *cl_p, cl_cap;
   uint32_t *ca_y, *ca_c, ca_cap;
@@ -454,8 +455,8 @@ __device__ __forceinline__ uint32_t pair_lookup(const DIndex& ix, uint32_t r, ui
 }
 
 // LDS staging of the commit roles (new facts / links of a block round)
-constexpr uint32_t QS_CAP = 1024;
-constexpr uint32_t QL_CAP = 1024;
+constexpr uint32_t QS_CAP = 2048;  // (a block flushes ~QS_CAP/2 new facts per log atomic)
+constexpr uint32_t QL_CAP = 2048;
 
 // LDS slot for each predicated lane (one LDS atomic per wave)
 __device__ __forceinline__ uint32_t lds_reserve(uint32_t* qn, bool pred) {
@@ -492,6 +493,7 @@ struct WaveQ {
   uint32_t lx[WQ], lp[WQ];  // link candidates
   uint4 jb[WQJ];            // fan-out jobs
   uint32_t ns, nt, nl, nj;
+  uint32_t rs_base, rs_left;  // S queue: this wave's reserved slots (DState::cs_chunk)
 };
 struct BlockQ {
   WaveQ w[BLOCK / 64];
@@ -501,7 +503,7 @@ __device__ __forceinline__ WaveQ& wave_q(BlockQ& q) { return q.w[threadIdx.x >> 
 
 __device__ __forceinline__ void q_init(BlockQ& q) {
   WaveQ& w = wave_q(q);
-  if (lane_id() == 0) w.ns = w.nt = w.nl = w.nj = 0;
+  if (lane_id() == 0) w.ns = w.nt = w.nl = w.nj = w.rs_left = 0;
   for (uint32_t i = lane_id(); i < DEDUP_SLOTS; i += 64) w.seen[i] = ~0ull;
   __syncthreads();
 }
@@ -523,6 +525,46 @@ __device__ __forceinline__ void wq_publish(const T* qa, const uint32_t* qb, uint
       ga[slot] = qa[k];
       if (gb) gb[slot] = qb[k];
     }
+  }
+}
+
+// The S-candidate queue of a big step (G3's first superstep: 96 M candidates): a wave reserves
+// cs_chunk slots with one atomic and fills them over several publishes, instead of one atomic
+// on the queue counter per 256 records — 375 k same-address atomics at ~12 ns each
+// (MI355X_MICROARCH.md "fanin") were 4.5 ms of that step's k_jobs.  The reservation's unused
+// tail is marked x = NONE when the wave finishes (q_flush); the commit skips such holes.
+__device__ __forceinline__ void wq_publish_s(WaveQ& w, const DState& st, uint32_t n) {
+  if (n == 0) return;
+  const uint32_t chunk = st.cs_chunk;
+  if (chunk == 0) {
+    wq_publish(w.sx, w.sa, n, &st.ctr->cand_s, st.cs_x, st.cs_a, st.cs_cap);
+    return;
+  }
+  const unsigned long long act = __ballot(true);
+  const int leader = __ffsll((long long)act) - 1;
+  const uint32_t na = (uint32_t)__popcll(act), r = (uint32_t)__popcll(act & ((1ull << lane_id()) - 1ull));
+  uint32_t base = w.rs_base, left = w.rs_left;
+  for (uint32_t done = 0; done < n;) {
+    if (left == 0) {
+      uint32_t b = 0;
+      if ((int)lane_id() == leader) b = atomicAdd(&st.ctr->cand_s, chunk);
+      base = __shfl(b, leader);
+      left = chunk;
+    }
+    const uint32_t take = min(n - done, left), off = base + (chunk - left);
+    for (uint32_t k = r; k < take; k += na) {
+      const uint32_t slot = off + k;
+      if (slot < st.cs_cap) {
+        st.cs_x[slot] = w.sx[done + k];
+        st.cs_a[slot] = w.sa[done + k];
+      }
+    }
+    done += take;
+    left -= take;
+  }
+  if ((int)lane_id() == leader) {
+    w.rs_base = base;
+    w.rs_left = left;
   }
 }
 
@@ -559,7 +601,20 @@ __device__ __forceinline__ void emit_s(const DState& st, BlockQ& q, bool pred, u
       w.seen[slot] = key;
     }
   }
-  wq_push(w.sx, w.sa, w.ns, pred, x, a, &st.ctr->cand_s, st.cs_x, st.cs_a, st.cs_cap);
+  const unsigned long long m = __ballot(pred);
+  if (m == 0) return;
+  const uint32_t cnt = (uint32_t)__popcll(m);
+  uint32_t n = w.ns;
+  if (n + cnt > WQ) {
+    wq_publish_s(w, st, n);
+    n = 0;
+  }
+  if (pred) {
+    const uint32_t r = n + (uint32_t)__popcll(m & ((1ull << lane_id()) - 1ull));
+    w.sx[r] = x;
+    w.sa[r] = a;
+  }
+  if ((int)lane_id() == __ffsll((long long)__ballot(true)) - 1) w.ns = n + cnt;
 }
 
 __device__ __forceinline__ void emit_t(const DState& st, BlockQ& q, bool pred, uint32_t x, uint32_t a, Ev& ev) {
@@ -634,7 +689,15 @@ __device__ __forceinline__ void emit_p(const DState& st, bool pred, uint32_t pid
 // of its role, so the staged records of the step are all in the global queues).
 __device__ void q_flush(BlockQ& q, const DState& st) {
   WaveQ& w = wave_q(q);
-  wq_publish(w.sx, w.sa, w.ns, &st.ctr->cand_s, st.cs_x, st.cs_a, st.cs_cap);
+  wq_publish_s(w, st, w.ns);
+  if (st.cs_chunk) {  // the reservation's unused tail becomes holes
+    const unsigned long long act = __ballot(true);
+    const uint32_t na = (uint32_t)__popcll(act), r = (uint32_t)__popcll(act & ((1ull << lane_id()) - 1ull));
+    const uint32_t left = w.rs_left, off = w.rs_base + (st.cs_chunk - left);
+    for (uint32_t k = r; k < left; k += na)
+      if (off + k < st.cs_cap) st.cs_x[off + k] = NONE;
+    if ((int)lane_id() == __ffsll((long long)act) - 1) w.rs_left = 0;
+  }
   wq_publish(w.tx, w.ta, w.nt, &st.ctr->cand_t, st.ct_x, st.ct_a, st.ct_cap);
   wq_publish(w.lx, w.lp, w.nl, &st.ctr->cand_l, st.cl_x, st.cl_p, st.cl_cap);
   wq_publish<uint4>(w.jb, nullptr, w.nj, &st.ctr->jobs, st.jobs, nullptr, st.job_cap);
@@ -1193,7 +1256,7 @@ __device__ void commit_s(const DIndex& ix, const DState& st, CommitLds& sm, uint
     const uint32_t i = base + threadIdx.x;
     bool nw = false;
     uint32_t x = 0, a = 0;
-    if (i < n) {
+    if (i < n && qx[i] != NONE) {  // (NONE: a hole of a wave's reservation, wq_publish_s)
       x = qx[i];
       a = qa[i];
       ev.v[EL_EV_TRIG]++;
@@ -3125,6 +3188,13 @@ bool el_ctx::superstep(uint32_t mask, uint64_t sb, uint64_t se, uint64_t lb, uin
     ea.mask = mask | (!part() && l_count == l_base ? (uint32_t)M_LEMPTY : 0u) |
               (!part() && p_count == 0 ? (uint32_t)M_PEMPTY : 0u);
     ea.a_end = (uint32_t)a0;
+    // S-queue reservations for a big step, if the queue holds the holes too: at most one
+    // reservation's worth per wave of the expand and jobs launches (wq_publish_s)
+    if (!part() && !small_queues && (se - sb) + (le - lb) >= (1u << 18)) {
+      const uint64_t waves = (uint64_t)(ea.gs + ea.gl + ea.ga + ea.gp + tune_jobs) * (BLOCK / 64);
+      for (uint32_t c = 4096; c >= 1024 && !st.cs_chunk; c >>= 1)
+        if (4 * waves * c <= cs_cap) st.cs_chunk = c;
+    }
     if (split_expand) {  // the roles are independent: run them one launch each (rocprof sees each)
       const uint32_t g[4] = {ea.gs, ea.gl, ea.ga, ea.gp};
       // EL_SPLIT_EXPAND=2: the S role once more per rule group (CR1, CR2, CR3, CR4, the rest)
