@@ -1806,9 +1806,10 @@ __global__ void k_rehash(unsigned long long* t, unsigned long long mask, const u
 // el_init after a classification: only the words the fact log names can be non-zero, and
 // when the log is small next to the matrix, clearing those words beats streaming it all
 __global__ void k_clear_logged(DIndex ix, uint32_t* bits_base, const uint32_t* __restrict__ lx,
-                               const uint32_t* __restrict__ la, uint32_t n) {
+                               const uint32_t* __restrict__ la, uint32_t n, uint32_t row_from) {
   const uint32_t stride = gridDim.x * blockDim.x;
   for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    if (lx[i] < row_from) continue;  // (rows a releasing copy-back already cleared)
     const uint32_t c = col_of(ix, la[i]);
     if (c != NONE) bits_base[(uint64_t)lx[i] * ix.W + (c >> 5)] = 0u;
   }
@@ -2261,6 +2262,12 @@ struct el_ctx {
   const uint32_t* pid_rank = nullptr;        // device: pid -> q (an index buffer)
   std::vector<uint32_t> rank_role, rank_y;   // host: the pair (role, filler) of rank q
   hipStream_t cstream = nullptr;             // copy-back DMA, beside the row builds
+  // S-row read-out copy-back (el_copy_result): device staging chunks and their DMA stream
+  hipStream_t dstream = nullptr;
+  hipEvent_t ev_stage[2] = {nullptr, nullptr}, ev_dma[2] = {nullptr, nullptr};
+  uint32_t* stage[2] = {nullptr, nullptr};
+  uint64_t stage_cap = 0;
+  bool readout_off = getenv("EL_NO_READOUT") != nullptr;  // A/B: S rows by the log sort instead
   hipEvent_t ev_rows[2] = {nullptr, nullptr};
   // base links by predecessor (exrT: pid -> X) and by successor (exrC: X -> chain-second pid)
   const uint32_t *exrT_ptr = nullptr, *exrT_x = nullptr, *exrC_ptr = nullptr, *exrC_p = nullptr;
@@ -2480,6 +2487,7 @@ struct el_ctx {
   void reset_state();
   void ensure_capacity();
   void ensure_rows(bool facts, bool links);
+  void readout_rows(uint64_t* dptr, uint64_t* ptr_out, uint32_t* val_out, bool clear, hipEvent_t counted);
   // half: 0 = whole build, 1 = the part that reads the state, 2 = the rest (el_rows.h);
   // clear: the S-row build zeroes the bit matrix as it writes (a releasing copy-back)
   void build_rows(bool facts, hipStream_t s, uint64_t* ptr, uint32_t* dst, int half = 0, bool clear = false);
@@ -2489,7 +2497,10 @@ struct el_ctx {
   bool base_filling = false;                   // the set fill runs beside the first superstep
   void join_base();
   bool pre_reset = false;         // the device part of the next reset_state is already enqueued
-  void reset_device(hipStream_t s, bool matrix_clear = false);
+  // clear_from: the first row whose bits the reset clears (lo: all; hi: none — a releasing
+  // copy-back cleared the rows it read)
+  void reset_device(hipStream_t s, uint32_t clear_from);
+  void reset_device(hipStream_t s) { reset_device(s, lo); }
   void rehash_links(uint64_t cap);
   void rehash_acts(uint64_t cap);
   void rehash_props(uint64_t cap);
@@ -2716,7 +2727,11 @@ void el_ctx::column_window() {
   }
   ix.c_lo = c_lo;
   ix.c_hi = c_hi;
-  ix.W = (2 + (c_hi - c_lo) + 31) / 32;
+  // words per bit row, padded to 16 B (the S-row read-out streams rows with 16-B loads).  Not
+  // to whole 64-B lines: a row stride with a large power-of-two factor maps one column of
+  // every row onto a few L2 channels, and the CR4 fan-out walks columns (G3 with 64-B rows:
+  // +10 % saturation time)
+  ix.W = (((uint64_t)2 + (c_hi - c_lo) + 31) / 32 + 3) & ~3ull;
 }
 
 void el_ctx::free_index() {
@@ -2747,6 +2762,9 @@ void el_ctx::free_state() {
   dfree(cp_b);
   rs.release();
   rl.release();
+  if (dstream) (void)hipStreamSynchronize(dstream);
+  for (uint32_t*& p : stage) dfree(p);
+  stage_cap = 0;
   rsc.release();
   rsc_l.release();
   asc.release();
@@ -2946,15 +2964,16 @@ void el_ctx::alloc_state() {
 
 // The device part of reset_state on stream s: clear the bit matrix (by the fact log), the
 // sets, counters and gapped rows.  Reads only the logs and counts of the finished state.
-void el_ctx::reset_device(hipStream_t stream, bool matrix_clear) {
+void el_ctx::reset_device(hipStream_t stream, uint32_t clear_from) {
   FillArgs f{};
   auto add = [&](void* p, uint64_t bytes, uint32_t pattern) { f.seg[f.n++] = FillSeg{p, bytes, pattern}; };
   const uint64_t matrix_bytes = (uint64_t)(hi - lo) * W * sizeof(uint32_t);
-  if (matrix_clear) {
-    // the releasing copy-back's S-row sorts zero the matrix as they write the rows
-  } else if (bits_logged && s_count * 64 < matrix_bytes) {  // one 64-B line per logged fact vs. the whole matrix
+  if (clear_from >= hi) {
+    // the releasing copy-back zeroed the matrix as it read the rows
+  } else if (bits_logged && (clear_from > lo || s_count * 64 < matrix_bytes)) {
+    // one 64-B line per logged fact (of the rows still set) vs. the whole matrix
     hipLaunchKernelGGL(k_clear_logged, dim3(grid_for(s_count)), dim3(BLOCK), 0, stream, ix, dstate().bits, slog_x,
-                       slog_a, (uint32_t)s_count);
+                       slog_a, (uint32_t)s_count, clear_from);
     HIPCHK(hipGetLastError());
   } else {
     add(bits, matrix_bytes, 0u);
@@ -3109,6 +3128,62 @@ void el_ctx::build_rows(bool facts, hipStream_t s, uint64_t* ptr, uint32_t* dst,
   }
   if (half != 1)
     elrows::build_sort(s, sc, ptr, dst, clear ? elrows::Clear{dstate().bits, W, lo, ix.c_lo, ix.c_hi} : elrows::Clear{});
+}
+
+// S rows to the caller's page-locked buffers by read-out (el_copy_result): row counts from the
+// fact log, the offsets to the host (the caller's s_ptr or a scratch copy; one sync), then
+// chunks of rows read off the bit matrix into two device staging buffers in turn, each
+// shipped by DMA on dstream while the next is read.  clear: the read-out zeroes the matrix.
+void el_ctx::readout_rows(uint64_t* dptr, uint64_t* ptr_out, uint32_t* val_out, bool clear, hipEvent_t counted) {
+  const uint32_t R = uhi() - lo;
+  elrows::build_counts(stream, rsc, slog_x, s_count, lo, R, dptr);
+  if (counted) HIPCHK(hipEventRecord(counted, stream));
+  std::vector<uint64_t> tmp;
+  uint64_t* hp = ptr_out;
+  if (!hp) {
+    tmp.resize((size_t)R + 1);
+    hp = tmp.data();
+  }
+  HIPCHK(hipMemcpyAsync(hp, dptr, ((uint64_t)R + 1) * sizeof(uint64_t), hipMemcpyDeviceToHost, stream));
+  HIPCHK(hipStreamSynchronize(stream));
+  constexpr uint64_t CHUNK = 8u << 20;  // entries per DMA (32 MB)
+  uint64_t longest = 0;
+  for (uint32_t r = 0; r < R; ++r) longest = std::max(longest, hp[r + 1] - hp[r]);
+  const uint64_t need = std::max(CHUNK, longest);
+  if (need > stage_cap) {
+    HIPCHK(hipStreamSynchronize(dstream));
+    for (uint32_t*& p : stage) {
+      dfree(p);
+      p = dalloc<uint32_t>(need);
+    }
+    stage_cap = need;
+  }
+  const elrows::Clear m{dstate().bits, W, lo, ix.c_lo, ix.c_hi};
+  uint32_t k = 0;
+  for (uint32_t ra = 0; ra < R; ++k) {
+    uint32_t rb = ra + 1;  // rows while the chunk fits (at least one)
+    {
+      uint32_t lo_r = rb, hi_r = R;
+      while (lo_r < hi_r) {  // the last rb with hp[rb] - hp[ra] <= stage_cap
+        const uint32_t mid = lo_r + (hi_r - lo_r + 1) / 2;
+        if (hp[mid] - hp[ra] <= stage_cap)
+          lo_r = mid;
+        else
+          hi_r = mid - 1;
+      }
+      rb = lo_r;
+    }
+    const uint32_t slot = k & 1u;
+    if (k >= 2) HIPCHK(hipStreamWaitEvent(stream, ev_dma[slot], 0));  // the staging buffer is free
+    elrows::readout(stream, dptr, ra, rb, hp[ra], stage[slot], m, clear);
+    HIPCHK(hipEventRecord(ev_stage[slot], stream));
+    HIPCHK(hipStreamWaitEvent(dstream, ev_stage[slot], 0));
+    if (hp[rb] > hp[ra])
+      HIPCHK(hipMemcpyAsync(val_out + hp[ra], stage[slot], (hp[rb] - hp[ra]) * sizeof(uint32_t), hipMemcpyDeviceToHost,
+                            dstream));
+    HIPCHK(hipEventRecord(ev_dma[slot], dstream));
+    ra = rb;
+  }
 }
 
 // Device-resident result rows (el_get_subsumers, el_copy_facts / links, el_export_result),
@@ -3681,7 +3756,7 @@ void el_ctx::join_base() {
 
 // Carry a saturated state over to indexes rebuilt for old ∪ increment (el_add_axioms).
 void el_ctx::migrate_state(uint32_t N0, const std::vector<uint32_t>& pmap) {
-  const uint64_t N = hx.N, P = hx.P, W0 = W, W1 = (N + 31) / 32;
+  const uint64_t N = hx.N, P = hx.P, W0 = W, W1 = ix.W;  // (column_window of the new index)
   sync();
   if (N != N0) {  // wider bit rows, more rows: pitched copy of the old matrix
     uint32_t* nb = dalloc<uint32_t>(N * W1);
@@ -3872,6 +3947,9 @@ int el_create(el_ctx** out, const el_config* cfg) {
     HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
     HIPCHK(hipStreamCreateWithFlags(&c->cstream, hipStreamNonBlocking));
     HIPCHK(hipStreamCreateWithFlags(&c->rstream, hipStreamNonBlocking));
+    HIPCHK(hipStreamCreateWithFlags(&c->dstream, hipStreamNonBlocking));
+    for (hipEvent_t& e : c->ev_stage) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    for (hipEvent_t& e : c->ev_dma) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     for (hipEvent_t& e : c->ev_rows) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     HIPCHK(hipEventCreateWithFlags(&c->ev_reset, hipEventDisableTiming));
     for (hipEvent_t& e : c->ev_base) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
@@ -3884,10 +3962,15 @@ int el_create(el_ctx** out, const el_config* cfg) {
     if (c->stream) (void)hipStreamDestroy(c->stream);
     if (c->cstream) (void)hipStreamDestroy(c->cstream);
     if (c->rstream) (void)hipStreamDestroy(c->rstream);
+    if (c->dstream) (void)hipStreamDestroy(c->dstream);
     for (hipEvent_t e : c->ev_rows)
       if (e) (void)hipEventDestroy(e);
     if (c->ev_reset) (void)hipEventDestroy(c->ev_reset);
     for (hipEvent_t e : c->ev_base)
+      if (e) (void)hipEventDestroy(e);
+    for (hipEvent_t e : c->ev_stage)
+      if (e) (void)hipEventDestroy(e);
+    for (hipEvent_t e : c->ev_dma)
       if (e) (void)hipEventDestroy(e);
     delete c;
     return rc;
@@ -4271,9 +4354,10 @@ int el_copy_result(el_ctx* c, el_result* res) {
       uint64_t n;
       hipStream_t s;
       uint32_t* direct;
+      bool readout;  // S rows read off the bit matrix in chunks, each DMA'd behind its read-out
     };
-    Part parts[2] = {{false, res->l_ptr, res->l_pair, &c->rl, nl, c->cstream, nullptr},
-                     {true, res->s_ptr, res->s_val, &c->rs, nf, c->stream, nullptr}};
+    Part parts[2] = {{false, res->l_ptr, res->l_pair, &c->rl, nl, c->cstream, nullptr, false},
+                     {true, res->s_ptr, res->s_val, &c->rs, nf, c->stream, nullptr, false}};
     // the copy stream starts behind the saturation
     HIPCHK(hipEventRecord(c->ev_rows[1], c->stream));
     HIPCHK(hipStreamWaitEvent(c->cstream, c->ev_rows[1], 0));
@@ -4283,7 +4367,19 @@ int el_copy_result(el_ctx* c, el_result* res) {
       el_ctx::Rows& r = *p.rows;
       const uint64_t logged = p.facts ? c->s_count : c->l_count;  // Rows::n counts log entries
       p.direct = r.n == logged || !p.n ? nullptr : mapped_for_device(p.val_out);
-      if (p.direct) {  // sorted rows straight into the caller's page-locked buffer
+      // The S rows of a page-locked buffer come off the bit matrix when reading it (its row
+      // words up to each row's last entry) costs less than the log's count-scatter-sort: the
+      // read-out streams at HBM rate in chunks that the DMA engine ships at PCIe rate behind it,
+      // so the transfer starts after the row counts instead of after the whole build (G3:
+      // matrix 19 GB vs. 415 MB of rows; PCIe at ~57 GB/s is the bound either way).
+      // (measured: G3, matrix / rows = 46, read-out 0.6 ms faster; G5, 61, 0.17 ms slower)
+      p.readout = p.direct && p.facts && !c->readout_off && p.val_out && p.n >= (16u << 20) &&
+                  (uint64_t)(c->uhi() - c->lo) * c->W * 4 <= 48 * 4 * p.n;
+      if (p.readout) {
+        if (!r.ptr) r.ptr = dalloc<uint64_t>(R1);
+        r.n = ~0ull;
+        c->readout_rows(r.ptr, p.ptr_out, p.val_out, release, release ? c->ev_rows[0] : nullptr);
+      } else if (p.direct) {  // sorted rows straight into the caller's page-locked buffer
         if (!r.ptr) r.ptr = dalloc<uint64_t>(R1);
         r.n = ~0ull;  // r.ptr is reused; the device rows are not built
         c->build_rows(p.facts, p.s, r.ptr, p.direct, 1, fuse_clear);
@@ -4293,17 +4389,22 @@ int el_copy_result(el_ctx* c, el_result* res) {
       }
     }
     if (release) {  // the next classification's reset, beside the rest of the copy-back
-      HIPCHK(hipEventRecord(c->ev_rows[0], c->stream));
+      // (the read-out recorded ev_rows[0] once it had counted the rows: the reset touches no
+      // row it reads)
+      if (!parts[1].readout) HIPCHK(hipEventRecord(c->ev_rows[0], c->stream));
       HIPCHK(hipEventRecord(c->ev_rows[1], c->cstream));
       HIPCHK(hipStreamWaitEvent(c->rstream, c->ev_rows[0], 0));
       HIPCHK(hipStreamWaitEvent(c->rstream, c->ev_rows[1], 0));
-      c->reset_device(c->rstream, fuse_clear && parts[1].direct != nullptr);  // the S-row sorts clear the matrix
+      // rows the S-row sorts (all rows) or the read-out (the caller's rows) cleared as they went
+      const uint32_t clear_from = parts[1].readout ? c->uhi() : fuse_clear && parts[1].direct ? c->hi : c->lo;
+      c->reset_device(c->rstream, clear_from);
       HIPCHK(hipEventRecord(c->ev_reset, c->rstream));
     }
     // 2. the sorts into the caller's buffers, the device rows by DMA
     for (Part& p : parts) {
       if (!p.ptr_out && !p.val_out) continue;
       el_ctx::Rows& r = *p.rows;
+      if (p.readout) continue;  // (its DMAs are queued on dstream)
       if (p.direct) {
         c->build_rows(p.facts, p.s, r.ptr, p.direct, 2, fuse_clear);
         if (p.ptr_out) HIPCHK(hipMemcpyAsync(p.ptr_out, r.ptr, R1 * sizeof(uint64_t), hipMemcpyDeviceToHost, p.s));
@@ -4317,6 +4418,7 @@ int el_copy_result(el_ctx* c, el_result* res) {
     }
     HIPCHK(hipStreamSynchronize(c->cstream));
     HIPCHK(hipStreamSynchronize(c->stream));
+    HIPCHK(hipStreamSynchronize(c->dstream));
     if (release) {  // the reset may still run: el_init waits for it, free_state too
       c->pre_reset = true;
       c->inited = false;  // no state until el_init
@@ -4429,10 +4531,15 @@ void el_destroy(el_ctx* c) {
   if (c->stream) (void)hipStreamDestroy(c->stream);
   if (c->cstream) (void)hipStreamDestroy(c->cstream);
   if (c->rstream) (void)hipStreamDestroy(c->rstream);
+  if (c->dstream) (void)hipStreamDestroy(c->dstream);
   for (hipEvent_t e : c->ev_rows)
     if (e) (void)hipEventDestroy(e);
   if (c->ev_reset) (void)hipEventDestroy(c->ev_reset);
   for (hipEvent_t e : c->ev_base)
+    if (e) (void)hipEventDestroy(e);
+  for (hipEvent_t e : c->ev_stage)
+    if (e) (void)hipEventDestroy(e);
+  for (hipEvent_t e : c->ev_dma)
     if (e) (void)hipEventDestroy(e);
   delete c;
 }

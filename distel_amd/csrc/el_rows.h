@@ -15,6 +15,8 @@
 //   k_rows_lds      rows of <= 4096 entries: LDS bitonic sort, one workgroup per row -> dst
 //   k_rows_bits     longer rows with a bit matrix: the row's set bits in order (no sort) -> dst
 //   k_rows_global   longer rows without one: bitonic sort in place in tmp, then -> dst
+//   k_rows_readout  every row of a bit matrix, read off in column order (the S rows of a
+//                   large copy-back: build_counts + readout, chunked behind DMAs)
 //
 // dst may be device memory or page-locked host memory mapped for the device: the sort
 // kernels then write the sorted rows straight over PCIe (the copy-back is fused with the sort,
@@ -74,5 +76,15 @@ void build(hipStream_t s, Scratch& sc, const uint32_t* rows, const uint32_t* val
 void build_prep(hipStream_t s, Scratch& sc, const uint32_t* rows, const uint32_t* vals, uint64_t n, uint32_t row_lo,
                 uint32_t R, const uint32_t* keymap, uint64_t* ptr, uint32_t* dst, Clear matrix, bool clear);
 void build_sort(hipStream_t s, Scratch& sc, const uint64_t* ptr, uint32_t* dst, Clear cl);
+
+// Row offsets only (counts of the log's rows, scanned): ptr (device), R + 1 entries.
+void build_counts(hipStream_t s, Scratch& sc, const uint32_t* rows, uint64_t n, uint32_t row_lo, uint32_t R,
+                  uint64_t* ptr);
+// Rows [r0, r1) of a bit matrix whose rows hold exactly the counted entries (ptr from
+// build_counts over the same log), read off the matrix in column order — sorted without a
+// sort — into dst[ptr[r] - out0 ...] (device memory); clear zeroes the words read.  W must be a
+// multiple of 4 (rows 16-B aligned).
+void readout(hipStream_t s, const uint64_t* ptr, uint32_t r0, uint32_t r1, uint64_t out0, uint32_t* dst, Clear m,
+             bool clear);
 
 }  // namespace elrows

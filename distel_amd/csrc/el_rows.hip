@@ -8,6 +8,7 @@
 // one.
 #include "el_rows.h"
 
+#include <algorithm>
 #include <stdexcept>
 #include <string>
 
@@ -65,7 +66,7 @@ __global__ void __launch_bounds__(BLOCK) k_rows_count(const uint32_t* __restrict
     uint32_t base = 0;
     if (head) base = atomicAdd(cnt + x, end - lane);
     base = __shfl(base, (int)(h & 63u));
-    if (ok) rank[i] = base + (lane - h);
+    if (ok && rank) rank[i] = base + (lane - h);
   }
 }
 
@@ -352,6 +353,70 @@ __global__ void __launch_bounds__(BLOCK) k_rows_bits(const uint64_t* __restrict_
   }
 }
 
+// Rows [r0, r1) read off the bit matrix whole: the set columns of row r, in order, to
+// dst[ptr[r] - out0 ...] (the rows of a copy-back chunk, staged in device memory for a DMA).
+// One workgroup per row, 16 words per lane per round (four 16-B loads in flight), popcounts
+// and a block scan give each lane its output slots.  A row stops at its last entry (ptr says
+// how many): the columns are concept ids and a closure's members are mostly older concepts.
+// clear: the read words are zeroed (the caller releases its state; only non-zero words are
+// written).
+__global__ void __launch_bounds__(BLOCK) k_rows_readout(const uint64_t* __restrict__ ptr, uint32_t r0, uint32_t r1,
+                                                        uint64_t out0, uint32_t* __restrict__ dst, Clear m,
+                                                        bool clear) {
+  __shared__ uint32_t wsum[BLOCK / 64];
+  const uint32_t tid = threadIdx.x, lane = __lane_id(), wv = tid >> 6;
+  const uint64_t W4 = m.W / 4;
+  for (uint32_t r = r0 + blockIdx.x; r < r1; r += gridDim.x) {
+    const uint64_t b = ptr[r], len = ptr[r + 1] - b;
+    if (len == 0) continue;  // (block-uniform)
+    uint4* __restrict__ row = reinterpret_cast<uint4*>(m.bits + (uint64_t)(r + m.lo) * m.W);
+    uint64_t done = 0;
+    for (uint64_t q0 = 0; q0 < W4 && done < len; q0 += BLOCK * 4) {
+      uint4 v[4];
+      uint32_t c = 0;
+#pragma unroll
+      for (uint32_t i = 0; i < 4; ++i) {
+        const uint64_t q = q0 + tid * 4 + i;
+        v[i] = q < W4 ? row[q] : make_uint4(0u, 0u, 0u, 0u);
+        c += __popc(v[i].x) + __popc(v[i].y) + __popc(v[i].z) + __popc(v[i].w);
+      }
+      uint32_t inc = c;
+#pragma unroll
+      for (uint32_t o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(inc, o);
+        if (lane >= o) inc += y;
+      }
+      if (lane == 63) wsum[wv] = inc;
+      __syncthreads();
+      uint32_t before = 0, total = 0;
+#pragma unroll
+      for (uint32_t k = 0; k < BLOCK / 64; ++k) {
+        before += k < wv ? wsum[k] : 0u;
+        total += wsum[k];
+      }
+      uint32_t* o = dst + (b - out0) + done + before + inc - c;
+#pragma unroll
+      for (uint32_t i = 0; i < 4; ++i) {
+        const uint64_t q = q0 + tid * 4 + i;
+        const uint32_t wd[4] = {v[i].x, v[i].y, v[i].z, v[i].w};
+#pragma unroll
+        for (uint32_t j = 0; j < 4; ++j) {
+          uint32_t word = wd[j];
+          const uint32_t cb = (uint32_t)((q * 4 + j) * 32);
+          while (word) {
+            const uint32_t col = cb + (uint32_t)__ffs(word) - 1;
+            *o++ = col < 2u ? col : col + m.c_lo - 2u;  // column -> concept
+            word &= word - 1;
+          }
+        }
+        if (clear && (v[i].x | v[i].y | v[i].z | v[i].w)) row[q] = make_uint4(0u, 0u, 0u, 0u);
+      }
+      done += total;
+      __syncthreads();  // wsum is reused
+    }
+  }
+}
+
 // Long rows without a bit matrix: bitonic sort in place in tmp, one workgroup per row, then
 // the row to dst.  The network only ever puts the smaller value at the lower index (the first
 // merge step of each stage compares mirrored positions), so positions past the row act as
@@ -450,6 +515,36 @@ void build_sort(hipStream_t s, Scratch& sc, const uint64_t* ptr, uint32_t* dst, 
     hipLaunchKernelGGL(k_rows_global, dim3(512), dim3(BLOCK), 0, s, ptr, sc.tmp, dst, sc.lists, sc.nlist, R);
     RCHK(hipGetLastError());
   }
+}
+
+void build_counts(hipStream_t s, Scratch& sc, const uint32_t* rows, uint64_t n, uint32_t row_lo, uint32_t R,
+                  uint64_t* ptr) {
+  ensure(sc.cnt, sc.cnt_cap, (uint64_t)R + 1);
+  ensure(sc.lists, sc.list_cap, 2 * (uint64_t)R + 2);
+  if (!sc.nlist) RCHK(hipMalloc((void**)&sc.nlist, 128 * sizeof(uint32_t)));
+  RCHK(hipMemsetAsync(sc.cnt, 0, ((uint64_t)R + 1) * sizeof(uint32_t), s));
+  RCHK(hipMemsetAsync(sc.nlist, 0, 128 * sizeof(uint32_t), s));
+  if (n) {
+    hipLaunchKernelGGL(k_rows_count, dim3(grid(n, 2048)), dim3(BLOCK), 0, s, rows, n, row_lo, R, sc.cnt,
+                       (uint32_t*)nullptr);
+    RCHK(hipGetLastError());
+  }
+  const uint32_t tiles = (uint32_t)(((uint64_t)R + 1 + SCAN_TILE - 1) / SCAN_TILE);
+  ensure(sc.tile, sc.tile_cap, tiles);
+  hipLaunchKernelGGL(k_rows_tiles, dim3(tiles), dim3(BLOCK), 0, s, sc.cnt, R + 1, sc.tile);
+  RCHK(hipGetLastError());
+  hipLaunchKernelGGL(k_rows_tile_scan, dim3(1), dim3(BLOCK), 0, s, sc.tile, tiles);
+  RCHK(hipGetLastError());
+  hipLaunchKernelGGL(k_rows_offsets, dim3(tiles), dim3(BLOCK), 0, s, sc.cnt, R, sc.tile, ptr, sc.lists, sc.nlist);
+  RCHK(hipGetLastError());
+}
+
+void readout(hipStream_t s, const uint64_t* ptr, uint32_t r0, uint32_t r1, uint64_t out0, uint32_t* dst, Clear m,
+             bool clear) {
+  if (r1 <= r0) return;
+  hipLaunchKernelGGL(k_rows_readout, dim3(std::min<uint32_t>(r1 - r0, 4096)), dim3(BLOCK), 0, s, ptr, r0, r1, out0,
+                     dst, m, clear);
+  RCHK(hipGetLastError());
 }
 
 void build(hipStream_t s, Scratch& sc, const uint32_t* rows, const uint32_t* vals, uint64_t n, uint32_t row_lo,
