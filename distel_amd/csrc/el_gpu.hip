@@ -2304,6 +2304,14 @@ struct el_ctx {
   uint64_t l_base = 0;  // base links at the head of the link log (ix.base; install_base)
   bool fresh = false;   // el_init ran and no superstep since: el_saturate installs the base links
   void install_base();
+  // The logs are indexed by uint32 counters on the device (DCounters): a step whose logs could
+  // pass 2^32 entries (count + every candidate new) fails with EL_ENOMEM instead of wrapping.
+  void check_u32_room() const {
+    const uint64_t lim = 0xffffffffull;
+    if (s_count + cs_cap + ct_cap > lim || l_count + cl_cap + remote_bound() > lim ||
+        a_count + ca_cap + remote_bound() > lim || p_count + cp_cap + remote_bound() > lim)
+      throw ElError{EL_ENOMEM, "a log would pass 2^32 entries (uint32 device counters)"};
+  }
   uint64_t wm_s[EL_NUM_RULE_TYPES] = {}, wm_l[EL_NUM_RULE_TYPES] = {}, wm_a[EL_NUM_RULE_TYPES] = {},
            wm_p[EL_NUM_RULE_TYPES] = {}, wm_x = 0;
   el_stats last{};
@@ -3223,6 +3231,7 @@ bool el_ctx::superstep(uint32_t mask, uint64_t sb, uint64_t se, uint64_t lb, uin
   if (!(se > sb || le > lb || do_a || do_p)) return false;
   const uint64_t s0 = s_count, l0 = l_count, a0 = a_count, p0 = p_count;
   for (int attempt = 0;; ++attempt) {
+    check_u32_room();
     // ---- capacities: every candidate could be new.  Growth copies device arrays outside
     // the stream, so the previous step's kernels must have finished first.
     const bool grow = s_count + cs_cap + ct_cap > slog_cap || l_count + cl_cap > llog_cap ||
