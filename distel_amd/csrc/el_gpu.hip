@@ -2815,11 +2815,16 @@ void el_ctx::alloc_state() {
   W = ix.W;  // bit-row words: ⊥, ⊤ and the column window
   bits = dalloc<uint32_t>((uint64_t)(hi - lo) * W);  // owned rows only
   bits_logged = false;
-  slog_cap = std::max<uint64_t>(1u << 20, 8 * N);
+  // capacities follow the owned rows (a partition of a ×8 ontology holds one copy's rows: its
+  // queues and logs are sized for those, not for the whole index it loads)
+  const uint64_t Nown = hi - lo;
+  uint64_t told_own = 0;  // the first superstep emits the told closure of every owned row
+  for (uint32_t x = lo; x < hi; ++x) told_own += hx.told.ptr[x + 1] - hx.told.ptr[x];
+  slog_cap = std::max<uint64_t>(1u << 20, 8 * Nown);
   slog_x = dalloc<uint32_t>(slog_cap);
   slog_a = dalloc<uint32_t>(slog_cap);
   slog_f = dalloc<uint8_t>(slog_cap);
-  llog_cap = std::max<uint64_t>(1u << 20, 4 * N);
+  llog_cap = std::max<uint64_t>(1u << 20, 4 * Nown);
   llog_x = dalloc<uint32_t>(llog_cap);
   llog_p = dalloc<uint32_t>(llog_cap);
   lhash_cap = next_pow2(2 * llog_cap);
@@ -2858,7 +2863,7 @@ void el_ctx::alloc_state() {
       }
     }
   }
-  cs_cap = std::max<uint64_t>(std::max<uint64_t>(1u << 20, 4 * N), next_pow2(b_conj + b_conj / 4));
+  cs_cap = std::max<uint64_t>(std::max<uint64_t>(1u << 20, 4 * Nown), next_pow2(b_conj + b_conj / 4));
   cl_cap = std::max<uint64_t>(1u << 20, next_pow2(b_link + b_link / 4));
   if (const char* e = getenv("EL_QUEUE_CAP")) {  // tests: small queues force overflowing steps
     cs_cap = cl_cap = std::max<uint64_t>(256, next_pow2(strtoull(e, nullptr, 10)));
@@ -2923,7 +2928,7 @@ void el_ctx::alloc_state() {
   cs_x = dalloc<uint32_t>(cs_cap);
   cs_a = dalloc<uint32_t>(cs_cap);
   // the first superstep emits the whole told closure of every concept (its init fact X ∈ S(X))
-  ct_cap = std::max<uint64_t>(cs_cap, next_pow2(2 * (uint64_t)hx.told.a.size() + 1024));
+  ct_cap = std::max<uint64_t>(cs_cap, next_pow2(2 * told_own + 1024));
   ct_x = dalloc<uint32_t>(ct_cap);
   ct_a = dalloc<uint32_t>(ct_cap);
   cl_x = dalloc<uint32_t>(cl_cap);
@@ -2942,7 +2947,7 @@ void el_ctx::alloc_state() {
       slog_f = dalloc<uint8_t>(slog_cap);
     }
   }
-  job_cap = std::max<uint64_t>(1u << 20, 2 * N);
+  job_cap = std::max<uint64_t>(1u << 20, 2 * Nown);
   jobs = dalloc<uint4>(job_cap);
   ctr = dalloc<DCounters>(1);
   // coherent: k_commit's stores reach the host while later kernels of the step still run
