@@ -132,8 +132,9 @@ struct DIndex {
   // hold (el_ctx::column_window; the whole ontology: 2, N, i.e. column = concept id)
   uint32_t c_lo, c_hi;
   uint32_t part;               // 1 = partitioned protocol (oracle/partition_model.py)
-  uint32_t base;               // 1 = the base links {(X, p) : p ∈ exr(X)} are in the link log and
-                               // rows but not in the link set (el_ctx::install_base)
+  uint32_t base;               // 1 = the base links {(X, p) : p ∈ exr(X)} and base propagations
+                               // are in their logs and rows but not in their sets (install_base)
+  const uint32_t *bpp_ptr, *bpp_b;  // base propagations: pid -> B, ascending
   const uint8_t* role_chs;     // r -> r is the second role of some chain (its links are exchanged)
 };
 
@@ -439,6 +440,28 @@ __device__ __forceinline__ bool link_known(const DIndex& ix, const DState& st, u
   if (lempty) return false;
   ev.v[EL_EV_HASH]++;
   return hash_contains(st.lhash, st.lmask, link_key(pid, x));
+}
+
+// ((r, Y), B) known at t-1: a base propagation (binary search of bpp(pid)), or in the set
+__device__ __forceinline__ bool prop_known(const DIndex& ix, const DState& st, uint32_t pid, uint32_t b,
+                                           bool pempty, Ev& ev) {
+  if (ix.base) {
+    ev.v[EL_EV_ROW]++;
+    uint32_t lo = ix.bpp_ptr[pid], hi = ix.bpp_ptr[pid + 1];
+    while (lo < hi) {
+      const uint32_t mid = (lo + hi) >> 1;
+      ev.v[EL_EV_ENT]++;
+      const uint32_t v = ix.bpp_b[mid];
+      if (v == b) return true;
+      if (v < b)
+        lo = mid + 1;
+      else
+        hi = mid;
+    }
+  }
+  if (pempty) return false;
+  ev.v[EL_EV_HASH]++;
+  return hash_contains(st.phash, st.pmask, link_key(pid, b));
 }
 
 // (role, filler) -> pid by a scan of the filler's pair range (sorted by role)
@@ -910,7 +933,8 @@ __device__ void expand_s(const DIndex& ix, const DState& st, BlockQ& q, uint32_t
     }
     {  // A ∈ S(Y=X) new, ∃r.A ⊑ B  =>  propagation ((r, Y), B)
        // (Type3_1AxiomProcessorBase.java:208-234 writes "Yr" -> B)
-      const bool on = star && (mask & M_R4Y);
+      // (an init fact's own propagations are the base propagations, already in place)
+      const bool on = star && (mask & M_R4Y) && !(ix.base && f == 2);
       if (on) ev.v[EL_EV_ROW]++;
       wave_rows(on ? m0.w : 0u, on ? m1.w : 0u, [&](bool v, uint32_t own, uint32_t j) {
         const uint32_t Yo = __shfl(X, (int)own);
@@ -922,11 +946,7 @@ __device__ void expand_s(const DIndex& ix, const DState& st, BlockQ& q, uint32_t
           ev.v[EL_EV_ENT] += 2;
           pid = pair_lookup(ix, r, Yo, ev);
           if (pid != NONE) {
-            fresh = true;
-            if (!(mask & M_PEMPTY)) {
-              ev.v[EL_EV_HASH]++;
-              fresh = !hash_contains(st.phash, st.pmask, link_key(pid, B));
-            }
+            fresh = !prop_known(ix, st, pid, B, mask & M_PEMPTY, ev);
             if (fresh && (mask & M_R4D)) {  // fused mode: B reaches today's predecessors now
               ev.v[EL_EV_ROW]++;
               const uint2 row = gap_row(st.pr, pid);
@@ -2302,6 +2322,7 @@ struct el_ctx {
   bool events_queued = false;
   uint64_t s_count = 0, l_count = 0, a_count = 0, p_count = 0, s_init = 0;
   uint64_t l_base = 0;  // base links at the head of the link log (ix.base; install_base)
+  uint64_t p_base = 0;  // base propagations at the head of the propagation log
   bool fresh = false;   // el_init ran and no superstep since: el_saturate installs the base links
   void install_base();
   // The logs are indexed by uint32 counters on the device (DCounters): a step whose logs could
@@ -2593,6 +2614,8 @@ std::string el_ctx::install_index(el::HostIndex&& hnew) {
   exrT_x = up32(h.exrT.a);
   exrC_ptr = up32(h.exrC.ptr);
   exrC_p = up32(h.exrC.a);
+  d.bpp_ptr = up32(h.bpp.ptr);
+  d.bpp_b = up32(h.bpp.a);
   {  // link export order: pair ids ranked by (role, filler)
     std::vector<uint32_t> ord(h.P), rank(h.P);
     std::iota(ord.begin(), ord.end(), 0u);
@@ -3029,7 +3052,7 @@ void el_ctx::reset_state() {
   s_count = l_count = a_count = p_count = s_init = x_count = 0;
   if (base_filling) HIPCHK(hipStreamWaitEvent(stream, ev_base[1], 0));  // (an interrupted saturation)
   base_filling = false;
-  l_base = 0;
+  l_base = p_base = 0;
   ix.base = 0;
   rs.n = rl.n = ~0ull;  // result rows are stale
   act_n = ~0ull;
@@ -3069,14 +3092,15 @@ void el_ctx::rehash_acts(uint64_t cap) {
 }
 
 void el_ctx::rehash_props(uint64_t cap) {
+  if (base_filling) HIPCHK(hipEventSynchronize(ev_base[1]));  // (not while the set fill writes it)
   dfree(phash);
   phash_cap = cap;
   phash = dalloc<unsigned long long>(cap);
   HIPCHK(hipMemsetAsync(phash, 0xff, cap * sizeof(unsigned long long), stream));
-  if (p_count)
+  if (p_count > p_base)  // the base propagations stay out of the set
     launch(EL_K_REHASH, [&] {
-      hipLaunchKernelGGL(k_rehash, dim3(grid_for(p_count)), dim3(BLOCK), 0, stream, phash, cap - 1,
-                         plog_b, plog_p, (uint32_t)p_count);
+      hipLaunchKernelGGL(k_rehash, dim3(grid_for(p_count - p_base)), dim3(BLOCK), 0, stream, phash, cap - 1,
+                         plog_b + p_base, plog_p + p_base, (uint32_t)(p_count - p_base));
     });
 }
 
@@ -3242,7 +3266,7 @@ bool el_ctx::superstep(uint32_t mask, uint64_t sb, uint64_t se, uint64_t lb, uin
     const bool grow = s_count + cs_cap + ct_cap > slog_cap || l_count + cl_cap > llog_cap ||
                       2 * (l_count - l_base + cl_cap) > lhash_cap || a_count + ca_cap > alog_cap ||
                       2 * (a_count + ca_cap) > ahash_cap || p_count + cp_cap > plog_cap ||
-                      2 * (p_count + cp_cap) > phash_cap;
+                      2 * (p_count - p_base + cp_cap) > phash_cap;
     if (grow) sync();
     auto grow_log = [&](uint64_t used, uint64_t add, uint64_t& cap, uint32_t*& a, uint32_t*& b) {
       if (used + add <= cap) return;
@@ -3261,7 +3285,7 @@ bool el_ctx::superstep(uint32_t mask, uint64_t sb, uint64_t se, uint64_t lb, uin
     grow_log(a_count, ca_cap, alog_cap, alog_y, alog_c);
     if (2 * (a_count + ca_cap) > ahash_cap) rehash_acts(next_pow2(2 * (a_count + ca_cap)));
     grow_log(p_count, cp_cap, plog_cap, plog_p, plog_b);
-    if (2 * (p_count + cp_cap) > phash_cap) rehash_props(next_pow2(2 * (p_count + cp_cap)));
+    if (2 * (p_count - p_base + cp_cap) > phash_cap) rehash_props(next_pow2(2 * (p_count - p_base + cp_cap)));
 
     // ---- generation (reads only the state of step t-1; candidate counters are zero here)
     refresh_acts();
@@ -3275,7 +3299,7 @@ bool el_ctx::superstep(uint32_t mask, uint64_t sb, uint64_t se, uint64_t lb, uin
     ea.ab = (uint32_t)ab, ea.ae = (uint32_t)ae, ea.pb = (uint32_t)pb, ea.pe = (uint32_t)pe;
     // an empty link / propagation set (the first superstep): their probes cannot hit
     ea.mask = mask | (!part() && l_count == l_base ? (uint32_t)M_LEMPTY : 0u) |
-              (!part() && p_count == 0 ? (uint32_t)M_PEMPTY : 0u);
+              (!part() && p_count == p_base ? (uint32_t)M_PEMPTY : 0u);
     ea.a_end = (uint32_t)a0;
     // S-queue reservations for a big step, if the queue holds the holes too: at most one
     // reservation's worth per wave of the expand and jobs launches (wq_publish_s)
@@ -3743,10 +3767,41 @@ void el_ctx::install_base() {
   // superstep finds them by binary search and inserts only other links, and concurrent
   // inserts of distinct keys are safe); the second superstep waits for it (join_base) and
   // from then on membership is one probe of the set, as for every other link.
+  // Base propagations likewise (the CR4 half-1 records of the init facts, bpp): the log, the
+  // propagation rows (presized for them), the set beside the first superstep.  That superstep's
+  // base links then pull them (CR4 half-2, per link, X-major) instead of the init facts' fresh
+  // propagations fanning out over the base predecessors.
+  const uint64_t nbp = hx.bpp.a.size();
+  const bool props = nbp && use_props && PP.live && PP.start0;
+  if (props) {
+    if (nbp + cp_cap > plog_cap) {
+      sync();
+      plog_cap = next_pow2(nbp + cp_cap + (nbp + cp_cap) / 2);
+      dgrow(plog_p, 0, plog_cap);
+      dgrow(plog_b, 0, plog_cap);
+    }
+    if (2 * (nbp + cp_cap) > phash_cap) rehash_props(next_pow2(2 * (nbp + cp_cap)));
+    launch(EL_K_INIT, [&] {
+      hipLaunchKernelGGL(k_csr_scatter, dim3(grid(nbp)), dim3(256), 0, stream, ix.bpp_ptr, ix.bpp_b, P, (uint32_t)nbp,
+                         plog_p, plog_b, nullptr, nullptr);
+      hipLaunchKernelGGL(k_gap_len, dim3(grid(P)), dim3(256), 0, stream, ix.bpp_ptr, P, PP.len);
+      hipLaunchKernelGGL(k_csr_scatter, dim3(grid(nbp)), dim3(256), 0, stream, ix.bpp_ptr, ix.bpp_b, P, (uint32_t)nbp,
+                         nullptr, nullptr, PP.start, PP.val);
+    });
+    hipLaunchKernelGGL(k_set_u32, dim3(1), dim3(1), 0, stream, &ctr->p_log, (uint32_t)nbp);
+    HIPCHK(hipGetLastError());
+    p_count = p_base = nbp;
+    for (int r = 0; r < EL_NUM_RULE_TYPES; ++r) wm_p[r] = nbp;  // (nothing left to fan out)
+    host_ev[EL_K_INIT][EL_EV_ENT] += 2 * nbp;
+    host_ev[EL_K_INIT][EL_EV_EMIT] += nbp;
+  }
   HIPCHK(hipEventRecord(ev_base[0], stream));
   HIPCHK(hipStreamWaitEvent(rstream, ev_base[0], 0));
   hipLaunchKernelGGL(k_rehash, dim3(grid_for(nb, 2048)), dim3(BLOCK), 0, rstream, lhash, lhash_cap - 1, llog_x, llog_p,
                      (uint32_t)nb);
+  if (props)
+    hipLaunchKernelGGL(k_rehash, dim3(grid_for(nbp, 2048)), dim3(BLOCK), 0, rstream, phash, phash_cap - 1, plog_b,
+                       plog_p, (uint32_t)nbp);
   HIPCHK(hipGetLastError());
   HIPCHK(hipEventRecord(ev_base[1], rstream));
   base_filling = true;
@@ -3763,8 +3818,8 @@ void el_ctx::join_base() {
   if (!base_filling) return;
   HIPCHK(hipStreamWaitEvent(stream, ev_base[1], 0));
   base_filling = false;
-  host_ev[EL_K_REHASH][EL_EV_HASH] += l_base;
-  l_base = 0;
+  host_ev[EL_K_REHASH][EL_EV_HASH] += l_base + p_base;
+  l_base = p_base = 0;
   ix.base = 0;
 }
 
@@ -3805,7 +3860,7 @@ void el_ctx::migrate_state(uint32_t N0, const std::vector<uint32_t>& pmap) {
     dfree(dmap);
   }
   join_base();
-  l_base = 0;  // every link goes into the set: the base links of the old index are plain links now
+  l_base = p_base = 0;  // every link goes into the set: the base links of the old index are plain links now
   ix.base = 0;
   fresh = false;
   rehash_links(lhash_cap);

@@ -421,6 +421,19 @@ std::string build_index(const el_axioms& ax_in, HostIndex& o, uint32_t flags) {
       o.exrC.ptr[x + 1] = (uint32_t)o.exrC.a.size();
     }
   }
+  // Base propagations: the CR4 half-1 records every init fact Y ∈ S(Y) makes over its told
+  // closure, {((r, Y), B) : (r, B) ∈ exl(Y), (r, Y) a pair} — installed with the base links.
+  // Rows by pid: Y ascending and exl(Y) sorted by (r, B), pids sorted by (Y, r), so the rows
+  // come out pid-major with B ascending and unique.
+  o.bpp.ptr.assign(o.P + 1, 0);
+  for (uint32_t y = 0; y < N; ++y)
+    for (uint32_t j = o.exl.ptr[y]; j < o.exl.ptr[y + 1]; ++j) {
+      const uint32_t pid = pid_of(o.exl.a[j], y);
+      if (pid == 0xffffffffu) continue;
+      o.bpp.a.push_back(o.exl.b[j]);
+      o.bpp.ptr[pid + 1]++;
+    }
+  for (uint32_t p = 0; p < o.P; ++p) o.bpp.ptr[p + 1] += o.bpp.ptr[p];
 #undef CHECK
   return "";
 }

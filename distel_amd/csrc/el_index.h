@@ -43,6 +43,7 @@ struct HostIndex {
   std::vector<uint8_t> role_has_exl;  // r -> any ∃r.A ⊑ B
   Csr exrT;       // pid -> X with pid ∈ exr(X), X ascending      base links by predecessor
   Csr exrC;       // X -> pids of exr(X) whose role is second in a chain   base links by successor
+  Csr bpp;        // pid = (r, Y) -> B with (r, B) ∈ exl(Y), ascending        base propagations
 };
 
 // Owned copy of the typed axioms (el_load copies its input; el_add_axioms appends an

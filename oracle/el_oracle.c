@@ -249,7 +249,8 @@ struct elo_ctx {
   /* base links {(X, p) : p ∈ exr(X)} installed by elo_saturate before its first superstep
    * (el_ctx::install_base): the head of the link log, not in the link set */
   int base, fresh;
-  uint64_t l_base;
+  uint64_t l_base, p_base;
+  uint32_t* bpn; /* base propagations per pid: the head of prow[pid], B ascending */
   int need_pred, need_succ; /* the GPU maintains these CSRs only when they have readers */
   int has_bot;              /* some axiom concludes ⊥: else the ⊥ rule cannot fire (skipped, as on the GPU) */
   /* slack capacities of the GPU's gapped CSR rows (predecessors, successors, propagations)
@@ -612,6 +613,7 @@ int elo_create(elo_ctx** out, const el_axioms* ax, int mode) {
   c->has_act = (uint8_t*)calloc(c->N, 1);
   c->actrow = (vec*)calloc(c->N, sizeof(vec));
   c->prow = (vec*)calloc(c->P ? c->P : 1, sizeof(vec));
+  c->bpn = (uint32_t*)calloc(c->P ? c->P : 1, sizeof(uint32_t));
   c->cap_pr = (uint32_t*)malloc((c->P ? c->P : 1) * sizeof(uint32_t));
   c->cap_pp = (uint32_t*)malloc((c->P ? c->P : 1) * sizeof(uint32_t));
   c->cap_sc = (uint32_t*)malloc((c->N ? c->N : 1) * sizeof(uint32_t));
@@ -740,6 +742,28 @@ static int link_known(elo_ctx* c, int kern, uint32_t x, uint32_t pid, int lempty
   return hs_has(&c->links, lkey(pid, x));
 }
 
+/* ((r, Y), B) known at t-1: a base propagation (binary search of the head of prow[pid], as
+ * prop_known searches bpp on the GPU), or in the set (pempty: the set is empty, no probe) */
+static int prop_known(elo_ctx* c, int kern, uint32_t pid, uint32_t b, int pempty) {
+  if (c->base) {
+    uint32_t lo = 0, hi = c->bpn[pid];
+    EV(kern, EL_EV_ROW);
+    while (lo < hi) {
+      uint32_t mid = (lo + hi) >> 1, v;
+      EV(kern, EL_EV_ENT);
+      v = c->prow[pid].v[mid];
+      if (v == b) return 1;
+      if (v < b)
+        lo = mid + 1;
+      else
+        hi = mid;
+    }
+  }
+  if (pempty) return 0;
+  EV(kern, EL_EV_HASH);
+  return hs_has(&c->props, lkey(pid, b));
+}
+
 /* predecessor / succ / S-row "CSR" views: begin offset is irrelevant on the CPU, the
  * job carries the list identity (kind + owner) instead */
 static void expand_s(elo_ctx* c, cands* k, uint32_t mask, uint64_t b, uint64_t e, uint64_t a_end) {
@@ -802,15 +826,16 @@ static void expand_s(elo_ctx* c, cands* k, uint32_t mask, uint64_t b, uint64_t e
         if (!link_known(c, K, X, pid, (mask & M_LEMPTY) != 0)) emit_l(c, k, K, X, pid);
       }
     }
-    if ((mask & M_R4Y) && c->slog_f.v[i] != 1) { /* A ∈ S(Y=X) new, ∃r.A ⊑ B => propagation ((r, Y), B) */
+    /* A ∈ S(Y=X) new, ∃r.A ⊑ B => propagation ((r, Y), B); an init fact's own propagations are
+     * the base propagations, already in place */
+    if ((mask & M_R4Y) && c->slog_f.v[i] != 1 && !(c->base && c->slog_f.v[i] == 2)) {
       EV(K, EL_EV_ROW);
       for (j = c->exl.ptr[A]; j < c->exl.ptr[A + 1]; ++j) {
         uint32_t r = c->exl.a[j], B = c->exl.b[j], pid;
         EVN(K, EL_EV_ENT, 2);
         pid = pair_lookup(c, K, r, X);
         if (pid != NONE) {
-          if (!(mask & M_PEMPTY)) EV(K, EL_EV_HASH);
-          if ((mask & M_PEMPTY) || !hs_has(&c->props, lkey(pid, B))) {
+          if (!prop_known(c, K, pid, B, (mask & M_PEMPTY) != 0)) {
             EV(K, EL_EV_EMIT);
             vpush(&k->pp, pid);
             vpush(&k->pb, B);
@@ -1070,7 +1095,7 @@ static int superstep(elo_ctx* c, uint32_t mask, uint64_t sb, uint64_t se, uint64
   int do_a = (mask & M_RRNG) && ae > ab, do_p = (mask & M_R4P) && pe > pb;
   if (!(se > sb || le > lb || do_a || do_p)) return 0;
   if (c->llog_x.n == c->l_base) mask |= M_LEMPTY; /* empty sets: their probes are skipped (as on the GPU) */
-  if (c->plog_p.n == 0) mask |= M_PEMPTY;
+  if (c->plog_p.n == c->p_base) mask |= M_PEMPTY;
   memset(&k, 0, sizeof k);
   /* generation: reads only the state of the previous step */
   expand_s(c, &k, mask, sb, se, a0);
@@ -1300,6 +1325,29 @@ static void base_links(elo_ctx* c) {
   EVN(EL_K_INIT, EL_EV_EMIT, nb);
   c->l_base = nb;
   c->base = 1;
+  /* base propagations: the CR4 half-1 records of every init fact Y ∈ S(Y), ((r, Y), B) for
+   * (r, B) ∈ exl(Y) over its told closure — pid-major, B ascending (pids sort by (Y, r)) */
+  {
+    uint64_t nbp = 0;
+    uint32_t y, p;
+    for (y = 0; y < c->N; ++y)
+      for (j = c->exl.ptr[y]; j < c->exl.ptr[y + 1]; ++j) {
+        PID_OF(c->exl.a[j], y, p);
+        if (p == NONE) continue;
+        vpush(&c->plog_p, p);
+        vpush(&c->plog_b, c->exl.b[j]);
+        vpush(&c->prow[p], c->exl.b[j]);
+        c->bpn[p]++;
+        ++nbp;
+      }
+    if (nbp) {
+      int r;
+      EVN(EL_K_INIT, EL_EV_ENT, 2 * nbp);
+      EVN(EL_K_INIT, EL_EV_EMIT, nbp);
+      for (r = 0; r < EL_NUM_RULE_TYPES; ++r) c->wm_p[r] = nbp; /* nothing left to fan out */
+    }
+    c->p_base = nbp;
+  }
 }
 
 /* after the first superstep the link set holds the base links (the GPU fills it beside that
@@ -1308,9 +1356,11 @@ static void base_join(elo_ctx* c) {
   uint64_t i;
   if (!c->base) return;
   for (i = 0; i < c->l_base; ++i) hs_add(&c->links, lkey(c->llog_p.v[i], c->llog_x.v[i]));
-  EVN(EL_K_REHASH, EL_EV_HASH, c->l_base);
+  for (i = 0; i < c->p_base; ++i) hs_add(&c->props, lkey(c->plog_p.v[i], c->plog_b.v[i]));
+  EVN(EL_K_REHASH, EL_EV_HASH, c->l_base + c->p_base);
   c->base = 0;
   c->l_base = 0;
+  c->p_base = 0;
 }
 
 int elo_step(elo_ctx* c, int rule, int* changed) {
@@ -1494,7 +1544,7 @@ void elo_destroy(elo_ctx* c) {
     for (i = 0; i < c->P; ++i) free(c->pred[i].v);
   if (c->prow)
     for (i = 0; i < c->P; ++i) free(c->prow[i].v);
-  free(c->prow), free(c->props.t), free(c->plog_p.v), free(c->plog_b.v);
+  free(c->prow), free(c->bpn), free(c->props.t), free(c->plog_p.v), free(c->plog_b.v);
   if (c->actrow)
     for (uint32_t y = 0; y < c->N; ++y) free(c->actrow[y].v);
   free(c->actrow);

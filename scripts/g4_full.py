@@ -25,7 +25,19 @@ def used_gb():
     return (total.value - free.value) / 1e9
 
 
+def heartbeat():
+    import threading
+    t0 = time.time()
+
+    def beat():
+        while True:
+            time.sleep(30)
+            print(f"... {time.time() - t0:.0f} s", file=sys.stderr, flush=True)
+    threading.Thread(target=beat, daemon=True).start()
+
+
 def main():
+    heartbeat()
     scale = float(sys.argv[1]) if len(sys.argv) > 1 else 1.0
     k = int(sys.argv[2]) if len(sys.argv) > 2 else 8
     out = {"workload": f"G3 x{k} (scale {scale})", "copies": k}
