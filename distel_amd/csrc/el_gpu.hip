@@ -516,7 +516,7 @@ struct WaveQ {
   uint32_t lx[WQ], lp[WQ];  // link candidates
   uint4 jb[WQJ];            // fan-out jobs
   uint32_t ns, nt, nl, nj;
-  uint32_t rs_base, rs_left;  // S queue: this wave's reserved slots (DState::cs_chunk)
+  uint32_t rs_base, rs_left, rs_next;  // S queue: this wave's reserved slots, next reservation size
 };
 struct BlockQ {
   WaveQ w[BLOCK / 64];
@@ -526,7 +526,7 @@ __device__ __forceinline__ WaveQ& wave_q(BlockQ& q) { return q.w[threadIdx.x >> 
 
 __device__ __forceinline__ void q_init(BlockQ& q) {
   WaveQ& w = wave_q(q);
-  if (lane_id() == 0) w.ns = w.nt = w.nl = w.nj = w.rs_left = 0;
+  if (lane_id() == 0) w.ns = w.nt = w.nl = w.nj = w.rs_left = w.rs_next = 0;
   for (uint32_t i = lane_id(); i < DEDUP_SLOTS; i += 64) w.seen[i] = ~0ull;
   __syncthreads();
 }
@@ -552,10 +552,12 @@ __device__ __forceinline__ void wq_publish(const T* qa, const uint32_t* qb, uint
 }
 
 // The S-candidate queue of a big step (G3's first superstep: 96 M candidates): a wave reserves
-// cs_chunk slots with one atomic and fills them over several publishes, instead of one atomic
-// on the queue counter per 256 records — 375 k same-address atomics at ~12 ns each
-// (MI355X_MICROARCH.md "fanin") were 4.5 ms of that step's k_jobs.  The reservation's unused
-// tail is marked x = NONE when the wave finishes (q_flush); the commit skips such holes.
+// queue slots in growing chunks (its first publish exactly, then 512, 1024, … up to cs_chunk)
+// and fills them over several publishes, instead of one atomic on the queue counter per 256
+// records — 375 k same-address atomics at ~12 ns each (MI355X_MICROARCH.md "fanin") were 4.5 ms
+// of that step's k_jobs.  The last reservation's unused tail is marked x = NONE when the wave
+// finishes (q_flush) and the commit skips such holes; growing chunks keep the holes below the
+// wave's own output (a wave of a small step that publishes once leaves none).
 __device__ __forceinline__ void wq_publish_s(WaveQ& w, const DState& st, uint32_t n) {
   if (n == 0) return;
   const uint32_t chunk = st.cs_chunk;
@@ -566,15 +568,17 @@ __device__ __forceinline__ void wq_publish_s(WaveQ& w, const DState& st, uint32_
   const unsigned long long act = __ballot(true);
   const int leader = __ffsll((long long)act) - 1;
   const uint32_t na = (uint32_t)__popcll(act), r = (uint32_t)__popcll(act & ((1ull << lane_id()) - 1ull));
-  uint32_t base = w.rs_base, left = w.rs_left;
+  uint32_t base = w.rs_base, left = w.rs_left, next = w.rs_next, size = 0;
   for (uint32_t done = 0; done < n;) {
     if (left == 0) {
+      size = next == 0 ? n - done : next;  // (the first reservation: exactly this publish)
+      next = next == 0 ? min(2u * WQ, chunk) : min(2u * next, chunk);
       uint32_t b = 0;
-      if ((int)lane_id() == leader) b = atomicAdd(&st.ctr->cand_s, chunk);
-      base = __shfl(b, leader);
-      left = chunk;
+      if ((int)lane_id() == leader) b = atomicAdd(&st.ctr->cand_s, size);
+      base = __shfl(b, leader) + size;  // base: the reservation's end
+      left = size;
     }
-    const uint32_t take = min(n - done, left), off = base + (chunk - left);
+    const uint32_t take = min(n - done, left), off = base - left;
     for (uint32_t k = r; k < take; k += na) {
       const uint32_t slot = off + k;
       if (slot < st.cs_cap) {
@@ -588,6 +592,7 @@ __device__ __forceinline__ void wq_publish_s(WaveQ& w, const DState& st, uint32_
   if ((int)lane_id() == leader) {
     w.rs_base = base;
     w.rs_left = left;
+    w.rs_next = next;
   }
 }
 
@@ -716,7 +721,7 @@ __device__ void q_flush(BlockQ& q, const DState& st) {
   if (st.cs_chunk) {  // the reservation's unused tail becomes holes
     const unsigned long long act = __ballot(true);
     const uint32_t na = (uint32_t)__popcll(act), r = (uint32_t)__popcll(act & ((1ull << lane_id()) - 1ull));
-    const uint32_t left = w.rs_left, off = w.rs_base + (st.cs_chunk - left);
+    const uint32_t left = w.rs_left, off = w.rs_base - left;
     for (uint32_t k = r; k < left; k += na)
       if (off + k < st.cs_cap) st.cs_x[off + k] = NONE;
     if ((int)lane_id() == __ffsll((long long)act) - 1) w.rs_left = 0;
