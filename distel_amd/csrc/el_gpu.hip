@@ -2293,6 +2293,9 @@ struct el_ctx {
   uint32_t* stage[2] = {nullptr, nullptr};
   uint64_t stage_cap = 0;
   bool readout_off = getenv("EL_NO_READOUT") != nullptr;  // A/B: S rows by the log sort instead
+  bool links_direct = getenv("EL_LINKS_DIRECT") != nullptr;  // A/B: link-row sorts write the host buffer
+  bool s_dma = getenv("EL_S_DMA") != nullptr;                // A/B: small S results by device sort + DMA
+  uint64_t readout_chunk = (uint64_t)env_u32("EL_READOUT_CHUNK_MB", 32) << 18;  // entries per read-out DMA
   hipEvent_t ev_rows[2] = {nullptr, nullptr};
   // base links by predecessor (exrT: pid -> X) and by successor (exrC: X -> chain-second pid)
   const uint32_t *exrT_ptr = nullptr, *exrT_x = nullptr, *exrC_ptr = nullptr, *exrC_p = nullptr;
@@ -3188,7 +3191,7 @@ void el_ctx::readout_rows(uint64_t* dptr, uint64_t* ptr_out, uint32_t* val_out, 
   }
   HIPCHK(hipMemcpyAsync(hp, dptr, ((uint64_t)R + 1) * sizeof(uint64_t), hipMemcpyDeviceToHost, stream));
   HIPCHK(hipStreamSynchronize(stream));
-  constexpr uint64_t CHUNK = 8u << 20;  // entries per DMA (32 MB)
+  const uint64_t CHUNK = readout_chunk;  // entries per DMA (32 MB)
   uint64_t longest = 0;
   for (uint32_t r = 0; r < R; ++r) longest = std::max(longest, hp[r + 1] - hp[r]);
   const uint64_t need = std::max(CHUNK, longest);
@@ -4429,9 +4432,10 @@ int el_copy_result(el_ctx* c, el_result* res) {
       hipStream_t s;
       uint32_t* direct;
       bool readout;  // S rows read off the bit matrix in chunks, each DMA'd behind its read-out
+      bool queued;   // the rows' transfers are already enqueued (read-out, or device sort + DMA)
     };
-    Part parts[2] = {{false, res->l_ptr, res->l_pair, &c->rl, nl, c->cstream, nullptr, false},
-                     {true, res->s_ptr, res->s_val, &c->rs, nf, c->stream, nullptr, false}};
+    Part parts[2] = {{false, res->l_ptr, res->l_pair, &c->rl, nl, c->cstream, nullptr, false, false},
+                     {true, res->s_ptr, res->s_val, &c->rs, nf, c->stream, nullptr, false, false}};
     // the copy stream starts behind the saturation
     HIPCHK(hipEventRecord(c->ev_rows[1], c->stream));
     HIPCHK(hipStreamWaitEvent(c->cstream, c->ev_rows[1], 0));
@@ -4453,6 +4457,24 @@ int el_copy_result(el_ctx* c, el_result* res) {
         if (!r.ptr) r.ptr = dalloc<uint64_t>(R1);
         r.n = ~0ull;
         c->readout_rows(r.ptr, p.ptr_out, p.val_out, release, release ? c->ev_rows[0] : nullptr);
+        p.queued = true;
+      } else if (p.direct && (p.facts ? c->s_dma : !c->links_direct)) {
+        // rows sorted into device memory on the part's stream, then one DMA each for the
+        // offsets and the rows (the DMA engine keeps PCIe busier than the sorts' own writes
+        // to host memory, which share it with the S read-out's DMAs: G3 copy-back 13.8 -> 12.7 ms)
+        const uint64_t logged = p.facts ? c->s_count : c->l_count;
+        if (!r.ptr) r.ptr = dalloc<uint64_t>(R1);
+        if (p.n > r.cap || !r.val) {
+          dfree(r.val);
+          r.cap = p.n + p.n / 8 + 1024;
+          r.val = dalloc<uint32_t>(r.cap);
+        }
+        c->build_rows(p.facts, p.s, r.ptr, r.val);
+        r.n = logged;
+        if (p.ptr_out) HIPCHK(hipMemcpyAsync(p.ptr_out, r.ptr, R1 * sizeof(uint64_t), hipMemcpyDeviceToHost, p.s));
+        HIPCHK(hipMemcpyAsync(p.val_out, r.val, p.n * sizeof(uint32_t), hipMemcpyDeviceToHost, p.s));
+        p.queued = true;  // (phase 2 skips it)
+        p.direct = nullptr;
       } else if (p.direct) {  // sorted rows straight into the caller's page-locked buffer
         if (!r.ptr) r.ptr = dalloc<uint64_t>(R1);
         r.n = ~0ull;  // r.ptr is reused; the device rows are not built
@@ -4478,7 +4500,7 @@ int el_copy_result(el_ctx* c, el_result* res) {
     for (Part& p : parts) {
       if (!p.ptr_out && !p.val_out) continue;
       el_ctx::Rows& r = *p.rows;
-      if (p.readout) continue;  // (its DMAs are queued on dstream)
+      if (p.queued) continue;  // (its transfers are enqueued)
       if (p.direct) {
         c->build_rows(p.facts, p.s, r.ptr, p.direct, 2, fuse_clear);
         if (p.ptr_out) HIPCHK(hipMemcpyAsync(p.ptr_out, r.ptr, R1 * sizeof(uint64_t), hipMemcpyDeviceToHost, p.s));

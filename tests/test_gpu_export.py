@@ -167,3 +167,40 @@ def test_copy_result_release(oracle_lib):
     eng.saturate()
     _check_result(eng, o, ax)
     eng.close()
+
+
+def _result_digest(res, role, filler):
+    """SHA-256 of a copy-back in the pinned digests' format (tests/golden/closure_digests.txt):
+    facts (x, a) then links (x, r, y), each lexicographically sorted."""
+    import hashlib
+    x, a = res.facts()
+    n = res.row_hi - res.row_lo
+    lx = np.repeat(np.arange(res.row_lo, res.row_hi, dtype=np.uint32), np.diff(res.l_ptr[:n + 1]).astype(np.int64))
+    q = res.l_pair[:res.n_links]
+    h = hashlib.sha256()
+    for arr in (x, a, lx, role[q], filler[q]):
+        h.update(np.ascontiguousarray(arr, dtype=np.uint32).tobytes())
+    return h.hexdigest()
+
+
+def test_copy_result_release_g3_pinned():
+    """The bench's step at full G3 — init, saturate, copy-back with release (S rows by bit-matrix
+    read-out, the next reset beside it) — twice, each copy hashing to the closure digest the
+    oracle and the independent worklist saturator agreed on."""
+    want = None
+    for line in open(os.path.join(os.path.dirname(__file__), "golden", "closure_digests.txt")):
+        f = line.split()
+        if len(f) == 4 and f[0] == "g3" and float(f[1]) == 1.0:
+            want = f[3]
+    assert want
+    ax = generators.workload("g3")
+    eng = engine.Engine(device=0)
+    eng.load(ax)
+    role, filler = eng.pair_table()
+    res = engine.Result()
+    for _ in range(2):
+        eng.init()
+        eng.saturate()
+        eng.copy_result(res, release=True)
+        assert _result_digest(res, role, filler) == want
+    eng.close()
