@@ -770,7 +770,7 @@ __global__ void k_fill(FillArgs f) {
 // inside the row, and a wave's log stores are coalesced.  Row X's facts: X (closure flag:
 // its closure is written right here), ⊤ for classes and individuals, then told*(X) (flagged)
 // without a second ⊤.
-__global__ void k_init(DIndex ix, DState st, uint32_t lo, uint32_t hi, uint32_t base) {
+__global__ void k_init(DIndex ix, DState st, uint32_t lo, uint32_t hi, uint32_t base, uint32_t set_bits) {
   Ev ev;
   const uint32_t o0 = ix.init_off[lo], n = ix.init_off[hi] - o0;
   const uint32_t stride = gridDim.x * blockDim.x;
@@ -804,7 +804,7 @@ __global__ void k_init(DIndex ix, DState st, uint32_t lo, uint32_t hi, uint32_t 
       ev.v[EL_EV_ENT]++;
     }
     const uint32_t c = col_of(ix, v);  // (the told closure lies inside the window)
-    if (c != NONE)
+    if (set_bits && c != NONE)  // (else k_init_bits writes the rows' init words)
       __hip_atomic_fetch_or(st.bits + (uint64_t)x * ix.W + (c >> 5), 1u << (c & 31u), __ATOMIC_RELAXED,
                             __HIP_MEMORY_SCOPE_AGENT);
     st.slog_x[base + k] = x;
@@ -817,6 +817,17 @@ __global__ void k_init(DIndex ix, DState st, uint32_t lo, uint32_t hi, uint32_t 
 }
 
 __global__ void k_set_u32(uint32_t* p, uint32_t v) { *p = v; }
+
+// The init facts' bits as whole words: word (row x, w) of the owned rows gets its mask of
+// {x, ⊤} ∪ told*(x) (host-merged at el_load, one entry per distinct word), so the words are
+// written with plain stores — the matrix is zero at el_init and no word is listed twice —
+// instead of one returning atomic per init fact (G3: 25 M, 0.9 ms).
+__global__ void k_init_bits(uint32_t* __restrict__ bits, uint64_t W, const uint32_t* __restrict__ row,
+                            const uint32_t* __restrict__ word, const uint32_t* __restrict__ mask, uint32_t n) {
+  const uint32_t stride = gridDim.x * blockDim.x;
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
+    bits[(uint64_t)row[i] * W + word[i]] = mask[i];
+}
 
 // Wave-cooperative loop over one CSR row per lane, [b, e) (an idle lane passes b = e): the
 // wave walks the concatenation of its lanes' rows 64 entries at a time, so a lane with a
@@ -1883,9 +1894,10 @@ __global__ void k_gap_move(const uint32_t* __restrict__ s_old, const uint32_t* _
   }
 }
 
-// ---- base links (el_ctx::install_base): CSR rows written out whole, one entry per thread.
-// A block takes 256 consecutive entries; two lanes find the rows of its first and last entry
-// (binary searches of ptr), then each entry's row is searched within that span only — a hub
+// ---- base links (el_ctx::install_base): CSR rows written out whole, one entry per lane.
+// A block takes 4096 consecutive entries a round; two lanes find the rows of its first and last
+// entry (binary searches of ptr: at 256 entries a round these latency chains were most of the
+// 0.3 ms per 25 M entries), then each entry's row is searched within that span only — a hub
 // row (a filler with 10^5 predecessors) spreads over many blocks instead of one wave.
 // out_row != null: flat (row, value) pairs at the entry's index (the link log from exr);
 // else: the entry at its row's slot of a gapped CSR just laid out (predecessor rows from exrT,
@@ -1901,22 +1913,29 @@ __device__ __forceinline__ uint32_t csr_row_of(const uint32_t* __restrict__ ptr,
   }
   return lo;
 }
+constexpr uint32_t SCATTER_ITEMS = 16;  // entries per thread and round: 4096 per block round
 __global__ void __launch_bounds__(256) k_csr_scatter(const uint32_t* __restrict__ ptr, const uint32_t* __restrict__ a,
                                                      uint32_t rows, uint32_t n, uint32_t* __restrict__ out_row,
                                                      uint32_t* __restrict__ out_val, const uint32_t* __restrict__ start,
                                                      uint32_t* __restrict__ val) {
   __shared__ uint32_t span[2];
-  for (uint32_t base = blockIdx.x * 256u; base < n; base += gridDim.x * 256u) {
-    if (threadIdx.x < 2) span[threadIdx.x] = csr_row_of(ptr, 0, rows - 1, threadIdx.x ? min(base + 255u, n - 1) : base);
+  constexpr uint32_t TILE = 256 * SCATTER_ITEMS;
+  for (uint32_t base = blockIdx.x * TILE; base < n; base += gridDim.x * TILE) {
+    // the rows of the tile's first and last entry (one search over all rows per 4096 entries)
+    if (threadIdx.x < 2) span[threadIdx.x] = csr_row_of(ptr, 0, rows - 1, threadIdx.x ? min(base + TILE - 1, n - 1) : base);
     __syncthreads();
-    const uint32_t j = base + threadIdx.x;
-    if (j < n) {
-      const uint32_t r = csr_row_of(ptr, span[0], span[1], j), v = a[j];
-      if (out_row) {
-        out_row[j] = r;
-        out_val[j] = v;
-      } else {
-        val[start[r] + (j - ptr[r])] = v;
+    const uint32_t s0 = span[0], s1 = span[1];
+#pragma unroll 4
+    for (uint32_t k = 0; k < SCATTER_ITEMS; ++k) {  // coalesced: consecutive lanes, consecutive entries
+      const uint32_t j = base + k * 256 + threadIdx.x;
+      if (j < n) {
+        const uint32_t r = csr_row_of(ptr, s0, s1, j), v = a[j];
+        if (out_row) {
+          out_row[j] = r;
+          out_val[j] = v;
+        } else {
+          val[start[r] + (j - ptr[r])] = v;
+        }
       }
     }
     __syncthreads();
@@ -2568,6 +2587,10 @@ struct el_ctx {
   uint64_t user_count(bool facts);  // facts / links of the result rows (= the log's without fresh rows)
   uint64_t uc_s_n = ~0ull, uc_s = 0, uc_l_n = ~0ull, uc_l = 0;
   std::vector<uint32_t> init_off;  // host copy of DIndex::init_off
+  // init words (k_init_bits): (row - lo, word, mask) of the owned rows' init facts
+  uint32_t *iw_row = nullptr, *iw_word = nullptr, *iw_mask = nullptr;
+  uint32_t iw_n = 0;
+  void build_init_words();
 };
 
 // Upload the indexes of hx and derive what the kernels need from them (which CSRs have
@@ -2704,6 +2727,7 @@ std::string el_ctx::install_index(el::HostIndex&& hnew) {
   d.hi = hi;
   column_window();
   d.part = part() ? 1u : 0u;
+  build_init_words();
   return "";
 }
 
@@ -2716,6 +2740,36 @@ std::string el_ctx::install_index(el::HostIndex&& hnew) {
 // (CR3, CR5 supers, CR6 results), and the ranges of every role a link into it can carry
 // (DistEL's range rule puts them into each S(X) that holds the link's target).  For OntologyMultiplier copies aligned with the partition
 // (G4) the window is the rank's own copy: 8 × 19 GB for SNOMED×8 instead of 8 × 152 GB.
+void el_ctx::build_init_words() {
+  const el::HostIndex& h = hx;
+  std::vector<uint32_t> r, w, m, cols;
+  for (uint32_t x = lo; x < hi; ++x) {
+    const bool two = x != EL_TOP && x != EL_BOTTOM && h.kind[x] != EL_KIND_DATATYPE;
+    cols.clear();
+    auto col = [&](uint32_t a) { return a < 2u ? a : (a >= ix.c_lo && a < ix.c_hi ? a - ix.c_lo + 2u : NONE); };
+    cols.push_back(col(x));
+    if (two) cols.push_back(col(EL_TOP));
+    for (uint32_t j = h.told.ptr[x]; j < h.told.ptr[x + 1]; ++j) cols.push_back(col(h.told.a[j]));
+    std::sort(cols.begin(), cols.end());
+    for (size_t k = 0; k < cols.size();) {
+      const uint32_t wd = cols[k] >> 5;
+      if (cols[k] == NONE) break;  // (outside the window: not set, as k_init skips it)
+      uint32_t mk = 0;
+      for (; k < cols.size() && cols[k] != NONE && (cols[k] >> 5) == wd; ++k) mk |= 1u << (cols[k] & 31u);
+      r.push_back(x - lo);
+      w.push_back(wd);
+      m.push_back(mk);
+    }
+  }
+  iw_n = (uint32_t)r.size();
+  iw_row = dupload(r);
+  iw_word = dupload(w);
+  iw_mask = dupload(m);
+  index_bufs.push_back(iw_row);
+  index_bufs.push_back(iw_word);
+  index_bufs.push_back(iw_mask);
+}
+
 void el_ctx::column_window() {
   const el::HostIndex& h = hx;
   uint32_t c_lo = 2, c_hi = std::max<uint32_t>(h.N, 2);
@@ -3705,8 +3759,13 @@ void el_ctx::init_rows(uint32_t a, uint32_t b) {
     slog_cap = c;
   }
   DState st = dstate();
+  const bool whole = a == lo && b == hi && s_count == 0;  // a fresh state: the init words as whole words
   launch(EL_K_INIT, [&] {
-    hipLaunchKernelGGL(k_init, dim3(grid_for(n, 2048)), dim3(BLOCK), 0, stream, ix, st, a, b, (uint32_t)s_count);
+    hipLaunchKernelGGL(k_init, dim3(grid_for(n, 2048)), dim3(BLOCK), 0, stream, ix, st, a, b, (uint32_t)s_count,
+                       whole ? 0u : 1u);
+    if (whole)
+      hipLaunchKernelGGL(k_init_bits, dim3(grid_for(iw_n, 2048)), dim3(BLOCK), 0, stream, bits, W, iw_row, iw_word,
+                         iw_mask, iw_n);
   });
   hipLaunchKernelGGL(k_set_u32, dim3(1), dim3(1), 0, stream, &ctr->s_log, (uint32_t)(s_count + n));
   HIPCHK(hipGetLastError());
@@ -3752,7 +3811,9 @@ void el_ctx::install_base() {
   // second superstep's candidates now (an empty set: no re-insertion)
   if (2 * (nb + cl_cap) > lhash_cap) rehash_links(next_pow2(2 * (nb + cl_cap)));
   const uint32_t N = hx.N, P = hx.P, nc = (uint32_t)hx.exrC.a.size();
-  auto grid = [](uint64_t n) { return (uint32_t)std::min<uint64_t>(8192, std::max<uint64_t>(1, (n + 255) / 256)); };
+  auto grid = [](uint64_t n) {  // one block per 4096 entries (k_csr_scatter), at most 2048
+    return (uint32_t)std::min<uint64_t>(2048, std::max<uint64_t>(1, (n + 256 * SCATTER_ITEMS - 1) / (256 * SCATTER_ITEMS)));
+  };
   launch(EL_K_INIT, [&] {
     hipLaunchKernelGGL(k_csr_scatter, dim3(grid(nb)), dim3(256), 0, stream, ix.exr_ptr, ix.exr_pid, N, (uint32_t)nb,
                        llog_x, llog_p, nullptr, nullptr);
