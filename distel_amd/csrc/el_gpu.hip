@@ -1913,20 +1913,19 @@ __device__ __forceinline__ uint32_t csr_row_of(const uint32_t* __restrict__ ptr,
   }
   return lo;
 }
-constexpr uint32_t SCATTER_ITEMS = 16;  // entries per thread and round: 4096 per block round
+// items: entries per lane and round (1..16, from the entry count: small builds keep many blocks)
 __global__ void __launch_bounds__(256) k_csr_scatter(const uint32_t* __restrict__ ptr, const uint32_t* __restrict__ a,
                                                      uint32_t rows, uint32_t n, uint32_t* __restrict__ out_row,
                                                      uint32_t* __restrict__ out_val, const uint32_t* __restrict__ start,
-                                                     uint32_t* __restrict__ val) {
+                                                     uint32_t* __restrict__ val, uint32_t items) {
   __shared__ uint32_t span[2];
-  constexpr uint32_t TILE = 256 * SCATTER_ITEMS;
+  const uint32_t TILE = 256 * items;
   for (uint32_t base = blockIdx.x * TILE; base < n; base += gridDim.x * TILE) {
     // the rows of the tile's first and last entry (one search over all rows per 4096 entries)
     if (threadIdx.x < 2) span[threadIdx.x] = csr_row_of(ptr, 0, rows - 1, threadIdx.x ? min(base + TILE - 1, n - 1) : base);
     __syncthreads();
     const uint32_t s0 = span[0], s1 = span[1];
-#pragma unroll 4
-    for (uint32_t k = 0; k < SCATTER_ITEMS; ++k) {  // coalesced: consecutive lanes, consecutive entries
+    for (uint32_t k = 0; k < items; ++k) {  // coalesced: consecutive lanes, consecutive entries
       const uint32_t j = base + k * 256 + threadIdx.x;
       if (j < n) {
         const uint32_t r = csr_row_of(ptr, s0, s1, j), v = a[j];
@@ -3811,24 +3810,27 @@ void el_ctx::install_base() {
   // second superstep's candidates now (an empty set: no re-insertion)
   if (2 * (nb + cl_cap) > lhash_cap) rehash_links(next_pow2(2 * (nb + cl_cap)));
   const uint32_t N = hx.N, P = hx.P, nc = (uint32_t)hx.exrC.a.size();
-  auto grid = [](uint64_t n) {  // one block per 4096 entries (k_csr_scatter), at most 2048
-    return (uint32_t)std::min<uint64_t>(2048, std::max<uint64_t>(1, (n + 256 * SCATTER_ITEMS - 1) / (256 * SCATTER_ITEMS)));
+  // k_csr_scatter shape: up to 2048 blocks, 1..16 entries per lane and round
+  auto items = [](uint64_t n) { return (uint32_t)std::min<uint64_t>(16, std::max<uint64_t>(1, n / (2048 * 256))); };
+  auto grid = [&](uint64_t n) {
+    const uint64_t t = 256ull * items(n);
+    return (uint32_t)std::min<uint64_t>(2048, std::max<uint64_t>(1, (n + t - 1) / t));
   };
   launch(EL_K_INIT, [&] {
     hipLaunchKernelGGL(k_csr_scatter, dim3(grid(nb)), dim3(256), 0, stream, ix.exr_ptr, ix.exr_pid, N, (uint32_t)nb,
-                       llog_x, llog_p, nullptr, nullptr);
+                       llog_x, llog_p, nullptr, nullptr, items(nb));
   });
   if (PR.live)
     launch(EL_K_INIT, [&] {
       hipLaunchKernelGGL(k_gap_len, dim3(grid(P)), dim3(256), 0, stream, exrT_ptr, P, PR.len);
       hipLaunchKernelGGL(k_csr_scatter, dim3(grid(nb)), dim3(256), 0, stream, exrT_ptr, exrT_x, P, (uint32_t)nb,
-                         nullptr, nullptr, PR.start, PR.val);
+                         nullptr, nullptr, PR.start, PR.val, items(nb));
     });
   if (SC.live && nc)
     launch(EL_K_INIT, [&] {
       hipLaunchKernelGGL(k_gap_len, dim3(grid(N)), dim3(256), 0, stream, exrC_ptr, N, SC.len);
       hipLaunchKernelGGL(k_csr_scatter, dim3(grid(nc)), dim3(256), 0, stream, exrC_ptr, exrC_p, N, nc, nullptr,
-                         nullptr, SC.start, SC.val);
+                         nullptr, SC.start, SC.val, items(nc));
     });
   hipLaunchKernelGGL(k_set_u32, dim3(1), dim3(1), 0, stream, &ctr->l_log, (uint32_t)nb);
   HIPCHK(hipGetLastError());
@@ -3852,10 +3854,10 @@ void el_ctx::install_base() {
     if (2 * (nbp + cp_cap) > phash_cap) rehash_props(next_pow2(2 * (nbp + cp_cap)));
     launch(EL_K_INIT, [&] {
       hipLaunchKernelGGL(k_csr_scatter, dim3(grid(nbp)), dim3(256), 0, stream, ix.bpp_ptr, ix.bpp_b, P, (uint32_t)nbp,
-                         plog_p, plog_b, nullptr, nullptr);
+                         plog_p, plog_b, nullptr, nullptr, items(nbp));
       hipLaunchKernelGGL(k_gap_len, dim3(grid(P)), dim3(256), 0, stream, ix.bpp_ptr, P, PP.len);
       hipLaunchKernelGGL(k_csr_scatter, dim3(grid(nbp)), dim3(256), 0, stream, ix.bpp_ptr, ix.bpp_b, P, (uint32_t)nbp,
-                         nullptr, nullptr, PP.start, PP.val);
+                         nullptr, nullptr, PP.start, PP.val, items(nbp));
     });
     hipLaunchKernelGGL(k_set_u32, dim3(1), dim3(1), 0, stream, &ctr->p_log, (uint32_t)nbp);
     HIPCHK(hipGetLastError());
