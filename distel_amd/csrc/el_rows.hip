@@ -355,15 +355,18 @@ __global__ void __launch_bounds__(BLOCK) k_rows_bits(const uint64_t* __restrict_
 
 // Rows [r0, r1) read off the bit matrix whole: the set columns of row r, in order, to
 // dst[ptr[r] - out0 ...] (the rows of a copy-back chunk, staged in device memory for a DMA).
-// One workgroup per row, 16 words per lane per round (four 16-B loads in flight), popcounts
-// and a block scan give each lane its output slots.  A row stops at its last entry (ptr says
+// One workgroup per row, 16 words per lane per round (four coalesced 16-B loads in flight:
+// with each lane's four loads adjacent instead, every load instruction touched 64 lines and the
+// read-out ran at 1.7 TB/s), popcounts and block scans give each lane its output slots.  A row stops at its last entry (ptr says
 // how many): the columns are concept ids and a closure's members are mostly older concepts.
 // clear: the read words are zeroed (the caller releases its state; only non-zero words are
 // written).
 __global__ void __launch_bounds__(BLOCK) k_rows_readout(const uint64_t* __restrict__ ptr, uint32_t r0, uint32_t r1,
                                                         uint64_t out0, uint32_t* __restrict__ dst, Clear m,
                                                         bool clear) {
-  __shared__ uint32_t wsum[BLOCK / 64];
+  // loads: segment i of a round is 256 consecutive 16-B words, lane t takes the t-th (each load
+  // instruction of a wave covers 1 KB contiguous); the set columns are ordered by (i, t)
+  __shared__ uint32_t wsum[4][BLOCK / 64];
   const uint32_t tid = threadIdx.x, lane = __lane_id(), wv = tid >> 6;
   const uint64_t W4 = m.W / 4;
   for (uint32_t r = r0 + blockIdx.x; r < r1; r += gridDim.x) {
@@ -373,31 +376,38 @@ __global__ void __launch_bounds__(BLOCK) k_rows_readout(const uint64_t* __restri
     uint64_t done = 0;
     for (uint64_t q0 = 0; q0 < W4 && done < len; q0 += BLOCK * 4) {
       uint4 v[4];
-      uint32_t c = 0;
+      uint32_t c[4], inc[4];
 #pragma unroll
       for (uint32_t i = 0; i < 4; ++i) {
-        const uint64_t q = q0 + tid * 4 + i;
+        const uint64_t q = q0 + i * BLOCK + tid;
         v[i] = q < W4 ? row[q] : make_uint4(0u, 0u, 0u, 0u);
-        c += __popc(v[i].x) + __popc(v[i].y) + __popc(v[i].z) + __popc(v[i].w);
+        c[i] = __popc(v[i].x) + __popc(v[i].y) + __popc(v[i].z) + __popc(v[i].w);
+        inc[i] = c[i];
       }
-      uint32_t inc = c;
 #pragma unroll
       for (uint32_t o = 1; o < 64; o <<= 1) {
-        const uint32_t y = __shfl_up(inc, o);
-        if (lane >= o) inc += y;
-      }
-      if (lane == 63) wsum[wv] = inc;
-      __syncthreads();
-      uint32_t before = 0, total = 0;
 #pragma unroll
-      for (uint32_t k = 0; k < BLOCK / 64; ++k) {
-        before += k < wv ? wsum[k] : 0u;
-        total += wsum[k];
+        for (uint32_t i = 0; i < 4; ++i) {
+          const uint32_t y = __shfl_up(inc[i], o);
+          if (lane >= o) inc[i] += y;
+        }
       }
-      uint32_t* o = dst + (b - out0) + done + before + inc - c;
+      if (lane == 63) {
+#pragma unroll
+        for (uint32_t i = 0; i < 4; ++i) wsum[i][wv] = inc[i];
+      }
+      __syncthreads();
+      uint32_t total = 0;  // the round's entries before segment i
 #pragma unroll
       for (uint32_t i = 0; i < 4; ++i) {
-        const uint64_t q = q0 + tid * 4 + i;
+        uint32_t before = 0, tot = 0;
+#pragma unroll
+        for (uint32_t k = 0; k < BLOCK / 64; ++k) {
+          before += k < wv ? wsum[i][k] : 0u;
+          tot += wsum[i][k];
+        }
+        uint32_t* o = dst + (b - out0) + done + total + before + inc[i] - c[i];
+        const uint64_t q = q0 + i * BLOCK + tid;
         const uint32_t wd[4] = {v[i].x, v[i].y, v[i].z, v[i].w};
 #pragma unroll
         for (uint32_t j = 0; j < 4; ++j) {
@@ -409,7 +419,8 @@ __global__ void __launch_bounds__(BLOCK) k_rows_readout(const uint64_t* __restri
             word &= word - 1;
           }
         }
-        if (clear && (v[i].x | v[i].y | v[i].z | v[i].w)) row[q] = make_uint4(0u, 0u, 0u, 0u);
+        if (clear && c[i]) row[q] = make_uint4(0u, 0u, 0u, 0u);
+        total += tot;
       }
       done += total;
       __syncthreads();  // wsum is reused
