@@ -2307,8 +2307,9 @@ struct el_ctx {
   hipStream_t cstream = nullptr;             // copy-back DMA, beside the row builds
   // S-row read-out copy-back (el_copy_result): device staging chunks and their DMA stream
   hipStream_t dstream = nullptr;
-  hipEvent_t ev_stage[2] = {nullptr, nullptr}, ev_dma[2] = {nullptr, nullptr};
-  uint32_t* stage[2] = {nullptr, nullptr};
+  static constexpr uint32_t NSTAGE = 4;  // staging buffers: the read-out runs up to 3 chunks ahead of the DMA
+  hipEvent_t ev_stage[NSTAGE] = {}, ev_dma[NSTAGE] = {};
+  uint32_t* stage[NSTAGE] = {};
   uint64_t stage_cap = 0;
   bool readout_off = getenv("EL_NO_READOUT") != nullptr;  // A/B: S rows by the log sort instead
   bool links_direct = getenv("EL_LINKS_DIRECT") != nullptr;  // A/B: link-row sorts write the host buffer
@@ -3230,7 +3231,7 @@ void el_ctx::build_rows(bool facts, hipStream_t s, uint64_t* ptr, uint32_t* dst,
 
 // S rows to the caller's page-locked buffers by read-out (el_copy_result): row counts from the
 // fact log, the offsets to the host (the caller's s_ptr or a scratch copy; one sync), then
-// chunks of rows read off the bit matrix into two device staging buffers in turn, each
+// chunks of rows read off the bit matrix into four device staging buffers in turn, each
 // shipped by DMA on dstream while the next is read.  clear: the read-out zeroes the matrix.
 void el_ctx::readout_rows(uint64_t* dptr, uint64_t* ptr_out, uint32_t* val_out, bool clear, hipEvent_t counted) {
   const uint32_t R = uhi() - lo;
@@ -3271,8 +3272,8 @@ void el_ctx::readout_rows(uint64_t* dptr, uint64_t* ptr_out, uint32_t* val_out, 
       }
       rb = lo_r;
     }
-    const uint32_t slot = k & 1u;
-    if (k >= 2) HIPCHK(hipStreamWaitEvent(stream, ev_dma[slot], 0));  // the staging buffer is free
+    const uint32_t slot = k % NSTAGE;
+    if (k >= NSTAGE) HIPCHK(hipStreamWaitEvent(stream, ev_dma[slot], 0));  // the staging buffer is free
     elrows::readout(stream, dptr, ra, rb, hp[ra], stage[slot], m, clear);
     HIPCHK(hipEventRecord(ev_stage[slot], stream));
     HIPCHK(hipStreamWaitEvent(dstream, ev_stage[slot], 0));

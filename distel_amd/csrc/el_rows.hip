@@ -9,6 +9,7 @@
 #include "el_rows.h"
 
 #include <algorithm>
+#include <cstdlib>
 #include <stdexcept>
 #include <string>
 
@@ -553,7 +554,11 @@ void build_counts(hipStream_t s, Scratch& sc, const uint32_t* rows, uint64_t n, 
 void readout(hipStream_t s, const uint64_t* ptr, uint32_t r0, uint32_t r1, uint64_t out0, uint32_t* dst, Clear m,
              bool clear) {
   if (r1 <= r0) return;
-  hipLaunchKernelGGL(k_rows_readout, dim3(std::min<uint32_t>(r1 - r0, 4096)), dim3(BLOCK), 0, s, ptr, r0, r1, out0,
+  static const uint32_t maxb = [] {
+    const char* e = getenv("EL_READOUT_BLOCKS");  // A/B: workgroups of the read-out (leaves CUs to the DMA blits)
+    return e ? (uint32_t)std::max(1l, strtol(e, nullptr, 10)) : 4096u;
+  }();
+  hipLaunchKernelGGL(k_rows_readout, dim3(std::min<uint32_t>(r1 - r0, maxb)), dim3(BLOCK), 0, s, ptr, r0, r1, out0,
                      dst, m, clear);
   RCHK(hipGetLastError());
 }
