@@ -3262,9 +3262,12 @@ void el_ctx::readout_rows(uint64_t* dptr, uint64_t* ptr_out, uint32_t* val_out, 
     uint32_t rb = ra + 1;  // rows while the chunk fits (at least one)
     {
       uint32_t lo_r = rb, hi_r = R;
-      while (lo_r < hi_r) {  // the last rb with hp[rb] - hp[ra] <= stage_cap
+      // chunks grow from 1 MB: the first DMA starts after a short read-out (PCIe idles until then)
+      const uint64_t lim = std::max<uint64_t>(std::min<uint64_t>(stage_cap, (uint64_t)(1u << 18) << std::min(k, 8u)),
+                                              longest);
+      while (lo_r < hi_r) {  // the last rb with hp[rb] - hp[ra] <= lim
         const uint32_t mid = lo_r + (hi_r - lo_r + 1) / 2;
-        if (hp[mid] - hp[ra] <= stage_cap)
+        if (hp[mid] - hp[ra] <= lim)
           lo_r = mid;
         else
           hi_r = mid - 1;
