@@ -1509,6 +1509,15 @@ int elo_copy_links(const elo_ctx* c, uint32_t* x, uint32_t* r, uint32_t* y, size
   return EL_OK;
 }
 
+/* The fact log in append order (init facts, then superstep by superstep): diagnostics
+ * (scripts/commit_floor.py splits it by superstep with elo_trace). */
+int elo_copy_log(const elo_ctx* c, uint32_t* x, uint32_t* a, size_t cap) {
+  if (cap < c->slog_x.n) return EL_ERANGE;
+  memcpy(x, c->slog_x.v, c->slog_x.n * sizeof(uint32_t));
+  memcpy(a, c->slog_a.v, c->slog_a.n * sizeof(uint32_t));
+  return EL_OK;
+}
+
 int elo_trace(const elo_ctx* c, uint64_t* ds, uint64_t* dl, uint64_t* da, size_t cap) {
   size_t i;
   if (cap < c->tr_s.n) return EL_ERANGE;

@@ -39,6 +39,7 @@ uint64_t elo_num_acts(const elo_ctx* c);
 uint32_t elo_supersteps(const elo_ctx* c);
 /* facts sorted by (x, a) */
 int elo_copy_facts(const elo_ctx* c, uint32_t* x, uint32_t* a, size_t cap);
+int elo_copy_log(const elo_ctx* c, uint32_t* x, uint32_t* a, size_t cap);
 /* links sorted by (x, r, y) */
 int elo_copy_links(const elo_ctx* c, uint32_t* x, uint32_t* r, uint32_t* y, size_t cap);
 /* per-superstep |ΔS|, |Δlink|, |Δact| of the last elo_saturate */

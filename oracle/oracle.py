@@ -52,6 +52,7 @@ def _load():
     lib.elo_supersteps.argtypes = [P]
     lib.elo_supersteps.restype = C.c_uint32
     lib.elo_copy_facts.argtypes = [P, u32p, u32p, C.c_size_t]
+    lib.elo_copy_log.argtypes = [P, u32p, u32p, C.c_size_t]
     lib.elo_copy_links.argtypes = [P, u32p, u32p, u32p, C.c_size_t]
     lib.elo_trace.argtypes = [P, u64p, u64p, u64p, C.c_size_t]
     lib.elo_events.argtypes = [P, u64p, C.c_size_t]
