@@ -7,8 +7,12 @@ result copy-back — el_init (S(X) = {X, ⊤}) + el_saturate + el_copy_result (t
 rows X -> {B} and the role links X -> {(r, Y)} as CSR into page-locked host buffers).
 ``value`` = derived axioms per second over all ranks (D = Σ|S(X)| − init facts + Σ|R(r)|).
 Default workload: G3, the SNOMED-shaped generator = BASELINE.json configs[2], the largest
-config that fits one GPU.  ``saturate_ms`` (no copy-back) and ``copyback_ms`` are the
-two parts of ``ms_per_step``, measured inside the same timed steps.
+config that fits one GPU.  Two engines (each with its own state and result buffers)
+alternate: one classification's copy-back is enqueued asynchronously (EL_RESULT_ASYNC) and
+crosses PCIe while the other engine saturates, so ``ms_per_step`` = wall time of K complete
+classifications (the last copy-backs drained inside the timed region) ÷ K.  ``latency_ms`` is
+one classification with its copy-back and nothing beside it (``saturate_ms`` + ``copyback_ms``);
+``--inflight 1`` times that serial schedule.
 
 Multi-GPU (``torch.distributed.run``): weak scaling.  Rank i classifies its own
 disjoint copy of the workload (OntologyMultiplier ×N semantics, the G4 config);
@@ -38,6 +42,9 @@ import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
+# Two engines in flight use 8 HIP streams; with HIP's default of 4 hardware queues, streams of
+# different engines would share a queue and one engine's DMAs would hold up the other's kernels.
+os.environ.setdefault("GPU_MAX_HW_QUEUES", "12")
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 
@@ -106,6 +113,9 @@ def parse():
     ap.add_argument("--partition", default="copies", choices=["copies", "exchange"],
                     help="copies: one disjoint copy per rank, no collective; exchange: row-partitioned "
                          "engine over the ×N ontology with the RCCL delta all-gather")
+    ap.add_argument("--inflight", type=int, default=2, choices=[1, 2],
+                    help="classifications in flight: 2 = two engines alternate, one's result copy-back "
+                         "(EL_RESULT_ASYNC) rides over PCIe under the other's saturation; 1 = serial")
     ap.add_argument("--verbose", action="store_true")
     return ap.parse_args()
 
@@ -148,31 +158,62 @@ def main():
         eng.load(ax)  # host index build + upload: AxiomLoader's part, reported separately
         load_s = time.time() - t0
 
-    res = engine.Result()  # page-locked result buffers, reused by every step
+    engines = [eng]
+    inflight = args.inflight if args.partition == "copies" else 1  # (exchange: one collective engine)
+    if inflight == 2:
+        eng2 = engine.Engine(device=local if has_cuda else 0)
+        eng2.load(ax)
+        engines.append(eng2)
+    results = [engine.Result() for _ in engines]  # page-locked result buffers, reused by every step
     split = []  # (classification, copy-back) seconds per step; the last `steps` are the timed ones
+    turn = [0]
 
     def classify():
+        # one classification: el_init + el_saturate + result copy-back (part of the metric,
+        # SURVEY.md §8(d)); the state is released behind the copy (the next init's reset overlaps
+        # the PCIe transfer).  Two engines in flight: this engine's copy-back is enqueued
+        # (EL_RESULT_ASYNC) and lands while the other engine saturates; an engine's next call
+        # waits for its previous copy-back, and drain() waits for the last ones.
+        i = turn[0] % len(engines)
+        turn[0] += 1
+        e, res = engines[i], results[i]
         t0 = time.perf_counter()
-        eng.init()
-        st = eng.saturate()
+        e.init()
+        st = e.saturate()
         t1 = time.perf_counter()
-        # result copy-back: part of the metric; the state is released behind it
-        # (the next init's reset overlaps the PCIe transfer)
-        eng.copy_result(res, release=True)
+        e.copy_result(res, release=True, wait=len(engines) == 1)
         split.append((t1 - t0, time.perf_counter() - t1))
         return st
 
-    t_max, derived_all, st = D.run_weak(rk, classify, args.steps, args.warmup)
+    def drain():
+        for e in engines:
+            e.result_wait()
+
+    t_max, derived_all, st = D.run_weak(rk, classify, args.steps, args.warmup, drain=drain)
     ms_per_step = 1e3 * t_max / args.steps
     value = derived_all * args.steps / t_max
     timed = split[-args.steps:]
     saturate_ms = 1e3 * sum(t[0] for t in timed) / len(timed)
     copyback_ms = 1e3 * sum(t[1] for t in timed) / len(timed)
+    res = results[(turn[0] - 1) % len(engines)]
     copy_bytes = 8 * 2 * (res.row_hi - res.row_lo + 1) + 4 * (res.n_facts + res.n_links)
     # the copy-back holds every row of the caller's concepts (el_stats also counts the rows of
     # ELK range fillers, internal concepts, when the ontology has range axioms)
-    assert (res.n_facts, res.n_links) == (st["s_facts"], st["links"]) or len(ax.range), "copy-back lost facts"
-    eng.close()
+    for r in results:
+        assert (r.n_facts, r.n_links) == (st["s_facts"], st["links"]) or len(ax.range), "copy-back lost facts"
+    # latency of ONE classification with its copy-back, nothing in flight beside it
+    lat = []
+    for _ in range(3):
+        t0 = time.perf_counter()
+        eng.init()
+        eng.saturate()
+        t1 = time.perf_counter()
+        eng.copy_result(results[0], release=True)
+        lat.append((time.perf_counter() - t0, time.perf_counter() - t1))
+    latency_ms = 1e3 * min(t[0] for t in lat)
+    serial_copyback_ms = 1e3 * min(t[1] for t in lat)
+    for e in engines:
+        e.close()
 
     roofline = None
     kernels = None
@@ -261,10 +302,13 @@ def main():
             "supersteps": st["supersteps"],
             "load_s": round(load_s, 3),
             "generate_s": round(gen_s, 3),
+            "inflight": len(engines),
             "saturate_ms": round(saturate_ms, 4),
-            "copyback_ms": round(copyback_ms, 4),
+            "copyback_host_ms": round(copyback_ms, 4),
+            "latency_ms": round(latency_ms, 4),
+            "copyback_ms": round(serial_copyback_ms, 4),
             "copyback_bytes": int(copy_bytes),
-            "copyback_gbs": round(copy_bytes / (copyback_ms * 1e-3) / 1e9, 2) if copyback_ms > 0 else None,
+            "copyback_gbs": round(copy_bytes / (serial_copyback_ms * 1e-3) / 1e9, 2) if serial_copyback_ms > 0 else None,
             "roofline": roofline,
             "cpu_baseline": cpu,
         }

@@ -71,16 +71,23 @@ def allreduce(rk: Ranks, value: float, op: str = "max") -> float:
     return t.item()
 
 
-def run_weak(rk: Ranks, classify: Callable[[], dict], steps: int, warmup: int) -> Tuple[float, int, dict]:
-    """Warm up, then time exactly ``steps`` classifications between barriers.
+def run_weak(rk: Ranks, classify: Callable[[], dict], steps: int, warmup: int,
+             drain: Optional[Callable[[], None]] = None) -> Tuple[float, int, dict]:
+    """Warm up, then time exactly ``steps`` classifications between barriers.  ``drain`` waits
+    for work a classification left in flight (asynchronous copy-backs); it runs inside the
+    timed region, before the closing barrier.
     Returns (max-over-ranks seconds, derived axioms summed over ranks per step, last stats)."""
     st = {}
     for _ in range(warmup):
         st = classify()
+    if drain:
+        drain()
     barrier_sync(rk)
     t0 = time.perf_counter()
     for _ in range(steps):
         st = classify()
+    if drain:
+        drain()
     barrier_sync(rk)
     elapsed = time.perf_counter() - t0
     t_max = float(allreduce(rk, float(elapsed), "max"))

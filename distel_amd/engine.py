@@ -23,6 +23,7 @@ LAYOUT_X_TO_B, LAYOUT_B_TO_X = 0, 1
 EL_FLAG_COMPAT_DISTEL_CHAIN = 0x1  # el_config.flags: hazard H2 reproduced (include/el_gpu.h)
 EL_FLAG_COMPAT_DISTEL_RANGE = 0x2  # el_config.flags: DistEL's range reading (H1); default ELK's
 EL_RESULT_RELEASE = 0x1  # el_result.flags: the state is released behind the copy-back
+EL_RESULT_ASYNC = 0x2    # el_result.flags: return once enqueued; el_result_wait() = landed
 
 # work phases (el_kernel); "kernel:role" where several phases share one launch
 KERNEL_NAMES = ["k_expand:s", "k_expand:l", "k_jobs", "k_expand:a", "k_commit:s", "k_commit:l", "k_commit:a",
@@ -101,7 +102,7 @@ EXPORTED_SYMBOLS = [
     "el_abi_version", "el_device_count", "el_create", "el_load", "el_init", "el_step", "el_saturate",
     "el_get_stats", "el_kernel_stats", "el_superstep_trace", "el_get_subsumers", "el_copy_facts",
     "el_copy_links", "el_export_result", "el_last_error", "el_destroy", "el_group_create", "el_group_destroy",
-    "el_rccl_unique_id", "el_add_axioms", "el_result_info", "el_copy_result", "el_pair_table", "el_host_alloc",
+    "el_rccl_unique_id", "el_add_axioms", "el_result_info", "el_copy_result", "el_result_wait", "el_pair_table", "el_host_alloc",
     "el_host_free", "el_fresh_fillers",
 ]
 
@@ -137,6 +138,7 @@ def load_library(path: Optional[str] = None) -> C.CDLL:
     lib.el_copy_links.argtypes = [P, _u32p, _u32p, _u32p, C.c_size_t, C.POINTER(C.c_size_t)]
     lib.el_export_result.argtypes = [P, C.c_int, _SINK, C.c_void_p]
     lib.el_result_info.argtypes = [P, C.POINTER(_ElResult)]
+    lib.el_result_wait.argtypes = [P]
     lib.el_copy_result.argtypes = [P, C.POINTER(_ElResult)]
     lib.el_pair_table.argtypes = [P, _u32p, _u32p, C.c_size_t, C.POINTER(C.c_size_t)]
     lib.el_host_alloc.argtypes = [C.c_size_t]
@@ -434,15 +436,18 @@ class Engine:
         return r
 
     def copy_result(self, out: Optional[Result] = None, pinned: bool = True, facts: bool = True,
-                    links: bool = True, release: bool = False) -> Result:
+                    links: bool = True, release: bool = False, wait: bool = True) -> Result:
         """Result copy-back into ``out`` (reused across calls; page-locked buffers by default).
         release: EL_RESULT_RELEASE — the next init()'s reset runs behind the copy-back; the engine
-        has no state until init()."""
+        has no state until init().  wait=False (with release): EL_RESULT_ASYNC — returns once the
+        copy is enqueued; ``out`` is complete after result_wait() (or any later call on this engine)."""
+        if not wait and not release:
+            raise ValueError("an asynchronous copy-back releases the state (release=True)")
         info = self.result_info()
         out = out or Result()
         out._fit(info.row_hi - info.row_lo, info.n_facts if facts else 0, info.n_links if links else 0, pinned)
         r = _ElResult()
-        r.flags = EL_RESULT_RELEASE if release else 0
+        r.flags = (EL_RESULT_RELEASE if release else 0) | (0 if wait else EL_RESULT_ASYNC)
         if facts:
             r.s_ptr = out.s_ptr.ctypes.data_as(C.POINTER(C.c_uint64))
             r.s_val = out.s_val.ctypes.data_as(_u32p)
@@ -455,6 +460,10 @@ class Engine:
         out.row_lo, out.row_hi, out.n_facts, out.n_links, out.n_pairs = (r.row_lo, r.row_hi, r.n_facts, r.n_links,
                                                                          r.n_pairs)
         return out
+
+    def result_wait(self) -> None:
+        """Block until an asynchronous copy-back (copy_result(wait=False)) has landed."""
+        self._check(self._lib.el_result_wait(self._ctx), "el_result_wait")
 
     def fresh_fillers(self) -> Tuple[np.ndarray, np.ndarray]:
         """ELK range fillers: concept n_concepts + i = filler[i] ⊓ ranges*(role[i])."""

@@ -283,9 +283,14 @@ int el_superstep_trace(el_ctx* ctx, uint64_t* ds, uint64_t* dl, uint64_t* da, si
  * straight over PCIe (no device staging copy).
  * flags: EL_RESULT_RELEASE = the caller is done with this classification: once the state has
  * been read, the next el_init's reset runs beside the rest of the copy-back, and the context
- * has no state (EL_ESTATE) until el_init. */
+ * has no state (EL_ESTATE) until el_init.
+ * EL_RESULT_ASYNC (with EL_RESULT_RELEASE) = return once the copy-back is enqueued: the
+ * buffers are complete when el_result_wait(ctx) returns (every other call on the context waits
+ * for them first).  The caller may classify on ANOTHER context meanwhile, so one context's
+ * copy-back rides over PCIe under the other's saturation (stream overlap, no extra work). */
 #define EL_RESULT_RELEASE 0x1u
-#define EL_RESULT_FLAGS_KNOWN (EL_RESULT_RELEASE)
+#define EL_RESULT_ASYNC 0x2u
+#define EL_RESULT_FLAGS_KNOWN (EL_RESULT_RELEASE | EL_RESULT_ASYNC)
 typedef struct el_result {
   uint32_t row_lo, row_hi;  /* out: rows of this context (whole ontology: 0, n_concepts) */
   uint64_t n_facts;         /* out: Σ_X |S(X)| over the rows */
@@ -302,6 +307,7 @@ typedef struct el_result {
 
 int el_result_info(el_ctx* ctx, el_result* res);   /* the out fields only */
 int el_copy_result(el_ctx* ctx, el_result* res);   /* EL_ERANGE if a buffer is too small */
+int el_result_wait(el_ctx* ctx);                    /* an EL_RESULT_ASYNC copy-back has landed */
 /* pair q -> (role, filler), q ascending = (role, filler) ascending */
 int el_pair_table(el_ctx* ctx, uint32_t* role, uint32_t* filler, size_t cap, size_t* n);
 /* ELK range fillers (default range reading): fresh concept n_concepts + i stands for

@@ -204,3 +204,59 @@ def test_copy_result_release_g3_pinned():
         eng.copy_result(res, release=True)
         assert _result_digest(res, role, filler) == want
     eng.close()
+
+
+def _g3_digest():
+    for line in open(os.path.join(os.path.dirname(__file__), "golden", "closure_digests.txt")):
+        f = line.split()
+        if len(f) == 4 and f[0] == "g3" and float(f[1]) == 1.0:
+            return f[3]
+    raise AssertionError("no pinned G3 digest")
+
+
+def test_copy_result_async_two_engines_g3():
+    """The bench's pipelined schedule at full G3: two engines alternate, each copy-back enqueued
+    with EL_RESULT_ASYNC so it lands while the other engine saturates.  Every copy — read after
+    result_wait(), or after the engine's next call waited for it — hashes to the pinned digest."""
+    want = _g3_digest()
+    ax = generators.workload("g3")
+    engs = [engine.Engine(device=0) for _ in range(2)]
+    for e in engs:
+        e.load(ax)
+    role, filler = engs[0].pair_table()
+    results = [engine.Result(), engine.Result()]
+    for i in range(5):
+        e, res = engs[i % 2], results[i % 2]
+        e.init()  # (waits for this engine's previous copy-back)
+        e.saturate()
+        e.copy_result(res, release=True, wait=False)
+        if i >= 1:  # the other engine's copy-back landed behind this saturation
+            o = engs[(i + 1) % 2]
+            o.result_wait()
+            assert _result_digest(results[(i + 1) % 2], role, filler) == want
+    engs[0].result_wait()
+    assert _result_digest(results[0], role, filler) == want
+    with pytest.raises(ValueError):
+        engs[1].copy_result(results[1], wait=False)  # asynchronous needs release
+    for e in engs:
+        e.close()
+
+
+def test_copy_result_async_g2_close_in_flight(oracle_lib):
+    """An async copy-back still in flight when the engine is closed or re-initialised."""
+    ax = generators.workload("g2", scale=0.3)
+    o = oracle_lib.saturate(ax, 0)
+    ox, oa = o.facts()
+    eng = engine.Engine(device=0)
+    eng.load(ax)
+    res = engine.Result()
+    for _ in range(2):
+        eng.init()
+        eng.saturate()
+        eng.copy_result(res, release=True, wait=False)
+    eng.init()  # waits for the copy-back
+    x, a = res.facts()
+    assert np.array_equal(x, ox) and np.array_equal(a, oa)
+    eng.saturate()
+    eng.copy_result(res, release=True, wait=False)
+    eng.close()  # drains it
