@@ -39,6 +39,7 @@ import json
 import os
 import sys
 import time
+from concurrent.futures import ThreadPoolExecutor
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
@@ -165,8 +166,13 @@ def main():
         eng2.load(ax)
         engines.append(eng2)
     results = [engine.Result() for _ in engines]  # page-locked result buffers, reused by every step
-    split = []  # (classification, copy-back) seconds per step; the last `steps` are the timed ones
+    split = []  # (classification, copy-back enqueue) seconds per step; the last `steps` are the timed ones
     turn = [0]
+    # Two engines in flight: a helper thread enqueues one engine's copy-back (it waits ~1 ms on the
+    # device for the row counts) while this thread starts the other engine's classification;
+    # ctypes drops the GIL inside the library, and the two threads never share an engine.
+    pool = ThreadPoolExecutor(max_workers=1) if len(engines) == 2 else None
+    copying = [None] * len(engines)
 
     def classify():
         # one classification: el_init + el_saturate + result copy-back (part of the metric,
@@ -177,16 +183,25 @@ def main():
         i = turn[0] % len(engines)
         turn[0] += 1
         e, res = engines[i], results[i]
+        if copying[i] is not None:
+            copying[i].result()  # (the enqueue finished long ago; errors surface here)
+            copying[i] = None
         t0 = time.perf_counter()
         e.init()
         st = e.saturate()
         t1 = time.perf_counter()
-        e.copy_result(res, release=True, wait=len(engines) == 1)
+        if pool is None:
+            e.copy_result(res, release=True)
+        else:
+            copying[i] = pool.submit(e.copy_result, res, release=True, wait=False)
         split.append((t1 - t0, time.perf_counter() - t1))
         return st
 
     def drain():
-        for e in engines:
+        for i, e in enumerate(engines):
+            if copying[i] is not None:
+                copying[i].result()
+                copying[i] = None
             e.result_wait()
 
     t_max, derived_all, st = D.run_weak(rk, classify, args.steps, args.warmup, drain=drain)
@@ -212,6 +227,8 @@ def main():
         lat.append((time.perf_counter() - t0, time.perf_counter() - t1))
     latency_ms = 1e3 * min(t[0] for t in lat)
     serial_copyback_ms = 1e3 * min(t[1] for t in lat)
+    if pool is not None:
+        pool.shutdown()
     for e in engines:
         e.close()
 
@@ -304,7 +321,7 @@ def main():
             "generate_s": round(gen_s, 3),
             "inflight": len(engines),
             "saturate_ms": round(saturate_ms, 4),
-            "copyback_host_ms": round(copyback_ms, 4),
+            "copyback_enqueue_ms": round(copyback_ms, 4),
             "latency_ms": round(latency_ms, 4),
             "copyback_ms": round(serial_copyback_ms, 4),
             "copyback_bytes": int(copy_bytes),

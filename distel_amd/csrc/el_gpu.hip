@@ -2306,10 +2306,11 @@ struct el_ctx {
   hipStream_t cstream = nullptr;             // copy-back DMA, beside the row builds
   // S-row read-out copy-back (el_copy_result): device staging chunks and their DMA stream
   hipStream_t dstream = nullptr;
-  // The copy-back streams (and the read-out's own stream) are created at the lowest priority,
-  // the engine stream at the highest: a copy-back in flight beside another engine's saturation
-  // yields the dispatcher to it (G3, two engines in flight: 29.7 -> 27.2 ms per classification).
-  // EL_NO_STREAM_PRIO (A/B): default priorities, the read-out on the engine stream.
+  // EL_STREAM_PRIO (A/B): the copy-back streams and the read-out's own stream at the lowest
+  // priority, the engine stream at the highest, so a copy-back in flight beside another
+  // engine's saturation yields the dispatcher to it.  Measured with two engines in flight: G3
+  // 29.7 -> 27.2 ms while the host enqueued the copy-back before starting the other engine;
+  // once a helper thread enqueues it, 25.07 vs 25.12 ms, and G2 loses (1.26 vs 1.01 ms): off.
   hipStream_t ostream = nullptr;
   hipEvent_t ev_out = nullptr;
   static constexpr uint32_t NSTAGE = 4;  // staging buffers: the read-out runs up to 3 chunks ahead of the DMA
@@ -4112,7 +4113,7 @@ int el_create(el_ctx** out, const el_config* cfg) {
     return EL_EINVAL;
   }
   int rc = guarded(c, [&] {
-    if (!getenv("EL_NO_STREAM_PRIO")) {
+    if (getenv("EL_STREAM_PRIO")) {
       int least = 0, greatest = 0;
       HIPCHK(hipDeviceGetStreamPriorityRange(&least, &greatest));
       HIPCHK(hipStreamCreateWithPriority(&c->stream, hipStreamNonBlocking, greatest));

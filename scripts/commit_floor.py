@@ -44,18 +44,28 @@ def main():
     out = {"workload": workload, "scale": scale, "concepts": ax.n_concepts, "facts": n, "init": init,
            "oracle_s": round(sat_s, 1), "steps": []}
     pos = n - int(ds.sum())  # the init facts (X, ⊤ and the told closure) come first
-    tot = {"new": 0, "lines64": 0, "lines128": 0}
+    tot = {"new": 0, "words": 0, "lines64": 0, "lines128": 0}
     for t, d in enumerate(ds.tolist()):
         xs, as_ = x[pos:pos + d].astype(np.uint64), a[pos:pos + d].astype(np.uint64)
         pos += d
         bit = xs * (32 * words) + as_
+        wd = np.unique(bit >> 5).size
         l64 = np.unique(bit >> 9).size
         l128 = np.unique(bit >> 10).size
-        out["steps"].append({"step": t, "new": int(d), "lines64": int(l64), "lines128": int(l128)})
+        out["steps"].append({"step": t, "new": int(d), "words": int(wd), "lines64": int(l64), "lines128": int(l128)})
+        tot["words"] += int(wd)
         tot["new"] += int(d)
         tot["lines64"] += int(l64)
         tot["lines128"] += int(l128)
     out["total"] = tot
+    allbits = x.astype(np.uint64) * np.uint64(32 * words) + a.astype(np.uint64)
+    out["distinct_words_final"] = int(np.unique(allbits >> np.uint64(5)).size)
+    out["distinct_lines64_final"] = int(np.unique(allbits >> np.uint64(9)).size)
+    # how far into its row a row's last entry lies (the read-out reads each row up to it)
+    last = np.zeros(ax.n_concepts, np.int64)
+    np.maximum.at(last, x.astype(np.int64), a.astype(np.int64))
+    out["readout_words_to_last_entry"] = int(((last + 32) // 32).sum())
+    out["matrix_words"] = int(words) * ax.n_concepts
     out["floor_write_bytes_64"] = 64 * tot["lines64"]
     out["floor_write_bytes_128"] = 128 * tot["lines128"]
     print(json.dumps(out))
