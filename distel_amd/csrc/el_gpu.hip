@@ -507,7 +507,10 @@ constexpr uint32_t WQJ = 64;   // fan-out job records per wave
 // subsumers) and each would cost a queue slot, a global write and read and a bit-word
 // atomic; the cache drops those it still holds.  Lossy by design: a key evicted or raced
 // by another lane just reaches the commit, whose atomicOr dedups exactly.
-constexpr uint32_t DEDUP_SLOTS = 128;
+#ifndef EL_DEDUP_BITS
+#define EL_DEDUP_BITS 7
+#endif
+constexpr uint32_t DEDUP_SLOTS = 1u << EL_DEDUP_BITS;
 
 struct WaveQ {
   unsigned long long seen[DEDUP_SLOTS];  // S-candidate keys (x << 32 | a), ~0 = empty
@@ -620,8 +623,7 @@ __device__ __forceinline__ void emit_s(const DState& st, BlockQ& q, bool pred, u
   if (pred) ev.v[EL_EV_EMIT]++;
   if (pred && st.dedup) {
     const unsigned long long key = ((unsigned long long)x << 32) | a;
-    const uint32_t slot = ((x * 2654435761u) ^ (a * 2246822519u)) >> (32 - 7);
-    static_assert(DEDUP_SLOTS == 128, "slot = top 7 bits");
+    const uint32_t slot = ((x * 2654435761u) ^ (a * 2246822519u)) >> (32 - EL_DEDUP_BITS);
     if (w.seen[slot] == key) {
       pred = false;  // the wave queued (x, a) already in this launch
       ev.dup++;
