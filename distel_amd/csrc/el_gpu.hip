@@ -111,6 +111,9 @@ struct DIndex {
   const uint8_t* kind;
   const uint32_t *told_ptr, *told_b;
   const uint32_t *cidx_ptr, *cidx_c;
+  // per cidx entry j of A: a binary conjunction {A, p} ⊑ B as p | (p sorts before A) << 31 and B
+  // (cidx_p = NONE: another arity, walked through conj_ptr / conj_ops)
+  const uint32_t *cidx_p, *cidx_b;
   const uint32_t *conj_ptr, *conj_ops, *conj_b;
   const uint32_t *exr_ptr, *exr_pid;
   const uint32_t *exl_ptr, *exl_r, *exl_b;
@@ -905,9 +908,29 @@ __device__ void expand_s(const DIndex& ix, const DState& st, BlockQ& q, uint32_t
     if (act && (mask & M_R2)) {  // A1..An ∈ S(X), ⊓Ai ⊑ B  =>  B ∈ S(X)
       ev.v[EL_EV_ROW]++;
       for (uint32_t j = m0.y; j < m1.y; ++j) {
-        const uint32_t c = ix.cidx_c[j];
+        const uint32_t pp = ix.cidx_p[j];
         ev.v[EL_EV_ENT]++;
         ev.v[EL_EV_ROW]++;
+        if (pp != NONE) {
+          // binary A ⊓ p ⊑ B from the entry itself: two independent loads instead of the chain
+          // conj id -> operand row -> operands.  Events as the operand walk counts them (the
+          // sorted operands: A's entry is read before p's, or after it only if p ∈ S(X))
+          const uint32_t p = pp & 0x7fffffffu, B = ix.cidx_b[j];
+          const bool p_first = pp >> 31;
+          ev.v[EL_EV_ENT]++;
+          ev.v[EL_EV_TEST]++;
+          const bool ok = test_bit(ix, st.bits, X, p);
+          if (ok || !p_first) ev.v[EL_EV_ENT]++;
+          bool nw = false;
+          if (ok) {
+            ev.v[EL_EV_ENT]++;
+            ev.v[EL_EV_TEST]++;
+            nw = !test_bit(ix, st.bits, X, B);
+          }
+          emit_s(st, q, nw, X, B, ev);
+          continue;
+        }
+        const uint32_t c = ix.cidx_c[j];
         const uint32_t o1 = ix.conj_ptr[c + 1];
         bool ok = true;
         for (uint32_t k = ix.conj_ptr[c]; k < o1; ++k) {
@@ -2632,6 +2655,20 @@ std::string el_ctx::install_index(el::HostIndex&& hnew) {
   d.told_b = up32(h.told.a);
   d.cidx_ptr = up32(h.cidx.ptr);
   d.cidx_c = up32(h.cidx.a);
+  {
+    std::vector<uint32_t> cp(h.cidx.a.size(), NONE), cb(h.cidx.a.size(), 0);
+    for (uint32_t a = 0; a < h.N; ++a)
+      for (uint32_t j = h.cidx.ptr[a]; j < h.cidx.ptr[a + 1]; ++j) {
+        const uint32_t c = h.cidx.a[j], o0 = h.conj.ptr[c];
+        cb[j] = h.conj_b[c];
+        if (h.conj.ptr[c + 1] - o0 != 2 || h.N > 0x7fffffffu) continue;
+        const uint32_t u = h.conj.a[o0], v = h.conj.a[o0 + 1];  // (sorted, distinct)
+        if (u != a && v != a) continue;
+        cp[j] = a == u ? v : u | 0x80000000u;
+      }
+    d.cidx_p = up32(cp);
+    d.cidx_b = up32(cb);
+  }
   d.conj_ptr = up32(h.conj.ptr);
   d.conj_ops = up32(h.conj.a);
   d.conj_b = up32(h.conj_b);
