@@ -501,7 +501,10 @@ __device__ __forceinline__ uint32_t lds_reserve(uint32_t* qn, bool pred) {
 // global atomic (WQ records).  No block barrier is involved, so a wave may flush in the
 // middle of a divergent inner loop (a told closure, a fan-out row): only the wave's
 // active lanes take part, and LDS accesses of one wave execute in program order.
-constexpr uint32_t WQ = 256;   // (x, a) / (x, pid) records per wave and queue
+#ifndef EL_WQ
+#define EL_WQ 256
+#endif
+constexpr uint32_t WQ = EL_WQ;  // (x, a) / (x, pid) records per wave and queue
 constexpr uint32_t WQJ = 64;   // fan-out job records per wave
 
 // In-wave duplicate filter for S candidates: a direct-mapped cache of the wave's recent
