@@ -2386,6 +2386,13 @@ struct el_ctx {
   uint64_t p_base = 0;  // base propagations at the head of the propagation log
   bool fresh = false;   // el_init ran and no superstep since: el_saturate installs the base links
   void install_base();
+  // Base links / propagations enqueued on stream s for the NEXT classification, behind the
+  // reset of a releasing copy-back (el_copy_result): the scatters and the set fills then run
+  // beside the transfer instead of before / beside the first superstep.  Returns false (nothing
+  // enqueued) when a buffer would have to grow first.  pre_base: enqueued, not yet accounted.
+  bool enqueue_base(hipStream_t s);
+  void undo_base();  // the next state is not a fresh saturation (el_step, el_add_axioms)
+  bool pre_base = false;
   // The logs are indexed by uint32 counters on the device (DCounters): a step whose logs could
   // pass 2^32 entries (count + every candidate new) fails with EL_ENOMEM instead of wrapping.
   void check_u32_room() const {
@@ -2890,6 +2897,7 @@ void el_ctx::free_index() {
 void el_ctx::free_state() {
   if (rstream) (void)hipStreamSynchronize(rstream);  // a reset behind a releasing copy-back
   pre_reset = false;
+  pre_base = false;
   dfree(bits);
   dfree(slog_x);
   dfree(slog_a);
@@ -3164,6 +3172,7 @@ void el_ctx::reset_state() {
     pre_reset = false;
   } else {
     reset_device(stream);
+    pre_base = false;  // (the full reset cleared it)
   }
   bits_logged = true;  // from here on every set bit is in the fact log (k_init and k_commit append)
   s_count = l_count = a_count = p_count = s_init = x_count = 0;
@@ -3850,8 +3859,104 @@ void el_ctx::init_rows(uint32_t a, uint32_t b) {
 // them), and the link set stays without them (link_known: a binary search of exr(X)).  The
 // first superstep then expands the base links, which the second did before; its queues start
 // at what the second got.  The CPU oracle installs the same links (el_oracle.c, base_links).
+bool el_ctx::enqueue_base(hipStream_t s) {
+  const uint64_t nb = hx.exr.a.size(), nbp = hx.bpp.a.size();
+  if (nb == 0 || part() || (PR.live && !PR.start0) || (SC.live && !SC.start0)) return false;
+  const bool props = nbp && use_props && PP.live && PP.start0;
+  if (nb + cl_cap > llog_cap || 2 * (nb + cl_cap) > lhash_cap) return false;
+  if (props && (nbp + cp_cap > plog_cap || 2 * (nbp + cp_cap) > phash_cap)) return false;
+  const uint32_t N = hx.N, P = hx.P, nc = (uint32_t)hx.exrC.a.size();
+  auto items = [](uint64_t n) { return (uint32_t)std::min<uint64_t>(16, std::max<uint64_t>(1, n / (2048 * 256))); };
+  auto grid = [&](uint64_t n) {
+    const uint64_t t = 256ull * items(n);
+    return (uint32_t)std::min<uint64_t>(2048, std::max<uint64_t>(1, (n + t - 1) / t));
+  };
+  // the same launches as install_base, in one stream (the reset before them, el_init after)
+  hipLaunchKernelGGL(k_csr_scatter, dim3(grid(nb)), dim3(256), 0, s, ix.exr_ptr, ix.exr_pid, N, (uint32_t)nb, llog_x,
+                     llog_p, nullptr, nullptr, items(nb));
+  if (PR.live) {
+    hipLaunchKernelGGL(k_gap_len, dim3(grid(P)), dim3(256), 0, s, exrT_ptr, P, PR.len);
+    hipLaunchKernelGGL(k_csr_scatter, dim3(grid(nb)), dim3(256), 0, s, exrT_ptr, exrT_x, P, (uint32_t)nb, nullptr,
+                       nullptr, PR.start, PR.val, items(nb));
+  }
+  if (SC.live && nc) {
+    hipLaunchKernelGGL(k_gap_len, dim3(grid(N)), dim3(256), 0, s, exrC_ptr, N, SC.len);
+    hipLaunchKernelGGL(k_csr_scatter, dim3(grid(nc)), dim3(256), 0, s, exrC_ptr, exrC_p, N, nc, nullptr, nullptr,
+                       SC.start, SC.val, items(nc));
+  }
+  hipLaunchKernelGGL(k_set_u32, dim3(1), dim3(1), 0, s, &ctr->l_log, (uint32_t)nb);
+  if (props) {
+    hipLaunchKernelGGL(k_csr_scatter, dim3(grid(nbp)), dim3(256), 0, s, ix.bpp_ptr, ix.bpp_b, P, (uint32_t)nbp, plog_p,
+                       plog_b, nullptr, nullptr, items(nbp));
+    hipLaunchKernelGGL(k_gap_len, dim3(grid(P)), dim3(256), 0, s, ix.bpp_ptr, P, PP.len);
+    hipLaunchKernelGGL(k_csr_scatter, dim3(grid(nbp)), dim3(256), 0, s, ix.bpp_ptr, ix.bpp_b, P, (uint32_t)nbp, nullptr,
+                       nullptr, PP.start, PP.val, items(nbp));
+    hipLaunchKernelGGL(k_set_u32, dim3(1), dim3(1), 0, s, &ctr->p_log, (uint32_t)nbp);
+  }
+  hipLaunchKernelGGL(k_rehash, dim3(grid_for(nb, 2048)), dim3(BLOCK), 0, s, lhash, lhash_cap - 1, llog_x, llog_p,
+                     (uint32_t)nb);
+  if (props)
+    hipLaunchKernelGGL(k_rehash, dim3(grid_for(nbp, 2048)), dim3(BLOCK), 0, s, phash, phash_cap - 1, plog_b, plog_p,
+                       (uint32_t)nbp);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipEventRecord(ev_base[1], s));  // (join_base waits for it; the set is full by then)
+  return true;
+}
+
+void el_ctx::undo_base() {
+  if (!pre_base) return;
+  pre_base = false;
+  // the link / propagation logs, sets and rows as the reset leaves them (the S state is kept)
+  hipLaunchKernelGGL(k_set_u32, dim3(1), dim3(1), 0, stream, &ctr->l_log, 0u);
+  hipLaunchKernelGGL(k_set_u32, dim3(1), dim3(1), 0, stream, &ctr->p_log, 0u);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipMemsetAsync(lhash, 0xff, lhash_cap * sizeof(unsigned long long), stream));
+  HIPCHK(hipMemsetAsync(phash, 0xff, phash_cap * sizeof(unsigned long long), stream));
+  for (GapCsr* g : {&PR, &SC, &PP}) {
+    if (!g->live) continue;
+    hipLaunchKernelGGL(k_gap_init, dim3(grid_for(g->rows + 1)), dim3(BLOCK), 0, stream, g->start, g->len, g->rows,
+                       g->start0);
+    HIPCHK(hipGetLastError());
+  }
+}
+
 void el_ctx::install_base() {
   const uint64_t nb = hx.exr.a.size();
+  if (pre_base) {  // enqueued behind the last copy-back (enqueue_base): account for it only
+    pre_base = false;
+    const uint64_t nbp = hx.bpp.a.size();
+    const bool props = nbp && use_props && PP.live && PP.start0;
+    const uint64_t trig = s_count + nb;
+    if (!small_queues) {
+      if (const uint64_t want = std::min<uint64_t>(4 * trig, 1ull << 28); want > cs_cap) {
+        sync();
+        cs_cap = next_pow2(want);
+        dfree(cs_x);
+        dfree(cs_a);
+        cs_x = dalloc<uint32_t>(cs_cap);
+        cs_a = dalloc<uint32_t>(cs_cap);
+      }
+      if (const uint64_t want = std::min<uint64_t>(trig, 1ull << 26); want > job_cap) {
+        sync();
+        job_cap = next_pow2(want);
+        dfree(jobs);
+        jobs = dalloc<uint4>(job_cap);
+      }
+    }
+    launches[EL_K_INIT] += 1 + (PR.live ? 1 : 0) + (SC.live && hx.exrC.a.size() ? 1 : 0) + (props ? 1 : 0);
+    if (props) {
+      p_count = p_base = nbp;
+      for (int r = 0; r < EL_NUM_RULE_TYPES; ++r) wm_p[r] = nbp;
+      host_ev[EL_K_INIT][EL_EV_ENT] += 2 * nbp;
+      host_ev[EL_K_INIT][EL_EV_EMIT] += nbp;
+    }
+    base_filling = true;
+    l_count = l_base = nb;
+    ix.base = 1;
+    host_ev[EL_K_INIT][EL_EV_ENT] += nb + (PR.live ? nb : 0) + (SC.live ? hx.exrC.a.size() : 0);
+    host_ev[EL_K_INIT][EL_EV_EMIT] += nb;
+    return;
+  }
   if (nb == 0 || l_count != 0 || (PR.live && !PR.start0) || (SC.live && !SC.start0)) return;
   const uint64_t trig = s_count + nb;
   if (!small_queues) {
@@ -4279,6 +4384,7 @@ int el_add_axioms(el_ctx* c, const el_axioms* inc) {
     el::HostIndex hx;
     if (e.empty()) e = el::build_index(store.view(), hx, c->flags);
     if (!e.empty()) return fail(c, EL_EINVAL, e);
+    c->undo_base();  // (base links enqueued for a saturation of the old index)
     c->sync();
     if (!c->inited) {  // nothing saturated yet: a plain reload
       c->free_state();
@@ -4330,6 +4436,7 @@ int el_step(el_ctx* c, el_rule rule, int* changed) {
   return guarded(c, [&] {
     const int r = (int)rule;
     c->fresh = false;  // per-rule stepping derives every link (DistEL's granularity)
+    c->undo_base();
     const uint64_t se = c->s_count, le = c->l_count, ae = c->a_count, pe = c->p_count;
     bool ch = c->superstep(kRuleMask[r], c->wm_s[r], se, c->wm_l[r], le, c->wm_a[r], ae, c->wm_p[r], pe);
     c->wm_s[r] = se;
@@ -4646,6 +4753,7 @@ int el_copy_result(el_ctx* c, el_result* res) {
       // rows the S-row sorts (all rows) or the read-out (the caller's rows) cleared as they went
       const uint32_t clear_from = parts[1].readout ? c->uhi() : fuse_clear && parts[1].direct ? c->hi : c->lo;
       c->reset_device(c->rstream, clear_from);
+      c->pre_base = !c->part() && c->enqueue_base(c->rstream);
       HIPCHK(hipEventRecord(c->ev_reset, c->rstream));
     }
     // 2. the sorts into the caller's buffers, the device rows by DMA

@@ -260,3 +260,53 @@ def test_copy_result_async_g2_close_in_flight(oracle_lib):
     eng.saturate()
     eng.copy_result(res, release=True, wait=False)
     eng.close()  # drains it
+
+
+def test_release_then_step_or_increment(oracle_lib):
+    """A releasing copy-back enqueues the next classification's base links and propagations
+    behind its reset.  A next state that is not a fresh saturation must not see them: per-rule
+    stepping (el_step) after el_init, and an increment (el_add_axioms) after el_init, both reach
+    the oracle's closure; a plain saturation after them is exact again."""
+    import sys
+    sys.path.insert(0, os.path.dirname(__file__))
+    from test_gpu_incremental import _split
+    ax = generators.workload("g1", scale=0.2)
+    o = oracle_lib.saturate(ax, 0)
+    ox, oa = o.facts()
+    res = engine.Result()
+    eng = engine.Engine(device=0)
+    eng.load(ax)
+    eng.init()
+    eng.saturate()
+    eng.copy_result(res, release=True)
+    eng.init()  # per-rule stepping on the state the release prepared
+    for _ in range(200):
+        if not any([eng.step(r) for r in range(8)]):
+            break
+    gx, ga = eng.facts()
+    assert np.array_equal(gx, ox) and np.array_equal(ga, oa)
+    for g, c in zip(eng.links(), o.links()):
+        assert np.array_equal(g, c)
+    eng.copy_result(res, release=True, wait=False)
+    eng.init()
+    eng.saturate()
+    x, a = eng.facts()
+    assert np.array_equal(x, ox) and np.array_equal(a, oa)
+    eng.close()
+    # an increment after el_init on a released state
+    pieces = _split(ax, 2, 11, grow=False)
+    eng = engine.Engine(device=0, compat_range=True)
+    eng.load(pieces[0])
+    eng.init()
+    eng.saturate()
+    eng.copy_result(res, release=True)
+    eng.init()
+    eng.add_axioms(pieces[1])
+    eng.saturate()
+    o2 = oracle_lib.saturate(ax, 0, compat_range=True)
+    gx, ga = eng.facts()
+    ox2, oa2 = o2.facts()
+    assert np.array_equal(gx, ox2) and np.array_equal(ga, oa2)
+    for g, c in zip(eng.links(), o2.links()):
+        assert np.array_equal(g, c)
+    eng.close()
