@@ -199,6 +199,8 @@ __host__ __device__ constexpr uint32_t gap_cap(uint32_t n) { return GAP_MUL * n 
 
 struct DState {
   uint32_t* bits;
+  uint8_t* summ;  // block summary of the bits (virtual row base like bits): row x, 512-B block k
+  uint32_t SB;    // at summ[x·SB + k]; nullptr: none (EL_NO_SUMMARY)
   uint32_t *slog_x, *slog_a;
   uint8_t* slog_f;  // 1: the fact came out of a CR1 told closure (its own closure, links and
                     // propagations are already out); 2: an init fact X ∈ S(X) whose closure
@@ -812,9 +814,11 @@ __global__ void k_init(DIndex ix, DState st, uint32_t lo, uint32_t hi, uint32_t 
       ev.v[EL_EV_ENT]++;
     }
     const uint32_t c = col_of(ix, v);  // (the told closure lies inside the window)
-    if (set_bits && c != NONE)  // (else k_init_bits writes the rows' init words)
+    if (set_bits && c != NONE) {  // (else k_init_bits writes the rows' init words)
       __hip_atomic_fetch_or(st.bits + (uint64_t)x * ix.W + (c >> 5), 1u << (c & 31u), __ATOMIC_RELAXED,
                             __HIP_MEMORY_SCOPE_AGENT);
+      if (st.summ) st.summ[(uint64_t)x * st.SB + (c >> 12)] = 1;
+    }
     st.slog_x[base + k] = x;
     st.slog_a[base + k] = v;
     st.slog_f[base + k] = f;
@@ -831,10 +835,21 @@ __global__ void k_set_u32(uint32_t* p, uint32_t v) { *p = v; }
 // written with plain stores — the matrix is zero at el_init and no word is listed twice —
 // instead of one returning atomic per init fact (G3: 25 M, 0.9 ms).
 __global__ void k_init_bits(uint32_t* __restrict__ bits, uint64_t W, const uint32_t* __restrict__ row,
-                            const uint32_t* __restrict__ word, const uint32_t* __restrict__ mask, uint32_t n) {
+                            const uint32_t* __restrict__ word, const uint32_t* __restrict__ mask, uint32_t n,
+                            uint8_t* __restrict__ summ, uint32_t SB) {
   const uint32_t stride = gridDim.x * blockDim.x;
-  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
     bits[(uint64_t)row[i] * W + word[i]] = mask[i];
+    if (summ) summ[(uint64_t)row[i] * SB + (word[i] >> 7)] = 1;
+  }
+}
+
+// The block summary of whole rows from the matrix (after an increment re-laid the matrix out).
+__global__ void k_summ_build(const uint32_t* __restrict__ bits, uint64_t W, uint64_t words, uint8_t* __restrict__ summ,
+                             uint32_t SB) {
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < words; i += stride)
+    if (bits[i]) summ[(i / W) * SB + (i % W >> 7)] = 1;
 }
 
 // Wave-cooperative loop over one CSR row per lane, [b, e) (an idle lane passes b = e): the
@@ -1329,6 +1344,7 @@ __device__ void commit_s(const DIndex& ix, const DState& st, CommitLds& sm, uint
       const uint32_t m = 1u << (c & 31u);
       const uint32_t old = c != NONE ? atomicOr(st.bits + (uint64_t)x * ix.W + (c >> 5), m) : m;
       nw = (old & m) == 0;
+      if (nw && st.summ) st.summ[(uint64_t)x * st.SB + (c >> 12)] = 1;  // (idempotent: plain store)
       if (nw) ev.v[EL_EV_EMIT]++;
     }
     // one LDS slot per new fact; blockDim <= QS_CAP/2 so a round never overflows
@@ -2286,6 +2302,14 @@ struct el_ctx {
   // state
   uint32_t* bits = nullptr;
   uint64_t W = 0;
+  // Block summary of the bit rows: one byte per 512-B block (128 words) of each owned row, set
+  // with a plain store by every writer of a bit (k_commit, k_init, k_init_bits), cleared with
+  // the matrix; the copy-back read-out loads only the blocks it marks.
+  uint8_t* summ = nullptr;
+  uint32_t SB = 0;
+  bool no_summary = getenv("EL_NO_SUMMARY") != nullptr;  // A/B: dense read-out
+  // one byte per 128 words, rows padded to 16 B (k_fill clears from any row with 16-B stores)
+  static uint32_t summ_stride(uint64_t w) { return (uint32_t)((((w + 127) / 128) + 15) & ~15ull); }
   uint32_t *slog_x = nullptr, *slog_a = nullptr;
   uint8_t* slog_f = nullptr;  // told-closure flags of the facts (slog_cap)
   uint64_t slog_cap = 0;
@@ -2346,6 +2370,7 @@ struct el_ctx {
   uint32_t* stage[NSTAGE] = {};
   uint64_t stage_cap = 0;
   bool readout_off = getenv("EL_NO_READOUT") != nullptr;  // A/B: S rows by the log sort instead
+  uint64_t readout_min = env_u32("EL_READOUT_MIN", 16u << 20);  // tests: the read-out for small results too
   bool links_direct = getenv("EL_LINKS_DIRECT") != nullptr;  // A/B: link-row sorts write the host buffer
   bool s_dma = getenv("EL_S_DMA") != nullptr;                // A/B: small S results by device sort + DMA
   uint64_t readout_chunk = (uint64_t)env_u32("EL_READOUT_CHUNK_MB", 32) << 18;  // entries per read-out DMA
@@ -2445,6 +2470,8 @@ struct el_ctx {
     DState s{};
     // virtual row base: row x of the owned range [lo, hi) is bits + (x - lo) * W
     s.bits = reinterpret_cast<uint32_t*>(reinterpret_cast<uintptr_t>(bits) - (uintptr_t)lo * W * sizeof(uint32_t));
+    s.summ = summ ? summ - (uintptr_t)lo * SB : nullptr;
+    s.SB = SB;
     s.slog_x = slog_x;
     s.slog_a = slog_a;
     s.slog_f = slog_f;
@@ -2603,8 +2630,11 @@ struct el_ctx {
   bool pre_reset = false;         // the device part of the next reset_state is already enqueued
   // clear_from: the first row whose bits the reset clears (lo: all; hi: none — a releasing
   // copy-back cleared the rows it read)
-  void reset_device(hipStream_t s, uint32_t clear_from);
-  void reset_device(hipStream_t s) { reset_device(s, lo); }
+  // summ_from: the first row whose block summary the reset clears (a releasing read-out
+  // cleared the summary of the rows it read, and may still be reading it: the reset must not
+  // touch those rows)
+  void reset_device(hipStream_t s, uint32_t clear_from, uint32_t summ_from);
+  void reset_device(hipStream_t s) { reset_device(s, lo, lo); }
   void rehash_links(uint64_t cap);
   void rehash_acts(uint64_t cap);
   void rehash_props(uint64_t cap);
@@ -2899,6 +2929,7 @@ void el_ctx::free_state() {
   pre_reset = false;
   pre_base = false;
   dfree(bits);
+  dfree(summ);
   dfree(slog_x);
   dfree(slog_a);
   dfree(slog_f);
@@ -2962,6 +2993,8 @@ void el_ctx::alloc_state() {
   const uint64_t N = hx.N, P = hx.P;
   W = ix.W;  // bit-row words: ⊥, ⊤ and the column window
   bits = dalloc<uint32_t>((uint64_t)(hi - lo) * W);  // owned rows only
+  SB = summ_stride(W);
+  summ = no_summary ? nullptr : dalloc<uint8_t>((uint64_t)(hi - lo) * SB);
   bits_logged = false;
   // capacities follow the owned rows (a partition of a ×8 ontology holds one copy's rows: its
   // queues and logs are sized for those, not for the whole index it loads)
@@ -3125,7 +3158,7 @@ void el_ctx::alloc_state() {
 
 // The device part of reset_state on stream s: clear the bit matrix (by the fact log), the
 // sets, counters and gapped rows.  Reads only the logs and counts of the finished state.
-void el_ctx::reset_device(hipStream_t stream, uint32_t clear_from) {
+void el_ctx::reset_device(hipStream_t stream, uint32_t clear_from, uint32_t summ_from) {
   FillArgs f{};
   auto add = [&](void* p, uint64_t bytes, uint32_t pattern) { f.seg[f.n++] = FillSeg{p, bytes, pattern}; };
   const uint64_t matrix_bytes = (uint64_t)(hi - lo) * W * sizeof(uint32_t);
@@ -3139,6 +3172,8 @@ void el_ctx::reset_device(hipStream_t stream, uint32_t clear_from) {
   } else {
     add(bits, matrix_bytes, 0u);
   }
+  if (summ && summ_from < hi)  // (whichever way the bits were cleared)
+    add(summ + (uint64_t)(summ_from - lo) * SB, (uint64_t)(hi - summ_from) * SB, 0u);
   // the link set is by far the largest (G3: 2 GB): the runtime's fill reaches a higher write
   // rate than k_fill's grid-stride loop for it (k_fill: 2.0 ms per G3 classification)
   if (lhash_cap * sizeof(unsigned long long) >= (64ull << 20))
@@ -3321,7 +3356,11 @@ void el_ctx::readout_rows(uint64_t* dptr, uint64_t* ptr_out, uint32_t* val_out, 
     }
     stage_cap = need;
   }
-  const elrows::Clear m{dstate().bits, W, lo, ix.c_lo, ix.c_hi};
+  elrows::Clear m{dstate().bits, W, lo, ix.c_lo, ix.c_hi};
+  if (summ) {
+    m.summ = dstate().summ;
+    m.SB = SB;
+  }
   hipStream_t os = ostream ? ostream : stream;  // (the counts above are done: the host waited)
   uint32_t k = 0;
   for (uint32_t ra = 0; ra < R; ++k) {
@@ -3843,7 +3882,7 @@ void el_ctx::init_rows(uint32_t a, uint32_t b) {
                        whole ? 0u : 1u);
     if (whole)
       hipLaunchKernelGGL(k_init_bits, dim3(grid_for(iw_n, 2048)), dim3(BLOCK), 0, stream, bits, W, iw_row, iw_word,
-                         iw_mask, iw_n);
+                         iw_mask, iw_n, summ, SB);
   });
   hipLaunchKernelGGL(k_set_u32, dim3(1), dim3(1), 0, stream, &ctr->s_log, (uint32_t)(s_count + n));
   HIPCHK(hipGetLastError());
@@ -4086,6 +4125,14 @@ void el_ctx::migrate_state(uint32_t N0, const std::vector<uint32_t>& pmap) {
     bits = nb;
     has_act = ha;
     W = W1;
+  }
+  if (summ) {  // the summary of the (re-laid-out) matrix
+    dfree(summ);
+    SB = summ_stride(W);
+    summ = dalloc<uint8_t>((uint64_t)(hi - lo) * SB);
+    HIPCHK(hipMemsetAsync(summ, 0, (uint64_t)(hi - lo) * SB, stream));
+    hipLaunchKernelGGL(k_summ_build, dim3(2048), dim3(BLOCK), 0, stream, bits, W, (uint64_t)(hi - lo) * W, summ, SB);
+    HIPCHK(hipGetLastError());
   }
   rs.release();  // result rows: more rows, remapped pair ids — rebuilt on demand
   rl.release();
@@ -4710,8 +4757,10 @@ int el_copy_result(el_ctx* c, el_result* res) {
       // so the transfer starts after the row counts instead of after the whole build (G3:
       // matrix 19 GB vs. 415 MB of rows; PCIe at ~57 GB/s is the bound either way).
       // (measured: G3, matrix / rows = 46, read-out 0.6 ms faster; G5, 61, 0.17 ms slower)
-      p.readout = p.direct && p.facts && !c->readout_off && p.val_out && p.n >= (16u << 20) &&
-                  (uint64_t)(c->uhi() - c->lo) * c->W * 4 <= 48 * 4 * p.n;
+      // With the block summary the read-out loads only marked blocks, so the matrix-to-rows ratio
+      // no longer decides (the dense read-out keeps it).
+      p.readout = p.direct && p.facts && !c->readout_off && p.val_out && p.n >= c->readout_min &&
+                  (c->summ || (uint64_t)(c->uhi() - c->lo) * c->W * 4 <= 48 * 4 * p.n);
       if (p.readout) {
         if (!r.ptr) r.ptr = dalloc<uint64_t>(R1);
         r.n = ~0ull;
@@ -4752,7 +4801,7 @@ int el_copy_result(el_ctx* c, el_result* res) {
       HIPCHK(hipStreamWaitEvent(c->rstream, c->ev_rows[1], 0));
       // rows the S-row sorts (all rows) or the read-out (the caller's rows) cleared as they went
       const uint32_t clear_from = parts[1].readout ? c->uhi() : fuse_clear && parts[1].direct ? c->hi : c->lo;
-      c->reset_device(c->rstream, clear_from);
+      c->reset_device(c->rstream, clear_from, parts[1].readout ? c->uhi() : c->lo);
       c->pre_base = !c->part() && c->enqueue_base(c->rstream);
       HIPCHK(hipEventRecord(c->ev_reset, c->rstream));
     }

@@ -38,6 +38,10 @@ struct Clear {
   uint64_t W = 0;
   uint32_t lo = 0;
   uint32_t c_lo = 2, c_hi = 0xffffffffu;
+  // optional block summary: byte x·SB + k is non-zero if row x may hold a set bit in its 512-B
+  // block k (words [128 k, 128 k + 128)); the read-out then reads only those blocks
+  uint8_t* summ = nullptr;  // (the read-out zeroes a row's bytes with its words when clearing)
+  uint32_t SB = 0;
   __device__ void bit(uint32_t r, uint32_t v) const;
 };
 

@@ -473,6 +473,104 @@ __global__ void __launch_bounds__(BLOCK) k_rows_global(const uint64_t* __restric
 
 }  // namespace
 
+// k_rows_readout over the block summary: a row's non-zero 512-B blocks (summary bytes set by
+// every writer of the matrix) are listed in LDS in column order, and the read-out loads only
+// those — G3's rows hold their 104 M facts in 9.9 M of 37 M blocks, so the copy-back reads
+// ≈5 GB of the 19 GB matrix instead of ≈18.5 GB (every word up to each row's last entry).
+// Rounds of 32 listed blocks: segment i = 8 blocks, lane t loads 16 B (block 8i + t/32, quad
+// t%32), so each load instruction covers two whole blocks; output slots from popcounts and
+// block scans, in (block, word) order = column order.
+constexpr uint32_t RB = 32;  // listed blocks per round
+__global__ void __launch_bounds__(BLOCK) k_rows_readout_sparse(const uint64_t* __restrict__ ptr, uint32_t r0,
+                                                               uint32_t r1, uint64_t out0, uint32_t* __restrict__ dst,
+                                                               Clear m, bool clear) {
+  __shared__ uint32_t wsum[4][BLOCK / 64];
+  __shared__ uint32_t blk[BLOCK];  // listed blocks of the current chunk of summary bytes
+  __shared__ uint32_t nblk;
+  const uint32_t tid = threadIdx.x, lane = __lane_id(), wv = tid >> 6;
+  const uint64_t W4 = m.W / 4;
+  for (uint32_t r = r0 + blockIdx.x; r < r1; r += gridDim.x) {
+    const uint64_t b = ptr[r], len = ptr[r + 1] - b;
+    if (len == 0) continue;  // (block-uniform)
+    uint4* __restrict__ row = reinterpret_cast<uint4*>(m.bits + (uint64_t)(r + m.lo) * m.W);
+    uint8_t* __restrict__ sr = m.summ + (uint64_t)(r + m.lo) * m.SB;
+    uint64_t done = 0;
+    for (uint32_t k0 = 0; k0 < m.SB && done < len; k0 += BLOCK) {
+      // list this chunk's non-zero blocks, ascending (wave ballots, then the waves in order)
+      const bool nz = k0 + tid < m.SB && sr[k0 + tid] != 0;
+      if (clear && nz) sr[k0 + tid] = 0;  // (the reset leaves the read-out's rows to it)
+      const unsigned long long bal = __ballot(nz);
+      if (lane == 0) wsum[0][wv] = (uint32_t)__popcll(bal);
+      __syncthreads();
+      uint32_t before = 0, total = 0;
+#pragma unroll
+      for (uint32_t k = 0; k < BLOCK / 64; ++k) {
+        before += k < wv ? wsum[0][k] : 0u;
+        total += wsum[0][k];
+      }
+      if (nz) blk[before + (uint32_t)__popcll(bal & ((1ull << lane) - 1ull))] = k0 + tid;
+      if (tid == 0) nblk = total;
+      __syncthreads();
+      const uint32_t nb = nblk;
+      for (uint32_t j0 = 0; j0 < nb && done < len; j0 += RB) {
+        uint4 v[4];
+        uint32_t c[4], inc[4];
+        uint64_t qq[4];
+#pragma unroll
+        for (uint32_t i = 0; i < 4; ++i) {
+          const uint32_t j = j0 + i * 8 + (tid >> 5);
+          const uint64_t q = j < nb ? (uint64_t)blk[j] * 32 + (tid & 31u) : W4;
+          qq[i] = q;
+          v[i] = q < W4 ? row[q] : make_uint4(0u, 0u, 0u, 0u);
+          c[i] = __popc(v[i].x) + __popc(v[i].y) + __popc(v[i].z) + __popc(v[i].w);
+          inc[i] = c[i];
+        }
+#pragma unroll
+        for (uint32_t o = 1; o < 64; o <<= 1) {
+#pragma unroll
+          for (uint32_t i = 0; i < 4; ++i) {
+            const uint32_t y = __shfl_up(inc[i], o);
+            if (lane >= o) inc[i] += y;
+          }
+        }
+        __syncthreads();  // (wsum[0] of the listing is read)
+        if (lane == 63) {
+#pragma unroll
+          for (uint32_t i = 0; i < 4; ++i) wsum[i][wv] = inc[i];
+        }
+        __syncthreads();
+        uint32_t rtot = 0;  // the round's entries before segment i
+#pragma unroll
+        for (uint32_t i = 0; i < 4; ++i) {
+          uint32_t bef = 0, tot = 0;
+#pragma unroll
+          for (uint32_t k = 0; k < BLOCK / 64; ++k) {
+            bef += k < wv ? wsum[i][k] : 0u;
+            tot += wsum[i][k];
+          }
+          uint32_t* o = dst + (b - out0) + done + rtot + bef + inc[i] - c[i];
+          const uint64_t q = qq[i];
+          const uint32_t wd[4] = {v[i].x, v[i].y, v[i].z, v[i].w};
+#pragma unroll
+          for (uint32_t jj = 0; jj < 4; ++jj) {
+            uint32_t word = wd[jj];
+            const uint32_t cb = (uint32_t)((q * 4 + jj) * 32);
+            while (word) {
+              const uint32_t col = cb + (uint32_t)__ffs(word) - 1;
+              *o++ = col < 2u ? col : col + m.c_lo - 2u;  // column -> concept
+              word &= word - 1;
+            }
+          }
+          if (clear && c[i]) row[q] = make_uint4(0u, 0u, 0u, 0u);
+          rtot += tot;
+        }
+        done += rtot;
+        __syncthreads();  // wsum / blk are reused
+      }
+    }
+  }
+}
+
 void Scratch::release() {
   for (void* p : {(void*)rank, (void*)tmp, (void*)cnt, (void*)lists, (void*)nlist, (void*)tile})
     if (p) (void)hipFree(p);
@@ -561,8 +659,12 @@ void readout(hipStream_t s, const uint64_t* ptr, uint32_t r0, uint32_t r1, uint6
     const char* e = getenv("EL_READOUT_BLOCKS");
     return e ? (uint32_t)std::max(1l, strtol(e, nullptr, 10)) : 1024u;
   }();
-  hipLaunchKernelGGL(k_rows_readout, dim3(std::min<uint32_t>(r1 - r0, maxb)), dim3(BLOCK), 0, s, ptr, r0, r1, out0,
-                     dst, m, clear);
+  if (m.summ)
+    hipLaunchKernelGGL(k_rows_readout_sparse, dim3(std::min<uint32_t>(r1 - r0, maxb)), dim3(BLOCK), 0, s, ptr, r0, r1,
+                       out0, dst, m, clear);
+  else
+    hipLaunchKernelGGL(k_rows_readout, dim3(std::min<uint32_t>(r1 - r0, maxb)), dim3(BLOCK), 0, s, ptr, r0, r1, out0,
+                       dst, m, clear);
   RCHK(hipGetLastError());
 }
 

@@ -61,6 +61,8 @@ def main():
     allbits = x.astype(np.uint64) * np.uint64(32 * words) + a.astype(np.uint64)
     out["distinct_words_final"] = int(np.unique(allbits >> np.uint64(5)).size)
     out["distinct_lines64_final"] = int(np.unique(allbits >> np.uint64(9)).size)
+    for sh, nm in ((12, "blocks512_final"), (15, "pages4k_final")):
+        out[nm] = int(np.unique(allbits >> np.uint64(sh)).size)
     # how far into its row a row's last entry lies (the read-out reads each row up to it)
     last = np.zeros(ax.n_concepts, np.int64)
     np.maximum.at(last, x.astype(np.int64), a.astype(np.int64))

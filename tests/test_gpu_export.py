@@ -310,3 +310,43 @@ def test_release_then_step_or_increment(oracle_lib):
     for g, c in zip(eng.links(), o2.links()):
         assert np.array_equal(g, c)
     eng.close()
+
+
+@pytest.mark.parametrize("release", [False, True])
+def test_readout_block_summary(release, oracle_lib, monkeypatch):
+    """S rows by the bit-matrix read-out over the block summary (forced for small results with
+    EL_READOUT_MIN=0): KATs, a long-row ontology, G2, and an increment (the summary rebuilt
+    from the re-laid-out matrix), each copy against the oracle; with release, twice in a row
+    (the reset clears the summary with the matrix)."""
+    monkeypatch.setenv("EL_READOUT_MIN", "0")
+    cases = [kat.load_kat(p)[0] for p in kat.kat_files()[:6]]
+    cases += [_long_rows_ontology(), generators.workload("g2", scale=0.5)]
+    for ax in cases:
+        o = oracle_lib.saturate(ax, 0)
+        ptr, oa = _oracle_rows(o, ax.n_concepts)
+        eng = engine.Engine(device=0)
+        eng.load(ax)
+        res = engine.Result()
+        for _ in range(2 if release else 1):
+            eng.init()
+            eng.saturate()
+            eng.copy_result(res, release=release)
+            assert np.array_equal(res.s_ptr, ptr) and np.array_equal(res.s_val[:res.n_facts], oa)
+        eng.close()
+    import sys
+    sys.path.insert(0, os.path.dirname(__file__))
+    from test_gpu_incremental import _split
+    ax = generators.workload("g1", scale=0.3)
+    pieces = _split(ax, 3, 5, grow=True)
+    eng = engine.Engine(device=0, compat_range=True)
+    eng.load(pieces[0])
+    eng.init()
+    eng.saturate()
+    for inc in pieces[1:]:
+        eng.add_axioms(inc)
+        eng.saturate()
+    res = eng.copy_result(release=release)
+    o = oracle_lib.saturate(ax, 0, compat_range=True)
+    ptr, oa = _oracle_rows(o, ax.n_concepts)
+    assert np.array_equal(res.s_ptr, ptr) and np.array_equal(res.s_val[:res.n_facts], oa)
+    eng.close()
