@@ -7,7 +7,7 @@ OUT=$R/gpurun_out/$TAG
 mkdir -p $OUT
 cd $R
 i=0
-for env in "X=0" "EL_NO_READOUT=1" "EL_NO_READOUT=1 EL_S_DMA=1" "EL_READOUT_BLOCKS=1024"; do
+for env in "X=0" "EL_READOUT_MIN=0"; do
   i=$((i+1))
   env $env timeout -k 10 300 python bench.py --workload $W --inflight 2 --no-cpu --no-profile --steps 20 --warmup 5 > $OUT/r$i.json 2> $OUT/r$i.err || { tail -5 $OUT/r$i.err; exit 1; }
   python -c "import json; d=json.load(open('$OUT/r$i.json')); print('$env', d['ms_per_step'], 'ms', 'sat', d['saturate_ms'], 'lat', d['latency_ms'], 'copy', d['copyback_ms'], round(d['value']/1e9,3), 'G/s')"
