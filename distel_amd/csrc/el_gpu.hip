@@ -2418,6 +2418,13 @@ struct el_ctx {
   bool enqueue_base(hipStream_t s);
   void undo_base();  // the next state is not a fresh saturation (el_step, el_add_axioms)
   bool pre_base = false;
+  bool base_fits();  // enqueue_base would run (no buffer has to grow first)
+  // Snapshots of the link / propagation sets holding exactly the base links / propagations,
+  // built once per index and capacity: enqueue_base copies them over the sets (a streaming
+  // copy) instead of clearing the sets and inserting 25 M + 2.6 M keys with random CAS.
+  unsigned long long *lsnap = nullptr, *psnap = nullptr;
+  uint64_t lsnap_cap = 0, psnap_cap = 0;
+  bool no_snap = getenv("EL_NO_SET_SNAPSHOT") != nullptr;  // A/B
   // The logs are indexed by uint32 counters on the device (DCounters): a step whose logs could
   // pass 2^32 entries (count + every candidate new) fails with EL_ENOMEM instead of wrapping.
   void check_u32_room() const {
@@ -2633,7 +2640,7 @@ struct el_ctx {
   // summ_from: the first row whose block summary the reset clears (a releasing read-out
   // cleared the summary of the rows it read, and may still be reading it: the reset must not
   // touch those rows)
-  void reset_device(hipStream_t s, uint32_t clear_from, uint32_t summ_from);
+  void reset_device(hipStream_t s, uint32_t clear_from, uint32_t summ_from, bool sets_follow = false);
   void reset_device(hipStream_t s) { reset_device(s, lo, lo); }
   void rehash_links(uint64_t cap);
   void rehash_acts(uint64_t cap);
@@ -2928,6 +2935,9 @@ void el_ctx::free_state() {
   if (rstream) (void)hipStreamSynchronize(rstream);  // a reset behind a releasing copy-back
   pre_reset = false;
   pre_base = false;
+  dfree(lsnap);
+  dfree(psnap);
+  lsnap_cap = psnap_cap = 0;
   dfree(bits);
   dfree(summ);
   dfree(slog_x);
@@ -3158,7 +3168,7 @@ void el_ctx::alloc_state() {
 
 // The device part of reset_state on stream s: clear the bit matrix (by the fact log), the
 // sets, counters and gapped rows.  Reads only the logs and counts of the finished state.
-void el_ctx::reset_device(hipStream_t stream, uint32_t clear_from, uint32_t summ_from) {
+void el_ctx::reset_device(hipStream_t stream, uint32_t clear_from, uint32_t summ_from, bool sets_follow) {
   FillArgs f{};
   auto add = [&](void* p, uint64_t bytes, uint32_t pattern) { f.seg[f.n++] = FillSeg{p, bytes, pattern}; };
   const uint64_t matrix_bytes = (uint64_t)(hi - lo) * W * sizeof(uint32_t);
@@ -3176,13 +3186,16 @@ void el_ctx::reset_device(hipStream_t stream, uint32_t clear_from, uint32_t summ
     add(summ + (uint64_t)(summ_from - lo) * SB, (uint64_t)(hi - summ_from) * SB, 0u);
   // the link set is by far the largest (G3: 2 GB): the runtime's fill reaches a higher write
   // rate than k_fill's grid-stride loop for it (k_fill: 2.0 ms per G3 classification)
-  if (lhash_cap * sizeof(unsigned long long) >= (64ull << 20))
+  if (sets_follow) {
+    // (enqueue_base copies the base snapshots over the link and propagation sets next)
+  } else if (lhash_cap * sizeof(unsigned long long) >= (64ull << 20)) {
     HIPCHK(hipMemsetAsync(lhash, 0xff, lhash_cap * sizeof(unsigned long long), stream));
-  else
+  } else {
     add(lhash, lhash_cap * sizeof(unsigned long long), ~0u);
+  }
   add(ahash, ahash_cap * sizeof(unsigned long long), ~0u);
   add(has_act, hx.N, 0u);
-  add(phash, phash_cap * sizeof(unsigned long long), ~0u);
+  if (!sets_follow) add(phash, phash_cap * sizeof(unsigned long long), ~0u);
   add(ctr, sizeof(DCounters), 0u);
   add(commit_done, (DONE_SHARDS + 1) * CTR_STRIDE * sizeof(uint32_t), 0u);
   add(ev, EV_WORDS * sizeof(unsigned long long), 0u);
@@ -3898,12 +3911,19 @@ void el_ctx::init_rows(uint32_t a, uint32_t b) {
 // them), and the link set stays without them (link_known: a binary search of exr(X)).  The
 // first superstep then expands the base links, which the second did before; its queues start
 // at what the second got.  The CPU oracle installs the same links (el_oracle.c, base_links).
-bool el_ctx::enqueue_base(hipStream_t s) {
+bool el_ctx::base_fits() {
   const uint64_t nb = hx.exr.a.size(), nbp = hx.bpp.a.size();
   if (nb == 0 || part() || (PR.live && !PR.start0) || (SC.live && !SC.start0)) return false;
   const bool props = nbp && use_props && PP.live && PP.start0;
   if (nb + cl_cap > llog_cap || 2 * (nb + cl_cap) > lhash_cap) return false;
   if (props && (nbp + cp_cap > plog_cap || 2 * (nbp + cp_cap) > phash_cap)) return false;
+  return true;
+}
+
+bool el_ctx::enqueue_base(hipStream_t s) {
+  if (!base_fits()) return false;
+  const uint64_t nb = hx.exr.a.size(), nbp = hx.bpp.a.size();
+  const bool props = nbp && use_props && PP.live && PP.start0;
   const uint32_t N = hx.N, P = hx.P, nc = (uint32_t)hx.exrC.a.size();
   auto items = [](uint64_t n) { return (uint32_t)std::min<uint64_t>(16, std::max<uint64_t>(1, n / (2048 * 256))); };
   auto grid = [&](uint64_t n) {
@@ -3932,12 +3952,32 @@ bool el_ctx::enqueue_base(hipStream_t s) {
                        nullptr, PP.start, PP.val, items(nbp));
     hipLaunchKernelGGL(k_set_u32, dim3(1), dim3(1), 0, s, &ctr->p_log, (uint32_t)nbp);
   }
-  hipLaunchKernelGGL(k_rehash, dim3(grid_for(nb, 2048)), dim3(BLOCK), 0, s, lhash, lhash_cap - 1, llog_x, llog_p,
-                     (uint32_t)nb);
-  if (props)
-    hipLaunchKernelGGL(k_rehash, dim3(grid_for(nbp, 2048)), dim3(BLOCK), 0, s, phash, phash_cap - 1, plog_b, plog_p,
-                       (uint32_t)nbp);
-  HIPCHK(hipGetLastError());
+  if (no_snap) {  // the sets were cleared by the reset: insert
+    hipLaunchKernelGGL(k_rehash, dim3(grid_for(nb, 2048)), dim3(BLOCK), 0, s, lhash, lhash_cap - 1, llog_x, llog_p,
+                       (uint32_t)nb);
+    if (props)
+      hipLaunchKernelGGL(k_rehash, dim3(grid_for(nbp, 2048)), dim3(BLOCK), 0, s, phash, phash_cap - 1, plog_b,
+                         plog_p, (uint32_t)nbp);
+    HIPCHK(hipGetLastError());
+  } else {  // the snapshots (built on first use at this capacity) over the sets
+    auto snap = [&](unsigned long long*& sn, uint64_t& sn_cap, unsigned long long* set, uint64_t cap,
+                    const uint32_t* kx, const uint32_t* kp, uint64_t n) {
+      if (sn_cap != cap) {
+        dfree(sn);
+        sn = dalloc<unsigned long long>(cap);
+        sn_cap = cap;
+        HIPCHK(hipMemsetAsync(sn, 0xff, cap * sizeof(unsigned long long), s));
+        hipLaunchKernelGGL(k_rehash, dim3(grid_for(n, 2048)), dim3(BLOCK), 0, s, sn, cap - 1, kx, kp, (uint32_t)n);
+        HIPCHK(hipGetLastError());
+      }
+      HIPCHK(hipMemcpyAsync(set, sn, cap * sizeof(unsigned long long), hipMemcpyDeviceToDevice, s));
+    };
+    snap(lsnap, lsnap_cap, lhash, lhash_cap, llog_x, llog_p, nb);
+    if (props)
+      snap(psnap, psnap_cap, phash, phash_cap, plog_b, plog_p, nbp);
+    else
+      HIPCHK(hipMemsetAsync(phash, 0xff, phash_cap * sizeof(unsigned long long), s));
+  }
   HIPCHK(hipEventRecord(ev_base[1], s));  // (join_base waits for it; the set is full by then)
   return true;
 }
@@ -4112,6 +4152,9 @@ void el_ctx::join_base() {
 void el_ctx::migrate_state(uint32_t N0, const std::vector<uint32_t>& pmap) {
   const uint64_t N = hx.N, P = hx.P, W0 = W, W1 = ix.W;  // (column_window of the new index)
   sync();
+  dfree(lsnap);  // base-set snapshots of the old index
+  dfree(psnap);
+  lsnap_cap = psnap_cap = 0;
   if (N != N0) {  // wider bit rows, more rows: pitched copy of the old matrix
     uint32_t* nb = dalloc<uint32_t>(N * W1);
     HIPCHK(hipMemsetAsync(nb, 0, N * W1 * sizeof(uint32_t), stream));
@@ -4801,8 +4844,9 @@ int el_copy_result(el_ctx* c, el_result* res) {
       HIPCHK(hipStreamWaitEvent(c->rstream, c->ev_rows[1], 0));
       // rows the S-row sorts (all rows) or the read-out (the caller's rows) cleared as they went
       const uint32_t clear_from = parts[1].readout ? c->uhi() : fuse_clear && parts[1].direct ? c->hi : c->lo;
-      c->reset_device(c->rstream, clear_from, parts[1].readout ? c->uhi() : c->lo);
-      c->pre_base = !c->part() && c->enqueue_base(c->rstream);
+      const bool base = c->base_fits();
+      c->reset_device(c->rstream, clear_from, parts[1].readout ? c->uhi() : c->lo, base && !c->no_snap);
+      c->pre_base = base && c->enqueue_base(c->rstream);
       HIPCHK(hipEventRecord(c->ev_reset, c->rstream));
     }
     // 2. the sorts into the caller's buffers, the device rows by DMA

@@ -481,6 +481,7 @@ __global__ void __launch_bounds__(BLOCK) k_rows_global(const uint64_t* __restric
 // t%32), so each load instruction covers two whole blocks; output slots from popcounts and
 // block scans, in (block, word) order = column order.
 constexpr uint32_t RB = 32;  // listed blocks per round
+constexpr uint32_t NONE32 = 0xffffffffu;
 __global__ void __launch_bounds__(BLOCK) k_rows_readout_sparse(const uint64_t* __restrict__ ptr, uint32_t r0,
                                                                uint32_t r1, uint64_t out0, uint32_t* __restrict__ dst,
                                                                Clear m, bool clear) {
@@ -566,6 +567,76 @@ __global__ void __launch_bounds__(BLOCK) k_rows_readout_sparse(const uint64_t* _
         }
         done += rtot;
         __syncthreads();  // wsum / blk are reused
+      }
+    }
+  }
+}
+
+// k_rows_readout_sparse with one wave per row (no workgroup barriers): the wave lists 64
+// summary bytes at a time with one ballot, takes the marked blocks two per load instruction
+// (lanes 0-31: the lower block's 32 quads, lanes 32-63: the next one's), four loads in flight,
+// and places the set columns by wave scans.  A row of G3 (≈25 marked blocks, ≈266 entries)
+// is a handful of independent loads instead of a chain of block-wide rounds.
+__global__ void __launch_bounds__(BLOCK) k_rows_readout_wave(const uint64_t* __restrict__ ptr, uint32_t r0,
+                                                             uint32_t r1, uint64_t out0, uint32_t* __restrict__ dst,
+                                                             Clear m, bool clear) {
+  const uint32_t lane = __lane_id(), wpb = blockDim.x >> 6;
+  const uint32_t gw = blockIdx.x * wpb + (threadIdx.x >> 6), nw = gridDim.x * wpb;
+  const uint64_t W4 = m.W / 4;
+  for (uint32_t r = r0 + gw; r < r1; r += nw) {  // (wave-uniform)
+    const uint64_t b = ptr[r], len = ptr[r + 1] - b;
+    if (len == 0) continue;
+    uint4* __restrict__ row = reinterpret_cast<uint4*>(m.bits + (uint64_t)(r + m.lo) * m.W);
+    uint8_t* __restrict__ sr = m.summ + (uint64_t)(r + m.lo) * m.SB;
+    uint32_t* __restrict__ out = dst + (b - out0);
+    uint64_t done = 0;
+    for (uint32_t k0 = 0; k0 < m.SB && done < len; k0 += 64) {
+      const bool nz = k0 + lane < m.SB && sr[k0 + lane] != 0;
+      if (clear && nz) sr[k0 + lane] = 0;  // (the reset leaves the read-out's rows to it)
+      unsigned long long bal = __ballot(nz);
+      while (bal && done < len) {
+        uint4 v[4];
+        uint64_t q[4];
+        uint32_t c[4];
+#pragma unroll
+        for (uint32_t i = 0; i < 4; ++i) {  // two marked blocks per load instruction
+          uint32_t blkA = NONE32, blkB = NONE32;
+          if (bal) {
+            blkA = k0 + (uint32_t)__ffsll((long long)bal) - 1;
+            bal &= bal - 1;
+          }
+          if (bal) {
+            blkB = k0 + (uint32_t)__ffsll((long long)bal) - 1;
+            bal &= bal - 1;
+          }
+          const uint32_t blk = lane < 32 ? blkA : blkB;
+          q[i] = blk != NONE32 ? (uint64_t)blk * 32 + (lane & 31u) : W4;
+          v[i] = q[i] < W4 ? row[q[i]] : make_uint4(0u, 0u, 0u, 0u);
+        }
+#pragma unroll
+        for (uint32_t i = 0; i < 4; ++i) {
+          c[i] = __popc(v[i].x) + __popc(v[i].y) + __popc(v[i].z) + __popc(v[i].w);
+          uint32_t inc = c[i];
+#pragma unroll
+          for (uint32_t o = 1; o < 64; o <<= 1) {
+            const uint32_t y = __shfl_up(inc, o);
+            if (lane >= o) inc += y;
+          }
+          uint32_t* o = out + done + inc - c[i];
+          const uint32_t wd[4] = {v[i].x, v[i].y, v[i].z, v[i].w};
+#pragma unroll
+          for (uint32_t jj = 0; jj < 4; ++jj) {
+            uint32_t word = wd[jj];
+            const uint32_t cb = (uint32_t)((q[i] * 4 + jj) * 32);
+            while (word) {
+              const uint32_t col = cb + (uint32_t)__ffs(word) - 1;
+              *o++ = col < 2u ? col : col + m.c_lo - 2u;  // column -> concept
+              word &= word - 1;
+            }
+          }
+          if (clear && c[i]) row[q[i]] = make_uint4(0u, 0u, 0u, 0u);
+          done += __shfl(inc, 63);
+        }
       }
     }
   }
@@ -659,7 +730,11 @@ void readout(hipStream_t s, const uint64_t* ptr, uint32_t r0, uint32_t r1, uint6
     const char* e = getenv("EL_READOUT_BLOCKS");
     return e ? (uint32_t)std::max(1l, strtol(e, nullptr, 10)) : 1024u;
   }();
-  if (m.summ)
+  static const bool per_wg = getenv("EL_READOUT_WG") != nullptr;  // A/B: one workgroup per row
+  if (m.summ && !per_wg)
+    hipLaunchKernelGGL(k_rows_readout_wave, dim3(std::min<uint32_t>((r1 - r0 + 3) / 4, maxb)), dim3(BLOCK), 0, s, ptr,
+                       r0, r1, out0, dst, m, clear);
+  else if (m.summ)
     hipLaunchKernelGGL(k_rows_readout_sparse, dim3(std::min<uint32_t>(r1 - r0, maxb)), dim3(BLOCK), 0, s, ptr, r0, r1,
                        out0, dst, m, clear);
   else
