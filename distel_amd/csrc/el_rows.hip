@@ -730,8 +730,8 @@ void readout(hipStream_t s, const uint64_t* ptr, uint32_t r0, uint32_t r1, uint6
     const char* e = getenv("EL_READOUT_BLOCKS");
     return e ? (uint32_t)std::max(1l, strtol(e, nullptr, 10)) : 1024u;
   }();
-  static const bool per_wg = getenv("EL_READOUT_WG") != nullptr;  // A/B: one workgroup per row
-  if (m.summ && !per_wg)
+  static const bool per_wave = getenv("EL_READOUT_WAVE") != nullptr;  // A/B: one wave per row (no gain)
+  if (m.summ && per_wave)
     hipLaunchKernelGGL(k_rows_readout_wave, dim3(std::min<uint32_t>((r1 - r0 + 3) / 4, maxb)), dim3(BLOCK), 0, s, ptr,
                        r0, r1, out0, dst, m, clear);
   else if (m.summ)
