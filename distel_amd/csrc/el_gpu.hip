@@ -482,6 +482,18 @@ __device__ __forceinline__ uint32_t pair_lookup(const DIndex& ix, uint32_t r, ui
   return NONE;
 }
 
+// pair_lookup over a pair range [b, e) of the filler already read (same events)
+__device__ __forceinline__ uint32_t pair_scan(const DIndex& ix, uint32_t r, uint32_t b, uint32_t e, Ev& ev) {
+  ev.v[EL_EV_ROW]++;
+  for (uint32_t p = b; p < e; ++p) {
+    ev.v[EL_EV_ENT]++;
+    uint32_t rr = ix.pair_role[p];
+    if (rr == r) return p;
+    if (rr > r) return NONE;
+  }
+  return NONE;
+}
+
 // LDS staging of the commit roles (new facts / links of a block round)
 constexpr uint32_t QS_CAP = 2048;  // (a block flushes ~QS_CAP/2 new facts per log atomic)
 constexpr uint32_t QL_CAP = 2048;
@@ -993,17 +1005,32 @@ __device__ void expand_s(const DIndex& ix, const DState& st, BlockQ& q, uint32_t
     {  // A ∈ S(Y=X) new, ∃r.A ⊑ B  =>  propagation ((r, Y), B)
        // (Type3_1AxiomProcessorBase.java:208-234 writes "Yr" -> B)
       // (an init fact's own propagations are the base propagations, already in place)
-      const bool on = star && (mask & M_R4Y) && !(ix.base && f == 2);
+      bool on = star && (mask & M_R4Y) && !(ix.base && f == 2);
       if (on) ev.v[EL_EV_ROW]++;
+      // Y's pair range (the roles r with (r, Y) a link target), read once per trigger; when Y
+      // is no link target at all, no entry can find a pair: the row is not walked, and its
+      // events — two entries and one pair-row lookup per entry, as the walk counts them — are
+      // added at once
+      uint32_t fpb = 0, fpe = 0;
+      if (on && m1.w > m0.w) {
+        fpb = ix.fp_ptr[X];
+        fpe = ix.fp_ptr[X + 1];
+        if (fpb == fpe) {
+          ev.v[EL_EV_ENT] += 2 * (m1.w - m0.w);
+          ev.v[EL_EV_ROW] += m1.w - m0.w;
+          on = false;
+        }
+      }
       wave_rows(on ? m0.w : 0u, on ? m1.w : 0u, [&](bool v, uint32_t own, uint32_t j) {
         const uint32_t Yo = __shfl(X, (int)own);
+        const uint32_t pb0 = __shfl(fpb, (int)own), pe0 = __shfl(fpe, (int)own);
         uint32_t pid = NONE, B = 0, pb = 0, pl = 0;
         bool fresh = false;
         if (v) {
           const uint32_t r = ix.exl_r[j];
           B = ix.exl_b[j];
           ev.v[EL_EV_ENT] += 2;
-          pid = pair_lookup(ix, r, Yo, ev);
+          pid = pair_scan(ix, r, pb0, pe0, ev);
           if (pid != NONE) {
             fresh = !prop_known(ix, st, pid, B, mask & M_PEMPTY, ev);
             if (fresh && (mask & M_R4D)) {  // fused mode: B reaches today's predecessors now
