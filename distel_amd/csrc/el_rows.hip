@@ -285,15 +285,78 @@ __device__ __forceinline__ void sort_row(const uint32_t* __restrict__ src, uint3
   }
 }
 
+// One row of 65..256 entries per wave, in registers only: lane l holds the elements
+// e = 64 i + l, i < E (E = 2 up to 128 entries, else 4); stages with j >= 64 compare a lane's
+// own registers (no LDS, no barriers), the others shuffle.
+template <uint32_t E>
+__device__ __forceinline__ void sort_row_wave(const uint32_t* __restrict__ src, uint32_t* __restrict__ dst,
+                                              uint32_t len, const Clear& cl, uint32_t r) {
+  const uint32_t lane = __lane_id();
+  constexpr uint32_t P = 64 * E;
+  uint32_t v[E];
+#pragma unroll
+  for (uint32_t i = 0; i < E; ++i) {
+    const uint32_t e = 64 * i + lane;
+    v[i] = e < len ? src[e] : NONE;
+  }
+#pragma unroll
+  for (uint32_t k = 2; k <= P; k <<= 1) {
+#pragma unroll
+    for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+      if (j >= 64) {
+        const uint32_t d = j / 64;
+#pragma unroll
+        for (uint32_t i = 0; i < E; ++i) {
+          if (i & d) continue;  // (the pair (i, i + d): the lower element's lane does both)
+          const uint32_t e = 64 * i + lane;
+          const bool up = (e & k) == 0;
+          const uint32_t a = v[i], c = v[i + d];
+          v[i] = up ? min(a, c) : max(a, c);
+          v[i + d] = up ? max(a, c) : min(a, c);
+        }
+      } else {
+#pragma unroll
+        for (uint32_t i = 0; i < E; ++i) v[i] = bitonic_xor(v[i], 64 * i + lane, k, j);
+      }
+    }
+  }
+#pragma unroll
+  for (uint32_t i = 0; i < E; ++i) {
+    const uint32_t e = 64 * i + lane;
+    if (e < len) {
+      dst[e] = v[i];
+      cl.bit(r, v[i]);
+    }
+  }
+}
+
+// The listed rows of 65..256 entries, one per wave (k_rows_lds takes the longer ones).
+__global__ void __launch_bounds__(BLOCK) k_rows_wave(const uint64_t* __restrict__ ptr, const uint32_t* __restrict__ tmp,
+                                                     uint32_t* __restrict__ dst, const uint32_t* __restrict__ lists,
+                                                     const uint32_t* __restrict__ nlist, Clear cl) {
+  const uint32_t nrows = *nlist;
+  const uint32_t waves = gridDim.x * (BLOCK / 64);
+  for (uint32_t q = blockIdx.x * (BLOCK / 64) + (threadIdx.x >> 6); q < nrows; q += waves) {
+    const uint32_t r = lists[q];
+    const uint64_t b = ptr[r];
+    const uint32_t len = (uint32_t)(ptr[r + 1] - b);
+    if (len <= 128)
+      sort_row_wave<2>(tmp + b, dst + b, len, cl, r);
+    else if (len <= 256)
+      sort_row_wave<4>(tmp + b, dst + b, len, cl, r);
+  }
+}
+
 __global__ void __launch_bounds__(BLOCK) k_rows_lds(const uint64_t* __restrict__ ptr, const uint32_t* __restrict__ tmp,
                                                     uint32_t* __restrict__ dst, const uint32_t* __restrict__ lists,
-                                                    const uint32_t* __restrict__ nlist, Clear cl) {
+                                                    const uint32_t* __restrict__ nlist, Clear cl, bool waves_took_256) {
   __shared__ uint32_t s[LDS_MAX];
   const uint32_t nrows = *nlist;
   for (uint32_t q = blockIdx.x; q < nrows; q += gridDim.x) {
     const uint32_t r = lists[q];
     const uint64_t b = ptr[r];
     const uint32_t len = (uint32_t)(ptr[r + 1] - b);
+    if (len <= 256 && waves_took_256) continue;  // (block-uniform: k_rows_wave sorted it)
     if (len <= 256)
       sort_row<1>(tmp + b, dst + b, len, s, cl, r);
     else if (len <= 512)
@@ -690,7 +753,12 @@ void build_sort(hipStream_t s, Scratch& sc, const uint64_t* ptr, uint32_t* dst, 
   hipLaunchKernelGGL(k_rows_small, dim3(grid(((uint64_t)R + 63) / 64 * 64, 2048)), dim3(BLOCK), 0, s, ptr, R, sc.tmp,
                      dst, cl);
   RCHK(hipGetLastError());
-  hipLaunchKernelGGL(k_rows_lds, dim3(1024), dim3(BLOCK), 0, s, ptr, sc.tmp, dst, sc.lists, sc.nlist, cl);
+  static const bool no_wave = getenv("EL_ROWS_NO_WAVE") != nullptr;  // A/B: rows <= 256 by the workgroup sort
+  if (!no_wave) {
+    hipLaunchKernelGGL(k_rows_wave, dim3(1024), dim3(BLOCK), 0, s, ptr, sc.tmp, dst, sc.lists, sc.nlist, cl);
+    RCHK(hipGetLastError());
+  }
+  hipLaunchKernelGGL(k_rows_lds, dim3(1024), dim3(BLOCK), 0, s, ptr, sc.tmp, dst, sc.lists, sc.nlist, cl, !no_wave);
   RCHK(hipGetLastError());
   if (!sc.bits) {
     hipLaunchKernelGGL(k_rows_global, dim3(512), dim3(BLOCK), 0, s, ptr, sc.tmp, dst, sc.lists, sc.nlist, R);
