@@ -20,32 +20,51 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, q):
+def _worker(rank, world, port, q, pipelined):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
                       WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
     sys.path[:0] = [ROOT, os.path.join(ROOT, "oracle")]
     import oracle
+    from concurrent.futures import ThreadPoolExecutor
     from distel_amd import dist as D
     from distel_amd import generators
     rk = D.init_from_env(prefer_nccl=False)
     ax = generators.workload("g1", scale=0.02)
+    pool = ThreadPoolExecutor(max_workers=1)
+    pending, landed = [], []
+
+    def copy_back(o):  # stands in for an EL_RESULT_ASYNC copy-back on a helper thread
+        landed.append(len(o.facts()[0]))
+        o.close()
 
     def classify():
         o = oracle.saturate(ax, 0)
         st = o.stats()
-        o.close()
+        if pipelined:  # bench.py's two-in-flight schedule: the copy-back lands later
+            pending.append(pool.submit(copy_back, o))
+        else:
+            o.close()
         return st
-    t_max, derived, st = D.run_weak(rk, classify, steps=2, warmup=1)
+
+    def drain():
+        for f in pending:
+            f.result()
+        pending.clear()
+    t_max, derived, st = D.run_weak(rk, classify, steps=2, warmup=1, drain=drain if pipelined else None)
+    # every classification's copy-back landed inside run_weak (warm-up and timed steps)
+    assert not pipelined or (not pending and len(landed) == 3 and set(landed) == {st["s_facts"]})
     q.put((rank, t_max, derived, st["derived"]))
+    pool.shutdown()
     D.shutdown(rk)
 
 
-def test_weak_scaling_two_ranks_gloo():
+@pytest.mark.parametrize("pipelined", [False, True])
+def test_weak_scaling_two_ranks_gloo(pipelined):
     world = 2
     port = _free_port()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q, pipelined)) for r in range(world)]
     for p in procs:
         p.start()
     res = [q.get(timeout=300) for _ in range(world)]
