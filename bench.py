@@ -311,7 +311,10 @@ def main():
                        "parallelism": (f"{world} disjoint copies, one per GPU (OntologyMultiplier ×{world})"
                                        if args.partition == "copies" else
                                        f"row partition of the ×{world} ontology over {world} GPUs, RCCL delta "
-                                       f"all-gather per superstep")},
+                                       f"all-gather per superstep"),
+                       "schedule": ("two classifications in flight per GPU: one's result copy-back "
+                                    "(EL_RESULT_ASYNC) overlaps the other's saturation; latency_ms = one alone"
+                                    if len(engines) == 2 else "one classification at a time")},
             "classification_wall_s": round(ms_per_step / 1e3, 6),
             "derived_axioms": derived_all,
             "s_facts_per_rank": st["s_facts"],
