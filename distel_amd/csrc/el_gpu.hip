@@ -50,6 +50,7 @@
 #include <string>
 #include <vector>
 
+#include "el_closure.h"
 #include "el_gpu.h"
 #include "el_index.h"
 #include "el_rows.h"
@@ -109,14 +110,16 @@ struct DIndex {
   uint32_t N, R, P;
   uint64_t W;  // uint32 words per bit row
   const uint8_t* kind;
-  const uint32_t *told_ptr, *told_b;
+  // the rows over the told closure (el_closure.h, rebuilt by every el_init): told*(A), exr*(A),
+  // exl*(A) at [begin, end) of meta below
+  const uint32_t* told_b;
   const uint32_t *cidx_ptr, *cidx_c;
   // per cidx entry j of A: a binary conjunction {A, p} ⊑ B as p | (p sorts before A) << 31 and B
   // (cidx_p = NONE: another arity, walked through conj_ptr / conj_ops)
   const uint32_t *cidx_p, *cidx_b;
   const uint32_t *conj_ptr, *conj_ops, *conj_b;
-  const uint32_t *exr_ptr, *exr_pid;
-  const uint32_t *exl_ptr, *exl_r, *exl_b;
+  const uint32_t* exr_pid;
+  const uint32_t *exl_r, *exl_b;
   const uint32_t *fp_ptr, *pair_role, *pair_y;
   const uint32_t *psup_ptr, *psup_pid;
   const uint32_t *chf_ptr, *chf_s, *chf_t;
@@ -124,9 +127,8 @@ struct DIndex {
   const uint32_t *dom_ptr, *dom_c;
   const uint32_t *rng_ptr, *rng_c;
   const uint8_t* role_has_exl;
-  const uint4* meta;  // per concept A: {told_ptr, cidx_ptr, exr_ptr, exl_ptr}[A] — one 32 B span for A, A+1
-  const uint32_t* init_off;  // N + 1: start of concept X's init facts in an init-ordered log
-  const uint32_t* init_row64;  // init_off[N] / 64 + 1: the row holding init slot 64·c
+  // per concept A, 32 B: meta[2A] = row begins {told*, cidx, exr*, exl*}, meta[2A + 1] = ends
+  const uint4* meta;
   uint32_t has_range;
   uint32_t has_bot;  // some axiom concludes ⊥ (or ∃r.⊥): else ⊥ ∈ S(Y) only for Y = ⊥, no link reaches ⊥
   // row partition (el_config.exchange != NONE): this context owns rows [lo, hi)
@@ -137,7 +139,8 @@ struct DIndex {
   uint32_t part;               // 1 = partitioned protocol (oracle/partition_model.py)
   uint32_t base;               // 1 = the base links {(X, p) : p ∈ exr(X)} and base propagations
                                // are in their logs and rows but not in their sets (install_base)
-  const uint32_t *bpp_ptr, *bpp_b;  // base propagations: pid -> B, ascending
+  // base propagations of pid: the propagation log's [bpp_s[pid], bpp_e[pid]) (B ascending)
+  const uint32_t *bpp_s, *bpp_e;
   const uint8_t* role_chs;     // r -> r is the second role of some chain (its links are exchanged)
 };
 
@@ -418,13 +421,13 @@ __device__ __forceinline__ bool hash_insert(unsigned long long* t, unsigned long
 }
 
 // Base links: the links every init fact X ∈ S(X) implies by CR3 over its told closure,
-// {(X, p) : p ∈ exr(X)} (G3: 25 M of 33 M links).  el_saturate writes them into the link log
+// {(X, p) : p ∈ exr*(X)} (G3: 25 M of 33 M links).  el_saturate writes them into the link log
 // and the predecessor / successor rows before the first superstep, with coalesced stores,
 // instead of deriving them as 25 M candidates that the commit would hash one by one; the
-// set of them is exr itself, so membership is a binary search of the row exr(X) (sorted).
+// set of them is exr* itself, so membership is a binary search of the row exr*(X) (sorted).
 __device__ __forceinline__ bool base_has(const DIndex& ix, uint32_t x, uint32_t pid, Ev& ev) {
   ev.v[EL_EV_ROW]++;
-  uint32_t lo = ix.exr_ptr[x], hi = ix.exr_ptr[x + 1];
+  uint32_t lo = ix.meta[2 * x].z, hi = ix.meta[2 * x + 1].z;
   while (lo < hi) {
     const uint32_t mid = (lo + hi) >> 1;
     ev.v[EL_EV_ENT]++;
@@ -452,11 +455,11 @@ __device__ __forceinline__ bool prop_known(const DIndex& ix, const DState& st, u
                                            bool pempty, Ev& ev) {
   if (ix.base) {
     ev.v[EL_EV_ROW]++;
-    uint32_t lo = ix.bpp_ptr[pid], hi = ix.bpp_ptr[pid + 1];
+    uint32_t lo = ix.bpp_s[pid], hi = ix.bpp_e[pid];
     while (lo < hi) {
       const uint32_t mid = (lo + hi) >> 1;
       ev.v[EL_EV_ENT]++;
-      const uint32_t v = ix.bpp_b[mid];
+      const uint32_t v = st.plog_b[mid];
       if (v == b) return true;
       if (v < b)
         lo = mid + 1;
@@ -783,78 +786,7 @@ __global__ void k_fill(FillArgs f) {
   }
 }
 
-// S(X) = {X, ⊤} for classes and individuals, {X} for ⊤, ⊥ and datatypes
-// (AxiomLoader.java:1237-1245 classes, :1281-1289 individuals), together with the told
-// closure of X — exactly what CR1 derives from the init fact X ∈ S(X) in the first
-// superstep — written without candidates: the init facts of rows [lo, hi) are the
-// contiguous log range [init_off[lo], init_off[hi]) (host prefix sums), so each thread takes
-// one log slot k, finds its row from init_row64 plus a short scan of init_off and its fact by the offset
-// inside the row, and a wave's log stores are coalesced.  Row X's facts: X (closure flag:
-// its closure is written right here), ⊤ for classes and individuals, then told*(X) (flagged)
-// without a second ⊤.
-__global__ void k_init(DIndex ix, DState st, uint32_t lo, uint32_t hi, uint32_t base, uint32_t set_bits) {
-  Ev ev;
-  const uint32_t o0 = ix.init_off[lo], n = ix.init_off[hi] - o0;
-  const uint32_t stride = gridDim.x * blockDim.x;
-  for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < n; k += stride) {
-    // the row: largest x < hi with init_off[x] <= o0 + k, from the row of the slot's 64-slot
-    // chunk (host table) by a short forward scan whose loads the wave shares
-    const uint32_t K = o0 + k;
-    uint32_t a = max(lo, ix.init_row64[K >> 6]);
-    while (a + 1 < hi && ix.init_off[a + 1] <= K) ++a;
-    const uint32_t x = a, j = k - (ix.init_off[x] - o0);
-    const bool two = x != EL_TOP && x != EL_BOTTOM && ix.kind[x] != EL_KIND_DATATYPE;
-    const uint32_t t0 = ix.told_ptr[x], t1 = ix.told_ptr[x + 1];
-    // ⊤ (id 1) sorts first or right after ⊥ in told*(X): for classes it is already there
-    const uint32_t ptop = !two ? NONE
-                          : (t0 < t1 && ix.told_b[t0] == EL_TOP)         ? 0u
-                          : (t0 + 1 < t1 && ix.told_b[t0 + 1] == EL_TOP) ? 1u
-                                                                         : NONE;
-    uint32_t v;
-    uint8_t f = 1;
-    if (j == 0) {
-      v = x;
-      f = 2;  // closure written here; its links / propagations come from the first superstep
-      ev.v[EL_EV_ENT] += 1 + (ptop != NONE);  // the row, and the skipped closure entry
-    } else if (two && j == 1) {
-      v = EL_TOP;
-      f = 0;
-    } else {
-      uint32_t c = j - 1 - (two ? 1u : 0u);
-      if (c >= ptop) ++c;
-      v = ix.told_b[t0 + c];
-      ev.v[EL_EV_ENT]++;
-    }
-    const uint32_t c = col_of(ix, v);  // (the told closure lies inside the window)
-    if (set_bits && c != NONE) {  // (else k_init_bits writes the rows' init words)
-      __hip_atomic_fetch_or(st.bits + (uint64_t)x * ix.W + (c >> 5), 1u << (c & 31u), __ATOMIC_RELAXED,
-                            __HIP_MEMORY_SCOPE_AGENT);
-      if (st.summ) st.summ[(uint64_t)x * st.SB + (c >> 12)] = 1;
-    }
-    st.slog_x[base + k] = x;
-    st.slog_a[base + k] = v;
-    st.slog_f[base + k] = f;
-    ev.v[EL_EV_RMW]++;
-    ev.v[EL_EV_EMIT]++;
-  }
-  ev_flush(st.ev, EL_K_INIT, ev);
-}
-
 __global__ void k_set_u32(uint32_t* p, uint32_t v) { *p = v; }
-
-// The init facts' bits as whole words: word (row x, w) of the owned rows gets its mask of
-// {x, ⊤} ∪ told*(x) (host-merged at el_load, one entry per distinct word), so the words are
-// written with plain stores — the matrix is zero at el_init and no word is listed twice —
-// instead of one returning atomic per init fact (G3: 25 M, 0.9 ms).
-__global__ void k_init_bits(uint32_t* __restrict__ bits, uint64_t W, const uint32_t* __restrict__ row,
-                            const uint32_t* __restrict__ word, const uint32_t* __restrict__ mask, uint32_t n,
-                            uint8_t* __restrict__ summ, uint32_t SB) {
-  const uint32_t stride = gridDim.x * blockDim.x;
-  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
-    bits[(uint64_t)row[i] * W + word[i]] = mask[i];
-    if (summ) summ[(uint64_t)row[i] * SB + (word[i] >> 7)] = 1;
-  }
-}
 
 // The block summary of whole rows from the matrix (after an increment re-laid the matrix out).
 __global__ void k_summ_build(const uint32_t* __restrict__ bits, uint64_t W, uint64_t words, uint8_t* __restrict__ summ,
@@ -914,8 +846,8 @@ __device__ void expand_s(const DIndex& ix, const DState& st, BlockQ& q, uint32_t
       A = st.slog_a[i];
       f = st.slog_f[i];
       ev.v[EL_EV_TRIG]++;
-      m0 = ix.meta[A];  // the four CSR rows of A at once
-      m1 = ix.meta[A + 1];
+      m0 = ix.meta[2 * A];  // the four rows of A at once: begins, ends
+      m1 = ix.meta[2 * A + 1];
     }
     // A ∈ S(X), A ⊑* B  =>  B ∈ S(X), over the told closure at once; a fact that came out
     // of a closure is not re-expanded (its closure is a subset of the one that produced it)
@@ -1934,16 +1866,8 @@ __global__ void k_gap_init(uint32_t* start, uint32_t* len, uint32_t rows, const 
   }
 }
 
-// ---- base links (el_ctx::install_base): CSR rows written out whole, one entry per lane.
-// A block takes 4096 consecutive entries a round; two lanes find the rows of its first and last
-// entry (binary searches of ptr: at 256 entries a round these latency chains were most of the
-// 0.3 ms per 25 M entries), then each entry's row is searched within that span only — a hub
-// row (a filler with 10^5 predecessors) spreads over many blocks instead of one wave.
-// out_row != null: flat (row, value) pairs at the entry's index (the link log from exr);
-// else: the entry at its row's slot of a gapped CSR just laid out (predecessor rows from exrT,
-// successor rows from exrC), whose lengths k_gap_len sets.
+// the largest r in [lo, hi] with ptr[r] <= j (ptr[lo] <= j)
 __device__ __forceinline__ uint32_t csr_row_of(const uint32_t* __restrict__ ptr, uint32_t lo, uint32_t hi, uint32_t j) {
-  // the largest r in [lo, hi] with ptr[r] <= j (ptr[lo] <= j)
   while (lo < hi) {
     const uint32_t mid = (lo + hi + 1) >> 1;
     if (ptr[mid] <= j)
@@ -1953,41 +1877,12 @@ __device__ __forceinline__ uint32_t csr_row_of(const uint32_t* __restrict__ ptr,
   }
   return lo;
 }
-// items: entries per lane and round (1..16, from the entry count: small builds keep many blocks)
-__global__ void __launch_bounds__(256) k_csr_scatter(const uint32_t* __restrict__ ptr, const uint32_t* __restrict__ a,
-                                                     uint32_t rows, uint32_t n, uint32_t* __restrict__ out_row,
-                                                     uint32_t* __restrict__ out_val, const uint32_t* __restrict__ start,
-                                                     uint32_t* __restrict__ val, uint32_t items) {
-  __shared__ uint32_t span[2];
-  const uint32_t TILE = 256 * items;
-  for (uint32_t base = blockIdx.x * TILE; base < n; base += gridDim.x * TILE) {
-    // the rows of the tile's first and last entry (one search over all rows per 4096 entries)
-    if (threadIdx.x < 2) span[threadIdx.x] = csr_row_of(ptr, 0, rows - 1, threadIdx.x ? min(base + TILE - 1, n - 1) : base);
-    __syncthreads();
-    const uint32_t s0 = span[0], s1 = span[1];
-    for (uint32_t k = 0; k < items; ++k) {  // coalesced: consecutive lanes, consecutive entries
-      const uint32_t j = base + k * 256 + threadIdx.x;
-      if (j < n) {
-        const uint32_t r = csr_row_of(ptr, s0, s1, j), v = a[j];
-        if (out_row) {
-          out_row[j] = r;
-          out_val[j] = v;
-        } else {
-          val[start[r] + (j - ptr[r])] = v;
-        }
-      }
-    }
-    __syncthreads();
-  }
-}
-__global__ void k_gap_len(const uint32_t* __restrict__ ptr, uint32_t rows, uint32_t* __restrict__ len) {
-  for (uint32_t r = blockIdx.x * blockDim.x + threadIdx.x; r < rows; r += gridDim.x * blockDim.x) len[r] = ptr[r + 1] - ptr[r];
-}
 
 // Re-layout move, one in-place entry per lane: entry e of the dense order (rows ascending,
 // pre = exclusive scan of the rows' in-place counts) goes from its old slot to its new one.
-// A block takes 256·items entries a round and finds their rows by the same span search as
-// k_csr_scatter; a row-per-lane move (64 rows per wave) ran at 0.65 TB/s
+// A block takes 256·items entries a round; two lanes find the rows of its first and last entry,
+// then each entry's row is searched within that span only (a hub row spreads over many blocks);
+// a row-per-lane move (64 rows per wave) ran at 0.65 TB/s
 // (G3: 28.6 M predecessors, 0.35 ms per re-layout).
 __global__ void __launch_bounds__(256) k_gap_move_e(const uint32_t* __restrict__ pre, uint32_t rows, uint32_t n,
                                                     const uint32_t* __restrict__ s_old,
@@ -2137,27 +2032,21 @@ struct GapCsr {
   uint32_t* ovq = nullptr;
   uint64_t ovq_cap = 0;
   bool live = false;  // maintained for this ontology (it has readers)
-  uint32_t* start0 = nullptr;  // initial row starts when presized (else r · gap_cap(0))
-  uint64_t total0 = 0;         // slots of the initial layout
-  // cap0: initial row capacities (the first superstep's expected appends, el_ctx::alloc_state),
-  // or null for gap_cap(0) per row
-  void alloc(uint32_t n, uint64_t ovq_entries, const std::vector<uint32_t>* cap0 = nullptr) {
+  // The classification's initial layout (el_init: a device scan of the row capacities the
+  // first supersteps ask for — the base links and their CR5 lifts; el_ctx::closure_state), or
+  // r · gap_cap(0) when `laid` is false.  undo / reset restore it (k_gap_init).
+  uint32_t* start0 = nullptr;
+  bool laid = false;
+  uint64_t total0 = 0;  // slots of the initial layout
+  void alloc(uint32_t n, uint64_t ovq_entries) {
     rows = n;
     start = dalloc<uint32_t>(n + 1);
     start2 = dalloc<uint32_t>(n + 1);
     pre = dalloc<uint32_t>(n + 1);
     len = dalloc<uint32_t>(n);
+    start0 = dalloc<uint32_t>(n + 1);
+    laid = false;
     total0 = (uint64_t)gap_cap(0) * n;
-    if (cap0) {
-      std::vector<uint32_t> s0(n + 1, 0);
-      uint64_t t = 0;
-      for (uint32_t r = 0; r < n; ++r) s0[r] = (uint32_t)t, t += gap_cap((*cap0)[r]);
-      if (t <= 0xffffffffull) {
-        s0[n] = (uint32_t)t;
-        start0 = dupload(s0);
-        total0 = t;
-      }
-    }
     val_cap = total0;
     val = dalloc<uint32_t>(val_cap);
     live = true;
@@ -2179,7 +2068,7 @@ struct GapCsr {
     dfree(ovq);
     dfree(start0);
     val_cap = val2_cap = ovq_cap = total0 = 0;
-    live = false;
+    live = laid = false;
   }
   DGap view(uint32_t* ov_count) const {
     return DGap{start, len, val, ovq, (uint32_t)ovq_cap, ov_count};
@@ -2402,8 +2291,6 @@ struct el_ctx {
   bool s_dma = getenv("EL_S_DMA") != nullptr;                // A/B: small S results by device sort + DMA
   uint64_t readout_chunk = (uint64_t)env_u32("EL_READOUT_CHUNK_MB", 32) << 18;  // entries per read-out DMA
   hipEvent_t ev_rows[2] = {nullptr, nullptr};
-  // base links by predecessor (exrT: pid -> X) and by successor (exrC: X -> chain-second pid)
-  const uint32_t *exrT_ptr = nullptr, *exrT_x = nullptr, *exrC_ptr = nullptr, *exrC_p = nullptr;
   GapCsr PR, SC, PP;   // predecessors per pid, successors per X, propagations per pid
   uint32_t* pin_word = nullptr;  // pinned scratch for the rare synchronous readbacks
   bool need_pred = true;      // predecessor CSR has readers (CR4, ⊥, CR6)
@@ -2438,20 +2325,38 @@ struct el_ctx {
   uint64_t p_base = 0;  // base propagations at the head of the propagation log
   bool fresh = false;   // el_init ran and no superstep since: el_saturate installs the base links
   void install_base();
-  // Base links / propagations enqueued on stream s for the NEXT classification, behind the
-  // reset of a releasing copy-back (el_copy_result): the scatters and the set fills then run
-  // beside the transfer instead of before / beside the first superstep.  Returns false (nothing
-  // enqueued) when a buffer would have to grow first.  pre_base: enqueued, not yet accounted.
-  bool enqueue_base(hipStream_t s);
-  void undo_base();  // the next state is not a fresh saturation (el_step, el_add_axioms)
-  bool pre_base = false;
-  bool base_fits();  // enqueue_base would run (no buffer has to grow first)
-  // Snapshots of the link / propagation sets holding exactly the base links / propagations,
-  // built once per index and capacity: enqueue_base copies them over the sets (a streaming
-  // copy) instead of clearing the sets and inserting 25 M + 2.6 M keys with random CAS.
-  unsigned long long *lsnap = nullptr, *psnap = nullptr;
-  uint64_t lsnap_cap = 0, psnap_cap = 0;
-  bool no_snap = getenv("EL_NO_SET_SNAPSHOT") != nullptr;  // A/B
+
+  // ---- the told closure and what it derives (el_closure.h), rebuilt by every el_init
+  elcl::Axioms cax{};  // the told axiom rows on the device (index buffers)
+  elcl::Out cl{};      // rows told*, exr*, exl*, meta, per-concept statistics, working storage
+  struct ClHost {      // pinned readback of a build: counters, the next level's flag, meta of ⊤
+    elcl::Ctr ctr;
+    uint32_t flag, pad[3];
+    uint4 top[2];
+  };
+  ClHost* clh = nullptr;
+  elcl::Ctr clt{};          // the last build's totals
+  uint32_t* cpos[3] = {};   // exclusive scans over the rows [a, b) of the last build: init facts,
+                            // base links, base propagations (b - a + 1 entries)
+  void* cscan_tmp = nullptr;
+  size_t cscan_bytes = 0;
+  void* csort_tmp = nullptr;
+  size_t csort_bytes = 0;
+  uint32_t *sk = nullptr, *sv = nullptr;  // the base links by pid (radix sort): predecessor rows
+  uint64_t sk_cap = 0;
+  uint32_t *pr_first = nullptr, *pr_last = nullptr;  // pid -> its run in sk
+  uint32_t *bpp_s = nullptr, *bpp_e = nullptr;       // pid -> its base propagations in the log
+  uint32_t *cap_pr = nullptr, *cap_pp = nullptr;     // first-superstep row capacities per pid
+  uint32_t key_bits = 1;     // bits of a pid (radix sort)
+  uint32_t level_hint = 32;  // Kahn levels launched before the first readback (grows to the depth seen)
+  uint64_t nb = 0, nbp = 0, nc = 0;  // base links, base propagations, chain-second base links
+  void alloc_closure();
+  void free_closure();
+  void set_closure_ix();
+  void closure_grow();
+  void closure_tail(uint32_t a, uint32_t b, uint32_t L);
+  void closure_rows(uint32_t a, uint32_t b);
+  void closure_state();
   // The logs are indexed by uint32 counters on the device (DCounters): a step whose logs could
   // pass 2^32 entries (count + every candidate new) fails with EL_ENOMEM instead of wrapping.
   void check_u32_room() const {
@@ -2667,7 +2572,7 @@ struct el_ctx {
   // summ_from: the first row whose block summary the reset clears (a releasing read-out
   // cleared the summary of the rows it read, and may still be reading it: the reset must not
   // touch those rows)
-  void reset_device(hipStream_t s, uint32_t clear_from, uint32_t summ_from, bool sets_follow = false);
+  void reset_device(hipStream_t s, uint32_t clear_from, uint32_t summ_from);
   void reset_device(hipStream_t s) { reset_device(s, lo, lo); }
   void rehash_links(uint64_t cap);
   void rehash_acts(uint64_t cap);
@@ -2689,7 +2594,6 @@ struct el_ctx {
   std::string install_index(el::HostIndex&& h);
   void column_window();
   void migrate_state(uint32_t N0, const std::vector<uint32_t>& pmap);
-  void init_rows(uint32_t a, uint32_t b);
   el::AxiomStore store;  // the loaded axioms (increments append to them)
   // ELK range fillers (el_index.h elk_ranges): concepts [n_user, N) are internal; the result
   // rows cover the caller's concepts [lo, uhi()) only
@@ -2697,12 +2601,7 @@ struct el_ctx {
   std::vector<uint32_t> fresh_b, fresh_r;
   uint32_t uhi() const { return std::max(lo, std::min(hi, n_user)); }
   uint64_t user_count(bool facts);  // facts / links of the result rows (= the log's without fresh rows)
-  uint64_t uc_s_n = ~0ull, uc_s = 0, uc_l_n = ~0ull, uc_l = 0;
-  std::vector<uint32_t> init_off;  // host copy of DIndex::init_off
-  // init words (k_init_bits): (row - lo, word, mask) of the owned rows' init facts
-  uint32_t *iw_row = nullptr, *iw_word = nullptr, *iw_mask = nullptr;
-  uint32_t iw_n = 0;
-  void build_init_words();
+  uint64_t uc_s_n = ~0ull, uc_s = 0, uc_l_n = ~0ull, uc_l = 0;  // (reset with every state and index)
 };
 
 // Upload the indexes of hx and derive what the kernels need from them (which CSRs have
@@ -2725,8 +2624,6 @@ std::string el_ctx::install_index(el::HostIndex&& hnew) {
   d.R = h.R;
   d.P = h.P;
   d.kind = up8(h.kind);
-  d.told_ptr = up32(h.told.ptr);
-  d.told_b = up32(h.told.a);
   d.cidx_ptr = up32(h.cidx.ptr);
   d.cidx_c = up32(h.cidx.a);
   {
@@ -2746,11 +2643,6 @@ std::string el_ctx::install_index(el::HostIndex&& hnew) {
   d.conj_ptr = up32(h.conj.ptr);
   d.conj_ops = up32(h.conj.a);
   d.conj_b = up32(h.conj_b);
-  d.exr_ptr = up32(h.exr.ptr);
-  d.exr_pid = up32(h.exr.a);
-  d.exl_ptr = up32(h.exl.ptr);
-  d.exl_r = up32(h.exl.a);
-  d.exl_b = up32(h.exl.b);
   d.fp_ptr = up32(h.fp_ptr);
   d.pair_role = up32(h.pair_role);
   d.pair_y = up32(h.pair_y);
@@ -2767,12 +2659,30 @@ std::string el_ctx::install_index(el::HostIndex&& hnew) {
   d.rng_ptr = up32(h.rng.ptr);
   d.rng_c = up32(h.rng.a);
   d.role_has_exl = up8(h.role_has_exl);
-  exrT_ptr = up32(h.exrT.ptr);
-  exrT_x = up32(h.exrT.a);
-  exrC_ptr = up32(h.exrC.ptr);
-  exrC_p = up32(h.exrC.a);
-  d.bpp_ptr = up32(h.bpp.ptr);
-  d.bpp_b = up32(h.bpp.a);
+  {  // the told axiom rows the device closure is built from (el_closure.h)
+    elcl::Axioms& a = cax;
+    a.N = h.N;
+    a.P = h.P;
+    a.par_ptr = up32(h.told.ptr);
+    a.par = up32(h.told.a);
+    a.chi_ptr = up32(h.toldT.ptr);
+    a.chi = up32(h.toldT.a);
+    a.xr_ptr = up32(h.exr.ptr);
+    a.xr = up32(h.exr.a);
+    a.xl_ptr = up32(h.exl.ptr);
+    a.xl_r = up32(h.exl.a);
+    a.xl_b = up32(h.exl.b);
+    a.cidx_ptr = d.cidx_ptr;
+    a.psup_ptr = d.psup_ptr;
+    a.sc_self = up8(h.sc_self);
+    a.sc_w = up32(h.sc_w);
+    a.fp_ptr = d.fp_ptr;
+    a.pair_role = d.pair_role;
+    a.kind = d.kind;
+    key_bits = 1;
+    while (key_bits < 32 && (1ull << key_bits) < h.P) ++key_bits;
+  }
+  uc_s_n = uc_l_n = ~0ull;
   {  // link export order: pair ids ranked by (role, filler)
     std::vector<uint32_t> ord(h.P), rank(h.P);
     std::iota(ord.begin(), ord.end(), 0u);
@@ -2788,36 +2698,7 @@ std::string el_ctx::install_index(el::HostIndex&& hnew) {
     }
     pid_rank = up32(rank);
   }
-  {
-    std::vector<uint32_t> meta(4 * (size_t)(h.N + 1));
-    for (uint32_t a = 0; a <= h.N; ++a) {
-      meta[4 * a + 0] = h.told.ptr[a];
-      meta[4 * a + 1] = h.cidx.ptr[a];
-      meta[4 * a + 2] = h.exr.ptr[a];
-      meta[4 * a + 3] = h.exl.ptr[a];
-    }
-    d.meta = (const uint4*)up32(meta);
-  }
   d.has_range = h.rng.a.empty() ? 0u : 1u;
-  {  // init facts per concept: X, ⊤ (classes, individuals), told*(X) without a second ⊤
-    init_off.assign(h.N + 1, 0);
-    for (uint32_t x = 0; x < h.N; ++x) {
-      const bool two = x != EL_TOP && x != EL_BOTTOM && h.kind[x] != EL_KIND_DATATYPE;
-      uint64_t n = 1 + two + (h.told.ptr[x + 1] - h.told.ptr[x]);
-      if (two && std::binary_search(h.told.a.begin() + h.told.ptr[x], h.told.a.begin() + h.told.ptr[x + 1], EL_TOP))
-        --n;
-      if ((uint64_t)init_off[x] + n > 0xffffffffull) return "init facts beyond 2^32";
-      init_off[x + 1] = init_off[x] + (uint32_t)n;
-    }
-    d.init_off = up32(init_off);
-    // every row has >= 1 init fact, so a slot's row is at most 63 rows past its chunk's row
-    std::vector<uint32_t> r64(init_off[h.N] / 64 + 1);
-    for (uint32_t x = 0, c = 0; c < r64.size(); ++c) {
-      while (x + 1 < h.N && init_off[x + 1] <= 64ull * c) ++x;
-      r64[c] = x;
-    }
-    d.init_row64 = up32(r64);
-  }
   {
     // ⊥ derivable only if some axiom mentions it (as a conclusion or a CR3 filler)
     auto has0 = [](const std::vector<uint32_t>& v) { return std::find(v.begin(), v.end(), EL_BOTTOM) != v.end(); };
@@ -2853,7 +2734,6 @@ std::string el_ctx::install_index(el::HostIndex&& hnew) {
   d.hi = hi;
   column_window();
   d.part = part() ? 1u : 0u;
-  build_init_words();
   return "";
 }
 
@@ -2866,36 +2746,6 @@ std::string el_ctx::install_index(el::HostIndex&& hnew) {
 // (CR3, CR5 supers, CR6 results), and the ranges of every role a link into it can carry
 // (DistEL's range rule puts them into each S(X) that holds the link's target).  For OntologyMultiplier copies aligned with the partition
 // (G4) the window is the rank's own copy: 8 × 19 GB for SNOMED×8 instead of 8 × 152 GB.
-void el_ctx::build_init_words() {
-  const el::HostIndex& h = hx;
-  std::vector<uint32_t> r, w, m, cols;
-  for (uint32_t x = lo; x < hi; ++x) {
-    const bool two = x != EL_TOP && x != EL_BOTTOM && h.kind[x] != EL_KIND_DATATYPE;
-    cols.clear();
-    auto col = [&](uint32_t a) { return a < 2u ? a : (a >= ix.c_lo && a < ix.c_hi ? a - ix.c_lo + 2u : NONE); };
-    cols.push_back(col(x));
-    if (two) cols.push_back(col(EL_TOP));
-    for (uint32_t j = h.told.ptr[x]; j < h.told.ptr[x + 1]; ++j) cols.push_back(col(h.told.a[j]));
-    std::sort(cols.begin(), cols.end());
-    for (size_t k = 0; k < cols.size();) {
-      const uint32_t wd = cols[k] >> 5;
-      if (cols[k] == NONE) break;  // (outside the window: not set, as k_init skips it)
-      uint32_t mk = 0;
-      for (; k < cols.size() && cols[k] != NONE && (cols[k] >> 5) == wd; ++k) mk |= 1u << (cols[k] & 31u);
-      r.push_back(x - lo);
-      w.push_back(wd);
-      m.push_back(mk);
-    }
-  }
-  iw_n = (uint32_t)r.size();
-  iw_row = dupload(r);
-  iw_word = dupload(w);
-  iw_mask = dupload(m);
-  index_bufs.push_back(iw_row);
-  index_bufs.push_back(iw_word);
-  index_bufs.push_back(iw_mask);
-}
-
 void el_ctx::column_window() {
   const el::HostIndex& h = hx;
   uint32_t c_lo = 2, c_hi = std::max<uint32_t>(h.N, 2);
@@ -2961,10 +2811,7 @@ void el_ctx::free_index() {
 void el_ctx::free_state() {
   if (rstream) (void)hipStreamSynchronize(rstream);  // a reset behind a releasing copy-back
   pre_reset = false;
-  pre_base = false;
-  dfree(lsnap);
-  dfree(psnap);
-  lsnap_cap = psnap_cap = 0;
+  free_closure();
   dfree(bits);
   dfree(summ);
   dfree(slog_x);
@@ -3033,11 +2880,11 @@ void el_ctx::alloc_state() {
   SB = summ_stride(W);
   summ = no_summary ? nullptr : dalloc<uint8_t>((uint64_t)(hi - lo) * SB);
   bits_logged = false;
-  // capacities follow the owned rows (a partition of a ×8 ontology holds one copy's rows: its
-  // queues and logs are sized for those, not for the whole index it loads)
+  // Capacities follow the owned rows (a partition of a ×8 ontology holds one copy's rows: its
+  // queues and logs are sized for those, not for the whole index it loads).  What the first
+  // superstep needs depends on the told closure, which only el_init derives: closure_state
+  // grows the logs and queues to it (grow-only, so later classifications allocate nothing).
   const uint64_t Nown = hi - lo;
-  uint64_t told_own = 0;  // the first superstep emits the told closure of every owned row
-  for (uint32_t x = lo; x < hi; ++x) told_own += hx.told.ptr[x + 1] - hx.told.ptr[x];
   slog_cap = std::max<uint64_t>(1u << 20, 8 * Nown);
   slog_x = dalloc<uint32_t>(slog_cap);
   slog_a = dalloc<uint32_t>(slog_cap);
@@ -3061,81 +2908,23 @@ void el_ctx::alloc_state() {
   cp_cap = plog_cap;
   cp_p = dalloc<uint32_t>(cp_cap);
   cp_b = dalloc<uint32_t>(cp_cap);
-  // The first superstep re-triggers every init fact (the told closures included), so the
-  // candidate queues start sized for it: bounds from the index, per owned row X over
-  // F(X) = {X, ⊤} ∪ told*(X) — CR3 links Σ|exr(A)|, CR2 candidates Σ|cidx(A)|, CR4
-  // propagations Σ|exl(A)| (an overflow would re-run the step).
-  uint64_t b_link = 0, b_conj = 0, b_prop = 0;
-  {
-    auto add = [&](uint32_t a) {
-      b_link += hx.exr.ptr[a + 1] - hx.exr.ptr[a];
-      b_conj += hx.cidx.ptr[a + 1] - hx.cidx.ptr[a];
-      b_prop += hx.exl.ptr[a + 1] - hx.exl.ptr[a];
-    };
-    for (uint32_t x = lo; x < hi; ++x) {  // exr / exl rows already span the told closure
-      add(x);
-      if (x != EL_TOP && x != EL_BOTTOM && hx.kind[x] != EL_KIND_DATATYPE) add(EL_TOP);
-      for (uint32_t j = hx.told.ptr[x]; j < hx.told.ptr[x + 1]; ++j) {
-        const uint32_t a = hx.told.a[j];
-        b_conj += hx.cidx.ptr[a + 1] - hx.cidx.ptr[a];  // the closure's facts still run CR2
-      }
-    }
-  }
-  cs_cap = std::max<uint64_t>(std::max<uint64_t>(1u << 20, 4 * Nown), next_pow2(b_conj + b_conj / 4));
-  cl_cap = std::max<uint64_t>(1u << 20, next_pow2(b_link + b_link / 4));
+  cs_cap = std::max<uint64_t>(1u << 20, 4 * Nown);
+  cl_cap = std::max<uint64_t>(1u << 20, 4 * Nown);
   if (const char* e = getenv("EL_QUEUE_CAP")) {  // tests: small queues force overflowing steps
     cs_cap = cl_cap = std::max<uint64_t>(256, next_pow2(strtoull(e, nullptr, 10)));
-  }
-  if (b_prop + b_prop / 4 > cp_cap) {
-    dfree(cp_p);
-    dfree(cp_b);
-    cp_cap = next_pow2(b_prop + b_prop / 4);
-    cp_p = dalloc<uint32_t>(cp_cap);
-    cp_b = dalloc<uint32_t>(cp_cap);
   }
   if (part()) {
     // records per rank per all-gather; grows on demand (EL_XCHG_CAP: a smaller start, tests)
     xcap = 1u << 12;
     if (const char* e = getenv("EL_XCHG_CAP")) xcap = std::max<uint64_t>(1, strtoull(e, nullptr, 10));
   }
-  // gapped CSRs, only where the rules read them; overflow queues hold a step's appends
-  // Row capacities for the first supersteps: every init fact X ∈ S(X) emits the pairs of
-  // exr(X) and CR5 lifts them to their super-role pairs (psup) one step later, so pid p's
-  // predecessor row receives its count of both and X's successor row the chain-second ones;
-  // slack gap_cap() as after a re-layout.  Spares the first steps'
-  // re-layouts (G3 step 0: 25 M links into 16-slot rows, 0.7 ms of moves and overflow
-  // placement).  The oracle sizes its rows the same way (el_oracle.c, elo_create).
-  std::vector<uint32_t> cap_pr, cap_sc;
-  if (!part() && ((P && need_pred) || need_succ)) {
-    cap_pr.assign(P, 0);
-    cap_sc.assign(N, 0);
-    for (uint32_t x = 0; x < N; ++x)
-      for (uint32_t j = hx.exr.ptr[x]; j < hx.exr.ptr[x + 1]; ++j) {
-        const uint32_t p = hx.exr.a[j], r = hx.pair_role[p];
-        ++cap_pr[p];
-        cap_sc[x] += hx.chs.ptr[r + 1] > hx.chs.ptr[r];
-        for (uint32_t k = hx.psup.ptr[p]; k < hx.psup.ptr[p + 1]; ++k) {  // CR5 lifts them next step
-          const uint32_t u = hx.psup.a[k], ru = hx.pair_role[u];
-          ++cap_pr[u];
-          cap_sc[x] += hx.chs.ptr[ru + 1] > hx.chs.ptr[ru];
-        }
-      }
-  }
-  // propagation rows: init fact X (as Y) records ((r, X), B) for every (r, B) of exl(X)
-  std::vector<uint32_t> cap_pp;
-  if (!part() && use_props) {
-    cap_pp.assign(P, 0);
-    for (uint32_t x = 0; x < N; ++x)
-      for (uint32_t j = hx.exl.ptr[x]; j < hx.exl.ptr[x + 1]; ++j)
-        for (uint32_t q = hx.fp_ptr[x]; q < hx.fp_ptr[x + 1]; ++q)
-          if (hx.pair_role[q] == hx.exl.a[j]) {
-            ++cap_pp[q];
-            break;
-          }
-  }
-  if (P && need_pred) PR.alloc((uint32_t)P, cl_cap, cap_pr.empty() ? nullptr : &cap_pr);
-  if (need_succ) SC.alloc((uint32_t)N, part() ? (uint64_t)part_count * xcap : cl_cap, cap_sc.empty() ? nullptr : &cap_sc);
-  if (use_props) PP.alloc((uint32_t)P, cp_cap + remote_bound(), cap_pp.empty() ? nullptr : &cap_pp);
+  // gapped CSRs, only where the rules read them; overflow queues hold a step's appends.  Their
+  // initial layouts are laid per classification (closure_state): rows sized for the first
+  // supersteps' links (the base links and their CR5 lifts, the base propagations), as the oracle
+  // sizes its rows (el_oracle.c, elo_create), so no early re-layout is needed
+  if (P && need_pred) PR.alloc((uint32_t)P, cl_cap);
+  if (need_succ) SC.alloc((uint32_t)N, part() ? (uint64_t)part_count * xcap : cl_cap);
+  if (use_props) PP.alloc((uint32_t)P, cp_cap + remote_bound());
   HIPCHK(hipHostMalloc((void**)&pin_word, sizeof(uint32_t), hipHostMallocDefault));
   // range activation candidates: a new link (X, r, Y) emits one (Y, C) per C ∈ rng(r), so a
   // step's links bound them; an undersized queue would re-run a whole generation
@@ -3145,26 +2934,13 @@ void el_ctx::alloc_state() {
   ca_cap = std::max<uint64_t>(ca_cap, next_pow2(cl_cap * max_rng));
   cs_x = dalloc<uint32_t>(cs_cap);
   cs_a = dalloc<uint32_t>(cs_cap);
-  // the first superstep emits the whole told closure of every concept (its init fact X ∈ S(X))
-  ct_cap = std::max<uint64_t>(cs_cap, next_pow2(2 * told_own + 1024));
+  ct_cap = cs_cap;
   ct_x = dalloc<uint32_t>(ct_cap);
   ct_a = dalloc<uint32_t>(ct_cap);
   cl_x = dalloc<uint32_t>(cl_cap);
   cl_p = dalloc<uint32_t>(cl_cap);
   ca_y = dalloc<uint32_t>(ca_cap);
   ca_c = dalloc<uint32_t>(ca_cap);
-  {  // the init facts (with the told closure) and one step of candidates fit from the start
-    const uint64_t need = (uint64_t)init_off[hi] - init_off[lo] + cs_cap + ct_cap;
-    if (need > slog_cap) {
-      dfree(slog_x);
-      dfree(slog_a);
-      dfree(slog_f);
-      slog_cap = next_pow2(need);
-      slog_x = dalloc<uint32_t>(slog_cap);
-      slog_a = dalloc<uint32_t>(slog_cap);
-      slog_f = dalloc<uint8_t>(slog_cap);
-    }
-  }
   job_cap = std::max<uint64_t>(1u << 20, 2 * Nown);
   jobs = dalloc<uint4>(job_cap);
   ctr = dalloc<DCounters>(1);
@@ -3191,11 +2967,13 @@ void el_ctx::alloc_state() {
     xsend = dalloc<uint32_t>(XH + 2 * xcap);
     xrecv = dalloc<uint32_t>((uint64_t)part_count * (XH + 2 * xcap));
   }
+  alloc_closure();
 }
 
 // The device part of reset_state on stream s: clear the bit matrix (by the fact log), the
-// sets, counters and gapped rows.  Reads only the logs and counts of the finished state.
-void el_ctx::reset_device(hipStream_t stream, uint32_t clear_from, uint32_t summ_from, bool sets_follow) {
+// sets and counters.  Reads only the logs and counts of the finished state.  (The gapped rows
+// get this classification's layout from el_init's closure_state.)
+void el_ctx::reset_device(hipStream_t stream, uint32_t clear_from, uint32_t summ_from) {
   FillArgs f{};
   auto add = [&](void* p, uint64_t bytes, uint32_t pattern) { f.seg[f.n++] = FillSeg{p, bytes, pattern}; };
   const uint64_t matrix_bytes = (uint64_t)(hi - lo) * W * sizeof(uint32_t);
@@ -3213,32 +2991,19 @@ void el_ctx::reset_device(hipStream_t stream, uint32_t clear_from, uint32_t summ
     add(summ + (uint64_t)(summ_from - lo) * SB, (uint64_t)(hi - summ_from) * SB, 0u);
   // the link set is by far the largest (G3: 2 GB): the runtime's fill reaches a higher write
   // rate than k_fill's grid-stride loop for it (k_fill: 2.0 ms per G3 classification)
-  if (sets_follow) {
-    // (enqueue_base copies the base snapshots over the link and propagation sets next)
-  } else if (lhash_cap * sizeof(unsigned long long) >= (64ull << 20)) {
+  if (lhash_cap * sizeof(unsigned long long) >= (64ull << 20)) {
     HIPCHK(hipMemsetAsync(lhash, 0xff, lhash_cap * sizeof(unsigned long long), stream));
   } else {
     add(lhash, lhash_cap * sizeof(unsigned long long), ~0u);
   }
   add(ahash, ahash_cap * sizeof(unsigned long long), ~0u);
   add(has_act, hx.N, 0u);
-  if (!sets_follow) add(phash, phash_cap * sizeof(unsigned long long), ~0u);
+  add(phash, phash_cap * sizeof(unsigned long long), ~0u);
   add(ctr, sizeof(DCounters), 0u);
   add(commit_done, (DONE_SHARDS + 1) * CTR_STRIDE * sizeof(uint32_t), 0u);
   add(ev, EV_WORDS * sizeof(unsigned long long), 0u);
   hipLaunchKernelGGL(k_fill, dim3(1024), dim3(BLOCK), 0, stream, f);
   HIPCHK(hipGetLastError());
-  for (GapCsr* g : {&PR, &SC, &PP}) {
-    if (!g->live) continue;
-    if (g->val_cap < g->total0) {  // (a re-layout may have shrunk nothing: val only grows)
-      dfree(g->val);
-      g->val_cap = g->total0;
-      g->val = dalloc<uint32_t>(g->val_cap);
-    }
-    hipLaunchKernelGGL(k_gap_init, dim3(grid_for(g->rows + 1)), dim3(BLOCK), 0, stream, g->start, g->len, g->rows,
-                       g->start0);
-    HIPCHK(hipGetLastError());
-  }
 }
 
 void el_ctx::reset_state() {
@@ -3247,9 +3012,9 @@ void el_ctx::reset_state() {
     pre_reset = false;
   } else {
     reset_device(stream);
-    pre_base = false;  // (the full reset cleared it)
   }
-  bits_logged = true;  // from here on every set bit is in the fact log (k_init and k_commit append)
+  bits_logged = true;  // from here on every set bit is in the fact log (the init facts and k_commit append)
+  uc_s_n = uc_l_n = ~0ull;
   s_count = l_count = a_count = p_count = s_init = x_count = 0;
   if (base_filling) HIPCHK(hipStreamWaitEvent(stream, ev_base[1], 0));  // (an interrupted saturation)
   base_filling = false;
@@ -3901,169 +3666,328 @@ void el_ctx::gap_build_from_log(GapCsr& g, const uint32_t* rows, const uint32_t*
   }
 }
 
-// Init facts of the rows [a, b), appended at s_count: X, ⊤ and the told closure of X (see
-// k_init).  The counts are known on the host (init_off), so nothing is read back and the
-// first superstep is enqueued without a sync.
-void el_ctx::init_rows(uint32_t a, uint32_t b) {
-  if (b <= a) return;
-  const uint64_t n = (uint64_t)init_off[b] - init_off[a];
-  if (s_count + n + cs_cap + ct_cap > slog_cap) {
-    sync();
-    const uint64_t c = next_pow2(s_count + n + cs_cap + ct_cap);
-    dgrow(slog_x, s_count, c);
-    dgrow(slog_a, s_count, c);
-    dgrow(slog_f, s_count, c);
-    slog_cap = c;
+// ---- the told closure on the device (el_closure.h), rebuilt inside every el_init: nothing
+// derived from the axioms survives from one classification to the next except buffer sizes
+
+void el_ctx::alloc_closure() {
+  const uint64_t N = hx.N, P = std::max<uint32_t>(hx.P, 1u);
+  auto cap32 = [](uint64_t v) { return (uint32_t)std::min<uint64_t>(v, 0x7fffffffull); };
+  cl.meta = dalloc<uint4>(2 * N);
+  cl.meta2 = dalloc<uint4>(2 * N);
+  // first guesses (G3: 24 M / 25 M / 36 M entries); an overflowing build grows and runs again
+  cl.t_cap = cap32(64 * N + (1u << 20));
+  cl.e_cap = cap32(64 * N + (1u << 20));
+  cl.l_cap = cap32(96 * N + (1u << 20));
+  cl.t_val = dalloc<uint32_t>(cl.t_cap);
+  cl.e_val = dalloc<uint32_t>(cl.e_cap);
+  cl.l_r = dalloc<uint32_t>(cl.l_cap);
+  cl.l_b = dalloc<uint32_t>(cl.l_cap);
+  cl.level = dalloc<uint32_t>(N);
+  cl.indeg = dalloc<uint32_t>(N);
+  cl.lvl_flag = dalloc<uint32_t>(N + 2);
+  cl.dirty = dalloc<uint8_t>(N);
+  cl.dirty2 = dalloc<uint8_t>(N);
+  cl.changed = dalloc<uint8_t>(N);
+  cl.nd = dalloc<uint32_t>(elcl::ND_NUM * (N + 1));
+  HIPCHK(hipMemset(cl.nd, 0, elcl::ND_NUM * (N + 1) * sizeof(uint32_t)));  // (entry N of a column stays 0)
+  cl.rsv = dalloc<uint32_t>(elcl::RSV_WORDS);
+  cl.scratch_cap = 1u << 20;
+  cl.scratch = dalloc<uint32_t>(cl.scratch_cap);
+  cl.ctr = dalloc<elcl::Ctr>(1);
+  HIPCHK(hipHostMalloc((void**)&clh, sizeof(ClHost), hipHostMallocDefault));
+  memset(clh, 0, sizeof(ClHost));
+  for (uint32_t*& p : cpos) p = dalloc<uint32_t>(N + 1);
+  cscan_bytes = std::max<size_t>(elcl::scan_temp_bytes((uint32_t)N + 1), 16);
+  cscan_tmp = dalloc<uint8_t>(cscan_bytes);
+  for (uint32_t** p : {&pr_first, &pr_last, &bpp_s, &bpp_e, &cap_pr, &cap_pp}) {
+    *p = dalloc<uint32_t>(P);
+    HIPCHK(hipMemset(*p, 0, P * sizeof(uint32_t)));
   }
-  DState st = dstate();
-  const bool whole = a == lo && b == hi && s_count == 0;  // a fresh state: the init words as whole words
-  launch(EL_K_INIT, [&] {
-    hipLaunchKernelGGL(k_init, dim3(grid_for(n, 2048)), dim3(BLOCK), 0, stream, ix, st, a, b, (uint32_t)s_count,
-                       whole ? 0u : 1u);
-    if (whole)
-      hipLaunchKernelGGL(k_init_bits, dim3(grid_for(iw_n, 2048)), dim3(BLOCK), 0, stream, bits, W, iw_row, iw_word,
-                         iw_mask, iw_n, summ, SB);
-  });
-  hipLaunchKernelGGL(k_set_u32, dim3(1), dim3(1), 0, stream, &ctr->s_log, (uint32_t)(s_count + n));
-  HIPCHK(hipGetLastError());
-  uint64_t two = 0;  // the {X, ⊤} part: init facts proper; the closure part is derived
-  for (uint32_t x = a; x < b; ++x) two += 1 + (x != EL_TOP && x != EL_BOTTOM && hx.kind[x] != EL_KIND_DATATYPE);
-  s_count += n;
-  s_init += two;
+  level_hint = 32;
+  set_closure_ix();
 }
 
-// The base links {(X, p) : p ∈ exr(X)} — what CR3 derives from the init facts X ∈ S(X) in the
-// first superstep — written before it: the link log gets exr in X order, the predecessor rows
-// exrT, the successor rows exrC (rows laid out for them by alloc_state: row capacities count
-// them), and the link set stays without them (link_known: a binary search of exr(X)).  The
-// first superstep then expands the base links, which the second did before; its queues start
-// at what the second got.  The CPU oracle installs the same links (el_oracle.c, base_links).
-bool el_ctx::base_fits() {
-  const uint64_t nb = hx.exr.a.size(), nbp = hx.bpp.a.size();
-  if (nb == 0 || part() || (PR.live && !PR.start0) || (SC.live && !SC.start0)) return false;
-  const bool props = nbp && use_props && PP.live && PP.start0;
-  if (nb + cl_cap > llog_cap || 2 * (nb + cl_cap) > lhash_cap) return false;
-  if (props && (nbp + cp_cap > plog_cap || 2 * (nbp + cp_cap) > phash_cap)) return false;
-  return true;
+void el_ctx::free_closure() {
+  dfree(cl.meta);
+  dfree(cl.meta2);
+  dfree(cl.t_val);
+  dfree(cl.e_val);
+  dfree(cl.l_r);
+  dfree(cl.l_b);
+  dfree(cl.level);
+  dfree(cl.indeg);
+  dfree(cl.lvl_flag);
+  dfree(cl.dirty);
+  dfree(cl.dirty2);
+  dfree(cl.changed);
+  dfree(cl.nd);
+  dfree(cl.rsv);
+  dfree(cl.scratch);
+  dfree(cl.ctr);
+  cl = elcl::Out{};
+  if (clh) (void)hipHostFree(clh);
+  clh = nullptr;
+  for (uint32_t*& p : cpos) dfree(p);
+  dfree(cscan_tmp);
+  dfree(csort_tmp);
+  cscan_bytes = csort_bytes = 0;
+  dfree(sk);
+  dfree(sv);
+  sk_cap = 0;
+  for (uint32_t** p : {&pr_first, &pr_last, &bpp_s, &bpp_e, &cap_pr, &cap_pp}) dfree(*p);
+  nb = nbp = nc = 0;
 }
 
-bool el_ctx::enqueue_base(hipStream_t s) {
-  if (!base_fits()) return false;
-  const uint64_t nb = hx.exr.a.size(), nbp = hx.bpp.a.size();
-  const bool props = nbp && use_props && PP.live && PP.start0;
-  const uint32_t N = hx.N, P = hx.P, nc = (uint32_t)hx.exrC.a.size();
-  auto items = [](uint64_t n) { return (uint32_t)std::min<uint64_t>(16, std::max<uint64_t>(1, n / (2048 * 256))); };
-  auto grid = [&](uint64_t n) {
-    const uint64_t t = 256ull * items(n);
-    return (uint32_t)std::min<uint64_t>(2048, std::max<uint64_t>(1, (n + t - 1) / t));
+// the kernels' view of this classification's rows
+void el_ctx::set_closure_ix() {
+  ix.told_b = cl.t_val;
+  ix.exr_pid = cl.e_val;
+  ix.exl_r = cl.l_r;
+  ix.exl_b = cl.l_b;
+  ix.meta = cl.meta;
+  ix.bpp_s = bpp_s;
+  ix.bpp_e = bpp_e;
+}
+
+// a build overflowed a row array or the big-row scratch: grow what overflowed (to what it asked
+// for, at least double) and build again
+void el_ctx::closure_grow() {
+  const elcl::Ctr& c = clh->ctr;
+  auto grow = [&](std::initializer_list<uint32_t**> ps, uint32_t& cap, uint64_t tail) {
+    if (tail <= cap) return;
+    uint64_t n = std::max<uint64_t>(2ull * cap, tail + tail / 2);
+    if (tail >= 0x7fffffffull) throw ElError{EL_ENOMEM, "told closure rows beyond 2^31 entries"};
+    n = std::min<uint64_t>(n, 0x7fffffffull);
+    for (uint32_t** p : ps) {
+      dfree(*p);
+      *p = dalloc<uint32_t>(n);
+    }
+    cap = (uint32_t)n;
   };
-  // the same launches as install_base, in one stream (the reset before them, el_init after)
-  hipLaunchKernelGGL(k_csr_scatter, dim3(grid(nb)), dim3(256), 0, s, ix.exr_ptr, ix.exr_pid, N, (uint32_t)nb, llog_x,
-                     llog_p, nullptr, nullptr, items(nb));
-  if (PR.live) {
-    hipLaunchKernelGGL(k_gap_len, dim3(grid(P)), dim3(256), 0, s, exrT_ptr, P, PR.len);
-    hipLaunchKernelGGL(k_csr_scatter, dim3(grid(nb)), dim3(256), 0, s, exrT_ptr, exrT_x, P, (uint32_t)nb, nullptr,
-                       nullptr, PR.start, PR.val, items(nb));
+  sync();
+  grow({&cl.t_val}, cl.t_cap, c.t_tail);
+  grow({&cl.e_val}, cl.e_cap, c.e_tail);
+  grow({&cl.l_r, &cl.l_b}, cl.l_cap, c.l_tail);
+  if (2 * c.s_tail > cl.scratch_cap) {
+    dfree(cl.scratch);
+    cl.scratch_cap = std::max<unsigned long long>(2 * cl.scratch_cap, 3 * c.s_tail);
+    cl.scratch = dalloc<uint32_t>(cl.scratch_cap);
   }
-  if (SC.live && nc) {
-    hipLaunchKernelGGL(k_gap_len, dim3(grid(N)), dim3(256), 0, s, exrC_ptr, N, SC.len);
-    hipLaunchKernelGGL(k_csr_scatter, dim3(grid(nc)), dim3(256), 0, s, exrC_ptr, exrC_p, N, nc, nullptr, nullptr,
-                       SC.start, SC.val, items(nc));
-  }
-  hipLaunchKernelGGL(k_set_u32, dim3(1), dim3(1), 0, s, &ctr->l_log, (uint32_t)nb);
-  if (props) {
-    hipLaunchKernelGGL(k_csr_scatter, dim3(grid(nbp)), dim3(256), 0, s, ix.bpp_ptr, ix.bpp_b, P, (uint32_t)nbp, plog_p,
-                       plog_b, nullptr, nullptr, items(nbp));
-    hipLaunchKernelGGL(k_gap_len, dim3(grid(P)), dim3(256), 0, s, ix.bpp_ptr, P, PP.len);
-    hipLaunchKernelGGL(k_csr_scatter, dim3(grid(nbp)), dim3(256), 0, s, ix.bpp_ptr, ix.bpp_b, P, (uint32_t)nbp, nullptr,
-                       nullptr, PP.start, PP.val, items(nbp));
-    hipLaunchKernelGGL(k_set_u32, dim3(1), dim3(1), 0, s, &ctr->p_log, (uint32_t)nbp);
-  }
-  if (no_snap) {  // the sets were cleared by the reset: insert
-    hipLaunchKernelGGL(k_rehash, dim3(grid_for(nb, 2048)), dim3(BLOCK), 0, s, lhash, lhash_cap - 1, llog_x, llog_p,
-                       (uint32_t)nb);
-    if (props)
-      hipLaunchKernelGGL(k_rehash, dim3(grid_for(nbp, 2048)), dim3(BLOCK), 0, s, phash, phash_cap - 1, plog_b,
-                         plog_p, (uint32_t)nbp);
-    HIPCHK(hipGetLastError());
-  } else {  // the snapshots (built on first use at this capacity) over the sets
-    auto snap = [&](unsigned long long*& sn, uint64_t& sn_cap, unsigned long long* set, uint64_t cap,
-                    const uint32_t* kx, const uint32_t* kp, uint64_t n) {
-      if (sn_cap != cap) {
-        dfree(sn);
-        sn = dalloc<unsigned long long>(cap);
-        sn_cap = cap;
-        HIPCHK(hipMemsetAsync(sn, 0xff, cap * sizeof(unsigned long long), s));
-        hipLaunchKernelGGL(k_rehash, dim3(grid_for(n, 2048)), dim3(BLOCK), 0, s, sn, cap - 1, kx, kp, (uint32_t)n);
-        HIPCHK(hipGetLastError());
-      }
-      HIPCHK(hipMemcpyAsync(set, sn, cap * sizeof(unsigned long long), hipMemcpyDeviceToDevice, s));
-    };
-    snap(lsnap, lsnap_cap, lhash, lhash_cap, llog_x, llog_p, nb);
-    if (props)
-      snap(psnap, psnap_cap, phash, phash_cap, plog_b, plog_p, nbp);
-    else
-      HIPCHK(hipMemsetAsync(phash, 0xff, phash_cap * sizeof(unsigned long long), s));
-  }
-  HIPCHK(hipEventRecord(ev_base[1], s));  // (join_base waits for it; the set is full by then)
-  return true;
+  set_closure_ix();
 }
 
-void el_ctx::undo_base() {
-  if (!pre_base) return;
-  pre_base = false;
-  // the link / propagation logs, sets and rows as the reset leaves them (the S state is kept)
-  hipLaunchKernelGGL(k_set_u32, dim3(1), dim3(1), 0, stream, &ctr->l_log, 0u);
-  hipLaunchKernelGGL(k_set_u32, dim3(1), dim3(1), 0, stream, &ctr->p_log, 0u);
+// After the Kahn levels launched so far: stuck concepts, totals over [a, b), the scans of the
+// rows' counts, and one readback (counters, the flag of level L, the rows of ⊤).
+void el_ctx::closure_tail(uint32_t a, uint32_t b, uint32_t L) {
+  HIPCHK(hipMemsetAsync(&cl.ctr->tot[elcl::T_STUCK], 0, sizeof(unsigned long long), stream));
+  elcl::check(stream, cax, cl);
+  HIPCHK(hipMemsetAsync(cl.ctr->tot, 0, elcl::T_STUCK * sizeof(unsigned long long), stream));
+  HIPCHK(hipMemsetAsync(cl.ctr->ev, 0, sizeof(cl.ctr->ev), stream));
+  elcl::totals(stream, cax, cl, a, b);
+  const uint64_t N1 = (uint64_t)hx.N + 1;
+  const uint32_t cols[3] = {elcl::ND_INIT, elcl::ND_EXR, elcl::ND_PROPS};
+  for (int i = 0; i < 3; ++i) elcl::scan(stream, cscan_tmp, cscan_bytes, cl.nd + cols[i] * N1 + a, cpos[i], b - a + 1);
+  HIPCHK(hipMemcpyAsync(&clh->ctr, cl.ctr, sizeof(elcl::Ctr), hipMemcpyDeviceToHost, stream));
+  HIPCHK(hipMemcpyAsync(&clh->flag, cl.lvl_flag + std::min<uint32_t>(L, hx.N + 1), sizeof(uint32_t),
+                        hipMemcpyDeviceToHost, stream));
+  HIPCHK(hipMemcpyAsync(clh->top, cl.meta + 2 * EL_TOP, 2 * sizeof(uint4), hipMemcpyDeviceToHost, stream));
+  sync();
+}
+
+// The rows told*, exr*, exl* of every concept (Kahn levels; relaxation rounds for told cycles)
+// and the totals / scans over the rows [a, b) (el_init: the owned rows; an increment: the new
+// ones).  Readbacks: one after the levels (two when the graph is deeper than the levels launched
+// up front), one per relaxation round.
+void el_ctx::closure_rows(uint32_t a, uint32_t b) {
+  const uint32_t N = hx.N;
+  const bool props = use_props && !part();
+  for (int attempt = 0;; ++attempt) {
+    if (attempt > 32) throw ElError{EL_EHIP, "told closure: the build did not fit its buffers"};
+    launch(EL_K_CLOSURE, [&] { elcl::start(stream, cax, cl); });
+    uint32_t L = 0;
+    bool redo = false;
+    for (;;) {
+      const uint32_t end = (uint32_t)std::min<uint64_t>((uint64_t)N + 1, (uint64_t)L + level_hint);
+      for (; L < end; ++L) launch(EL_K_CLOSURE, [&] { elcl::level(stream, cax, cl, L, props); });
+      closure_tail(a, b, L);
+      if (clh->ctr.ovf) {
+        redo = true;
+        break;
+      }
+      if (L <= N && clh->flag) {  // deeper than the levels launched: more of them
+        level_hint = std::min<uint32_t>(2 * level_hint, N + 1);
+        continue;
+      }
+      break;
+    }
+    if (!redo && clh->ctr.tot[elcl::T_STUCK]) {  // told cycles: relaxation rounds until no row grows
+      for (uint64_t round = 0;; ++round) {
+        launch(EL_K_CLOSURE, [&] { elcl::relax(stream, cax, cl, props); });
+        HIPCHK(hipMemcpyAsync(&clh->ctr, cl.ctr, sizeof(elcl::Ctr), hipMemcpyDeviceToHost, stream));
+        sync();
+        if (clh->ctr.ovf) {
+          redo = true;
+          break;
+        }
+        if (!clh->ctr.dirty) break;
+        if (round > (uint64_t)N + 1) throw ElError{EL_EHIP, "told closure: relaxation did not converge"};
+      }
+      if (!redo) closure_tail(a, b, L);
+    }
+    if (!redo) break;
+    closure_grow();
+  }
+  clt = clh->ctr;
+  host_ev[EL_K_CLOSURE][EL_EV_TRIG] += clt.ev[elcl::E_TRIG];
+  host_ev[EL_K_CLOSURE][EL_EV_ROW] += clt.ev[elcl::E_ROW];
+  host_ev[EL_K_CLOSURE][EL_EV_ENT] += clt.ev[elcl::E_ENT];
+  host_ev[EL_K_CLOSURE][EL_EV_RMW] += clt.ev[elcl::E_RMW];
+}
+
+// The owned rows' init facts S(X) = {X, ⊤} ∪ told*(X) (fact log + bits), and for a whole-ontology
+// context the base links / propagations in the heads of their logs (installed by el_saturate),
+// the base links by pid (radix sort) and this classification's gapped-row layouts.  Buffers
+// grow first to what the closure asks for (grow-only).
+void el_ctx::closure_state() {
+  const unsigned long long* T = clt.tot;
+  const uint64_t N = hx.N, P = hx.P;
+  const uint64_t n_init = T[elcl::T_INIT], two = T[elcl::T_TWO];
+  const uint4 tb = clh->top[0], te = clh->top[1];
+  // the first superstep re-triggers every init fact: CR3 over exr*, CR2 over the closures'
+  // conjunctions, CR4 half-1 over exl* (per own row X: X, ⊤ and the told closure)
+  const uint64_t b_link = T[elcl::T_EXR] + two * (te.z - tb.z);
+  const uint64_t b_conj = T[elcl::T_CIDX] + two * (te.y - tb.y) + T[elcl::T_CZ];
+  const uint64_t b_prop = T[elcl::T_EXL] + two * (te.w - tb.w);
+  const bool base = !part();
+  nb = base ? T[elcl::T_EXR] : 0;
+  nbp = base && use_props ? T[elcl::T_PROPS] : 0;
+  nc = base && SC.live ? T[elcl::T_SC0] : 0;
+  if (n_init > 0xffffffffull || nb > 0xffffffffull || nbp > 0xffffffffull)
+    throw ElError{EL_ENOMEM, "init facts or base links beyond 2^32 (uint32 device counters)"};
+  auto realloc2 = [](uint64_t cap, uint32_t*& a, uint32_t*& b) {
+    dfree(a);
+    dfree(b);
+    a = dalloc<uint32_t>(cap);
+    b = dalloc<uint32_t>(cap);
+  };
+  if (!small_queues) {
+    if (const uint64_t w = next_pow2(b_conj + b_conj / 4); w > cs_cap) realloc2(cs_cap = w, cs_x, cs_a);
+    if (const uint64_t w = next_pow2(b_link + b_link / 4); w > cl_cap) {
+      realloc2(cl_cap = w, cl_x, cl_p);
+      if (part()) realloc2(cl_cap, xs_x, xs_p);
+    }
+  }
+  if (const uint64_t w = next_pow2(b_prop + b_prop / 4); w > cp_cap) realloc2(cp_cap = w, cp_p, cp_b);
+  if (const uint64_t w = std::max<uint64_t>(cs_cap, next_pow2(2 * T[elcl::T_TOLD] + 1024)); w > ct_cap)
+    realloc2(ct_cap = w, ct_x, ct_a);
+  if (max_rng && next_pow2(cl_cap * max_rng) > ca_cap) realloc2(ca_cap = next_pow2(cl_cap * max_rng), ca_y, ca_c);
+  PR.set_ovq(cl_cap);
+  SC.set_ovq(part() ? (uint64_t)part_count * xcap : cl_cap);
+  PP.set_ovq(cp_cap + remote_bound());
+  if (n_init + cs_cap + ct_cap > slog_cap) {  // (s_count is 0: nothing to keep)
+    slog_cap = next_pow2(n_init + cs_cap + ct_cap);
+    realloc2(slog_cap, slog_x, slog_a);
+    dfree(slog_f);
+    slog_f = dalloc<uint8_t>(slog_cap);
+  }
+  if (nb + cl_cap > llog_cap) realloc2(llog_cap = next_pow2(nb + cl_cap + (nb + cl_cap) / 2), llog_x, llog_p);
+  if (2 * (nb + cl_cap) > lhash_cap) rehash_links(next_pow2(2 * (nb + cl_cap)));
+  if (nbp + cp_cap > plog_cap) realloc2(plog_cap = next_pow2(nbp + cp_cap + (nbp + cp_cap) / 2), plog_p, plog_b);
+  if (2 * (nbp + cp_cap) > phash_cap) rehash_props(next_pow2(2 * (nbp + cp_cap)));
+  // initial gapped layouts: row capacities gap_cap(c) for the first supersteps' entries c
+  auto fit_gap = [&](GapCsr& g, uint64_t entries) {
+    if (!g.live) return;
+    g.total0 = (uint64_t)GAP_MUL * entries + (uint64_t)gap_cap(0) * g.rows;
+    if (g.total0 > 0xffffffffull) throw ElError{EL_ENOMEM, "gapped CSR beyond 2^32 slots"};
+    if (g.val_cap < g.total0) {
+      dfree(g.val);
+      g.val_cap = g.total0;
+      g.val = dalloc<uint32_t>(g.val_cap);
+    }
+    g.laid = false;
+  };
+  fit_gap(PR, base ? nb + T[elcl::T_LIFT] : 0);
+  fit_gap(SC, base ? T[elcl::T_SC] : 0);
+  fit_gap(PP, nbp);
+  if (base && PR.live && nb) {
+    if (nb > sk_cap) {
+      sk_cap = nb + nb / 8;
+      realloc2(sk_cap, sk, sv);
+    }
+    const size_t need = elcl::sort_temp_bytes((uint32_t)nb);
+    if (need > csort_bytes) {
+      dfree(csort_tmp);
+      csort_bytes = need;
+      csort_tmp = dalloc<uint8_t>(need);
+    }
+  }
+  set_closure_ix();
+  // ---- the init facts
+  DState st = dstate();
+  launch(EL_K_INIT, [&] {
+    elcl::init_facts(stream, cax, cl, lo, hi, cpos[0], 0, slog_x, slog_a, slog_f, st.bits, W, ix.c_lo, ix.c_hi, st.summ,
+                     SB);
+  });
+  hipLaunchKernelGGL(k_set_u32, dim3(1), dim3(1), 0, stream, &ctr->s_log, (uint32_t)n_init);
   HIPCHK(hipGetLastError());
-  HIPCHK(hipMemsetAsync(lhash, 0xff, lhash_cap * sizeof(unsigned long long), stream));
-  HIPCHK(hipMemsetAsync(phash, 0xff, phash_cap * sizeof(unsigned long long), stream));
+  s_count = n_init;
+  s_init = T[elcl::T_OWN] + two;
+  // (per row X: its slots, the row's entries read)
+  host_ev[EL_K_INIT][EL_EV_ENT] += T[elcl::T_OWN] + T[elcl::T_TOLD];
+  host_ev[EL_K_INIT][EL_EV_RMW] += n_init;
+  host_ev[EL_K_INIT][EL_EV_EMIT] += n_init;
+  // ---- base links / propagations and the layouts they ask for
+  if (base) {
+    const uint32_t n32 = (uint32_t)N, p32 = (uint32_t)P;
+    if (nb) elcl::base_links(stream, cax, cl, lo, hi, cpos[1], llog_x, llog_p);
+    if (P) {
+      HIPCHK(hipMemsetAsync(bpp_s, 0, P * sizeof(uint32_t), stream));
+      HIPCHK(hipMemsetAsync(bpp_e, 0, P * sizeof(uint32_t), stream));
+    }
+    if (nbp) {
+      elcl::base_props(stream, cax, cl, lo, hi, cpos[2], plog_p, plog_b);
+      elcl::runs(stream, plog_p, (uint32_t)nbp, bpp_s, bpp_e);
+    }
+    if (PR.live) {
+      for (uint32_t* p : {pr_first, pr_last, cap_pr}) HIPCHK(hipMemsetAsync(p, 0, P * sizeof(uint32_t), stream));
+      if (nb) {
+        elcl::sort_pairs(stream, csort_tmp, csort_bytes, llog_p, sk, llog_x, sv, (uint32_t)nb, key_bits);
+        elcl::runs(stream, sk, (uint32_t)nb, pr_first, pr_last);
+      }
+      elcl::caps(stream, pr_first, pr_last, p32, ix.psup_ptr, ix.psup_pid, cap_pr, nullptr);
+      launch_gap_scan(cap_pr, p32, PR.start0);
+      PR.laid = true;
+    }
+    if (SC.live) {
+      launch_gap_scan(cl.nd + elcl::ND_SC * (N + 1), n32, SC.start0);
+      SC.laid = true;
+    }
+    if (PP.live) {
+      HIPCHK(hipMemsetAsync(cap_pp, 0, P * sizeof(uint32_t), stream));
+      elcl::caps(stream, bpp_s, bpp_e, p32, nullptr, nullptr, cap_pp, nullptr);
+      launch_gap_scan(cap_pp, p32, PP.start0);
+      PP.laid = true;
+    }
+  }
   for (GapCsr* g : {&PR, &SC, &PP}) {
     if (!g->live) continue;
     hipLaunchKernelGGL(k_gap_init, dim3(grid_for(g->rows + 1)), dim3(BLOCK), 0, stream, g->start, g->len, g->rows,
-                       g->start0);
+                       g->laid ? g->start0 : nullptr);
     HIPCHK(hipGetLastError());
   }
 }
 
+// The base links {(X, p) : p ∈ exr*(X)} — what CR3 derives from the init facts X ∈ S(X) in the
+// first superstep — installed before it (el_saturate of a fresh state): el_init left them in the
+// head of the link log (X order) and sorted by pid; here the predecessor rows take them
+// (pid-major), the successor rows their chain-second ones, and the link set gets them beside
+// the first superstep, which finds them by a binary search of exr*(X) meanwhile (link_known).
+// The base propagations likewise (the CR4 half-1 records of the init facts, pulled by the
+// base links in the first superstep).  The first superstep then expands the base links, which
+// the second did before; its queues start at what the second got.  The CPU oracle installs the
+// same links (el_oracle.c, base_links).
 void el_ctx::install_base() {
-  const uint64_t nb = hx.exr.a.size();
-  if (pre_base) {  // enqueued behind the last copy-back (enqueue_base): account for it only
-    pre_base = false;
-    const uint64_t nbp = hx.bpp.a.size();
-    const bool props = nbp && use_props && PP.live && PP.start0;
-    const uint64_t trig = s_count + nb;
-    if (!small_queues) {
-      if (const uint64_t want = std::min<uint64_t>(4 * trig, 1ull << 28); want > cs_cap) {
-        sync();
-        cs_cap = next_pow2(want);
-        dfree(cs_x);
-        dfree(cs_a);
-        cs_x = dalloc<uint32_t>(cs_cap);
-        cs_a = dalloc<uint32_t>(cs_cap);
-      }
-      if (const uint64_t want = std::min<uint64_t>(trig, 1ull << 26); want > job_cap) {
-        sync();
-        job_cap = next_pow2(want);
-        dfree(jobs);
-        jobs = dalloc<uint4>(job_cap);
-      }
-    }
-    launches[EL_K_INIT] += 1 + (PR.live ? 1 : 0) + (SC.live && hx.exrC.a.size() ? 1 : 0) + (props ? 1 : 0);
-    if (props) {
-      p_count = p_base = nbp;
-      for (int r = 0; r < EL_NUM_RULE_TYPES; ++r) wm_p[r] = nbp;
-      host_ev[EL_K_INIT][EL_EV_ENT] += 2 * nbp;
-      host_ev[EL_K_INIT][EL_EV_EMIT] += nbp;
-    }
-    base_filling = true;
-    l_count = l_base = nb;
-    ix.base = 1;
-    host_ev[EL_K_INIT][EL_EV_ENT] += nb + (PR.live ? nb : 0) + (SC.live ? hx.exrC.a.size() : 0);
-    host_ev[EL_K_INIT][EL_EV_EMIT] += nb;
-    return;
-  }
-  if (nb == 0 || l_count != 0 || (PR.live && !PR.start0) || (SC.live && !SC.start0)) return;
+  if (nb == 0 || l_count != 0 || part()) return;
   const uint64_t trig = s_count + nb;
   if (!small_queues) {
     if (const uint64_t want = std::min<uint64_t>(4 * trig, 1ull << 28); want > cs_cap) {
@@ -4081,64 +4005,20 @@ void el_ctx::install_base() {
       jobs = dalloc<uint4>(job_cap);
     }
   }
-  if (nb + cl_cap > llog_cap) {
-    sync();
-    llog_cap = next_pow2(nb + cl_cap + (nb + cl_cap) / 2);
-    dgrow(llog_x, 0, llog_cap);
-    dgrow(llog_p, 0, llog_cap);
-  }
-  // the link set takes the base links during the first superstep: room for them and the
-  // second superstep's candidates now (an empty set: no re-insertion)
-  if (2 * (nb + cl_cap) > lhash_cap) rehash_links(next_pow2(2 * (nb + cl_cap)));
-  const uint32_t N = hx.N, P = hx.P, nc = (uint32_t)hx.exrC.a.size();
-  // k_csr_scatter shape: up to 2048 blocks, 1..16 entries per lane and round
-  auto items = [](uint64_t n) { return (uint32_t)std::min<uint64_t>(16, std::max<uint64_t>(1, n / (2048 * 256))); };
-  auto grid = [&](uint64_t n) {
-    const uint64_t t = 256ull * items(n);
-    return (uint32_t)std::min<uint64_t>(2048, std::max<uint64_t>(1, (n + t - 1) / t));
-  };
-  launch(EL_K_INIT, [&] {
-    hipLaunchKernelGGL(k_csr_scatter, dim3(grid(nb)), dim3(256), 0, stream, ix.exr_ptr, ix.exr_pid, N, (uint32_t)nb,
-                       llog_x, llog_p, nullptr, nullptr, items(nb));
-  });
-  if (PR.live)
-    launch(EL_K_INIT, [&] {
-      hipLaunchKernelGGL(k_gap_len, dim3(grid(P)), dim3(256), 0, stream, exrT_ptr, P, PR.len);
-      hipLaunchKernelGGL(k_csr_scatter, dim3(grid(nb)), dim3(256), 0, stream, exrT_ptr, exrT_x, P, (uint32_t)nb,
-                         nullptr, nullptr, PR.start, PR.val, items(nb));
-    });
-  if (SC.live && nc)
-    launch(EL_K_INIT, [&] {
-      hipLaunchKernelGGL(k_gap_len, dim3(grid(N)), dim3(256), 0, stream, exrC_ptr, N, SC.len);
-      hipLaunchKernelGGL(k_csr_scatter, dim3(grid(nc)), dim3(256), 0, stream, exrC_ptr, exrC_p, N, nc, nullptr,
-                         nullptr, SC.start, SC.val, items(nc));
-    });
+  const uint32_t P = hx.P;
   hipLaunchKernelGGL(k_set_u32, dim3(1), dim3(1), 0, stream, &ctr->l_log, (uint32_t)nb);
   HIPCHK(hipGetLastError());
-  // The link set gets the base links beside the first superstep (a second stream; that
-  // superstep finds them by binary search and inserts only other links, and concurrent
-  // inserts of distinct keys are safe); the second superstep waits for it (join_base) and
-  // from then on membership is one probe of the set, as for every other link.
-  // Base propagations likewise (the CR4 half-1 records of the init facts, bpp): the log, the
-  // propagation rows (presized for them), the set beside the first superstep.  That superstep's
-  // base links then pull them (CR4 half-2, per link, X-major) instead of the init facts' fresh
-  // propagations fanning out over the base predecessors.
-  const uint64_t nbp = hx.bpp.a.size();
-  const bool props = nbp && use_props && PP.live && PP.start0;
-  if (props) {
-    if (nbp + cp_cap > plog_cap) {
-      sync();
-      plog_cap = next_pow2(nbp + cp_cap + (nbp + cp_cap) / 2);
-      dgrow(plog_p, 0, plog_cap);
-      dgrow(plog_b, 0, plog_cap);
-    }
-    if (2 * (nbp + cp_cap) > phash_cap) rehash_props(next_pow2(2 * (nbp + cp_cap)));
+  if (PR.live)
     launch(EL_K_INIT, [&] {
-      hipLaunchKernelGGL(k_csr_scatter, dim3(grid(nbp)), dim3(256), 0, stream, ix.bpp_ptr, ix.bpp_b, P, (uint32_t)nbp,
-                         plog_p, plog_b, nullptr, nullptr, items(nbp));
-      hipLaunchKernelGGL(k_gap_len, dim3(grid(P)), dim3(256), 0, stream, ix.bpp_ptr, P, PP.len);
-      hipLaunchKernelGGL(k_csr_scatter, dim3(grid(nbp)), dim3(256), 0, stream, ix.bpp_ptr, ix.bpp_b, P, (uint32_t)nbp,
-                         nullptr, nullptr, PP.start, PP.val, items(nbp));
+      elcl::group_fill(stream, sk, sv, (uint32_t)nb, pr_first, PR.start, PR.val);
+      elcl::caps(stream, pr_first, pr_last, P, nullptr, nullptr, nullptr, PR.len);
+    });
+  if (SC.live && nc) launch(EL_K_INIT, [&] { elcl::succ_fill(stream, cax, cl, lo, hi, SC.start, SC.len, SC.val); });
+  const bool props = nbp && use_props && PP.live;
+  if (props) {
+    launch(EL_K_INIT, [&] {
+      elcl::group_fill(stream, plog_p, plog_b, (uint32_t)nbp, bpp_s, PP.start, PP.val);
+      elcl::caps(stream, bpp_s, bpp_e, P, nullptr, nullptr, nullptr, PP.len);
     });
     hipLaunchKernelGGL(k_set_u32, dim3(1), dim3(1), 0, stream, &ctr->p_log, (uint32_t)nbp);
     HIPCHK(hipGetLastError());
@@ -4147,6 +4027,10 @@ void el_ctx::install_base() {
     host_ev[EL_K_INIT][EL_EV_ENT] += 2 * nbp;
     host_ev[EL_K_INIT][EL_EV_EMIT] += nbp;
   }
+  // The link set gets the base links beside the first superstep (a second stream; that
+  // superstep finds them by binary search and inserts only other links, and concurrent
+  // inserts of distinct keys are safe); the second superstep waits for it (join_base) and
+  // from then on membership is one probe of the set, as for every other link.
   HIPCHK(hipEventRecord(ev_base[0], stream));
   HIPCHK(hipStreamWaitEvent(rstream, ev_base[0], 0));
   hipLaunchKernelGGL(k_rehash, dim3(grid_for(nb, 2048)), dim3(BLOCK), 0, rstream, lhash, lhash_cap - 1, llog_x, llog_p,
@@ -4160,7 +4044,7 @@ void el_ctx::install_base() {
   l_count = l_base = nb;
   ix.base = 1;
   // the log entries read and written, the rows' entries
-  host_ev[EL_K_INIT][EL_EV_ENT] += nb + (PR.live ? nb : 0) + (SC.live ? hx.exrC.a.size() : 0);
+  host_ev[EL_K_INIT][EL_EV_ENT] += nb + (PR.live ? nb : 0) + (SC.live ? nc : 0);
   host_ev[EL_K_INIT][EL_EV_EMIT] += nb;
 }
 
@@ -4179,9 +4063,6 @@ void el_ctx::join_base() {
 void el_ctx::migrate_state(uint32_t N0, const std::vector<uint32_t>& pmap) {
   const uint64_t N = hx.N, P = hx.P, W0 = W, W1 = ix.W;  // (column_window of the new index)
   sync();
-  dfree(lsnap);  // base-set snapshots of the old index
-  dfree(psnap);
-  lsnap_cap = psnap_cap = 0;
   if (N != N0) {  // wider bit rows, more rows: pitched copy of the old matrix
     uint32_t* nb = dalloc<uint32_t>(N * W1);
     HIPCHK(hipMemsetAsync(nb, 0, N * W1 * sizeof(uint32_t), stream));
@@ -4244,8 +4125,15 @@ void el_ctx::migrate_state(uint32_t N0, const std::vector<uint32_t>& pmap) {
     PP.alloc((uint32_t)P, cp_cap + remote_bound());
     gap_build_from_log(PP, plog_p, plog_b, p_count);
   }
-  // the first superstep re-emits the told closure of every fact it re-triggers
-  const uint64_t ct_need = next_pow2(2 * (uint64_t)hx.told.a.size() + 1024);
+  // the told closure of the new index (every concept's: old closures may have grown), with the
+  // counts of the new concepts' init facts
+  free_closure();
+  alloc_closure();
+  closure_rows(N0, (uint32_t)N);
+  set_closure_ix();
+  // the first superstep re-emits the told closure of every fact it re-triggers (the row
+  // array's fill bounds the closures' total)
+  const uint64_t ct_need = next_pow2(2 * (uint64_t)clt.t_tail + 1024);
   if (ct_need > ct_cap) {
     dfree(ct_x);
     dfree(ct_a);
@@ -4255,8 +4143,31 @@ void el_ctx::migrate_state(uint32_t N0, const std::vector<uint32_t>& pmap) {
   }
   // every logged fact re-expands its told closure once (the closures may have grown)
   if (s_count) HIPCHK(hipMemsetAsync(slog_f, 0, s_count, stream));
-  // S(X) = {X, ⊤} ∪ told*(X) for the new concepts
-  if (N > N0) init_rows(N0, (uint32_t)N);
+  // S(X) = {X, ⊤} ∪ told*(X) for the new concepts, appended to the fact log
+  if (N > N0) {
+    const unsigned long long* T = clt.tot;
+    const uint64_t n = T[elcl::T_INIT];
+    if (s_count + n + cs_cap + ct_cap > slog_cap) {
+      const uint64_t c = next_pow2(s_count + n + cs_cap + ct_cap);
+      dgrow(slog_x, s_count, c);
+      dgrow(slog_a, s_count, c);
+      dgrow(slog_f, s_count, c);
+      slog_cap = c;
+    }
+    check_u32_room();
+    DState st = dstate();
+    launch(EL_K_INIT, [&] {
+      elcl::init_facts(stream, cax, cl, N0, (uint32_t)N, cpos[0], (uint32_t)s_count, slog_x, slog_a, slog_f, st.bits, W,
+                       ix.c_lo, ix.c_hi, st.summ, SB);
+    });
+    s_count += n;
+    s_init += T[elcl::T_OWN] + T[elcl::T_TWO];
+    hipLaunchKernelGGL(k_set_u32, dim3(1), dim3(1), 0, stream, &ctr->s_log, (uint32_t)s_count);
+    HIPCHK(hipGetLastError());
+    host_ev[EL_K_INIT][EL_EV_ENT] += T[elcl::T_OWN] + T[elcl::T_TOLD];
+    host_ev[EL_K_INIT][EL_EV_RMW] += n;
+    host_ev[EL_K_INIT][EL_EV_EMIT] += n;
+  }
   // every log re-triggers once against the new axioms, then the saturation is semi-naive again
   for (int r = 0; r < EL_NUM_RULE_TYPES; ++r) wm_s[r] = wm_l[r] = wm_a[r] = wm_p[r] = 0;
   wm_x = 0;
@@ -4501,7 +4412,6 @@ int el_add_axioms(el_ctx* c, const el_axioms* inc) {
     el::HostIndex hx;
     if (e.empty()) e = el::build_index(store.view(), hx, c->flags);
     if (!e.empty()) return fail(c, EL_EINVAL, e);
-    c->undo_base();  // (base links enqueued for a saturation of the old index)
     c->sync();
     if (!c->inited) {  // nothing saturated yet: a plain reload
       c->free_state();
@@ -4538,7 +4448,8 @@ int el_init(el_ctx* c) {
   if (!c->loaded) return fail(c, EL_ESTATE, "el_init before el_load");
   return guarded(c, [&] {
     c->reset_state();
-    c->init_rows(c->lo, c->hi);
+    c->closure_rows(c->lo, c->hi);  // told*, exr*, exl* of every concept (el_closure.h)
+    c->closure_state();             // the init facts; base links / propagations, row layouts
     c->fresh = true;
     c->inited = true;
     c->stats_stale = true;
@@ -4553,7 +4464,6 @@ int el_step(el_ctx* c, el_rule rule, int* changed) {
   return guarded(c, [&] {
     const int r = (int)rule;
     c->fresh = false;  // per-rule stepping derives every link (DistEL's granularity)
-    c->undo_base();
     const uint64_t se = c->s_count, le = c->l_count, ae = c->a_count, pe = c->p_count;
     bool ch = c->superstep(kRuleMask[r], c->wm_s[r], se, c->wm_l[r], le, c->wm_a[r], ae, c->wm_p[r], pe);
     c->wm_s[r] = se;
@@ -4871,9 +4781,7 @@ int el_copy_result(el_ctx* c, el_result* res) {
       HIPCHK(hipStreamWaitEvent(c->rstream, c->ev_rows[1], 0));
       // rows the S-row sorts (all rows) or the read-out (the caller's rows) cleared as they went
       const uint32_t clear_from = parts[1].readout ? c->uhi() : fuse_clear && parts[1].direct ? c->hi : c->lo;
-      const bool base = c->base_fits();
-      c->reset_device(c->rstream, clear_from, parts[1].readout ? c->uhi() : c->lo, base && !c->no_snap);
-      c->pre_base = base && c->enqueue_base(c->rstream);
+      c->reset_device(c->rstream, clear_from, parts[1].readout ? c->uhi() : c->lo);
       HIPCHK(hipEventRecord(c->ev_reset, c->rstream));
     }
     // 2. the sorts into the caller's buffers, the device rows by DMA

@@ -208,33 +208,12 @@ std::string build_index(const el_axioms& ax_in, HostIndex& o, uint32_t flags) {
       CHECK(bad_c(ax.sub_a[i]) || bad_c(ax.sub_b[i]), "sub", i);
       if (ax.sub_a[i] != ax.sub_b[i]) t.push_back({ax.sub_a[i], ax.sub_b[i], 0});
     }
-    // CR1 fires the whole told closure at once: a new A ∈ S(X) emits every B reachable from
-    // A over A ⊑ B axioms, so a taxonomy of depth d costs one superstep instead of d
-    // (facts that came out of a closure are not re-expanded: their closure is a subset).
-    const Csr told = make_csr(N, t, false);
-    std::vector<uint32_t> stamp(N, 0), queue;
-    queue.reserve(64);
-    o.told.ptr.assign(N + 1, 0);
-    o.told.a.clear();
-    for (uint32_t a = 0; a < N; ++a) {
-      const size_t base = o.told.a.size();
-      queue.clear();
-      queue.push_back(a);
-      stamp[a] = a + 1;
-      for (size_t h = 0; h < queue.size(); ++h) {
-        const uint32_t u = queue[h];
-        for (uint32_t j = told.ptr[u]; j < told.ptr[u + 1]; ++j) {
-          const uint32_t v = told.a[j];
-          if (stamp[v] == a + 1) continue;
-          stamp[v] = a + 1;
-          queue.push_back(v);
-          o.told.a.push_back(v);
-        }
-      }
-      std::sort(o.told.a.begin() + base, o.told.a.end());
-      if (o.told.a.size() > 0xffffffffull) return "told closure beyond 2^32 entries";
-      o.told.ptr[a + 1] = (uint32_t)o.told.a.size();
-    }
+    // CR1 fires the whole told closure at once (a new A ∈ S(X) emits every B reachable from
+    // A), but the closure itself is derived per classification on the device (el_closure.h,
+    // Kahn levels over this DAG): here only the told rows and their transpose.
+    o.told = make_csr(N, t, false);
+    for (auto& e : t) std::swap(e[0], e[1]);
+    o.toldT = make_csr(N, t, false);
   }
   // CR2 conjunctions: operands sorted/unique per conjunction, conj ids in input order
   {
@@ -335,36 +314,6 @@ std::string build_index(const el_axioms& ax_in, HostIndex& o, uint32_t flags) {
     }
     o.exl = make_csr(N, t, true);
   }
-  // CR3 and CR4 half-1 over the told closure: row A holds the entries of every
-  // B ∈ {A} ∪ told*(A).  A fact A new in S(X) then emits the links / propagations of its
-  // whole closure in the superstep that emits the closure itself, and the closure's facts
-  // (flagged) skip CR3 / CR4 half-1: one superstep less on every CR4 -> CR1 -> CR3 path.
-  {
-    auto star = [&](const Csr& c, bool two) {
-      Csr s;
-      s.ptr.assign(N + 1, 0);
-      std::vector<uint64_t> row;
-      for (uint32_t a = 0; a < N; ++a) {
-        row.clear();
-        auto add = [&](uint32_t u) {
-          for (uint32_t j = c.ptr[u]; j < c.ptr[u + 1]; ++j)
-            row.push_back(((uint64_t)c.a[j] << 32) | (two ? c.b[j] : 0u));
-        };
-        add(a);
-        for (uint32_t j = o.told.ptr[a]; j < o.told.ptr[a + 1]; ++j) add(o.told.a[j]);
-        std::sort(row.begin(), row.end());
-        row.erase(std::unique(row.begin(), row.end()), row.end());
-        for (uint64_t v : row) {
-          s.a.push_back((uint32_t)(v >> 32));
-          if (two) s.b.push_back((uint32_t)v);
-        }
-        s.ptr[a + 1] = (uint32_t)s.a.size();
-      }
-      return s;
-    };
-    o.exr = star(o.exr, false);
-    o.exl = star(o.exl, true);
-  }
   // CR5 per pair: pids of (s, Y) for every strict super-role s of r
   {
     std::vector<std::array<uint32_t, 3>> t;
@@ -400,40 +349,19 @@ std::string build_index(const el_axioms& ax_in, HostIndex& o, uint32_t flags) {
     o.dom = make_csr(R, d, false);
     o.rng = make_csr(R, g, false);
   }
-  // Base links: the links of the told closure, {(X, p) : p ∈ exr(X)} — the first superstep
-  // would derive all of them from the init facts X ∈ S(X).  el_init writes them directly:
-  // the link log in X order (exr itself), the predecessor rows from exrT (pid -> X, the
-  // transpose), the successor rows from exrC (X -> its chain-second pids).
+  // successor-row weights: a base link (X, p) of a chain-second role lands in X's successor
+  // row, and so do its CR5 lifts of such roles one step later (the device presizes the rows)
   {
-    o.exrT.ptr.assign(o.P + 1, 0);
-    for (uint32_t p : o.exr.a) o.exrT.ptr[p + 1]++;
-    for (uint32_t p = 0; p < o.P; ++p) o.exrT.ptr[p + 1] += o.exrT.ptr[p];
-    o.exrT.a.resize(o.exr.a.size());
-    std::vector<uint32_t> fill(o.exrT.ptr.begin(), o.exrT.ptr.end() - 1);
-    for (uint32_t x = 0; x < N; ++x)  // X ascending: every transposed row is sorted
-      for (uint32_t j = o.exr.ptr[x]; j < o.exr.ptr[x + 1]; ++j) o.exrT.a[fill[o.exr.a[j]]++] = x;
-    std::vector<uint8_t> second(R, 0);  // roles second in an indexed chain (the rows CR6 reads)
+    std::vector<uint8_t> second(R, 0);
     for (uint32_t r = 0; r < R; ++r) second[r] = o.chs.ptr[r + 1] > o.chs.ptr[r];
-    o.exrC.ptr.assign(N + 1, 0);
-    for (uint32_t x = 0; x < N; ++x) {
-      for (uint32_t j = o.exr.ptr[x]; j < o.exr.ptr[x + 1]; ++j)
-        if (second[o.pair_role[o.exr.a[j]]]) o.exrC.a.push_back(o.exr.a[j]);
-      o.exrC.ptr[x + 1] = (uint32_t)o.exrC.a.size();
+    o.sc_self.assign(o.P, 0);
+    o.sc_w.assign(o.P, 0);
+    for (uint32_t p = 0; p < o.P; ++p) {
+      uint32_t w = o.sc_self[p] = second[o.pair_role[p]];
+      for (uint32_t k = o.psup.ptr[p]; k < o.psup.ptr[p + 1]; ++k) w += second[o.pair_role[o.psup.a[k]]];
+      o.sc_w[p] = w;
     }
   }
-  // Base propagations: the CR4 half-1 records every init fact Y ∈ S(Y) makes over its told
-  // closure, {((r, Y), B) : (r, B) ∈ exl(Y), (r, Y) a pair} — installed with the base links.
-  // Rows by pid: Y ascending and exl(Y) sorted by (r, B), pids sorted by (Y, r), so the rows
-  // come out pid-major with B ascending and unique.
-  o.bpp.ptr.assign(o.P + 1, 0);
-  for (uint32_t y = 0; y < N; ++y)
-    for (uint32_t j = o.exl.ptr[y]; j < o.exl.ptr[y + 1]; ++j) {
-      const uint32_t pid = pid_of(o.exl.a[j], y);
-      if (pid == 0xffffffffu) continue;
-      o.bpp.a.push_back(o.exl.b[j]);
-      o.bpp.ptr[pid + 1]++;
-    }
-  for (uint32_t p = 0; p < o.P; ++p) o.bpp.ptr[p + 1] += o.bpp.ptr[p];
 #undef CHECK
   return "";
 }

@@ -26,12 +26,13 @@ struct HostIndex {
   uint32_t P = 0;   // (role, filler) pairs = link targets
   std::vector<uint8_t> kind;          // EntityType digit per concept
 
-  Csr told;       // A -> B, B ∈ told*(A)        CR1  (transitive closure of A ⊑ B, B != A)
+  Csr told;       // A -> B of told A ⊑ B (B != A), sorted    CR1 (the closure is built on the device)
+  Csr toldT;      // B -> A of told A ⊑ B: the transpose (the device closure's Kahn levels)
   Csr cidx;       // A -> conj id c              CR2  conjunct index (AxiomLoader.java:931-941, DB3)
   Csr conj;       // c -> operands (sorted)      CR2
   std::vector<uint32_t> conj_b;     // c -> B
-  Csr exr;        // A -> pid of A' ⊑ ∃r.B, A' ∈ {A} ∪ told*(A)          CR3 (over the told closure)
-  Csr exl;        // A -> (r, B) of ∃r.A' ⊑ B, A' ∈ {A} ∪ told*(A), sorted   CR4 half-1 (idem)
+  Csr exr;        // A -> pid of A ⊑ ∃r.B, sorted unique                 CR3 (told axioms only)
+  Csr exl;        // A -> (r, B) of ∃r.A ⊑ B, sorted by (r, B), unique   CR4 half-1 (idem)
   std::vector<uint32_t> fp_ptr;     // Y -> pid range (pairs sorted by (Y, r))
   std::vector<uint32_t> pair_role;  // pid -> r
   std::vector<uint32_t> pair_y;     // pid -> Y
@@ -41,9 +42,10 @@ struct HostIndex {
   Csr dom;        // r -> D
   Csr rng;        // r -> C
   std::vector<uint8_t> role_has_exl;  // r -> any ∃r.A ⊑ B
-  Csr exrT;       // pid -> X with pid ∈ exr(X), X ascending      base links by predecessor
-  Csr exrC;       // X -> pids of exr(X) whose role is second in a chain   base links by successor
-  Csr bpp;        // pid = (r, Y) -> B with (r, B) ∈ exl(Y), ascending        base propagations
+  // per pid: its role is second in a chain (its links feed the successor rows), and that count
+  // plus the same for its CR5 lifts (the successor-row capacity one base link asks for)
+  std::vector<uint8_t> sc_self;
+  std::vector<uint32_t> sc_w;
 };
 
 // Owned copy of the typed axioms (el_load copies its input; el_add_axioms appends an
@@ -57,8 +59,11 @@ struct AxiomStore {
   el_axioms view() const;
 };
 
-// Validates ids and builds the canonical indexes.  Returns "" on success or an
-// error message (the reference throws on unknown concepts, AxiomLoader.java:1343-1354).
+// Validates ids and builds the canonical indexes of the axioms as told: rows of the typed
+// axioms the way AxiomLoader.java:959-1132 keys them, plus the role tables (role hierarchy
+// closure, pair universe, chains).  Nothing here depends on a concept closure: told*(A) and
+// the rows over it are classification work (el_closure.h).  Returns "" on success or an error
+// message (the reference throws on unknown concepts, AxiomLoader.java:1343-1354).
 // flags: el_config.flags (EL_FLAG_COMPAT_DISTEL_CHAIN indexes the DistEL chain set).
 std::string build_index(const el_axioms& ax, HostIndex& out, uint32_t flags = 0);
 

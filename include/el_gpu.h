@@ -42,7 +42,7 @@
 extern "C" {
 #endif
 
-#define EL_ABI_VERSION 4
+#define EL_ABI_VERSION 5
 
 /* return codes */
 #define EL_OK        0
@@ -195,12 +195,13 @@ typedef enum el_kernel {
   EL_K_MERGE_PTR = 8,    /*   … and their scan into new row starts (library scan, carried by k_gap_caps) */
   EL_K_SCATTER_OLD = 9,  /* k_gap_move: in-place entries to their new rows */
   EL_K_SCATTER_NEW = 10, /* k_gap_ovf: overflow entries placed at their rank */
-  EL_K_INIT = 11,        /* k_init:      S(X) = {X, ⊤} */
+  EL_K_INIT = 11,        /* k_init_facts: S(X) = {X, ⊤} ∪ told*(X); the base links / propagations */
   EL_K_REHASH = 12,      /* k_rehash:    link / activation / propagation set growth */
   EL_K_EXPAND_P = 13,    /* k_expand, propagation role: new CR4 propagations × predecessors */
   EL_K_COMMIT_P = 14,    /* k_commit, propagation role: CR4 propagation set dedup ("Yr" -> B) */
   EL_K_COMMIT_T = 15,    /* k_commit_told: CR1 told-closure candidates, committed first */
-  EL_NUM_KERNELS = 16
+  EL_K_CLOSURE = 16,     /* k_level / k_relax: the told closure rows told*, exr*, exl* (el_init) */
+  EL_NUM_KERNELS = 17
 } el_kernel;
 
 /* Algorithmic event counters; identical in the CPU oracle. */

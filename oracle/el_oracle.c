@@ -224,6 +224,8 @@ struct elo_ctx {
   /* indexes */
   csr told, cidx, conj, exr, exl, psup, chf, chs, dom, rng;
   csr toldc;        /* told closure: A -> every B reachable over A ⊑ B axioms (B != A) */
+  uint32_t *xr_n, *xl_n; /* per A: its own A ⊑ ∃r.B pairs / ∃r.A ⊑ B entries (before the closure) */
+  uint32_t* nsub;        /* per B: told subs A ⊑ B */
   uint32_t* conj_b;
   uint32_t *fp_ptr, *pair_role, *pair_y;
   uint8_t* role_has_exl;
@@ -494,6 +496,14 @@ static int build_index(elo_ctx* c, const el_axioms* ax) {
     c->role_has_exl[ax->exl_r[i]] = 1;
   }
   c->exl = csr_build(N, t, n);
+  c->xr_n = (uint32_t*)calloc(N, sizeof(uint32_t));
+  c->xl_n = (uint32_t*)calloc(N, sizeof(uint32_t));
+  c->nsub = (uint32_t*)calloc(N, sizeof(uint32_t));
+  for (i = 0; i < N; ++i) {
+    c->xr_n[i] = c->exr.ptr[i + 1] - c->exr.ptr[i];
+    c->xl_n[i] = c->exl.ptr[i + 1] - c->exl.ptr[i];
+    for (j = c->told.ptr[i]; j < c->told.ptr[i + 1]; ++j) c->nsub[c->told.a[j]]++;
+  }
   /* CR3 / CR4 half-1 over the told closure (el_index.cpp): row A gathers the rows of every
    * B ∈ {A} ∪ told*(A), sorted and unique, so a fact emits its closure's links and
    * propagations in the superstep that emits the closure; closure facts skip both rules */
@@ -1255,10 +1265,34 @@ static int naive_saturate(elo_ctx* c) {
 
 /* ------------------------------------------------------------------ API */
 
+/* The device builds told*, exr*, exl* per classification (el_closure.hip, Kahn levels: each
+ * concept merges its told supers' rows); its events by the algorithm's definition, per concept
+ * A: one trigger; rows: its supers, its subs, its own exr / exl rows, the three rows of every
+ * super; entries: the supers, the subs, the rows gathered (the supers' rows, its own axioms)
+ * and the rows written; one pending-count decrement per sub. */
+static void closure_events(elo_ctx* c) {
+  uint32_t A, j;
+#define RL(cs, x) ((uint64_t)((cs).ptr[(x) + 1] - (cs).ptr[(x)]))
+  for (A = 0; A < c->N; ++A) {
+    uint64_t np = RL(c->told, A), g = 0;
+    for (j = c->told.ptr[A]; j < c->told.ptr[A + 1]; ++j) {
+      uint32_t p = c->told.a[j];
+      g += RL(c->toldc, p) + RL(c->exr, p) + 2 * RL(c->exl, p);
+    }
+    EV(EL_K_CLOSURE, EL_EV_TRIG);
+    EVN(EL_K_CLOSURE, EL_EV_ROW, 4 + 3 * np);
+    EVN(EL_K_CLOSURE, EL_EV_ENT, np + c->nsub[A] + g + c->xr_n[A] + 2ull * c->xl_n[A] + RL(c->toldc, A) + RL(c->exr, A) +
+                                     2 * RL(c->exl, A));
+    EVN(EL_K_CLOSURE, EL_EV_RMW, c->nsub[A]);
+  }
+#undef RL
+}
+
 int elo_init(elo_ctx* c) {
   uint32_t x;
   if (!c) return EL_EINVAL;
   uint64_t init = 0;
+  closure_events(c);
   /* S(X) = {X, ⊤} (classes, individuals) and the told closure of X, flagged — what CR1 would
    * derive from the init fact in the first superstep (k_init on the GPU) */
   for (x = 0; x < c->N; ++x) {
@@ -1545,6 +1579,7 @@ void elo_destroy(elo_ctx* c) {
   free(c->conj.ptr), free(c->conj.a), free(c->conj_b);
   free(c->fp_ptr), free(c->pair_role), free(c->pair_y), free(c->role_has_exl);
   free(c->supers_ptr), free(c->supers), free(c->kind), free(c->bits);
+  free(c->xr_n), free(c->xl_n), free(c->nsub);
   if (c->srow)
     for (i = 0; i < c->N; ++i) free(c->srow[i].v);
   if (c->succ)

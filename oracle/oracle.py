@@ -18,7 +18,7 @@ import numpy as np
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB = os.path.join(HERE, "libel_oracle.so")
 
-NUM_KERNELS = 16
+NUM_KERNELS = 17
 NUM_EVENTS = 8
 
 _lib = None
