@@ -2,17 +2,18 @@
 """Benchmark: EL+ classification (DistEL hot path) on MI355X.
 
 One "step" = one full classification of the workload as SURVEY.md §8(d) defines the
-metric: from the axiom indexes resident in HBM (IR-in-HBM) to the fixpoint PLUS the
-result copy-back — el_init (S(X) = {X, ⊤}) + el_saturate + el_copy_result (the result
-rows X -> {B} and the role links X -> {(r, Y)} as CSR into page-locked host buffers).
-``value`` = derived axioms per second over all ranks (D = Σ|S(X)| − init facts + Σ|R(r)|).
-Default workload: G3, the SNOMED-shaped generator = BASELINE.json configs[2], the largest
-config that fits one GPU.  Two engines (each with its own state and result buffers)
-alternate: one classification's copy-back is enqueued asynchronously (EL_RESULT_ASYNC) and
-crosses PCIe while the other engine saturates, so ``ms_per_step`` = wall time of K complete
-classifications (the last copy-backs drained inside the timed region) ÷ K.  ``latency_ms`` is
-one classification with its copy-back and nothing beside it (``saturate_ms`` + ``copyback_ms``);
-``--inflight 1`` times that serial schedule.
+metric: from the typed axioms resident in HBM (IR-in-HBM: the told axiom rows el_load
+uploads, AxiomLoader's layout) to the fixpoint PLUS the result copy-back — el_init (the told
+closure, its exr*/exl* rows, S(X) = {X, ⊤} ∪ told*(X), base links: all derived on the device
+inside the step) + el_saturate + el_copy_result (the result rows X -> {B} and the role links
+X -> {(r, Y)} as CSR into page-locked host buffers).  Nothing derived is carried from one
+step to the next.  ``value`` = derived axioms per second over all ranks (D = Σ|S(X)| − init
+facts + Σ|R(r)|).  Default workload: G3, the SNOMED-shaped generator = BASELINE.json
+configs[2], the largest config that fits one GPU.  Steps run one at a time, so
+``ms_per_step`` = ``classification_wall_s`` = the wall-clock of one classification, copy-back
+included (``init_ms`` + ``saturate_ms`` + ``copyback_ms`` split it).  ``throughput_inflight2``
+is a separately named figure: two engines (each with its own state and result buffers)
+alternate, one's copy-back (EL_RESULT_ASYNC) crossing PCIe while the other classifies.
 
 Multi-GPU (``torch.distributed.run``): weak scaling.  Rank i classifies its own
 disjoint copy of the workload (OntologyMultiplier ×N semantics, the G4 config);
@@ -114,9 +115,16 @@ def parse():
     ap.add_argument("--partition", default="copies", choices=["copies", "exchange"],
                     help="copies: one disjoint copy per rank, no collective; exchange: row-partitioned "
                          "engine over the ×N ontology with the RCCL delta all-gather")
-    ap.add_argument("--inflight", type=int, default=2, choices=[1, 2],
-                    help="classifications in flight: 2 = two engines alternate, one's result copy-back "
-                         "(EL_RESULT_ASYNC) rides over PCIe under the other's saturation; 1 = serial")
+    ap.add_argument("--inflight", type=int, default=1, choices=[1, 2],
+                    help="classifications in flight in the timed loop: 1 = one at a time (the default: "
+                         "ms_per_step is one classification's wall-clock); 2 = two engines alternate, one's "
+                         "result copy-back (EL_RESULT_ASYNC) rides over PCIe under the other's classification")
+    ap.add_argument("--copyback", default="stream", choices=["stream", "rows"],
+                    help="stream: the result node's facts and links cross PCIe as the supersteps commit them "
+                         "(el_stream_result; pairs in commit order); rows: after the fixpoint, as sorted CSR rows "
+                         "X -> {B} (el_copy_result)")
+    ap.add_argument("--no-throughput2", action="store_true",
+                    help="skip the separately reported two-in-flight throughput loop")
     ap.add_argument("--verbose", action="store_true")
     return ap.parse_args()
 
@@ -159,76 +167,84 @@ def main():
         eng.load(ax)  # host index build + upload: AxiomLoader's part, reported separately
         load_s = time.time() - t0
 
+    def timed(engines, steps, warmup):
+        """K classifications between barriers.  One engine: each step runs init + saturate +
+        copy-back to the end before the next starts.  Two engines: they alternate; a helper
+        thread enqueues one engine's copy-back (EL_RESULT_ASYNC; it waits ~1 ms on the device for
+        the row counts) while this thread starts the other's classification (ctypes drops the
+        GIL inside the library, and the two threads never share an engine); drain() waits for
+        the last copy-backs inside the timed region."""
+        stream = args.copyback == "stream"
+        results = [engine.Stream() if stream else engine.Result() for _ in engines]  # page-locked, reused
+        split = []  # (init, saturate, copy-back) seconds per step; the last `steps` are the timed ones
+        turn = [0]
+        pool = ThreadPoolExecutor(max_workers=1) if len(engines) == 2 else None
+        copying = [None] * len(engines)
+
+        def classify():
+            i = turn[0] % len(engines)
+            turn[0] += 1
+            e, res = engines[i], results[i]
+            if copying[i] is not None:
+                copying[i].result()  # (the enqueue finished long ago; errors surface here)
+                copying[i] = None
+            t0 = time.perf_counter()
+            e.init()
+            t1 = time.perf_counter()
+            if stream:  # the result crosses PCIe while the supersteps run
+                e.stream_result(res, release=True)
+            st = e.saturate()
+            t2 = time.perf_counter()
+            if stream:
+                if pool is None:
+                    e.result_wait()  # (two in flight: the next turn of this engine, or drain(), waits)
+            elif pool is None:
+                e.copy_result(res, release=True)
+            else:
+                copying[i] = pool.submit(e.copy_result, res, release=True, wait=False)
+            split.append((t1 - t0, t2 - t1, time.perf_counter() - t2))
+            return st
+
+        def drain():
+            for i, e in enumerate(engines):
+                if copying[i] is not None:
+                    copying[i].result()
+                    copying[i] = None
+                e.result_wait()
+
+        t_max, derived_all, st = D.run_weak(rk, classify, steps, warmup, drain=drain)
+        if pool is not None:
+            pool.shutdown()
+        for r in results:
+            assert (r.n_facts, r.n_links) == (st["s_facts"], st["links"]) or (len(ax.range) and not stream), \
+                "copy-back lost facts"
+        return t_max, derived_all, st, split[-steps:], results[(turn[0] - 1) % len(engines)]
+
     engines = [eng]
-    inflight = args.inflight if args.partition == "copies" else 1  # (exchange: one collective engine)
-    if inflight == 2:
+    if args.inflight == 2 and args.partition == "copies":
         eng2 = engine.Engine(device=local if has_cuda else 0)
         eng2.load(ax)
         engines.append(eng2)
-    results = [engine.Result() for _ in engines]  # page-locked result buffers, reused by every step
-    split = []  # (classification, copy-back enqueue) seconds per step; the last `steps` are the timed ones
-    turn = [0]
-    # Two engines in flight: a helper thread enqueues one engine's copy-back (it waits ~1 ms on the
-    # device for the row counts) while this thread starts the other engine's classification;
-    # ctypes drops the GIL inside the library, and the two threads never share an engine.
-    pool = ThreadPoolExecutor(max_workers=1) if len(engines) == 2 else None
-    copying = [None] * len(engines)
-
-    def classify():
-        # one classification: el_init + el_saturate + result copy-back (part of the metric,
-        # SURVEY.md §8(d)); the state is released behind the copy (the next init's reset overlaps
-        # the PCIe transfer).  Two engines in flight: this engine's copy-back is enqueued
-        # (EL_RESULT_ASYNC) and lands while the other engine saturates; an engine's next call
-        # waits for its previous copy-back, and drain() waits for the last ones.
-        i = turn[0] % len(engines)
-        turn[0] += 1
-        e, res = engines[i], results[i]
-        if copying[i] is not None:
-            copying[i].result()  # (the enqueue finished long ago; errors surface here)
-            copying[i] = None
-        t0 = time.perf_counter()
-        e.init()
-        st = e.saturate()
-        t1 = time.perf_counter()
-        if pool is None:
-            e.copy_result(res, release=True)
-        else:
-            copying[i] = pool.submit(e.copy_result, res, release=True, wait=False)
-        split.append((t1 - t0, time.perf_counter() - t1))
-        return st
-
-    def drain():
-        for i, e in enumerate(engines):
-            if copying[i] is not None:
-                copying[i].result()
-                copying[i] = None
-            e.result_wait()
-
-    t_max, derived_all, st = D.run_weak(rk, classify, args.steps, args.warmup, drain=drain)
+    t_max, derived_all, st, timed_split, res = timed(engines, args.steps, args.warmup)
     ms_per_step = 1e3 * t_max / args.steps
     value = derived_all * args.steps / t_max
-    timed = split[-args.steps:]
-    saturate_ms = 1e3 * sum(t[0] for t in timed) / len(timed)
-    copyback_ms = 1e3 * sum(t[1] for t in timed) / len(timed)
-    res = results[(turn[0] - 1) % len(engines)]
-    copy_bytes = 8 * 2 * (res.row_hi - res.row_lo + 1) + 4 * (res.n_facts + res.n_links)
+    init_ms = 1e3 * sum(t[0] for t in timed_split) / len(timed_split)
+    saturate_ms = 1e3 * sum(t[1] for t in timed_split) / len(timed_split)
+    copyback_ms = 1e3 * sum(t[2] for t in timed_split) / len(timed_split)
+    copy_bytes = (8 * (res.n_facts + res.n_links) if args.copyback == "stream" else
+                  8 * 2 * (res.row_hi - res.row_lo + 1) + 4 * (res.n_facts + res.n_links))
     # the copy-back holds every row of the caller's concepts (el_stats also counts the rows of
     # ELK range fillers, internal concepts, when the ontology has range axioms)
-    for r in results:
-        assert (r.n_facts, r.n_links) == (st["s_facts"], st["links"]) or len(ax.range), "copy-back lost facts"
-    # latency of ONE classification with its copy-back, nothing in flight beside it
-    lat = []
-    for _ in range(3):
-        t0 = time.perf_counter()
-        eng.init()
-        eng.saturate()
-        t1 = time.perf_counter()
-        eng.copy_result(results[0], release=True)
-        lat.append((time.perf_counter() - t0, time.perf_counter() - t1))
-    latency_ms = 1e3 * min(t[0] for t in lat)
-    serial_copyback_ms = 1e3 * min(t[1] for t in lat)
-    if pool is not None:
-        pool.shutdown()
+    throughput2 = None
+    if len(engines) == 1 and args.partition == "copies" and not args.no_throughput2:
+        eng2 = engine.Engine(device=local if has_cuda else 0)
+        eng2.load(ax)
+        t2_max, d2_all, _, _, _ = timed([eng, eng2], args.steps, args.warmup)
+        eng2.close()
+        throughput2 = {"value": round(d2_all * args.steps / t2_max, 1), "unit": "axioms/s",
+                       "ms_per_classification": round(1e3 * t2_max / args.steps, 4), "steps": args.steps,
+                       "schedule": "two engines alternate; one's result copy-back (EL_RESULT_ASYNC) overlaps "
+                                   "the other's classification"}
     for e in engines:
         e.close()
 
@@ -250,8 +266,8 @@ def main():
             g["bytes"] += k["bytes"]
             if k["kernel"] == k["group"]:
                 g["launches"], g["ms"] = k["launches"], k["ms"]
-        timed = [g for g in launches.values() if g["launches"] and g["ms"] > 0]
-        dom = max(timed, key=lambda g: g["ms"])
+        prof = [g for g in launches.values() if g["launches"] and g["ms"] > 0]
+        dom = max(prof, key=lambda g: g["ms"])
         per_launch_bytes = dom["bytes"] / dom["launches"]
         avg_ms = dom["ms"] / dom["launches"]
         achieved = per_launch_bytes / (avg_ms * 1e-3) / 1e9
@@ -288,7 +304,11 @@ def main():
                          f"(semi-naive Jacobi, 1 thread each, one per core): {cb['wall_s']:.3f} s wall; "
                          f"one alone: {cb['single_s']:.3f} s",
                "value_1core": round(cb["single_derived"] / cb["single_s"], 1),
-               "classification_s": round(cb["single_s"], 4)}
+               "classification_s": round(cb["single_s"], 4),
+               # the span the GPU step times: the told closure and its rows (elo_create's index
+               # build; el_init on the GPU) + init + saturation
+               "closure_index_s": round(cb["single_create_s"], 4),
+               "init_saturate_s": round(cb["single_s"] - cb["single_create_s"], 4)}
         if cpu_scale == args.scale:
             cpu["parity_derived_equal"] = cb["single_derived"] == st["derived"]
 
@@ -313,9 +333,9 @@ def main():
                                        f"row partition of the ×{world} ontology over {world} GPUs, RCCL delta "
                                        f"all-gather per superstep"),
                        "schedule": ("two classifications in flight per GPU: one's result copy-back "
-                                    "(EL_RESULT_ASYNC) overlaps the other's saturation; latency_ms = one alone"
-                                    if len(engines) == 2 else "one classification at a time")},
-            "classification_wall_s": round(ms_per_step / 1e3, 6),
+                                    "(EL_RESULT_ASYNC) overlaps the other's classification"
+                                    if len(engines) == 2 else "one classification at a time, copy-back included")},
+            "classification_wall_s": round(ms_per_step / 1e3, 6) if len(engines) == 1 else None,
             "derived_axioms": derived_all,
             "s_facts_per_rank": st["s_facts"],
             "links_per_rank": st["links"],
@@ -323,12 +343,18 @@ def main():
             "load_s": round(load_s, 3),
             "generate_s": round(gen_s, 3),
             "inflight": len(engines),
+            "init_ms": round(init_ms, 4),
             "saturate_ms": round(saturate_ms, 4),
-            "copyback_enqueue_ms": round(copyback_ms, 4),
-            "latency_ms": round(latency_ms, 4),
-            "copyback_ms": round(serial_copyback_ms, 4),
+            "copyback_ms": round(copyback_ms, 4),
+            "latency_ms": round(ms_per_step, 4) if len(engines) == 1 else None,
+            "copyback": ("streamed: the result node's (X, B) facts and (X, r, Y) links in commit order, "
+                         "crossing PCIe as the supersteps commit them (el_stream_result)"
+                         if args.copyback == "stream" else
+                         "rows: S(X) and links as sorted CSR rows after the fixpoint (el_copy_result)"),
             "copyback_bytes": int(copy_bytes),
-            "copyback_gbs": round(copy_bytes / (serial_copyback_ms * 1e-3) / 1e9, 2) if serial_copyback_ms > 0 else None,
+            "copyback_gbs": (round(copy_bytes / (copyback_ms * 1e-3) / 1e9, 2)
+                             if copyback_ms > 0 and args.copyback == "rows" else None),
+            "throughput_inflight2": throughput2,
             "roofline": roofline,
             "cpu_baseline": cpu,
         }

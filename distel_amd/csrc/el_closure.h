@@ -71,7 +71,7 @@ enum : uint32_t { E_TRIG = 0, E_ROW, E_ENT, E_RMW, E_NUM };
 struct Ctr {
   uint32_t t_tail, e_tail, l_tail;  // row arrays: next free entry
   uint32_t ovf;                     // a row or the scratch did not fit: the build is redone larger
-  unsigned long long s_tail;        // big-row scratch: next free 32-bit word
+  unsigned long long s_tail;        // big-row scratch: next free 64-bit word
   uint32_t dirty;                   // relaxation: some row changed in this round
   uint32_t pad[3];
   unsigned long long tot[T_NUM];
@@ -87,8 +87,9 @@ struct Out {
   uint32_t* level = nullptr;   // N: Kahn level of a concept (NONE: not ready)
   uint32_t* indeg = nullptr;   // N: told supers not yet closed
   uint32_t* lvl_flag = nullptr;  // N + 2: level L has at least one concept
-  uint8_t *dirty = nullptr, *dirty2 = nullptr, *changed = nullptr;  // N each (relaxation)
-  uint32_t* nd = nullptr;      // ND_NUM × N
+  uint8_t *dirty = nullptr, *dirty2 = nullptr;  // N each (relaxation)
+  uint32_t* changed = nullptr;  // N: relaxation: bit T = row type T grew this round
+  uint32_t* nd = nullptr;      // ND_NUM × (N + 1)
   uint32_t* rsv = nullptr;     // per wave slot: 3 × (next, end) row reservations
   uint32_t* scratch = nullptr;  // big rows
   unsigned long long scratch_cap = 0;  // 32-bit words
@@ -100,20 +101,26 @@ constexpr uint32_t GRID = 1024;
 constexpr uint32_t BLOCK = 256;
 constexpr uint32_t SLOTS = GRID * (BLOCK / 64);
 constexpr uint32_t RSV_WORDS = 6 * SLOTS;
+// per-wave row reservation (entries): a row array holds its rows plus at most one partly used
+// chunk per wave slot
+constexpr uint32_t CHUNK = 4096;
 
 // Everything is enqueued on s; nothing is read back (the caller reads Ctr).  Throws
 // std::runtime_error on a HIP error.
 // Kahn levels.  start: counters cleared, every concept's pending supers, level 0 = no told
 // supers, meta = empty rows (with the static cidx ranges), per-wave reservations cleared.
 void start(hipStream_t s, const Axioms& ax, const Out& o);
-// one level (reads its concepts off level[]; sets the next level's flag).  props: count the
-// base propagations (ND_PROPS).
-void level(hipStream_t s, const Axioms& ax, const Out& o, uint32_t L, bool props);
+// one level (reads its concepts off level[]; sets the next level's flag): the three row types
+// of each of its concepts are independent tasks spread over all waves
+void level(hipStream_t s, const Axioms& ax, const Out& o, uint32_t L);
 // after the levels: T_STUCK, and every stuck concept marked dirty for the relaxation
 void check(hipStream_t s, const Axioms& ax, const Out& o);
 // one relaxation round over the dirty concepts (told cycles), its grown rows committed;
 // Ctr::dirty = some row grew
-void relax(hipStream_t s, const Axioms& ax, const Out& o, bool props);
+void relax(hipStream_t s, const Axioms& ax, const Out& o);
+// per-concept statistics (Out::nd) of the final rows of [a, b); props: count the base
+// propagations (ND_PROPS)
+void stats(hipStream_t s, const Axioms& ax, const Out& o, uint32_t a, uint32_t b, bool props);
 // totals over the own rows [lo, hi) and the closure events over all rows (adds to Ctr::tot / ev)
 void totals(hipStream_t s, const Axioms& ax, const Out& o, uint32_t lo, uint32_t hi);
 

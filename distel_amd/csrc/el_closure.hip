@@ -21,7 +21,6 @@ namespace {
 
 constexpr uint32_t NONE = 0xffffffffu;
 constexpr uint32_t CAPW = 2048;   // LDS per wave: 2048 32-bit keys = 1024 64-bit keys (8 KB)
-constexpr uint32_t CHUNK = 4096;  // per-wave row reservation (entries)
 constexpr uint32_t TOP = 1, BOT = 0;
 constexpr uint8_t KIND_DATATYPE = 3;
 constexpr uint32_t WAVES = BLOCK / 64;
@@ -135,33 +134,149 @@ __device__ uint32_t sort_unique(K* b, uint32_t n, K excl) {
   return cnt;
 }
 
-// Row space: a wave appends its rows into a chunk it reserved (one atomic per CHUNK entries);
-// a row larger than a quarter chunk gets its own reservation.  NONE (and the overflow flag) when
-// the row array is full: the host grows it and builds again.
-__device__ uint32_t reserve(const Out& o, uint32_t which, uint32_t n, uint32_t cap, uint32_t* tail) {
-  if (n == 0) return 0;
-  uint32_t r = 0;
-  if (lane() == 0) {
-    const uint32_t slot = blockIdx.x * WAVES + (threadIdx.x >> 6);
-    uint32_t* st = o.rsv + 6 * slot + 2 * which;
-    if (n > CHUNK / 4) {
-      r = atomicAdd(tail, n);
-    } else {
-      uint32_t nx = st[0], en = st[1];
-      if (en - nx < n) {
-        nx = atomicAdd(tail, CHUNK);
-        en = nx + CHUNK;
+// Rows of up to 64·E keys sort in registers: lane l holds the keys 64 i + l (i < E); network
+// stages with a partner 64 or more keys away compare a lane's own registers, the others
+// shuffle (no LDS round trip per stage: a 128-key row is 28 stages of a few cycles each instead
+// of 28 LDS load / store rounds).  Then duplicates (and `excl`) drop out and the unique keys
+// are written back to b[0, cnt) in order.
+template <class K>
+__device__ __forceinline__ K bitonic_cx(K v, uint32_t e, uint32_t k, uint32_t j) {
+  const K u = __shfl_xor(v, (int)j);
+  const bool up = (e & k) == 0, lower = (e & j) == 0;
+  return (lower == up) ? (v < u ? v : u) : (v < u ? u : v);
+}
+
+template <uint32_t E, class K>
+__device__ uint32_t sort_unique_regs(K* b, uint32_t n, K excl) {
+  const K PAD = ~K(0);
+  const uint32_t ln = lane();
+  K v[E];
+#pragma unroll
+  for (uint32_t i = 0; i < E; ++i) v[i] = 64 * i + ln < n ? b[64 * i + ln] : PAD;
+#pragma unroll
+  for (uint32_t k = 2; k <= 64 * E; k <<= 1) {
+#pragma unroll
+    for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+      if (j >= 64) {  // partner in the same lane, register i ^ (j / 64)
+#pragma unroll
+        for (uint32_t i = 0; i < E; ++i) {
+          const uint32_t i2 = i ^ (j / 64);
+          if (i2 > i) {
+            const uint32_t e = 64 * i + ln;
+            const bool up = (e & k) == 0;
+            const K x = v[i], y = v[i2];
+            if ((x > y) == up) {
+              v[i] = y;
+              v[i2] = x;
+            }
+          }
+        }
+      } else {
+#pragma unroll
+        for (uint32_t i = 0; i < E; ++i) v[i] = bitonic_cx(v[i], 64 * i + ln, k, j);
       }
-      r = nx;
-      st[0] = nx + n;
-      st[1] = en;
-    }
-    if ((uint64_t)r + n > cap) {
-      atomicOr(&o.ctr->ovf, 1u);
-      r = NONE;
     }
   }
-  return __shfl(r, 0);
+  Lds::sync();  // (every lane has read b before any writes back)
+  uint32_t cnt = 0;
+  K prev = PAD;
+#pragma unroll
+  for (uint32_t i = 0; i < E; ++i) {
+    K pv = __shfl_up(v[i], 1);
+    if (ln == 0) pv = prev;
+    const bool keep = v[i] != PAD && v[i] != excl && v[i] != pv;
+    const unsigned long long mk = __ballot(keep);
+    prev = __shfl(v[i], 63);
+    if (keep) b[cnt + (uint32_t)__popcll(mk & ((1ull << ln) - 1ull))] = v[i];
+    cnt += (uint32_t)__popcll(mk);
+  }
+  Lds::sync();
+  return cnt;
+}
+
+// LDS rows: in registers up to 512 32-bit / 256 64-bit keys, else the LDS network
+template <class K>
+__device__ uint32_t sort_unique_lds(K* b, uint32_t n, K excl) {
+  if (n == 0) return 0;
+  if (n <= 64) return sort_unique_regs<1>(b, n, excl);
+  if (n <= 128) return sort_unique_regs<2>(b, n, excl);
+  if (n <= 256) return sort_unique_regs<4>(b, n, excl);
+  if (sizeof(K) == 4 && n <= 512) return sort_unique_regs<8>(b, n, excl);
+  return sort_unique<Lds>(b, n, excl);
+}
+
+// pid of (r, Y) by a binary search of Y's pair range (sorted by role), or NONE
+__device__ __forceinline__ uint32_t pid_of(const Axioms& ax, uint32_t r, uint32_t fb, uint32_t fe) {
+  while (fb < fe) {
+    const uint32_t mid = (fb + fe) >> 1, rr = ax.pair_role[mid];
+    if (rr == r) return mid;
+    if (rr < r)
+      fb = mid + 1;
+    else
+      fe = mid;
+  }
+  return NONE;
+}
+
+__device__ __forceinline__ bool two_of(const Axioms& ax, uint32_t x) {
+  return x != TOP && x != BOT && ax.kind[x] != KIND_DATATYPE;
+}
+
+// Row space: a wave appends its rows into a chunk it reserved (one atomic per CHUNK entries);
+// a row larger than a quarter chunk gets its own reservation.  A wave's chunk state stays in
+// registers for the launch (Out::rsv keeps it between launches).  NONE (and the overflow flag)
+// when the row array is full: the host grows it and builds again.
+struct Rsv {
+  uint32_t nx[3], en[3];
+};
+
+__device__ __forceinline__ uint32_t slot_id() { return blockIdx.x * WAVES + (threadIdx.x >> 6); }
+
+__device__ Rsv rsv_load(const Out& o) {
+  Rsv r;
+  const uint32_t* s = o.rsv + 6 * slot_id();
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    r.nx[i] = __builtin_amdgcn_readfirstlane(s[2 * i]);
+    r.en[i] = __builtin_amdgcn_readfirstlane(s[2 * i + 1]);
+  }
+  return r;
+}
+
+__device__ void rsv_store(const Out& o, const Rsv& r) {
+  if (lane() == 0) {
+    uint32_t* s = o.rsv + 6 * slot_id();
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      s[2 * i] = r.nx[i];
+      s[2 * i + 1] = r.en[i];
+    }
+  }
+}
+
+__device__ uint32_t reserve(const Out& o, Rsv& rs, uint32_t which, uint32_t n, uint32_t cap, uint32_t* tail) {
+  if (n == 0) return 0;
+  uint32_t r;
+  if (n > CHUNK / 4) {
+    uint32_t b = 0;
+    if (lane() == 0) b = atomicAdd(tail, n);
+    r = __builtin_amdgcn_readfirstlane(b);
+  } else {
+    if (rs.en[which] - rs.nx[which] < n) {
+      uint32_t b = 0;
+      if (lane() == 0) b = atomicAdd(tail, CHUNK);
+      b = __builtin_amdgcn_readfirstlane(b);
+      rs.nx[which] = b;
+      rs.en[which] = b + CHUNK;
+    }
+    r = rs.nx[which];
+    rs.nx[which] += n;
+  }
+  if ((uint64_t)r + n > cap) {
+    if (lane() == 0) atomicOr(&o.ctr->ovf, 1u);
+    return NONE;
+  }
+  return r;
 }
 
 // global scratch for a row that does not fit the LDS: pow2(n) keys of K (nullptr: overflow)
@@ -182,262 +297,138 @@ __device__ K* scratch_take(const Out& o, uint32_t n) {
   return r == ~0ull ? nullptr : reinterpret_cast<K*>(o.scratch + 2 * r);
 }
 
-template <class M>
-__device__ void copy_out(uint32_t* dst, uint32_t* src, uint32_t n) {
-  for (uint32_t i = lane(); i < n; i += 64) dst[i] = M::ld(src + i);
+// The three row types.  Each depends only on the rows of the same type of the told supers (and
+// the concept's own axioms), so the three of a concept are independent tasks.
+enum : uint32_t { R_TOLD = 0, R_EXR = 1, R_EXL = 2 };
+// meta word of a row type: told* -> .x, exr* -> .z, exl* -> .w (of the begin / end uint4)
+template <uint32_t T>
+struct RowT {
+  static constexpr uint32_t comp = T == R_TOLD ? 0u : T == R_EXR ? 2u : 3u;
+  using K = typename std::conditional<T == R_EXL, unsigned long long, uint32_t>::type;
+  static constexpr uint32_t lds_cap = T == R_EXL ? CAPW / 2 : CAPW;
+};
+
+__device__ __forceinline__ uint32_t meta_word(const uint4* meta, uint32_t A, uint32_t end, uint32_t comp) {
+  return reinterpret_cast<const uint32_t*>(meta + 2 * A + end)[comp];
 }
 
-// told*(A): the supers themselves and their rows
-template <class M>
-__device__ void gather_told(const Axioms& ax, const Out& o, uint32_t pb, uint32_t pe, uint32_t* buf) {
+// The rows of type T of the supers [pb, pe) (with each super itself first, for told*) after
+// A's own axioms, concatenated into buf.
+template <uint32_t T, class M>
+__device__ void gather(const Axioms& ax, const Out& o, uint32_t A, uint32_t pb, uint32_t pe,
+                       typename RowT<T>::K* buf) {
+  using K = typename RowT<T>::K;
   uint32_t off = 0;
+  if (T == R_EXR) {
+    const uint32_t b0 = ax.xr_ptr[A], n0 = ax.xr_ptr[A + 1] - b0;
+    for (uint32_t i = lane(); i < n0; i += 64) M::st(buf + i, (K)ax.xr[b0 + i]);
+    off = n0;
+  } else if (T == R_EXL) {
+    const uint32_t b0 = ax.xl_ptr[A], n0 = ax.xl_ptr[A + 1] - b0;
+    for (uint32_t i = lane(); i < n0; i += 64) M::st(buf + i, ((K)ax.xl_r[b0 + i] << 32) | ax.xl_b[b0 + i]);
+    off = n0;
+  }
   for (uint32_t q0 = pb; q0 < pe; q0 += 64) {
     const uint32_t q = q0 + lane();
     uint32_t p = 0, rb = 0, len = 0;
     if (q < pe) {
       p = ax.par[q];
-      const uint4 b = o.meta[2 * p], e = o.meta[2 * p + 1];
-      rb = b.x;
-      len = 1 + e.x - b.x;
+      rb = meta_word(o.meta, p, 0, RowT<T>::comp);
+      len = meta_word(o.meta, p, 1, RowT<T>::comp) - rb + (T == R_TOLD ? 1u : 0u);
     }
     off += wave_concat(len, [&](bool v, uint32_t own, uint32_t j, uint32_t k) {
       const uint32_t po = __shfl(p, (int)own), ro = __shfl(rb, (int)own);
-      if (v) M::st(buf + off + k, j == 0 ? po : o.t_val[ro + j - 1]);
+      if (!v) return;
+      K key;
+      if (T == R_TOLD)
+        key = j == 0 ? po : o.t_val[ro + j - 1];
+      else if (T == R_EXR)
+        key = o.e_val[ro + j];
+      else
+        key = ((K)o.l_r[ro + j] << 32) | o.l_b[ro + j];
+      M::st(buf + off + k, key);
     });
   }
 }
 
-// exr*(A): A's own pairs, then the supers' rows
-template <class M>
-__device__ void gather_exr(const Axioms& ax, const Out& o, uint32_t A, uint32_t pb, uint32_t pe, uint32_t* buf) {
-  const uint32_t xb = ax.xr_ptr[A], xn = ax.xr_ptr[A + 1] - xb;
-  for (uint32_t i = lane(); i < xn; i += 64) M::st(buf + i, ax.xr[xb + i]);
-  uint32_t off = xn;
-  for (uint32_t q0 = pb; q0 < pe; q0 += 64) {
-    const uint32_t q = q0 + lane();
-    uint32_t rb = 0, len = 0;
-    if (q < pe) {
-      const uint32_t p = ax.par[q];
-      const uint4 b = o.meta[2 * p], e = o.meta[2 * p + 1];
-      rb = b.z;
-      len = e.z - b.z;
-    }
-    off += wave_concat(len, [&](bool v, uint32_t own, uint32_t j, uint32_t k) {
-      const uint32_t ro = __shfl(rb, (int)own);
-      if (v) M::st(buf + off + k, o.e_val[ro + j]);
-    });
-  }
-}
-
-// exl*(A) as 64-bit keys (r << 32 | B)
-template <class M>
-__device__ void gather_exl(const Axioms& ax, const Out& o, uint32_t A, uint32_t pb, uint32_t pe,
-                           unsigned long long* buf) {
-  const uint32_t yb = ax.xl_ptr[A], yn = ax.xl_ptr[A + 1] - yb;
-  for (uint32_t i = lane(); i < yn; i += 64)
-    M::st(buf + i, ((unsigned long long)ax.xl_r[yb + i] << 32) | ax.xl_b[yb + i]);
-  uint32_t off = yn;
-  for (uint32_t q0 = pb; q0 < pe; q0 += 64) {
-    const uint32_t q = q0 + lane();
-    uint32_t rb = 0, len = 0;
-    if (q < pe) {
-      const uint32_t p = ax.par[q];
-      const uint4 b = o.meta[2 * p], e = o.meta[2 * p + 1];
-      rb = b.w;
-      len = e.w - b.w;
-    }
-    off += wave_concat(len, [&](bool v, uint32_t own, uint32_t j, uint32_t k) {
-      const uint32_t ro = __shfl(rb, (int)own);
-      if (v) M::st(buf + off + k, ((unsigned long long)o.l_r[ro + j] << 32) | o.l_b[ro + j]);
-    });
-  }
-}
-
-// pid of (r, Y) by a binary search of Y's pair range (sorted by role), or NONE
-__device__ __forceinline__ uint32_t pid_of(const Axioms& ax, uint32_t r, uint32_t fb, uint32_t fe) {
-  while (fb < fe) {
-    const uint32_t mid = (fb + fe) >> 1, rr = ax.pair_role[mid];
-    if (rr == r) return mid;
-    if (rr < r)
-      fb = mid + 1;
-    else
-      fe = mid;
-  }
-  return NONE;
-}
-
-__device__ __forceinline__ bool two_of(const Axioms& ax, uint32_t x) {
-  return x != TOP && x != BOT && ax.kind[x] != KIND_DATATYPE;
-}
-
-// One concept's three rows and statistics (a wave; A wave-uniform).  RELAX: a relaxation round
-// (told cycles): the concept's current rows are in meta; a row is rewritten only when it grew,
-// and the new ranges go to meta2 (committed after the round).
-template <bool RELAX>
-__device__ void node(const Axioms& ax, const Out& o, uint32_t A, uint32_t L, bool props, uint32_t* lbuf,
-                     bool& any) {
+// Row type T of concept A (a wave; A wave-uniform): gather, sort, drop duplicates (and A itself
+// from told*: a told cycle would put it there), append, record the range.  RELAX: a row is only
+// appended when it grew; its range goes to meta2 (committed after the round).  Returns whether
+// the row was written.
+template <uint32_t T, bool RELAX>
+__device__ bool task(const Axioms& ax, const Out& o, uint32_t A, uint32_t* lbuf, Rsv& rs) {
+  using K = typename RowT<T>::K;
   const uint32_t pb = ax.par_ptr[A], pe = ax.par_ptr[A + 1];
-  unsigned long long st = 0, se = 0, sl = 0;
+  unsigned long long raw = 0;
   for (uint32_t q = pb + lane(); q < pe; q += 64) {
     const uint32_t p = ax.par[q];
-    const uint4 b = o.meta[2 * p], e = o.meta[2 * p + 1];
-    st += 1 + e.x - b.x;
-    se += e.z - b.z;
-    sl += e.w - b.w;
+    raw += meta_word(o.meta, p, 1, RowT<T>::comp) - meta_word(o.meta, p, 0, RowT<T>::comp) + (T == R_TOLD ? 1u : 0u);
   }
-  st = wsum(st);
-  se = wsum(se) + (ax.xr_ptr[A + 1] - ax.xr_ptr[A]);
-  sl = wsum(sl) + (ax.xl_ptr[A + 1] - ax.xl_ptr[A]);
-  const uint4 ob = o.meta[2 * A], oe = o.meta[2 * A + 1];
-  uint4 nb = ob, ne = oe;
-  bool grew = false;
-  const uint32_t N1 = ax.N + 1;
-  uint32_t ninit = 0, cz = 0, sc = 0, sc0 = 0, lift = 0, np = 0;
-  const bool two = two_of(ax, A);
-  // ---- told*(A)
-  {
-    const bool big = st > CAPW;
-    uint32_t* buf = big ? scratch_take<uint32_t>(o, (uint32_t)st) : lbuf;
-    uint32_t n = 0;
-    if (buf) {
-      if (big) {
-        gather_told<Glb>(ax, o, pb, pe, buf);
-        n = sort_unique<Glb>(buf, (uint32_t)st, A);
-      } else {
-        gather_told<Lds>(ax, o, pb, pe, buf);
-        n = sort_unique<Lds>(buf, (uint32_t)st, A);
-      }
-      unsigned long long c = 0;
-      bool top = false;
+  raw = wsum(raw);
+  if (T == R_EXR) raw += ax.xr_ptr[A + 1] - ax.xr_ptr[A];
+  if (T == R_EXL) raw += ax.xl_ptr[A + 1] - ax.xl_ptr[A];
+  if (raw > 0x7fffffffull) {
+    if (lane() == 0) atomicOr(&o.ctr->ovf, 1u);
+    return false;
+  }
+  const bool big = raw > RowT<T>::lds_cap;
+  K* buf = big ? scratch_take<K>(o, (uint32_t)raw) : reinterpret_cast<K*>(lbuf);
+  if (!buf) return false;
+  const K excl = T == R_TOLD ? (K)A : ~K(0);
+  uint32_t n;
+  if (big) {
+    gather<T, Glb>(ax, o, A, pb, pe, buf);
+    n = sort_unique<Glb>(buf, (uint32_t)raw, excl);
+  } else {
+    gather<T, Lds>(ax, o, A, pb, pe, buf);
+    n = sort_unique_lds(buf, (uint32_t)raw, excl);
+  }
+  bool wrote = false;
+  const uint32_t ob = meta_word(o.meta, A, 0, RowT<T>::comp), oe = meta_word(o.meta, A, 1, RowT<T>::comp);
+  if (!RELAX || n != oe - ob) {
+    const uint32_t cap = T == R_TOLD ? o.t_cap : T == R_EXR ? o.e_cap : o.l_cap;
+    uint32_t* tail = T == R_TOLD ? &o.ctr->t_tail : T == R_EXR ? &o.ctr->e_tail : &o.ctr->l_tail;
+    const uint32_t r = reserve(o, rs, T, n, cap, tail);
+    if (r != NONE) {
       for (uint32_t i = lane(); i < n; i += 64) {
-        const uint32_t v = big ? Glb::ld(buf + i) : buf[i];
-        c += ax.cidx_ptr[v + 1] - ax.cidx_ptr[v];
-        top |= i < 2 && v == TOP;
-      }
-      cz = (uint32_t)wsum(c);
-      top = __ballot(top) != 0;
-      ninit = 1 + (two ? 1u : 0u) + n - ((two && top) ? 1u : 0u);
-      if (!RELAX || n != oe.x - ob.x) {
-        grew = true;
-        const uint32_t r = reserve(o, 0, n, o.t_cap, &o.ctr->t_tail);
-        if (r != NONE) {
-          if (big)
-            copy_out<Glb>(o.t_val + r, buf, n);
-          else
-            copy_out<Lds>(o.t_val + r, buf, n);
-          nb.x = r;
-          ne.x = r + n;
+        const K v = big ? Glb::ld(buf + i) : buf[i];
+        if (T == R_TOLD) {
+          o.t_val[r + i] = (uint32_t)v;
+        } else if (T == R_EXR) {
+          o.e_val[r + i] = (uint32_t)v;
+        } else {
+          o.l_r[r + i] = (uint32_t)((unsigned long long)v >> 32);
+          o.l_b[r + i] = (uint32_t)v;
         }
       }
-    }
-    Lds::sync();
-  }
-  // ---- exr*(A)
-  {
-    const bool big = se > CAPW;
-    uint32_t* buf = big ? scratch_take<uint32_t>(o, (uint32_t)se) : lbuf;
-    uint32_t n = 0;
-    if (buf) {
-      if (big) {
-        gather_exr<Glb>(ax, o, A, pb, pe, buf);
-        n = sort_unique<Glb>(buf, (uint32_t)se, NONE);
-      } else {
-        gather_exr<Lds>(ax, o, A, pb, pe, buf);
-        n = sort_unique<Lds>(buf, (uint32_t)se, NONE);
+      if (lane() == 0) {
+        uint4* m = RELAX ? o.meta2 : o.meta;
+        reinterpret_cast<uint32_t*>(m + 2 * A)[RowT<T>::comp] = r;
+        reinterpret_cast<uint32_t*>(m + 2 * A + 1)[RowT<T>::comp] = r + n;
       }
-      unsigned long long a = 0, b = 0, c = 0;
-      for (uint32_t i = lane(); i < n; i += 64) {
-        const uint32_t p = big ? Glb::ld(buf + i) : buf[i];
-        a += ax.sc_w[p];
-        b += ax.sc_self[p];
-        c += ax.psup_ptr[p + 1] - ax.psup_ptr[p];
-      }
-      sc = (uint32_t)wsum(a);
-      sc0 = (uint32_t)wsum(b);
-      lift = (uint32_t)wsum(c);
-      if (!RELAX || n != oe.z - ob.z) {
-        grew = true;
-        const uint32_t r = reserve(o, 1, n, o.e_cap, &o.ctr->e_tail);
-        if (r != NONE) {
-          if (big)
-            copy_out<Glb>(o.e_val + r, buf, n);
-          else
-            copy_out<Lds>(o.e_val + r, buf, n);
-          nb.z = r;
-          ne.z = r + n;
-        }
-      }
-    }
-    Lds::sync();
-  }
-  // ---- exl*(A)
-  {
-    const bool big = sl > CAPW / 2;
-    unsigned long long* buf =
-        big ? scratch_take<unsigned long long>(o, (uint32_t)sl) : reinterpret_cast<unsigned long long*>(lbuf);
-    uint32_t n = 0;
-    if (buf) {
-      if (big) {
-        gather_exl<Glb>(ax, o, A, pb, pe, buf);
-        n = sort_unique<Glb>(buf, (uint32_t)sl, ~0ull);
-      } else {
-        gather_exl<Lds>(ax, o, A, pb, pe, buf);
-        n = sort_unique<Lds>(buf, (uint32_t)sl, ~0ull);
-      }
-      const uint32_t fb = ax.fp_ptr[A], fe = ax.fp_ptr[A + 1];
-      const bool write = !RELAX || n != oe.w - ob.w;
-      const uint32_t r = write ? reserve(o, 2, n, o.l_cap, &o.ctr->l_tail) : NONE;
-      unsigned long long m = 0;
-      for (uint32_t i = lane(); i < n; i += 64) {
-        const unsigned long long k = big ? Glb::ld(buf + i) : buf[i];
-        if (r != NONE) {
-          o.l_r[r + i] = (uint32_t)(k >> 32);
-          o.l_b[r + i] = (uint32_t)k;
-        }
-        if (props && fb < fe) m += pid_of(ax, (uint32_t)(k >> 32), fb, fe) != NONE;
-      }
-      np = (uint32_t)wsum(m);
-      if (write) {
-        grew = true;
-        if (r != NONE) {
-          nb.w = r;
-          ne.w = r + n;
-        }
-      }
-    }
-    Lds::sync();
-  }
-  if (lane() == 0) {
-    o.nd[ND_INIT * N1 + A] = ninit;
-    o.nd[ND_EXR * N1 + A] = ne.z - nb.z;
-    o.nd[ND_PROPS * N1 + A] = np;
-    o.nd[ND_CZ * N1 + A] = cz;
-    o.nd[ND_SC * N1 + A] = sc;
-    o.nd[ND_SC0 * N1 + A] = sc0;
-    o.nd[ND_LIFT * N1 + A] = lift;
-    if (!RELAX) {
-      o.meta[2 * A] = nb;
-      o.meta[2 * A + 1] = ne;
-    } else if (grew) {
-      o.meta2[2 * A] = nb;
-      o.meta2[2 * A + 1] = ne;
-      o.changed[A] = 1;
-      o.ctr->dirty = 1;
+      wrote = true;
     }
   }
-  const uint32_t cb = ax.chi_ptr[A], ce = ax.chi_ptr[A + 1];
-  if (!RELAX) {  // a sub whose last super this was is ready for the next level
-    for (uint32_t q = cb + lane(); q < ce; q += 64) {
-      const uint32_t c = ax.chi[q];
-      if (atomicSub(o.indeg + c, 1u) == 1u) {
-        o.level[c] = L + 1;
-        any = true;
-      }
-    }
-  } else if (grew) {  // subs still being relaxed see the grown rows next round
-    for (uint32_t q = cb + lane(); q < ce; q += 64) {
-      const uint32_t c = ax.chi[q];
-      if (o.level[c] == NONE) o.dirty2[c] = 1;
+  Lds::sync();  // (lbuf is reused by the wave's next task)
+  return wrote;
+}
+
+// Tasks (A, T) of the concepts of one level (or of the dirty concepts: relaxation) are spread
+// over all waves: task t = 3A + T goes to wave t mod nw, so a level's concepts (often a
+// contiguous id range) and their three row types all run side by side.
+template <class Sel, class Run>
+__device__ __forceinline__ void for_tasks(uint32_t N, Sel&& sel, Run&& run) {
+  const uint32_t nw = gridDim.x * WAVES, w = slot_id();
+  const uint64_t ntask = 3ull * N;
+  for (uint64_t base = 0; base * nw + w < ntask; base += 64) {  // (wave-uniform)
+    const uint64_t t0 = (base + lane()) * nw + w;
+    const bool in = t0 < ntask && sel((uint32_t)(t0 / 3));
+    unsigned long long m = __ballot(in);
+    while (m) {
+      const uint32_t i = (uint32_t)__ffsll((long long)m) - 1;
+      m &= m - 1;
+      const uint64_t t = (base + i) * nw + w;
+      run((uint32_t)(t / 3), (uint32_t)(t % 3));
     }
   }
 }
@@ -457,24 +448,34 @@ __global__ void __launch_bounds__(BLOCK) k_start(Axioms ax, Out o) {
   if (root) o.lvl_flag[0] = 1;  // (zeroed by the host before this launch)
 }
 
-__global__ void __launch_bounds__(BLOCK) k_level(Axioms ax, Out o, uint32_t L, uint32_t props) {
+__global__ void __launch_bounds__(BLOCK) k_level(Axioms ax, Out o, uint32_t L) {
   if (o.lvl_flag[L] == 0) return;  // (block-uniform: nothing at this level)
   __shared__ unsigned long long lds[WAVES * (CAPW / 2)];
   __shared__ uint32_t sany;
   if (threadIdx.x == 0) sany = 0;
   __syncthreads();
   uint32_t* lbuf = reinterpret_cast<uint32_t*>(lds + (threadIdx.x >> 6) * (CAPW / 2));
+  Rsv rs = rsv_load(o);
   bool any = false;
-  const uint32_t nw = gridDim.x * WAVES, w = blockIdx.x * WAVES + (threadIdx.x >> 6);
-  for (uint32_t base = w * 64; base < ax.N; base += nw * 64) {  // (wave-uniform)
-    const uint32_t A0 = base + lane();
-    unsigned long long m = __ballot(A0 < ax.N && o.level[A0] == L);
-    while (m) {
-      const uint32_t i = (uint32_t)__ffsll((long long)m) - 1;
-      m &= m - 1;
-      node<false>(ax, o, base + i, L, props != 0, lbuf, any);
+  for_tasks(ax.N, [&](uint32_t A) { return o.level[A] == L; }, [&](uint32_t A, uint32_t T) {
+    if (T == R_EXR) {
+      task<R_EXR, false>(ax, o, A, lbuf, rs);
+    } else if (T == R_EXL) {
+      task<R_EXL, false>(ax, o, A, lbuf, rs);
+    } else {
+      task<R_TOLD, false>(ax, o, A, lbuf, rs);
+      // a sub whose last super this was is ready for the next level
+      const uint32_t cb = ax.chi_ptr[A], ce = ax.chi_ptr[A + 1];
+      for (uint32_t q = cb + lane(); q < ce; q += 64) {
+        const uint32_t c = ax.chi[q];
+        if (atomicSub(o.indeg + c, 1u) == 1u) {
+          o.level[c] = L + 1;
+          any = true;
+        }
+      }
     }
-  }
+  });
+  rsv_store(o, rs);
   if (any) sany = 1;
   __syncthreads();
   if (threadIdx.x == 0 && sany) o.lvl_flag[L + 1] = 1;
@@ -502,31 +503,110 @@ __global__ void __launch_bounds__(BLOCK) k_check(Axioms ax, Out o) {
   }
 }
 
-__global__ void __launch_bounds__(BLOCK) k_relax(Axioms ax, Out o, uint32_t props) {
+// One Jacobi relaxation round over the dirty concepts: each row type recomputed from the
+// committed rows (meta); a grown row lands in meta2, its concept's changed bit for the type is
+// set, and its subs still being relaxed are dirty next round.
+__global__ void __launch_bounds__(BLOCK) k_relax(Axioms ax, Out o) {
   __shared__ unsigned long long lds[WAVES * (CAPW / 2)];
   uint32_t* lbuf = reinterpret_cast<uint32_t*>(lds + (threadIdx.x >> 6) * (CAPW / 2));
-  bool any = false;
-  const uint32_t nw = gridDim.x * WAVES, w = blockIdx.x * WAVES + (threadIdx.x >> 6);
-  for (uint32_t base = w * 64; base < ax.N; base += nw * 64) {
-    const uint32_t A0 = base + lane();
-    unsigned long long m = __ballot(A0 < ax.N && o.dirty[A0]);
-    while (m) {
-      const uint32_t i = (uint32_t)__ffsll((long long)m) - 1;
-      m &= m - 1;
-      node<true>(ax, o, base + i, 0, props != 0, lbuf, any);
+  Rsv rs = rsv_load(o);
+  for_tasks(ax.N, [&](uint32_t A) { return o.dirty[A] != 0; }, [&](uint32_t A, uint32_t T) {
+    const bool grew = T == R_TOLD  ? task<R_TOLD, true>(ax, o, A, lbuf, rs)
+                      : T == R_EXR ? task<R_EXR, true>(ax, o, A, lbuf, rs)
+                                   : task<R_EXL, true>(ax, o, A, lbuf, rs);
+    if (!grew) return;
+    if (lane() == 0) {
+      atomicOr(o.changed + A, 1u << T);
+      o.ctr->dirty = 1;
     }
-  }
+    const uint32_t cb = ax.chi_ptr[A], ce = ax.chi_ptr[A + 1];
+    for (uint32_t q = cb + lane(); q < ce; q += 64) {
+      const uint32_t c = ax.chi[q];
+      if (o.level[c] == NONE) o.dirty2[c] = 1;
+    }
+  });
+  rsv_store(o, rs);
 }
 
 __global__ void __launch_bounds__(BLOCK) k_relax_commit(Axioms ax, Out o) {
   for (uint32_t A = blockIdx.x * blockDim.x + threadIdx.x; A < ax.N; A += gridDim.x * blockDim.x) {
-    if (o.changed[A]) {
-      o.meta[2 * A] = o.meta2[2 * A];
-      o.meta[2 * A + 1] = o.meta2[2 * A + 1];
+    const uint32_t ch = o.changed[A];
+    if (ch) {
+      uint32_t* b = reinterpret_cast<uint32_t*>(o.meta + 2 * A);
+      uint32_t* e = reinterpret_cast<uint32_t*>(o.meta + 2 * A + 1);
+      const uint32_t* b2 = reinterpret_cast<const uint32_t*>(o.meta2 + 2 * A);
+      const uint32_t* e2 = reinterpret_cast<const uint32_t*>(o.meta2 + 2 * A + 1);
+      for (uint32_t T = 0; T < 3; ++T)
+        if ((ch >> T) & 1u) {
+          const uint32_t c = T == R_TOLD ? 0u : T == R_EXR ? 2u : 3u;
+          b[c] = b2[c];
+          e[c] = e2[c];
+        }
       o.changed[A] = 0;
     }
     o.dirty[A] = o.dirty2[A];
     o.dirty2[A] = 0;
+  }
+}
+
+// Per-concept statistics of the final rows (for the state pass and the host's buffer sizes):
+// init facts, CR2 candidates over told*, successor-row weights and CR5 lifts over exr*, base
+// propagations over exl*.  Lanes own concepts; the wave walks the concatenation of its 64
+// concepts' rows (coalesced) and adds each entry's contribution to its owner in LDS.
+__global__ void __launch_bounds__(BLOCK) k_stats(Axioms ax, Out o, uint32_t lo, uint32_t hi, uint32_t props) {
+  __shared__ uint32_t acc[WAVES][6][64];
+  uint32_t(&a)[6][64] = acc[threadIdx.x >> 6];
+  const uint32_t N1 = ax.N + 1, nw = gridDim.x * WAVES, w = slot_id();
+  for (uint32_t x0 = lo + w * 64; x0 < hi; x0 += nw * 64) {  // (wave-uniform)
+    const uint32_t x = x0 + lane();
+    const bool ok = x < hi;
+    uint4 b = make_uint4(0, 0, 0, 0), e = b;
+    uint32_t fb = 0, fe = 0;
+    if (ok) {
+      b = o.meta[2 * x];
+      e = o.meta[2 * x + 1];
+      fb = ax.fp_ptr[x];
+      fe = ax.fp_ptr[x + 1];
+    }
+#pragma unroll
+    for (int k = 0; k < 6; ++k) a[k][lane()] = 0;
+    Lds::sync();
+    // told*: CR2 candidates (|cidx| of every entry), ⊤ among the first two entries
+    wave_concat(e.x - b.x, [&](bool v, uint32_t own, uint32_t j, uint32_t) {
+      const uint32_t ro = __shfl(b.x, (int)own);
+      if (!v) return;
+      const uint32_t t = o.t_val[ro + j];
+      atomicAdd(&a[0][own], ax.cidx_ptr[t + 1] - ax.cidx_ptr[t]);
+      if (j < 2 && t == TOP) a[1][own] = 1;
+    });
+    // exr*: successor-row weight, chain-second base links, CR5 lifts
+    wave_concat(e.z - b.z, [&](bool v, uint32_t own, uint32_t j, uint32_t) {
+      const uint32_t ro = __shfl(b.z, (int)own);
+      if (!v) return;
+      const uint32_t p = o.e_val[ro + j];
+      atomicAdd(&a[2][own], ax.sc_w[p]);
+      atomicAdd(&a[3][own], (uint32_t)ax.sc_self[p]);
+      atomicAdd(&a[4][own], ax.psup_ptr[p + 1] - ax.psup_ptr[p]);
+    });
+    // exl*: base propagations ((r, x), B) with (r, x) a pair
+    wave_concat(props && fe > fb ? e.w - b.w : 0u, [&](bool v, uint32_t own, uint32_t j, uint32_t) {
+      const uint32_t ro = __shfl(b.w, (int)own), f0 = __shfl(fb, (int)own), f1 = __shfl(fe, (int)own);
+      if (!v) return;
+      if (pid_of(ax, o.l_r[ro + j], f0, f1) != NONE) atomicAdd(&a[5][own], 1u);
+    });
+    Lds::sync();
+    if (ok) {
+      const bool two = two_of(ax, x);
+      const uint32_t tl = e.x - b.x;
+      o.nd[ND_INIT * N1 + x] = 1 + (two ? 1u : 0u) + tl - ((two && a[1][lane()]) ? 1u : 0u);
+      o.nd[ND_EXR * N1 + x] = e.z - b.z;
+      o.nd[ND_CZ * N1 + x] = a[0][lane()];
+      o.nd[ND_SC * N1 + x] = a[2][lane()];
+      o.nd[ND_SC0 * N1 + x] = a[3][lane()];
+      o.nd[ND_LIFT * N1 + x] = a[4][lane()];
+      o.nd[ND_PROPS * N1 + x] = a[5][lane()];
+    }
+    Lds::sync();
   }
 }
 
@@ -760,8 +840,8 @@ void start(hipStream_t s, const Axioms& ax, const Out& o) {
   CCHK(hipGetLastError());
 }
 
-void level(hipStream_t s, const Axioms& ax, const Out& o, uint32_t L, bool props) {
-  hipLaunchKernelGGL(k_level, dim3(GRID), dim3(BLOCK), 0, s, ax, o, L, props ? 1u : 0u);
+void level(hipStream_t s, const Axioms& ax, const Out& o, uint32_t L) {
+  hipLaunchKernelGGL(k_level, dim3(GRID), dim3(BLOCK), 0, s, ax, o, L);
   CCHK(hipGetLastError());
 }
 
@@ -770,10 +850,17 @@ void check(hipStream_t s, const Axioms& ax, const Out& o) {
   CCHK(hipGetLastError());
 }
 
-void relax(hipStream_t s, const Axioms& ax, const Out& o, bool props) {
+void relax(hipStream_t s, const Axioms& ax, const Out& o) {
   CCHK(hipMemsetAsync(&o.ctr->dirty, 0, sizeof(uint32_t), s));
-  hipLaunchKernelGGL(k_relax, dim3(GRID), dim3(BLOCK), 0, s, ax, o, props ? 1u : 0u);
+  hipLaunchKernelGGL(k_relax, dim3(GRID), dim3(BLOCK), 0, s, ax, o);
   hipLaunchKernelGGL(k_relax_commit, dim3(grid_for(ax.N)), dim3(BLOCK), 0, s, ax, o);
+  CCHK(hipGetLastError());
+}
+
+void stats(hipStream_t s, const Axioms& ax, const Out& o, uint32_t a, uint32_t b, bool props) {
+  if (b <= a) return;
+  hipLaunchKernelGGL(k_stats, dim3(grid_for((uint64_t)(b - a), 2048)), dim3(BLOCK), 0, s, ax, o, a, b,
+                     props ? 1u : 0u);
   CCHK(hipGetLastError());
 }
 

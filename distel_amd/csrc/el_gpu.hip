@@ -2558,11 +2558,20 @@ struct el_ctx {
   hipEvent_t ev_reset = nullptr;
   hipEvent_t ev_copied[3] = {nullptr, nullptr, nullptr};  // an async copy-back's streams drained
   bool copy_pending = false;
+  // (copy_pending is cleared only once every stream has drained: a failed copy keeps failing)
   void wait_copy() {
     if (!copy_pending) return;
-    copy_pending = false;
     for (hipEvent_t e : ev_copied) HIPCHK(hipEventSynchronize(e));
+    copy_pending = false;
   }
+  // Streamed result (el_stream_result): the committed segments of the fact and link logs, DMA'd
+  // on dstream into the caller's buffers while the saturation goes on
+  el_stream* strm = nullptr;      // armed for the next el_saturate
+  uint64_t strm_s = 0, strm_l = 0;  // log entries already enqueued
+  bool strm_ovf = false;          // a buffer was too small (el_result_wait: EL_ERANGE)
+  hipEvent_t ev_strm = nullptr;
+  void stream_out();
+  void stream_end(bool release);
   hipEvent_t ev_base[2] = {nullptr, nullptr};  // base links logged (stream) / in the link set (rstream)
   bool base_filling = false;                   // the set fill runs beside the first superstep
   void join_base();
@@ -3245,7 +3254,10 @@ bool el_ctx::superstep(uint32_t mask, uint64_t sb, uint64_t se, uint64_t lb, uin
                       2 * (l_count - l_base + cl_cap) > lhash_cap || a_count + ca_cap > alog_cap ||
                       2 * (a_count + ca_cap) > ahash_cap || p_count + cp_cap > plog_cap ||
                       2 * (p_count - p_base + cp_cap) > phash_cap;
-    if (grow) sync();
+    if (grow) {
+      sync();
+      if (strm) HIPCHK(hipStreamSynchronize(dstream));  // (a streamed result may still read the logs)
+    }
     auto grow_log = [&](uint64_t used, uint64_t add, uint64_t& cap, uint32_t*& a, uint32_t*& b) {
       if (used + add <= cap) return;
       uint64_t c = next_pow2(used + add + (used + add) / 2);
@@ -3481,6 +3493,7 @@ uint64_t el_ctx::superstep_part(uint32_t mask, uint64_t sb, uint64_t se, uint64_
                       x_count + part_count * xcap > xlog_cap;
     if (grow) {
       sync();
+      if (strm) HIPCHK(hipStreamSynchronize(dstream));
       auto grow_log = [&](uint64_t used, uint64_t add, uint64_t& cap, uint32_t*& a, uint32_t*& b) {
         if (used + add <= cap) return;
         uint64_t c = next_pow2(used + add + (used + add) / 2);
@@ -3675,9 +3688,10 @@ void el_ctx::alloc_closure() {
   cl.meta = dalloc<uint4>(2 * N);
   cl.meta2 = dalloc<uint4>(2 * N);
   // first guesses (G3: 24 M / 25 M / 36 M entries); an overflowing build grows and runs again
-  cl.t_cap = cap32(64 * N + (1u << 20));
-  cl.e_cap = cap32(64 * N + (1u << 20));
-  cl.l_cap = cap32(96 * N + (1u << 20));
+  const uint64_t waste = std::min<uint64_t>(N, elcl::SLOTS) * elcl::CHUNK;  // partly used chunks
+  cl.t_cap = cap32(64 * N + waste + (1u << 16));
+  cl.e_cap = cap32(64 * N + waste + (1u << 16));
+  cl.l_cap = cap32(96 * N + waste + (1u << 16));
   cl.t_val = dalloc<uint32_t>(cl.t_cap);
   cl.e_val = dalloc<uint32_t>(cl.e_cap);
   cl.l_r = dalloc<uint32_t>(cl.l_cap);
@@ -3687,7 +3701,7 @@ void el_ctx::alloc_closure() {
   cl.lvl_flag = dalloc<uint32_t>(N + 2);
   cl.dirty = dalloc<uint8_t>(N);
   cl.dirty2 = dalloc<uint8_t>(N);
-  cl.changed = dalloc<uint8_t>(N);
+  cl.changed = dalloc<uint32_t>(N);
   cl.nd = dalloc<uint32_t>(elcl::ND_NUM * (N + 1));
   HIPCHK(hipMemset(cl.nd, 0, elcl::ND_NUM * (N + 1) * sizeof(uint32_t)));  // (entry N of a column stays 0)
   cl.rsv = dalloc<uint32_t>(elcl::RSV_WORDS);
@@ -3781,6 +3795,7 @@ void el_ctx::closure_grow() {
 void el_ctx::closure_tail(uint32_t a, uint32_t b, uint32_t L) {
   HIPCHK(hipMemsetAsync(&cl.ctr->tot[elcl::T_STUCK], 0, sizeof(unsigned long long), stream));
   elcl::check(stream, cax, cl);
+  elcl::stats(stream, cax, cl, 0, hx.N, use_props && !part());  // (every row: the SC layout spans them)
   HIPCHK(hipMemsetAsync(cl.ctr->tot, 0, elcl::T_STUCK * sizeof(unsigned long long), stream));
   HIPCHK(hipMemsetAsync(cl.ctr->ev, 0, sizeof(cl.ctr->ev), stream));
   elcl::totals(stream, cax, cl, a, b);
@@ -3800,7 +3815,6 @@ void el_ctx::closure_tail(uint32_t a, uint32_t b, uint32_t L) {
 // up front), one per relaxation round.
 void el_ctx::closure_rows(uint32_t a, uint32_t b) {
   const uint32_t N = hx.N;
-  const bool props = use_props && !part();
   for (int attempt = 0;; ++attempt) {
     if (attempt > 32) throw ElError{EL_EHIP, "told closure: the build did not fit its buffers"};
     launch(EL_K_CLOSURE, [&] { elcl::start(stream, cax, cl); });
@@ -3808,7 +3822,7 @@ void el_ctx::closure_rows(uint32_t a, uint32_t b) {
     bool redo = false;
     for (;;) {
       const uint32_t end = (uint32_t)std::min<uint64_t>((uint64_t)N + 1, (uint64_t)L + level_hint);
-      for (; L < end; ++L) launch(EL_K_CLOSURE, [&] { elcl::level(stream, cax, cl, L, props); });
+      for (; L < end; ++L) launch(EL_K_CLOSURE, [&] { elcl::level(stream, cax, cl, L); });
       closure_tail(a, b, L);
       if (clh->ctr.ovf) {
         redo = true;
@@ -3822,7 +3836,7 @@ void el_ctx::closure_rows(uint32_t a, uint32_t b) {
     }
     if (!redo && clh->ctr.tot[elcl::T_STUCK]) {  // told cycles: relaxation rounds until no row grows
       for (uint64_t round = 0;; ++round) {
-        launch(EL_K_CLOSURE, [&] { elcl::relax(stream, cax, cl, props); });
+        launch(EL_K_CLOSURE, [&] { elcl::relax(stream, cax, cl); });
         HIPCHK(hipMemcpyAsync(&clh->ctr, cl.ctr, sizeof(elcl::Ctr), hipMemcpyDeviceToHost, stream));
         sync();
         if (clh->ctr.ovf) {
@@ -4046,6 +4060,52 @@ void el_ctx::install_base() {
   // the log entries read and written, the rows' entries
   host_ev[EL_K_INIT][EL_EV_ENT] += nb + (PR.live ? nb : 0) + (SC.live ? nc : 0);
   host_ev[EL_K_INIT][EL_EV_EMIT] += nb;
+}
+
+// Streamed result: enqueue the DMAs of the log entries committed since the last call (behind
+// the work enqueued on the engine stream so far: the entries below s_count / l_count are final).
+void el_ctx::stream_out() {
+  if (!strm) return;
+  const uint64_t s1 = s_count, l1 = l_count;
+  if (s1 == strm_s && l1 == strm_l) return;
+  HIPCHK(hipEventRecord(ev_strm, stream));
+  HIPCHK(hipStreamWaitEvent(dstream, ev_strm, 0));
+  auto dma = [&](uint32_t* dst, const uint32_t* src, uint64_t a, uint64_t b, uint64_t cap) {
+    b = std::min(b, cap);
+    if (dst && b > a)
+      HIPCHK(hipMemcpyAsync(dst + a, src + a, (b - a) * sizeof(uint32_t), hipMemcpyDeviceToHost, dstream));
+  };
+  dma(strm->s_x, slog_x, strm_s, s1, strm->s_cap);
+  dma(strm->s_b, slog_a, strm_s, s1, strm->s_cap);
+  dma(strm->l_x, llog_x, strm_l, l1, strm->l_cap);
+  dma(strm->l_p, llog_p, strm_l, l1, strm->l_cap);
+  if ((strm->s_x && s1 > strm->s_cap) || (strm->l_x && l1 > strm->l_cap)) strm_ovf = true;
+  strm_s = s1;
+  strm_l = l1;
+}
+
+// The fixpoint: the last segments, the counts, and (release) the next classification's reset on
+// the third stream beside the DMA tail (it reads the logs, as the DMA does; el_init waits for both).
+// A buffer that was too small keeps the state, so the caller can stream it again, fitted.
+void el_ctx::stream_end(bool release) {
+  if (!strm) return;
+  stream_out();
+  strm->n_facts = s_count;
+  strm->n_links = l_count;
+  strm = nullptr;
+  HIPCHK(hipEventRecord(ev_copied[0], cstream));
+  HIPCHK(hipEventRecord(ev_copied[1], stream));
+  HIPCHK(hipEventRecord(ev_copied[2], dstream));
+  copy_pending = true;
+  if (release && !strm_ovf) {
+    HIPCHK(hipEventRecord(ev_rows[0], stream));
+    HIPCHK(hipStreamWaitEvent(rstream, ev_rows[0], 0));
+    reset_device(rstream, lo, lo);
+    HIPCHK(hipEventRecord(ev_reset, rstream));
+    pre_reset = true;
+    inited = false;
+    rs.n = rl.n = ~0ull;
+  }
 }
 
 // After the first superstep: the link set holds the base links (k_rehash on rstream), so
@@ -4309,6 +4369,7 @@ int el_create(el_ctx** out, const el_config* cfg) {
     HIPCHK(hipEventCreateWithFlags(&c->ev_reset, hipEventDisableTiming));
     for (hipEvent_t& e : c->ev_copied) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     for (hipEvent_t& e : c->ev_base) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    HIPCHK(hipEventCreateWithFlags(&c->ev_strm, hipEventDisableTiming));
     if (c->xmode == EL_XCHG_LOCAL) c->xchg.reset(new LocalExchange(cfg->group, (int)c->part_rank));
     if (c->xmode == EL_XCHG_RCCL)  // collective: every rank of the group calls el_create
       c->xchg.reset(new RcclExchange((int)c->part_rank, (int)c->part_count, cfg->rccl_id));
@@ -4332,6 +4393,7 @@ int el_create(el_ctx** out, const el_config* cfg) {
       if (e) (void)hipEventDestroy(e);
     for (hipEvent_t e : c->ev_dma)
       if (e) (void)hipEventDestroy(e);
+    if (c->ev_strm) (void)hipEventDestroy(c->ev_strm);
     delete c;
     return rc;
   }
@@ -4483,6 +4545,7 @@ int el_saturate(el_ctx* c, el_stats* stats) {
     auto t0 = std::chrono::steady_clock::now();
     if (c->fresh && !c->part()) c->install_base();
     c->fresh = false;
+    c->stream_out();  // (a streamed result: the init facts and base links cross PCIe already)
     // all rule types share one frontier: start at the oldest watermark
     uint64_t sb = c->s_count, lb = c->l_count, ab = c->a_count, pb = c->p_count;
     for (int r = 0; r < EL_NUM_RULE_TYPES; ++r) {
@@ -4508,6 +4571,7 @@ int el_saturate(el_ctx* c, el_stats* stats) {
         c->tr_l.push_back(le - lb);
         c->tr_a.push_back(ae - ab);
         const uint64_t g = c->superstep_part(mask, sb, se, lb, le, ab, ae, pb, pe2, xb, xe);
+        c->stream_out();
         sb = se, lb = le, ab = ae, pb = pe2, xb = xe;
         if (g == 0) break;
       }
@@ -4522,6 +4586,7 @@ int el_saturate(el_ctx* c, el_stats* stats) {
       c->tr_a.push_back(ae - ab);
       c->superstep(pb < pe ? (M_ALL | M_R4P) : M_ALL, sb, se, lb, le, ab, ae, pb, pe);
       c->join_base();
+      c->stream_out();
       sb = se;
       lb = le;
       ab = ae;
@@ -4534,6 +4599,8 @@ int el_saturate(el_ctx* c, el_stats* stats) {
       c->wm_p[r] = c->p_count;
     }
     c->enqueue_events();  // hc is current (published by the last k_commit); events ride along
+    const bool rel = c->strm && (c->strm->flags & EL_RESULT_RELEASE);
+    c->stream_end(rel);
     c->sync();
     double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     c->fill_stats(stats, ms);
@@ -4820,7 +4887,34 @@ int el_copy_result(el_ctx* c, el_result* res) {
 }
 
 int el_result_wait(el_ctx* c) {
-  return guarded(c, [&] { return EL_OK; });  // (guarded waits for an async copy-back)
+  return guarded(c, [&] {  // (guarded waits for an async copy-back or a streamed result)
+    if (c->strm_ovf) return fail(c, EL_ERANGE, "streamed result: a buffer was smaller than its part");
+    return EL_OK;
+  });
+}
+
+int el_stream_result(el_ctx* c, el_stream* s) {
+  if (!c || !s) return EL_EINVAL;
+  if (!c->inited) return fail(c, EL_ESTATE, "el_stream_result before el_init");
+  if (s->flags & ~EL_RESULT_RELEASE) return fail(c, EL_EINVAL, "unknown el_stream flags");
+  return guarded(c, [&] {
+    c->strm = s;
+    c->strm_ovf = false;
+    // everything already logged is streamed too (from the first entry)
+    c->strm_s = c->strm_l = 0;
+    s->n_facts = s->n_links = 0;
+    return EL_OK;
+  });
+}
+
+int el_pid_table(el_ctx* c, uint32_t* role, uint32_t* filler, size_t cap, size_t* n) {
+  if (!c || !n) return EL_EINVAL;
+  if (!c->loaded) return fail(c, EL_ESTATE, "no ontology loaded");
+  *n = c->hx.P;
+  if (cap < *n) return EL_ERANGE;
+  if (role) std::copy(c->hx.pair_role.begin(), c->hx.pair_role.end(), role);
+  if (filler) std::copy(c->hx.pair_y.begin(), c->hx.pair_y.end(), filler);
+  return EL_OK;
 }
 
 int el_pair_table(el_ctx* c, uint32_t* role, uint32_t* filler, size_t cap, size_t* n) {
@@ -4943,6 +5037,7 @@ void el_destroy(el_ctx* c) {
     if (e) (void)hipEventDestroy(e);
   for (hipEvent_t e : c->ev_dma)
     if (e) (void)hipEventDestroy(e);
+  if (c->ev_strm) (void)hipEventDestroy(c->ev_strm);
   delete c;
 }
 

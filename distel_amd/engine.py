@@ -32,7 +32,7 @@ KERNEL_NAMES = ["k_expand:s", "k_expand:l", "k_jobs", "k_expand:a", "k_commit:s"
 EVENT_NAMES = ["trig", "row", "ent", "test", "hash", "emit", "job", "rmw"]
 EVENT_BYTES = [8, 8, 4, 4, 8, 8, 16, 8]
 NUM_KERNELS = len(KERNEL_NAMES)
-ABI_VERSION = 5  # include/el_gpu.h EL_ABI_VERSION
+ABI_VERSION = 6  # include/el_gpu.h EL_ABI_VERSION
 XCHG_NONE, XCHG_LOCAL, XCHG_RCCL = 0, 1, 2
 NUM_EVENTS = len(EVENT_NAMES)
 
@@ -96,6 +96,11 @@ class _ElResult(C.Structure):
                 ("l_ptr", C.POINTER(C.c_uint64)), ("l_pair", _u32p), ("l_cap", C.c_uint64)]
 
 
+class _ElStream(C.Structure):
+    _fields_ = [("flags", C.c_uint32), ("s_x", _u32p), ("s_b", _u32p), ("s_cap", C.c_uint64), ("l_x", _u32p),
+                ("l_p", _u32p), ("l_cap", C.c_uint64), ("n_facts", C.c_uint64), ("n_links", C.c_uint64)]
+
+
 _SINK = C.CFUNCTYPE(C.c_int, C.c_void_p, _u32p, _u32p, C.c_size_t)
 
 EXPORTED_SYMBOLS = [
@@ -103,7 +108,7 @@ EXPORTED_SYMBOLS = [
     "el_get_stats", "el_kernel_stats", "el_superstep_trace", "el_get_subsumers", "el_copy_facts",
     "el_copy_links", "el_export_result", "el_last_error", "el_destroy", "el_group_create", "el_group_destroy",
     "el_rccl_unique_id", "el_add_axioms", "el_result_info", "el_copy_result", "el_result_wait", "el_pair_table", "el_host_alloc",
-    "el_host_free", "el_fresh_fillers",
+    "el_host_free", "el_fresh_fillers", "el_stream_result", "el_pid_table",
 ]
 
 _lib: Optional[C.CDLL] = None
@@ -141,6 +146,8 @@ def load_library(path: Optional[str] = None) -> C.CDLL:
     lib.el_result_wait.argtypes = [P]
     lib.el_copy_result.argtypes = [P, C.POINTER(_ElResult)]
     lib.el_pair_table.argtypes = [P, _u32p, _u32p, C.c_size_t, C.POINTER(C.c_size_t)]
+    lib.el_pid_table.argtypes = [P, _u32p, _u32p, C.c_size_t, C.POINTER(C.c_size_t)]
+    lib.el_stream_result.argtypes = [P, C.POINTER(_ElStream)]
     lib.el_host_alloc.argtypes = [C.c_size_t]
     lib.el_host_alloc.restype = C.c_void_p
     lib.el_host_free.argtypes = [C.c_void_p]
@@ -246,6 +253,35 @@ class Result:
         return self.s_val[int(self.s_ptr[i]):int(self.s_ptr[i + 1])]
 
 
+class Stream:
+    """Streamed result (el_stream_result): the result node's writes in commit order, as they are
+    committed — S facts (s_x[i], s_b[i]) meaning s_b[i] ∈ S(s_x[i]), links (l_x[i], l_p[i]) with
+    pair id l_p[i] (Engine.pid_table()).  Page-locked buffers, reused across classifications;
+    complete after Engine.result_wait()."""
+
+    def __init__(self):
+        self.n_facts = self.n_links = 0
+        self.s_x = self.s_b = self.l_x = self.l_p = None
+        self._st = _ElStream()
+
+    def fit(self, n_facts: int, n_links: int) -> None:
+        if self.s_x is None or self.s_x.size < n_facts:
+            n = n_facts + n_facts // 8 + 1024
+            self.s_x, self.s_b = pinned_array(n, np.uint32), pinned_array(n, np.uint32)
+        if self.l_x is None or self.l_x.size < n_links:
+            n = n_links + n_links // 8 + 1024
+            self.l_x, self.l_p = pinned_array(n, np.uint32), pinned_array(n, np.uint32)
+
+    def facts(self, n_user: Optional[int] = None) -> Tuple[np.ndarray, np.ndarray]:
+        """(x, a) pairs sorted by (x, a); rows >= n_user (ELK range fillers) dropped when given."""
+        x, a = self.s_x[:self.n_facts].copy(), self.s_b[:self.n_facts].copy()
+        if n_user is not None:
+            keep = x < n_user
+            x, a = x[keep], a[keep]
+        o = np.lexsort((a, x))
+        return x[o], a[o]
+
+
 class Stats(dict):
     @staticmethod
     def from_c(s: _ElStats) -> "Stats":
@@ -316,6 +352,9 @@ class Engine:
             raise ElError(rc, f"el_create(device={device}) failed: no usable HIP device or bad partition")
         self.partition = partition
         self.ax: Optional[Axioms] = None
+        self._last: Optional[Stats] = None   # the last saturation's stats
+        self._streamed = None  # (Stream, release) of the last streamed result until result_wait
+        self._stream: Optional[Stream] = None  # a streamed result armed for the next saturate()
 
     def _check(self, rc: int, what: str) -> None:
         if rc != EL_OK:
@@ -344,6 +383,7 @@ class Engine:
         view = AxiomsView(ax)
         self._check(self._lib.el_load(self._ctx, C.byref(view.struct)), "el_load")
         self.ax = ax
+        self._last = None  # (its counts size streamed results of this ontology only)
 
     def init(self) -> None:
         self._check(self._lib.el_init(self._ctx), "el_init")
@@ -354,6 +394,7 @@ class Engine:
         view = AxiomsView(inc)
         self._check(self._lib.el_add_axioms(self._ctx, C.byref(view.struct)), "el_add_axioms")
         self.ax = merge_axioms(self.ax, inc) if self.ax is not None else inc
+        self._last = None
 
     def step(self, rule: int) -> bool:
         ch = C.c_int(0)
@@ -363,7 +404,11 @@ class Engine:
     def saturate(self) -> Stats:
         s = _ElStats()
         self._check(self._lib.el_saturate(self._ctx, C.byref(s)), "el_saturate")
-        return Stats.from_c(s)
+        self._last = Stats.from_c(s)
+        if self._stream is not None:  # (a streamed result: its counts are known now)
+            self._stream.n_facts, self._stream.n_links = int(self._stream._st.n_facts), int(self._stream._st.n_links)
+            self._stream = None
+        return self._last
 
     def stats(self) -> Stats:
         s = _ElStats()
@@ -461,9 +506,54 @@ class Engine:
                                                                          r.n_pairs)
         return out
 
+    def stream_result(self, out: Stream, release: bool = False, n_facts: int = 0, n_links: int = 0) -> Stream:
+        """Arm the next saturate() to stream its result into ``out`` while it runs; complete after
+        result_wait().  Buffers fit max(n_facts / n_links, the last saturation's counts), or
+        64 entries per concept when neither is known for the loaded ontology (result_wait raises
+        EL_ERANGE if short)."""
+        last = self._last
+        nf = max(n_facts, last["s_facts"] if last else 0) or 64 * max(self.ax.n_concepts if self.ax else 1, 1)
+        nl = max(n_links, last["links"] if last else 0) or 64 * max(self.ax.n_concepts if self.ax else 1, 1)
+        out.fit(nf, nl)
+        s = out._st
+        s.flags = EL_RESULT_RELEASE if release else 0
+        s.s_x = out.s_x.ctypes.data_as(_u32p)
+        s.s_b = out.s_b.ctypes.data_as(_u32p)
+        s.s_cap = out.s_x.size
+        s.l_x = out.l_x.ctypes.data_as(_u32p)
+        s.l_p = out.l_p.ctypes.data_as(_u32p)
+        s.l_cap = out.l_x.size
+        self._check(self._lib.el_stream_result(self._ctx, C.byref(s)), "el_stream_result")
+        self._stream = out
+        self._streamed = (out, release)
+        return out
+
+    def pid_table(self) -> Tuple[np.ndarray, np.ndarray]:
+        """pair id -> (role, filler), in pid order (the ids streamed links carry)."""
+        n = C.c_size_t(0)
+        rc = self._lib.el_pid_table(self._ctx, None, None, 0, C.byref(n))
+        if rc not in (EL_OK, EL_ERANGE):
+            self._check(rc, "el_pid_table")
+        role = np.zeros(n.value, np.uint32)
+        filler = np.zeros(n.value, np.uint32)
+        self._check(self._lib.el_pid_table(self._ctx, _ptr(role), _ptr(filler), n.value, C.byref(n)), "el_pid_table")
+        return role, filler
+
     def result_wait(self) -> None:
-        """Block until an asynchronous copy-back (copy_result(wait=False)) has landed."""
-        self._check(self._lib.el_result_wait(self._ctx), "el_result_wait")
+        """Block until an asynchronous copy-back (copy_result(wait=False)) or a streamed result
+        has landed.  A streamed result whose buffers were short (EL_ERANGE: the state was kept)
+        is streamed again at the fixpoint into buffers fitted to its counts."""
+        rc = self._lib.el_result_wait(self._ctx)
+        streamed, self._streamed = self._streamed, None
+        if rc == EL_ERANGE and streamed is not None:
+            out, release = streamed
+            last = self._last
+            self.stream_result(out, release, out.n_facts, out.n_links)
+            self.saturate()  # (no superstep: the whole logs stream)
+            self._last = last
+            self._streamed = None
+            rc = self._lib.el_result_wait(self._ctx)
+        self._check(rc, "el_result_wait")
 
     def fresh_fillers(self) -> Tuple[np.ndarray, np.ndarray]:
         """ELK range fillers: concept n_concepts + i = filler[i] ⊓ ranges*(role[i])."""

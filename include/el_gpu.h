@@ -42,7 +42,7 @@
 extern "C" {
 #endif
 
-#define EL_ABI_VERSION 5
+#define EL_ABI_VERSION 6
 
 /* return codes */
 #define EL_OK        0
@@ -305,6 +305,37 @@ typedef struct el_result {
   uint32_t* l_pair;         /* in: l_cap entries (>= n_links), or NULL */
   uint64_t l_cap;
 } el_result;
+
+/* Streamed result: the result node's writes as the supersteps commit them (the reference's
+ * classification output is result-node DB0, sets filled by ZADD as facts are derived; the
+ * X -> {B} flip is ResultRearranger's post-pass, ResultRearranger.java:57-105).  Armed after
+ * el_init, before el_saturate: while the saturation runs, every committed segment of the fact
+ * log and of the link log crosses PCIe into the caller's page-locked buffers (DMA beside the
+ * next supersteps; a fact once derived never changes), so little is left to copy at the fixpoint.
+ *   S facts  b ∈ S(x) as (s_x[i], s_b[i]), i < n_facts, in commit order (no duplicates)
+ *   links    (x, y) ∈ R(r) as (l_x[i], l_p[i]), i < n_links, (r, y) = el_pid_table()[l_p[i]]
+ * Rows x ≥ n_concepts are the ELK range fillers (el_fresh_fillers), internal concepts.
+ * n_facts / n_links are set when el_saturate returns; the buffers are complete when
+ * el_result_wait returns (every other call on the context waits for them first).  A buffer
+ * smaller than its part: the first s_cap / l_cap entries arrive, el_result_wait returns
+ * EL_ERANGE and the state is kept (not released): arm again with buffers of n_facts / n_links
+ * entries and call el_saturate, which at the fixpoint runs no superstep and streams the whole
+ * logs.  flags EL_RESULT_RELEASE: the state is released behind the saturation (no state until
+ * el_init), as for el_copy_result. */
+typedef struct el_stream {
+  uint32_t flags;           /* in: EL_RESULT_* (RELEASE) */
+  uint32_t* s_x;            /* in: s_cap entries each, or NULL */
+  uint32_t* s_b;
+  uint64_t s_cap;
+  uint32_t* l_x;            /* in: l_cap entries each, or NULL */
+  uint32_t* l_p;
+  uint64_t l_cap;
+  uint64_t n_facts;         /* out */
+  uint64_t n_links;         /* out */
+} el_stream;
+int el_stream_result(el_ctx* ctx, el_stream* s);  /* arms the next el_saturate; s stays valid until then */
+/* pair id -> (role, filler) in pid order (the ids the streamed links carry) */
+int el_pid_table(el_ctx* ctx, uint32_t* role, uint32_t* filler, size_t cap, size_t* n);
 
 int el_result_info(el_ctx* ctx, el_result* res);   /* the out fields only */
 int el_copy_result(el_ctx* ctx, el_result* res);   /* EL_ERANGE if a buffer is too small */

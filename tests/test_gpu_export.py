@@ -350,3 +350,117 @@ def test_readout_block_summary(release, oracle_lib, monkeypatch):
     ptr, oa = _oracle_rows(o, ax.n_concepts)
     assert np.array_equal(res.s_ptr, ptr) and np.array_equal(res.s_val[:res.n_facts], oa)
     eng.close()
+
+
+# ---- streamed result (el_stream_result): the result node's writes in commit order, DMA'd while
+# the supersteps run
+
+def _stream_sets(eng, strm, n_user):
+    """S facts sorted by (x, a) and links (x, r, y) sorted, from a streamed result."""
+    x, a = strm.facts(n_user)
+    role, filler = eng.pid_table()
+    lx, lp = strm.l_x[:strm.n_links], strm.l_p[:strm.n_links]
+    keep = lx < n_user
+    lx, lr, ly = lx[keep], role[lp[keep]], filler[lp[keep]]
+    o = np.lexsort((ly, lr, lx))
+    return x, a, lx[o], lr[o], ly[o]
+
+
+def _assert_stream_matches(eng, strm, o, n_user):
+    x, a, lx, lr, ly = _stream_sets(eng, strm, n_user)
+    ox, oa = o.facts()
+    assert np.array_equal(x, ox) and np.array_equal(a, oa)
+    for g, c in zip((lx, lr, ly), o.links()):
+        assert np.array_equal(g, c)
+
+
+@pytest.mark.parametrize("path", kat.kat_files()[:12], ids=lambda p: os.path.basename(p))
+def test_stream_result_kat(path, oracle_lib):
+    ax, _ = kat.load_kat(path)
+    eng = engine.Engine(device=0)
+    eng.load(ax)
+    eng.init()
+    strm = eng.stream_result(engine.Stream())
+    st = eng.saturate()
+    eng.result_wait()
+    # every logged fact / link streamed once (the ELK range fillers' rows included)
+    assert (strm.n_facts, strm.n_links) == (st["s_facts"], st["links"])
+    _assert_stream_matches(eng, strm, oracle_lib.saturate(ax, 0), ax.n_concepts)
+    eng.close()
+
+
+def test_stream_result_fuzz_release(oracle_lib):
+    """Random ontologies (told cycles included), streamed with release, one engine reused."""
+    eng = engine.Engine(device=0)
+    strm = engine.Stream()
+    for seed in range(60):
+        ax = generators.random_small(4400 + seed, n=8 + seed % 50, n_roles=1 + seed % 4)
+        eng.load(ax)
+        eng.init()
+        eng.stream_result(strm, release=True)
+        eng.saturate()
+        eng.result_wait()
+        _assert_stream_matches(eng, strm, oracle_lib.saturate(ax, 0), ax.n_concepts)
+    eng.close()
+
+
+def test_stream_result_small_buffers_erange():
+    ax = generators.workload("g1", 0.05)
+    eng = engine.Engine(device=0)
+    eng.load(ax)
+    eng.init()
+    st = eng.saturate()
+    eng.init()
+    strm = engine.Stream()
+    strm.fit(16, 16)
+    strm_sz = strm.s_x.size
+    eng._last = None
+    s = engine._ElStream()  # arm by hand with buffers far too small
+    s.s_x = strm.s_x.ctypes.data_as(engine._u32p)
+    s.s_b = strm.s_b.ctypes.data_as(engine._u32p)
+    s.s_cap = 16
+    s.l_x = strm.l_x.ctypes.data_as(engine._u32p)
+    s.l_p = strm.l_p.ctypes.data_as(engine._u32p)
+    s.l_cap = 16
+    assert eng._lib.el_stream_result(eng._ctx, engine.C.byref(s)) == engine.EL_OK
+    eng._lib.el_saturate(eng._ctx, None)
+    assert s.n_facts == st["s_facts"] and strm_sz >= 16
+    with pytest.raises(engine.ElError):
+        eng.result_wait()
+    eng.close()
+
+
+def test_stream_result_g3_digest_two_engines():
+    """The bench's schedule at full G3 with the streamed copy-back: one engine serial, then two
+    alternating (one's DMA tail beside the other's classification); every result hashes to the
+    pinned closure digest once sorted."""
+    import hashlib
+    want = _g3_digest()
+    ax = generators.workload("g3")
+    engs = [engine.Engine(device=0) for _ in range(2)]
+    for e in engs:
+        e.load(ax)
+    strms = [engine.Stream(), engine.Stream()]
+
+    def digest(e, s):
+        x, a, lx, lr, ly = _stream_sets(e, s, ax.n_concepts)
+        h = hashlib.sha256()
+        for arr in (x, a, lx, lr, ly):
+            h.update(np.ascontiguousarray(arr, dtype=np.uint32).tobytes())
+        return h.hexdigest()
+
+    for i in range(4):
+        e, s = engs[i % 2] if i >= 2 else engs[0], strms[i % 2] if i >= 2 else strms[0]
+        e.init()
+        e.stream_result(s, release=True)
+        e.saturate()
+        if i < 2:
+            e.result_wait()
+            assert digest(e, s) == want
+        elif i == 3:
+            engs[0].result_wait()  # (landed behind engine 1's classification)
+            assert digest(engs[0], strms[0]) == want
+            engs[1].result_wait()
+            assert digest(engs[1], strms[1]) == want
+    for e in engs:
+        e.close()
