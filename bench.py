@@ -15,13 +15,16 @@ included (``init_ms`` + ``saturate_ms`` + ``copyback_ms`` split it).  ``throughp
 is a separately named figure: two engines (each with its own state and result buffers)
 alternate, one's copy-back (EL_RESULT_ASYNC) crossing PCIe while the other classifies.
 
-Multi-GPU (``torch.distributed.run``): weak scaling.  Rank i classifies its own
-disjoint copy of the workload (OntologyMultiplier ×N semantics, the G4 config);
-copies share no concepts, so there is no data-path collective — only the
-barrier and the max-over-ranks timing (``--partition copies``, the default).
-``--partition exchange`` instead loads the whole ×N ontology on every rank and runs
-the row-partitioned engine (rank i owns copy i's rows) with the per-superstep RCCL
-delta all-gather of SURVEY.md §8(e) — the path for ontologies that do not decompose.
+Multi-GPU (``torch.distributed.run``): weak scaling over the OntologyMultiplier ×N ontology
+(BASELINE configs[3]: SNOMED×8 on 8 GPUs).  Two legs, both on the same ×N workload:
+  exchange  every rank loads the ×N ontology and runs the row-partitioned engine, rank i owning
+            copy i's rows, with the per-superstep RCCL delta all-gather and the delta-count sum
+            as the termination test (CommunicationHandler.java:49-84 is the
+            barrier it replaces).  This is the headline ``value`` at N > 1.
+  copies    rank i classifies only its own copy (the copies share no concepts, so no data-path
+            collective: barrier + max-over-ranks only) — reported as ``copies``.
+A watchdog bounds the exchange leg: if it fails or has not finished in --exchange-timeout
+seconds, rank 0 prints the line with the copies leg as ``value`` and the failure named.
 
 Extra objects on the JSON line:
   roofline      dominant kernel (largest Σ time in a profiled classification):
@@ -112,9 +115,15 @@ def parse():
     ap.add_argument("--cpu-procs", type=int, default=16, help="host cores for the cpu_baseline leg (at most 16)")
     ap.add_argument("--cpu-scale", type=float, default=0.0,
                     help="workload scale of the cpu_baseline sample (default: --scale, capped at ~100 k concepts)")
-    ap.add_argument("--partition", default="copies", choices=["copies", "exchange"],
-                    help="copies: one disjoint copy per rank, no collective; exchange: row-partitioned "
-                         "engine over the ×N ontology with the RCCL delta all-gather")
+    ap.add_argument("--partition", default="auto", choices=["auto", "copies", "exchange"],
+                    help="N > 1: copies = one disjoint copy per rank, no collective; exchange = row-partitioned "
+                         "engine over the ×N ontology with the RCCL delta all-gather; auto (default) = both, "
+                         "exchange as the headline")
+    ap.add_argument("--transport", default="rccl", choices=["rccl", "host"],
+                    help="exchange leg's all-gather: rccl = ncclAllGather over xGMI on the engine stream; host = "
+                         "EL_XCHG_HOST through a gloo group (a rehearsal of N ranks on one GPU)")
+    ap.add_argument("--exchange-timeout", type=float, default=420.0,
+                    help="seconds the exchange leg may take before rank 0 reports the copies leg alone")
     ap.add_argument("--inflight", type=int, default=1, choices=[1, 2],
                     help="classifications in flight in the timed loop: 1 = one at a time (the default: "
                          "ms_per_step is one classification's wall-clock); 2 = two engines alternate, one's "
@@ -131,41 +140,23 @@ def parse():
 
 def main():
     args = parse()
+    import threading
+
     import torch
 
     from distel_amd import dist as D
-    from distel_amd import engine, generators
+    from distel_amd import engine, generators, ir
 
     rk = D.init_from_env()
     world, rank, local = rk.world, rk.rank, rk.local
     has_cuda = torch.cuda.is_available()
+    dev = local if has_cuda else 0
 
     t0 = time.time()
     ax = generators.workload(args.workload, args.scale)   # this rank's copy (×world disjoint copies)
     gen_s = time.time() - t0
-
-    if args.partition == "exchange":
-        from distel_amd import ir
-        full = ir.replicate(ax, world) if world > 1 else ax
-        rows = ir.copy_slice(ax, world, rank) if world > 1 else (0, ax.n_concepts)
-        if rank == 0:
-            rows = (0, rows[1])  # ⊥ and ⊤ live on rank 0
-        uid = engine.rccl_unique_id() if rank == 0 else None
-        if world > 1:
-            box = [uid]
-            rk.dist.broadcast_object_list(box, src=0)
-            uid = box[0]
-        with _stdout_to_stderr():  # RCCL prints its version banner on stdout at communicator init
-            eng = engine.Engine(device=local if has_cuda else 0,
-                                partition=engine.Partition(rank, world, engine.XCHG_RCCL, rccl_id=uid, rows=rows))
-        t0 = time.time()
-        eng.load(full)
-        load_s = time.time() - t0
-    else:
-        eng = engine.Engine(device=local if has_cuda else 0)
-        t0 = time.time()
-        eng.load(ax)  # host index build + upload: AxiomLoader's part, reported separately
-        load_s = time.time() - t0
+    run_copies = args.partition != "exchange"
+    run_exchange = args.partition == "exchange" or (world > 1 and args.partition == "auto")
 
     def timed(engines, steps, warmup):
         """K classifications between barriers.  One engine: each step runs init + saturate +
@@ -216,43 +207,162 @@ def main():
         if pool is not None:
             pool.shutdown()
         for r in results:
-            assert (r.n_facts, r.n_links) == (st["s_facts"], st["links"]) or (len(ax.range) and not stream), \
-                "copy-back lost facts"
-        return t_max, derived_all, st, split[-steps:], results[(turn[0] - 1) % len(engines)]
+            assert (r.n_facts, r.n_links) == (st["s_facts"], st["links"]) or (len(ax.range) and not stream) or \
+                engines[0].partition is not None, "copy-back lost facts"
+        res = results[(turn[0] - 1) % len(engines)]
+        copy_bytes = (8 * (res.n_facts + res.n_links) if stream else
+                      8 * 2 * (res.row_hi - res.row_lo + 1) + 4 * (res.n_facts + res.n_links))
+        sp = split[-steps:]
+        return {"t_max": t_max, "derived": derived_all, "st": st, "ms_per_step": 1e3 * t_max / steps,
+                "value": derived_all * steps / t_max, "copy_bytes": int(copy_bytes),
+                "init_ms": 1e3 * sum(t[0] for t in sp) / len(sp), "saturate_ms": 1e3 * sum(t[1] for t in sp) / len(sp),
+                "copyback_ms": 1e3 * sum(t[2] for t in sp) / len(sp), "inflight": len(engines)}
 
-    engines = [eng]
-    if args.inflight == 2 and args.partition == "copies":
-        eng2 = engine.Engine(device=local if has_cuda else 0)
-        eng2.load(ax)
-        engines.append(eng2)
-    t_max, derived_all, st, timed_split, res = timed(engines, args.steps, args.warmup)
-    ms_per_step = 1e3 * t_max / args.steps
-    value = derived_all * args.steps / t_max
-    init_ms = 1e3 * sum(t[0] for t in timed_split) / len(timed_split)
-    saturate_ms = 1e3 * sum(t[1] for t in timed_split) / len(timed_split)
-    copyback_ms = 1e3 * sum(t[2] for t in timed_split) / len(timed_split)
-    copy_bytes = (8 * (res.n_facts + res.n_links) if args.copyback == "stream" else
-                  8 * 2 * (res.row_hi - res.row_lo + 1) + 4 * (res.n_facts + res.n_links))
-    # the copy-back holds every row of the caller's concepts (el_stats also counts the rows of
-    # ELK range fillers, internal concepts, when the ontology has range axioms)
-    throughput2 = None
-    if len(engines) == 1 and args.partition == "copies" and not args.no_throughput2:
-        eng2 = engine.Engine(device=local if has_cuda else 0)
-        eng2.load(ax)
-        t2_max, d2_all, _, _, _ = timed([eng, eng2], args.steps, args.warmup)
-        eng2.close()
-        throughput2 = {"value": round(d2_all * args.steps / t2_max, 1), "unit": "axioms/s",
-                       "ms_per_classification": round(1e3 * t2_max / args.steps, 4), "steps": args.steps,
-                       "schedule": "two engines alternate; one's result copy-back (EL_RESULT_ASYNC) overlaps "
-                                   "the other's classification"}
-    for e in engines:
-        e.close()
+    legs = {}
+    if run_copies:
+        # whole ontology (N = 1) / this rank's own copy (N > 1): no data-path collective
+        eng = engine.Engine(device=dev)
+        t0 = time.time()
+        eng.load(ax)  # host index build + upload: AxiomLoader's part, reported separately
+        load_s = time.time() - t0
+        engines = [eng]
+        if args.inflight == 2:
+            eng2 = engine.Engine(device=dev)
+            eng2.load(ax)
+            engines.append(eng2)
+        legs["copies"] = timed(engines, args.steps, args.warmup)
+        legs["copies"]["load_s"] = load_s
+        if len(engines) == 1 and world == 1 and not args.no_throughput2:
+            eng2 = engine.Engine(device=dev)
+            eng2.load(ax)
+            t2 = timed([eng, eng2], args.steps, args.warmup)
+            eng2.close()
+            legs["copies"]["throughput2"] = {
+                "value": round(t2["value"], 1), "unit": "axioms/s",
+                "ms_per_classification": round(t2["ms_per_step"], 4), "steps": args.steps,
+                "schedule": "two engines alternate; one's result copy-back (EL_RESULT_ASYNC) overlaps "
+                            "the other's classification"}
+        for e in engines:
+            e.close()
+
+    def exchange_leg():
+        full = ir.replicate(ax, world) if world > 1 else ax
+        rows = ir.copy_slice(ax, world, rank) if world > 1 else (0, ax.n_concepts)
+        if rank == 0:
+            rows = (0, rows[1])  # ⊥ and ⊤ live on rank 0
+        if args.transport == "host":
+            group = rk.dist.new_group(backend="gloo") if world > 1 else None
+            part = engine.Partition(rank, world, engine.XCHG_HOST, rows=rows,
+                                    allgather=engine.gloo_allgather(group) if world > 1 else
+                                    (lambda send, recv: recv.__setitem__(slice(None), send)))
+        else:
+            uid = engine.rccl_unique_id() if rank == 0 else None
+            if world > 1:
+                box = [uid]
+                rk.dist.broadcast_object_list(box, src=0)
+                uid = box[0]
+            part = engine.Partition(rank, world, engine.XCHG_RCCL, rccl_id=uid, rows=rows)
+        with _stdout_to_stderr():  # RCCL prints its version banner on stdout at communicator init
+            xeng = engine.Engine(device=dev, partition=part)
+        t0 = time.time()
+        xeng.load(full)
+        load_s = time.time() - t0
+        leg = timed([xeng], args.steps, args.warmup)
+        leg["load_s"] = load_s
+        xeng.close()
+        return leg
+
+    def build_line(head, head_name, extra):
+        st = head["st"]
+        copies = legs.get("copies")
+        return {
+            "metric": "derived_axioms_per_sec (EL+ classification, SURVEY.md §8(d))",
+            "value": round(head["value"], 1),
+            "unit": "axioms/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(head["ms_per_step"], 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u32",
+            "data": "synthetic",
+            "config": {"workload": WORKLOAD_DESC[args.workload] + (f" ×scale {args.scale}" if args.scale != 1 else "")
+                       + (f", OntologyMultiplier ×{world}" if world > 1 else ""),
+                       "concepts_per_rank": ax.n_concepts, "roles": ax.n_roles, "axioms": ax.counts(),
+                       "parallelism": (f"row partition of the ×{world} ontology over {world} GPUs (rank i owns copy "
+                                       f"i's rows), {'RCCL' if args.transport == 'rccl' else 'host-staged gloo'} "
+                                       f"delta all-gather + delta-count sum per superstep"
+                                       if head_name == "exchange" else
+                                       f"{world} disjoint copies, one per GPU, no data-path collective"
+                                       if world > 1 else "one GPU, whole ontology"),
+                       "schedule": ("two classifications in flight per GPU: one's result copy-back "
+                                    "(EL_RESULT_ASYNC) overlaps the other's classification"
+                                    if head["inflight"] == 2 else "one classification at a time, copy-back included")},
+            "classification_wall_s": round(head["ms_per_step"] / 1e3, 6) if head["inflight"] == 1 else None,
+            "derived_axioms": head["derived"],
+            "s_facts_per_rank": st["s_facts"],
+            "links_per_rank": st["links"],
+            "supersteps": st["supersteps"],
+            "load_s": round(head["load_s"], 3),
+            "generate_s": round(gen_s, 3),
+            "inflight": head["inflight"],
+            "init_ms": round(head["init_ms"], 4),
+            "saturate_ms": round(head["saturate_ms"], 4),
+            "copyback_ms": round(head["copyback_ms"], 4),
+            "latency_ms": round(head["ms_per_step"], 4) if head["inflight"] == 1 else None,
+            "copyback": ("streamed: the result node's (X, B) facts and (X, r, Y) links in commit order, "
+                         "crossing PCIe as the supersteps commit them (el_stream_result)"
+                         if args.copyback == "stream" else
+                         "rows: S(X) and links as sorted CSR rows after the fixpoint (el_copy_result)"),
+            "copyback_bytes": head["copy_bytes"],
+            "copyback_gbs": (round(head["copy_bytes"] / (head["copyback_ms"] * 1e-3) / 1e9, 2)
+                             if head["copyback_ms"] > 0 and args.copyback == "rows" else None),
+            "throughput_inflight2": copies.get("throughput2") if copies else None,
+            **extra,
+        }
+
+    def leg_summary(leg):
+        return {"value": round(leg["value"], 1), "ms_per_step": round(leg["ms_per_step"], 4),
+                "derived_axioms": leg["derived"], "supersteps": leg["st"]["supersteps"],
+                "saturate_ms": round(leg["saturate_ms"], 4), "load_s": round(leg["load_s"], 3)}
+
+    if run_exchange:
+        done = threading.Event()
+
+        def watchdog():
+            if done.wait(args.exchange_timeout):
+                return
+            if rank == 0 and "copies" in legs:
+                line = build_line(legs["copies"], "copies", {
+                    "exchange": {"error": f"exchange leg unfinished after {args.exchange_timeout:.0f} s"},
+                    "roofline": None, "cpu_baseline": None})
+                print(json.dumps(line), flush=True)
+            os._exit(0 if "copies" in legs else 1)
+        threading.Thread(target=watchdog, daemon=True).start()
+        try:
+            legs["exchange"] = exchange_leg()
+        except Exception as exc:  # noqa: BLE001 — reported on the line; the other ranks' watchdogs end them
+            legs["exchange_error"] = f"{type(exc).__name__}: {exc}"
+            print(f"rank {rank}: exchange leg failed: {legs['exchange_error']}", file=sys.stderr, flush=True)
+            if "copies" not in legs:
+                raise
+            if rank == 0:
+                line = build_line(legs["copies"], "copies", {"exchange": {"error": legs["exchange_error"]},
+                                                             "roofline": None, "cpu_baseline": None})
+                print(json.dumps(line), flush=True)
+            os._exit(0)
+        done.set()
+    head_name = "exchange" if "exchange" in legs else "copies"
+    head = legs[head_name]
+    st = head["st"]
 
     roofline = None
     kernels = None
     if rank == 0 and not args.no_profile:
         # profiled classification: HIP events bracket every launch on the engine stream
-        peng = engine.Engine(device=local if has_cuda else 0, profile=True)
+        peng = engine.Engine(device=dev, profile=True)
         peng.load(ax)
         peng.init()
         pst = peng.saturate()
@@ -309,55 +419,17 @@ def main():
                # build; el_init on the GPU) + init + saturation
                "closure_index_s": round(cb["single_create_s"], 4),
                "init_saturate_s": round(cb["single_s"] - cb["single_create_s"], 4)}
-        if cpu_scale == args.scale:
+        if cpu_scale == args.scale and world == 1:
             cpu["parity_derived_equal"] = cb["single_derived"] == st["derived"]
 
     if rank == 0:
-        line = {
-            "metric": "derived_axioms_per_sec (EL+ classification, SURVEY.md §8(d))",
-            "value": round(value, 1),
-            "unit": "axioms/s",
-            "n_gpus": world,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ms_per_step": round(ms_per_step, 4),
-            "higher_is_better": True,
-            "scaling": "weak",
-            "vs_baseline": None,
-            "dtype": "u32",
-            "data": "synthetic",
-            "config": {"workload": WORKLOAD_DESC[args.workload] + (f" ×scale {args.scale}" if args.scale != 1 else ""),
-                       "concepts_per_rank": ax.n_concepts, "roles": ax.n_roles, "axioms": ax.counts(),
-                       "parallelism": (f"{world} disjoint copies, one per GPU (OntologyMultiplier ×{world})"
-                                       if args.partition == "copies" else
-                                       f"row partition of the ×{world} ontology over {world} GPUs, RCCL delta "
-                                       f"all-gather per superstep"),
-                       "schedule": ("two classifications in flight per GPU: one's result copy-back "
-                                    "(EL_RESULT_ASYNC) overlaps the other's classification"
-                                    if len(engines) == 2 else "one classification at a time, copy-back included")},
-            "classification_wall_s": round(ms_per_step / 1e3, 6) if len(engines) == 1 else None,
-            "derived_axioms": derived_all,
-            "s_facts_per_rank": st["s_facts"],
-            "links_per_rank": st["links"],
-            "supersteps": st["supersteps"],
-            "load_s": round(load_s, 3),
-            "generate_s": round(gen_s, 3),
-            "inflight": len(engines),
-            "init_ms": round(init_ms, 4),
-            "saturate_ms": round(saturate_ms, 4),
-            "copyback_ms": round(copyback_ms, 4),
-            "latency_ms": round(ms_per_step, 4) if len(engines) == 1 else None,
-            "copyback": ("streamed: the result node's (X, B) facts and (X, r, Y) links in commit order, "
-                         "crossing PCIe as the supersteps commit them (el_stream_result)"
-                         if args.copyback == "stream" else
-                         "rows: S(X) and links as sorted CSR rows after the fixpoint (el_copy_result)"),
-            "copyback_bytes": int(copy_bytes),
-            "copyback_gbs": (round(copy_bytes / (copyback_ms * 1e-3) / 1e9, 2)
-                             if copyback_ms > 0 and args.copyback == "rows" else None),
-            "throughput_inflight2": throughput2,
-            "roofline": roofline,
-            "cpu_baseline": cpu,
-        }
+        extra = {}
+        if world > 1 or "exchange" in legs:
+            extra["exchange"] = leg_summary(legs["exchange"]) if "exchange" in legs else None
+            extra["copies"] = leg_summary(legs["copies"]) if "copies" in legs else None
+        extra["roofline"] = roofline
+        extra["cpu_baseline"] = cpu
+        line = build_line(head, head_name, extra)
         if args.verbose and kernels:
             line["kernels"] = kernels
         print(json.dumps(line), flush=True)

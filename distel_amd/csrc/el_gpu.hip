@@ -2143,6 +2143,39 @@ struct RcclExchange : Exchange {
   }
 };
 
+// The caller's transport (EL_XCHG_HOST): the send block is staged through page-locked host
+// memory, the caller all-gathers it, and the gathered blocks go back to the device.
+struct HostExchange : Exchange {
+  el_allgather_fn fn;
+  void* user;
+  void *hsend = nullptr, *hrecv = nullptr;
+  size_t cap = 0;
+  HostExchange(int r, int n, el_allgather_fn f, void* u) : fn(f), user(u) {
+    rank = r;
+    size = n;
+  }
+  ~HostExchange() override {
+    if (hsend) (void)hipHostFree(hsend);
+    if (hrecv) (void)hipHostFree(hrecv);
+  }
+  void allgather(const void* send, void* recv, size_t bytes, hipStream_t s) override {
+    if (bytes > cap) {
+      HIPCHK(hipStreamSynchronize(s));  // (the last gather's upload has read hrecv)
+      if (hsend) HIPCHK(hipHostFree(hsend));
+      if (hrecv) HIPCHK(hipHostFree(hrecv));
+      hsend = hrecv = nullptr;
+      HIPCHK(hipHostMalloc(&hsend, bytes, hipHostMallocDefault));
+      HIPCHK(hipHostMalloc(&hrecv, bytes * (size_t)size, hipHostMallocDefault));
+      cap = bytes;
+    }
+    HIPCHK(hipMemcpyAsync(hsend, send, bytes, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));  // (also: the last gather's upload has read hrecv)
+    if (fn(user, hsend, hrecv, bytes) != 0)
+      throw ElError{EL_ESTATE, "EL_XCHG_HOST: the caller's all-gather failed"};
+    HIPCHK(hipMemcpyAsync(recv, hrecv, bytes * (size_t)size, hipMemcpyHostToDevice, s));
+  }
+};
+
 }  // namespace
 
 // In-process group: n contexts driven by n host threads (tests, and one process driving
@@ -4325,7 +4358,8 @@ int el_create(el_ctx** out, const el_config* cfg) {
     c->profile = cfg->profile;
     c->xmode = cfg->exchange;
     if (c->xmode != EL_XCHG_NONE) {
-      const bool bad = (c->xmode != EL_XCHG_LOCAL && c->xmode != EL_XCHG_RCCL) || cfg->part_count < 1 ||
+      const bool bad = (c->xmode != EL_XCHG_LOCAL && c->xmode != EL_XCHG_RCCL && c->xmode != EL_XCHG_HOST) ||
+                       cfg->part_count < 1 || (c->xmode == EL_XCHG_HOST && !cfg->host_allgather) ||
                        cfg->part_rank >= cfg->part_count || cfg->row_hi < cfg->row_lo ||
                        (c->xmode == EL_XCHG_LOCAL && (!cfg->group || cfg->group->n != (int)cfg->part_count));
       if (bad) {
@@ -4373,6 +4407,8 @@ int el_create(el_ctx** out, const el_config* cfg) {
     if (c->xmode == EL_XCHG_LOCAL) c->xchg.reset(new LocalExchange(cfg->group, (int)c->part_rank));
     if (c->xmode == EL_XCHG_RCCL)  // collective: every rank of the group calls el_create
       c->xchg.reset(new RcclExchange((int)c->part_rank, (int)c->part_count, cfg->rccl_id));
+    if (c->xmode == EL_XCHG_HOST)
+      c->xchg.reset(new HostExchange((int)c->part_rank, (int)c->part_count, cfg->host_allgather, cfg->host_user));
     return EL_OK;
   });
   if (rc != EL_OK) {

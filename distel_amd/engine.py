@@ -9,7 +9,7 @@ from __future__ import annotations
 import ctypes as C
 import enum
 import os
-from typing import Dict, Iterator, List, Optional, Tuple
+from typing import Callable, Dict, Iterator, List, Optional, Tuple
 
 import numpy as np
 
@@ -32,8 +32,8 @@ KERNEL_NAMES = ["k_expand:s", "k_expand:l", "k_jobs", "k_expand:a", "k_commit:s"
 EVENT_NAMES = ["trig", "row", "ent", "test", "hash", "emit", "job", "rmw"]
 EVENT_BYTES = [8, 8, 4, 4, 8, 8, 16, 8]
 NUM_KERNELS = len(KERNEL_NAMES)
-ABI_VERSION = 6  # include/el_gpu.h EL_ABI_VERSION
-XCHG_NONE, XCHG_LOCAL, XCHG_RCCL = 0, 1, 2
+ABI_VERSION = 7  # include/el_gpu.h EL_ABI_VERSION
+XCHG_NONE, XCHG_LOCAL, XCHG_RCCL, XCHG_HOST = 0, 1, 2, 3
 NUM_EVENTS = len(EVENT_NAMES)
 
 
@@ -76,7 +76,8 @@ class _ElAxioms(C.Structure):
 class _ElConfig(C.Structure):
     _fields_ = [("device", C.c_int), ("profile", C.c_int), ("flags", C.c_uint32), ("exchange", C.c_int),
                 ("part_rank", C.c_uint32), ("part_count", C.c_uint32), ("row_lo", C.c_uint32),
-                ("row_hi", C.c_uint32), ("group", C.c_void_p), ("rccl_id", C.c_uint8 * 128)]
+                ("row_hi", C.c_uint32), ("group", C.c_void_p), ("rccl_id", C.c_uint8 * 128),
+                ("host_allgather", C.c_void_p), ("host_user", C.c_void_p)]
 
 
 class _ElStats(C.Structure):
@@ -102,6 +103,7 @@ class _ElStream(C.Structure):
 
 
 _SINK = C.CFUNCTYPE(C.c_int, C.c_void_p, _u32p, _u32p, C.c_size_t)
+_ALLGATHER = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t)
 
 EXPORTED_SYMBOLS = [
     "el_abi_version", "el_device_count", "el_create", "el_load", "el_init", "el_step", "el_saturate",
@@ -291,12 +293,46 @@ class Stats(dict):
 
 class Partition:
     """Row partition of one engine: this rank owns S(X) for X in
-    [row_lo, row_hi) (0, 0 = the equal split) and all-gathers its deltas each superstep."""
+    [row_lo, row_hi) (0, 0 = the equal split) and all-gathers its deltas each superstep.
+    allgather (EL_XCHG_HOST): fn(send: bytes-like, recv: writable, size × len(send)) that
+    all-gathers this rank's block over the caller's transport (e.g. ``gloo_allgather()``)."""
 
     def __init__(self, rank: int, count: int, exchange: int, group: "Optional[LocalGroup]" = None,
-                 rccl_id: Optional[bytes] = None, rows: Tuple[int, int] = (0, 0)):
+                 rccl_id: Optional[bytes] = None, rows: Tuple[int, int] = (0, 0),
+                 allgather: Optional[Callable[[memoryview, memoryview], None]] = None):
         self.rank, self.count, self.exchange, self.group, self.rccl_id, self.rows = (
             rank, count, exchange, group, rccl_id, rows)
+        self.allgather = allgather
+        self.error: Optional[BaseException] = None  # the transport's last exception
+        self._cfn = None
+        if allgather is not None:
+            def trampoline(_user, send, recv, nbytes):
+                try:
+                    allgather(memoryview((C.c_uint8 * nbytes).from_address(send)).cast("B"),
+                              memoryview((C.c_uint8 * (nbytes * count)).from_address(recv)).cast("B"))
+                    return 0
+                except Exception as exc:  # noqa: BLE001 - reported through the C return code
+                    self.error = exc
+                    return 1
+            self._cfn = _ALLGATHER(trampoline)  # kept alive as long as the partition
+
+
+def gloo_allgather(group=None) -> Callable[[memoryview, memoryview], None]:
+    """EL_XCHG_HOST transport over torch.distributed (any backend with CPU all_gather, e.g.
+    gloo): the per-superstep delta all-gather of SURVEY.md §8(e) staged through host memory."""
+    import torch
+    import torch.distributed as dist
+
+    def fn(send: memoryview, recv: memoryview) -> None:
+        n = len(send)
+        world = dist.get_world_size(group)
+        src = torch.from_numpy(np.frombuffer(send, dtype=np.uint8).copy())
+        out = [torch.empty(n, dtype=torch.uint8) for _ in range(world)]
+        dist.all_gather(out, src, group=group)
+        dst = np.frombuffer(recv, dtype=np.uint8)
+        for q, t in enumerate(out):
+            dst[q * n:(q + 1) * n] = t.numpy()
+    return fn
 
 
 class LocalGroup:
@@ -347,6 +383,8 @@ class Engine:
                 cfg.group = partition.group.ptr
             if partition.rccl_id is not None:
                 C.memmove(cfg.rccl_id, partition.rccl_id, 128)
+            if partition._cfn is not None:
+                cfg.host_allgather = C.cast(partition._cfn, C.c_void_p)
         rc = self._lib.el_create(C.byref(self._ctx), C.byref(cfg))
         if rc != EL_OK:
             raise ElError(rc, f"el_create(device={device}) failed: no usable HIP device or bad partition")
@@ -359,7 +397,8 @@ class Engine:
     def _check(self, rc: int, what: str) -> None:
         if rc != EL_OK:
             msg = self._lib.el_last_error(self._ctx)
-            raise ElError(rc, f"{what}: {msg.decode() if msg else ''}")
+            cause = self.partition.error if self.partition is not None else None
+            raise ElError(rc, f"{what}: {msg.decode() if msg else ''}") from cause
 
     def close(self) -> None:
         if self._ctx:

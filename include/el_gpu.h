@@ -42,7 +42,7 @@
 extern "C" {
 #endif
 
-#define EL_ABI_VERSION 6
+#define EL_ABI_VERSION 7
 
 /* return codes */
 #define EL_OK        0
@@ -143,8 +143,16 @@ typedef struct el_axioms {
 #define EL_XCHG_NONE  0   /* whole ontology, no partition (the default) */
 #define EL_XCHG_LOCAL 1   /* in-process group: one context per thread (el_group_create) */
 #define EL_XCHG_RCCL  2   /* one context per process/GPU, RCCL all-gather over xGMI */
+#define EL_XCHG_HOST  3   /* one context per process, all-gather by the caller's transport */
 
 typedef struct el_group el_group;
+
+/* EL_XCHG_HOST transport: the caller's all-gather over host memory (MPI, gloo, the JNI host's
+ * own sockets — what CommunicationHandler.java:49-84 does over Redis).  send holds this rank's
+ * `bytes`; recv (size × bytes) gets every rank's block in rank order.  Both are page-locked host
+ * buffers of the context, valid for the call only.  Return 0, or nonzero to fail the superstep
+ * (el_saturate returns EL_ESTATE).  Called on the thread that calls el_init / el_saturate. */
+typedef int (*el_allgather_fn)(void* user, const void* send, void* recv, size_t bytes);
 
 /* el_config.flags.  EL_FLAG_COMPAT_DISTEL_CHAIN reproduces parity hazard H2 (SURVEY.md
  * §8.H) deterministically: DistEL's CR6 joins DB1["Yr"] (X with (X,Y) ∈ R(r)) with DB4["Yr"]
@@ -176,6 +184,8 @@ typedef struct el_config {
   uint32_t row_lo, row_hi;  /* owned rows; row_lo = row_hi = 0: the equal split of [0, N) */
   el_group* group;       /* EL_XCHG_LOCAL: shared by the group's contexts */
   uint8_t rccl_id[128];  /* EL_XCHG_RCCL: ncclUniqueId made by el_rccl_unique_id on rank 0 */
+  el_allgather_fn host_allgather;  /* EL_XCHG_HOST: the transport */
+  void* host_user;                 /* EL_XCHG_HOST: its first argument */
 } el_config;
 
 /* Work-phase ids for el_kernel_stats.  Several phases share one launch: the

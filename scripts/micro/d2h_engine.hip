@@ -25,6 +25,13 @@ __global__ void k_read(const uint4* __restrict__ a, size_t n, unsigned* out) {
   if (s == 0x12345678u) out[0] = s;
 }
 
+// zero-copy push: a few workgroups store device data straight into mapped page-locked host
+// memory (vector stores over PCIe), so the transfer occupies `grid` workgroups, not a blit grid
+__global__ void k_push(const uint4* __restrict__ a, uint4* __restrict__ h, size_t n) {
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
+    h[i] = a[i];
+}
+
 int main() {
   const size_t cb = 512ull << 20, kb = 4ull << 30;
   void *d, *big, *h;
@@ -96,6 +103,31 @@ int main() {
       CK(hipEventElapsedTime(&ms, b0, b1));
       printf("%s beside 8 kernels: copy %.3f ms, kernels %.3f ms (%.3f each)\n", m.name, ms, kms, kms / 8);
     }
+  }
+  uint4* hd = nullptr;
+  CK(hipHostGetDevicePointer((void**)&hd, h, 0));
+  for (int g : {8, 16, 32, 64, 128}) {
+    memset(h, 0, cb);
+    hipLaunchKernelGGL(k_push, dim3(g), dim3(256), 0, s1, (const uint4*)d, hd, cb / 16);
+    CK(hipDeviceSynchronize());
+    printf("push grid %d: data %s\n", g, ((unsigned char*)h)[cb - 1] == 0x5a ? "ok" : "WRONG");
+    CK(hipEventRecord(b0, s1));
+    hipLaunchKernelGGL(k_push, dim3(g), dim3(256), 0, s1, (const uint4*)d, hd, cb / 16);
+    CK(hipEventRecord(b1, s1));
+    CK(hipDeviceSynchronize());
+    CK(hipEventElapsedTime(&ms, b0, b1));
+    printf("push grid %d alone: %.3f ms (%.1f GB/s)\n", g, ms, cb / ms / 1e6);
+    CK(hipEventRecord(b0, s1));
+    hipLaunchKernelGGL(k_push, dim3(g), dim3(256), 0, s1, (const uint4*)d, hd, cb / 16);
+    CK(hipEventRecord(b1, s1));
+    CK(hipEventRecord(a0, s0));
+    for (int i = 0; i < 8; ++i) kern();
+    CK(hipEventRecord(a1, s0));
+    CK(hipDeviceSynchronize());
+    float kms;
+    CK(hipEventElapsedTime(&kms, a0, a1));
+    CK(hipEventElapsedTime(&ms, b0, b1));
+    printf("push grid %d beside 8 kernels: copy %.3f ms, kernels %.3f ms (%.3f each)\n", g, ms, kms, kms / 8);
   }
   return 0;
 }
