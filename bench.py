@@ -130,7 +130,7 @@ def parse():
                          "result copy-back (EL_RESULT_ASYNC) rides over PCIe under the other's classification")
     ap.add_argument("--copyback", default="stream", choices=["stream", "rows"],
                     help="stream: the result node's facts and links cross PCIe as the supersteps commit them "
-                         "(el_stream_result; pairs in commit order); rows: after the fixpoint, as sorted CSR rows "
+                         "(el_stream_result; commit order, row-run encoded); rows: after the fixpoint, as sorted CSR rows "
                          "X -> {B} (el_copy_result)")
     ap.add_argument("--no-throughput2", action="store_true",
                     help="skip the separately reported two-in-flight throughput loop")
@@ -210,7 +210,7 @@ def main():
             assert (r.n_facts, r.n_links) == (st["s_facts"], st["links"]) or (len(ax.range) and not stream) or \
                 engines[0].partition is not None, "copy-back lost facts"
         res = results[(turn[0] - 1) % len(engines)]
-        copy_bytes = (8 * (res.n_facts + res.n_links) if stream else
+        copy_bytes = (4 * (res.n_facts + res.n_links) + 8 * (res.n_s_runs + res.n_l_runs) if stream else
                       8 * 2 * (res.row_hi - res.row_lo + 1) + 4 * (res.n_facts + res.n_links))
         sp = split[-steps:]
         return {"t_max": t_max, "derived": derived_all, "st": st, "ms_per_step": 1e3 * t_max / steps,
@@ -312,8 +312,9 @@ def main():
             "saturate_ms": round(head["saturate_ms"], 4),
             "copyback_ms": round(head["copyback_ms"], 4),
             "latency_ms": round(head["ms_per_step"], 4) if head["inflight"] == 1 else None,
-            "copyback": ("streamed: the result node's (X, B) facts and (X, r, Y) links in commit order, "
-                         "crossing PCIe as the supersteps commit them (el_stream_result)"
+            "copyback": ("streamed: the result node's facts and links in commit order, row-run encoded "
+                         "(B / pair id per entry + (X, end) per run), crossing PCIe as the supersteps commit "
+                         "them (el_stream_result)"
                          if args.copyback == "stream" else
                          "rows: S(X) and links as sorted CSR rows after the fixpoint (el_copy_result)"),
             "copyback_bytes": head["copy_bytes"],
@@ -326,7 +327,8 @@ def main():
     def leg_summary(leg):
         return {"value": round(leg["value"], 1), "ms_per_step": round(leg["ms_per_step"], 4),
                 "derived_axioms": leg["derived"], "supersteps": leg["st"]["supersteps"],
-                "saturate_ms": round(leg["saturate_ms"], 4), "load_s": round(leg["load_s"], 3)}
+                "saturate_ms": round(leg["saturate_ms"], 4), "load_s": round(leg["load_s"], 3),
+                "exchange_bytes_per_rank": leg["st"].get("exchange_bytes", 0)}
 
     if run_exchange:
         done = threading.Event()

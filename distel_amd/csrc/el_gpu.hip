@@ -51,6 +51,7 @@
 #include <vector>
 
 #include "el_closure.h"
+#include "el_stream.h"
 #include "el_gpu.h"
 #include "el_index.h"
 #include "el_rows.h"
@@ -2420,7 +2421,10 @@ struct el_ctx {
   uint32_t *xs_x = nullptr, *xs_p = nullptr;      // this step's local chain links to send (cl_cap)
   uint32_t* xsend = nullptr;                      // exchange slot: XH + 2 * xcap words
   uint32_t* xrecv = nullptr;                      // part_count slots
+  uint32_t* xhdr = nullptr;                       // part_count headers (the header round)
+  uint32_t* xhdr_h = nullptr;                     // their page-locked host copy
   uint64_t xcap = 0;                              // records per rank per exchange (grows on overflow)
+  uint64_t xrounds_bytes = 0;                     // bytes all-gathered (received) since el_init
   bool part() const { return xmode != EL_XCHG_NONE; }
   bool bits_logged = false;
   bool trace_cands = getenv("EL_TRACE_CANDS") != nullptr;  // every set bit of the matrix is in the fact log (not after el_load)
@@ -2597,18 +2601,29 @@ struct el_ctx {
     for (hipEvent_t e : ev_copied) HIPCHK(hipEventSynchronize(e));
     copy_pending = false;
   }
-  // Streamed result (el_stream_result): the committed segments of the fact and link logs, DMA'd
-  // on dstream into the caller's buffers while the saturation goes on
+  // Streamed result (el_stream_result): the committed segments of the fact and link logs cross
+  // PCIe while the saturation goes on: their values (b, pid) by DMA on dstream, their runs of x
+  // (el_stream.h) encoded on nstream straight into the caller's mapped run buffers
   el_stream* strm = nullptr;      // armed for the next el_saturate
   uint64_t strm_s = 0, strm_l = 0;  // log entries already enqueued
   bool strm_ovf = false;          // a buffer was too small (el_result_wait: EL_ERANGE)
   hipEvent_t ev_strm = nullptr;
+  hipStream_t nstream = nullptr;  // run encoding (never queued behind the DMAs)
+  uint2 *s_run_dev = nullptr, *l_run_dev = nullptr;  // device addresses of the caller's run buffers
+  uint32_t *rcnt = nullptr, *roff = nullptr;  // per-tile run counts / their scan
+  uint64_t rtiles_cap = 0;
+  void* rscan_tmp = nullptr;
+  size_t rscan_bytes = 0;
+  unsigned long long* rbase = nullptr;    // runs written so far: S, links (device)
+  unsigned long long* rbase_h = nullptr;  // their page-locked copy at the fixpoint
+  void stream_runs(const uint32_t* keys, uint64_t a, uint64_t b, uint2* out, uint64_t cap, int which);
   void stream_out();
   void stream_end(bool release);
   hipEvent_t ev_base[2] = {nullptr, nullptr};  // base links logged (stream) / in the link set (rstream)
   bool base_filling = false;                   // the set fill runs beside the first superstep
   void join_base();
   bool pre_reset = false;         // the device part of the next reset_state is already enqueued
+  bool reset_wait = false;        // ... and the engine stream has not waited for it yet
   // clear_from: the first row whose bits the reset clears (lo: all; hi: none — a releasing
   // copy-back cleared the rows it read)
   // summ_from: the first row whose block summary the reset clears (a releasing read-out
@@ -2911,6 +2926,9 @@ void el_ctx::free_state() {
   dfree(xs_p);
   dfree(xsend);
   dfree(xrecv);
+  dfree(xhdr);
+  if (xhdr_h) (void)hipHostFree(xhdr_h);
+  xhdr_h = nullptr;
   if (pin_word) (void)hipHostFree(pin_word);
   pin_word = nullptr;
 }
@@ -3008,6 +3026,8 @@ void el_ctx::alloc_state() {
     xs_p = dalloc<uint32_t>(cl_cap);
     xsend = dalloc<uint32_t>(XH + 2 * xcap);
     xrecv = dalloc<uint32_t>((uint64_t)part_count * (XH + 2 * xcap));
+    xhdr = dalloc<uint32_t>((uint64_t)part_count * XH);
+    HIPCHK(hipHostMalloc((void**)&xhdr_h, (uint64_t)part_count * XH * sizeof(uint32_t), hipHostMallocDefault));
   }
   alloc_closure();
 }
@@ -3050,7 +3070,10 @@ void el_ctx::reset_device(hipStream_t stream, uint32_t clear_from, uint32_t summ
 
 void el_ctx::reset_state() {
   if (pre_reset) {  // done behind the copy-back that released the state (el_copy_result)
-    HIPCHK(hipStreamWaitEvent(stream, ev_reset, 0));
+    // the told closure (el_init's first part) touches none of what the reset clears: the
+    // engine stream waits for the reset only before the init facts (closure_state), so the
+    // reset's matrix clear runs beside the closure build
+    reset_wait = true;
     pre_reset = false;
   } else {
     reset_device(stream);
@@ -3066,6 +3089,7 @@ void el_ctx::reset_state() {
   act_n = ~0ull;
   for (int r = 0; r < EL_NUM_RULE_TYPES; ++r) wm_s[r] = wm_l[r] = wm_a[r] = wm_p[r] = 0;
   wm_x = 0;
+  xrounds_bytes = 0;
   memset(launches, 0, sizeof launches);
   memset(host_ev, 0, sizeof host_ev);
   memset(kms, 0, sizeof kms);
@@ -3481,7 +3505,10 @@ void el_ctx::grow_part(uint64_t new_xcap) {
 }
 
 // Pack this rank's new records, all-gather every rank's, import them, merge the CSRs.
-// Returns after the import published; hc then holds the global g_* words.
+// Two rounds: the headers first (XH words per rank), whose record counts size the second
+// round to the largest rank's records this superstep (not the capacity: late supersteps send
+// almost nothing), then the records.  Returns the largest rank's record count after the import
+// published; hc then holds the global g_* words (g_max > xcap: nothing was imported).
 uint32_t el_ctx::exchange_round(uint32_t s0, uint32_t l0, uint32_t a0, uint32_t p0) {
   DState st = dstate();
   XchgArgs xa{};
@@ -3495,9 +3522,25 @@ uint32_t el_ctx::exchange_round(uint32_t s0, uint32_t l0, uint32_t a0, uint32_t 
   xa.cp_cap = (uint32_t)cp_cap, xa.job_cap = (uint32_t)job_cap, xa.ct_cap = (uint32_t)ct_cap;
   hipLaunchKernelGGL(k_xpack, dim3(grid_for(xcap, 64)), dim3(BLOCK), 0, stream, st, xa);
   HIPCHK(hipGetLastError());
-  xchg->allgather(xsend, xrecv, (XH + 2 * xcap) * sizeof(uint32_t), stream);
+  xchg->allgather(xsend, xhdr, XH * sizeof(uint32_t), stream);
+  HIPCHK(hipMemcpyAsync(xhdr_h, xhdr, (uint64_t)part_count * XH * sizeof(uint32_t), hipMemcpyDeviceToHost, stream));
+  HIPCHK(hipStreamSynchronize(stream));
+  uint32_t m = 0;
+  for (uint32_t q = 0; q < part_count; ++q) {
+    const uint32_t* h = xhdr_h + (uint64_t)q * XH;
+    m = std::max(m, h[XH_NP] + h[XH_NA] + h[XH_NX]);
+  }
+  // this round's records per rank; a rank past xcap: headers only, the import takes nothing and
+  // publishes g_max (the caller grows and redoes; the commit's gapped-row overflows are placed first)
+  xa.cap = m > xcap ? 0u : std::min<uint32_t>((uint32_t)xcap, (m + 63) & ~63u);
+  if (xa.cap) {
+    xchg->allgather(xsend, xrecv, (XH + 2 * (uint64_t)xa.cap) * sizeof(uint32_t), stream);
+  } else {
+    xa.recv = xhdr;  // headers only
+  }
+  xrounds_bytes += (uint64_t)part_count * (2 * XH + 2 * (uint64_t)xa.cap) * sizeof(uint32_t);
   const uint32_t seq = ++commit_seq;
-  hipLaunchKernelGGL(k_ximport, dim3(grid_for((uint64_t)part_count * xcap, 256)), dim3(BLOCK), 0, stream, ix, st,
+  hipLaunchKernelGGL(k_ximport, dim3(grid_for((uint64_t)part_count * xa.cap, 256)), dim3(BLOCK), 0, stream, ix, st,
                      xa, PubArgs{hc_dev, commit_done, seq});
   HIPCHK(hipGetLastError());
   wait_commit(seq);
@@ -3896,6 +3939,10 @@ void el_ctx::closure_rows(uint32_t a, uint32_t b) {
 // the base links by pid (radix sort) and this classification's gapped-row layouts.  Buffers
 // grow first to what the closure asks for (grow-only).
 void el_ctx::closure_state() {
+  if (reset_wait) {
+    HIPCHK(hipStreamWaitEvent(stream, ev_reset, 0));
+    reset_wait = false;
+  }
   const unsigned long long* T = clt.tot;
   const uint64_t N = hx.N, P = hx.P;
   const uint64_t n_init = T[elcl::T_INIT], two = T[elcl::T_TWO];
@@ -4103,18 +4150,41 @@ void el_ctx::stream_out() {
   if (s1 == strm_s && l1 == strm_l) return;
   HIPCHK(hipEventRecord(ev_strm, stream));
   HIPCHK(hipStreamWaitEvent(dstream, ev_strm, 0));
+  HIPCHK(hipStreamWaitEvent(nstream, ev_strm, 0));
   auto dma = [&](uint32_t* dst, const uint32_t* src, uint64_t a, uint64_t b, uint64_t cap) {
     b = std::min(b, cap);
     if (dst && b > a)
       HIPCHK(hipMemcpyAsync(dst + a, src + a, (b - a) * sizeof(uint32_t), hipMemcpyDeviceToHost, dstream));
   };
-  dma(strm->s_x, slog_x, strm_s, s1, strm->s_cap);
   dma(strm->s_b, slog_a, strm_s, s1, strm->s_cap);
-  dma(strm->l_x, llog_x, strm_l, l1, strm->l_cap);
   dma(strm->l_p, llog_p, strm_l, l1, strm->l_cap);
-  if ((strm->s_x && s1 > strm->s_cap) || (strm->l_x && l1 > strm->l_cap)) strm_ovf = true;
+  if ((strm->s_b && s1 > strm->s_cap) || (strm->l_p && l1 > strm->l_cap)) strm_ovf = true;
+  if (s_run_dev) stream_runs(slog_x, strm_s, s1, s_run_dev, strm->s_run_cap, 0);
+  if (l_run_dev) stream_runs(llog_x, strm_l, l1, l_run_dev, strm->l_run_cap, 1);
   strm_s = s1;
   strm_l = l1;
+}
+
+// The runs of x over keys[a, b) (a log segment) into the caller's run buffer, numbered on from
+// the runs of the earlier segments (rbase[which]); on nstream, which waited for the commit.
+void el_ctx::stream_runs(const uint32_t* keys, uint64_t a, uint64_t b, uint2* out, uint64_t cap, int which) {
+  if (b <= a) return;
+  const uint64_t nt = elst::tiles(b - a);
+  if (nt > rtiles_cap) {
+    HIPCHK(hipStreamSynchronize(nstream));  // (the scratch of the last segment is free)
+    dfree(rcnt);
+    dfree(roff);
+    dfree(rscan_tmp);
+    rtiles_cap = std::max<uint64_t>(2 * nt, 4096);
+    if (rtiles_cap > 0x7fffffffull) throw ElError{EL_ENOMEM, "streamed result: log segment too long"};
+    rcnt = dalloc<uint32_t>(rtiles_cap);
+    roff = dalloc<uint32_t>(rtiles_cap);
+    rscan_bytes = elcl::scan_temp_bytes((uint32_t)rtiles_cap);
+    rscan_tmp = dalloc<uint8_t>(rscan_bytes);
+  }
+  elst::count(nstream, keys, a, b, rcnt);
+  elcl::scan(nstream, rscan_tmp, rscan_bytes, rcnt, roff, (uint32_t)nt);
+  elst::emit(nstream, keys, a, b, roff, rcnt, out, cap, rbase + which);
 }
 
 // The fixpoint: the last segments, the counts, and (release) the next classification's reset on
@@ -4125,6 +4195,13 @@ void el_ctx::stream_end(bool release) {
   stream_out();
   strm->n_facts = s_count;
   strm->n_links = l_count;
+  // the run counts (the encoding is short work on its own stream: a short run buffer is known
+  // here, before the release decision)
+  HIPCHK(hipMemcpyAsync(rbase_h, rbase, 2 * sizeof(unsigned long long), hipMemcpyDeviceToHost, nstream));
+  HIPCHK(hipStreamSynchronize(nstream));
+  strm->n_s_runs = s_run_dev ? rbase_h[0] : 0;
+  strm->n_l_runs = l_run_dev ? rbase_h[1] : 0;
+  if (strm->n_s_runs > strm->s_run_cap || strm->n_l_runs > strm->l_run_cap) strm_ovf = true;
   strm = nullptr;
   HIPCHK(hipEventRecord(ev_copied[0], cstream));
   HIPCHK(hipEventRecord(ev_copied[1], stream));
@@ -4296,6 +4373,7 @@ void el_ctx::fill_stats(el_stats* out, double ms) {
     for (int e = 0; e < EL_NUM_EVENTS; ++e) bytes += (hev[k][e] + host_ev[k][e]) * width[e];
   st.bytes = bytes;
   st.ms = ms;
+  st.exchange_bytes = xrounds_bytes;
   last = st;
   stats_stale = false;
   if (out) *out = st;
@@ -4389,6 +4467,7 @@ int el_create(el_ctx** out, const el_config* cfg) {
       HIPCHK(hipStreamCreateWithPriority(&c->cstream, hipStreamNonBlocking, least));
       HIPCHK(hipStreamCreateWithPriority(&c->rstream, hipStreamNonBlocking, least));
       HIPCHK(hipStreamCreateWithPriority(&c->dstream, hipStreamNonBlocking, least));
+      HIPCHK(hipStreamCreateWithPriority(&c->nstream, hipStreamNonBlocking, least));
       HIPCHK(hipStreamCreateWithPriority(&c->ostream, hipStreamNonBlocking, least));
       HIPCHK(hipEventCreateWithFlags(&c->ev_out, hipEventDisableTiming));
     } else {
@@ -4396,6 +4475,7 @@ int el_create(el_ctx** out, const el_config* cfg) {
       HIPCHK(hipStreamCreateWithFlags(&c->cstream, hipStreamNonBlocking));
       HIPCHK(hipStreamCreateWithFlags(&c->rstream, hipStreamNonBlocking));
       HIPCHK(hipStreamCreateWithFlags(&c->dstream, hipStreamNonBlocking));
+      HIPCHK(hipStreamCreateWithFlags(&c->nstream, hipStreamNonBlocking));
     }
     for (hipEvent_t& e : c->ev_stage) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     for (hipEvent_t& e : c->ev_dma) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
@@ -4416,6 +4496,7 @@ int el_create(el_ctx** out, const el_config* cfg) {
     if (c->cstream) (void)hipStreamDestroy(c->cstream);
     if (c->rstream) (void)hipStreamDestroy(c->rstream);
     if (c->dstream) (void)hipStreamDestroy(c->dstream);
+    if (c->nstream) (void)hipStreamDestroy(c->nstream);
     if (c->ostream) (void)hipStreamDestroy(c->ostream);
     if (c->ev_out) (void)hipEventDestroy(c->ev_out);
     for (hipEvent_t e : c->ev_rows)
@@ -4934,11 +5015,21 @@ int el_stream_result(el_ctx* c, el_stream* s) {
   if (!c->inited) return fail(c, EL_ESTATE, "el_stream_result before el_init");
   if (s->flags & ~EL_RESULT_RELEASE) return fail(c, EL_EINVAL, "unknown el_stream flags");
   return guarded(c, [&] {
+    // the run buffers are written by the device: page-locked and mapped (el_host_alloc)
+    c->s_run_dev = reinterpret_cast<uint2*>(mapped_for_device(s->s_run));
+    c->l_run_dev = reinterpret_cast<uint2*>(mapped_for_device(s->l_run));
+    if ((s->s_run && !c->s_run_dev) || (s->l_run && !c->l_run_dev))
+      return fail(c, EL_EINVAL, "el_stream run buffers must be page-locked host memory (el_host_alloc)");
+    if (!c->rbase) {
+      c->rbase = dalloc<unsigned long long>(2);
+      HIPCHK(hipHostMalloc((void**)&c->rbase_h, 2 * sizeof(unsigned long long), hipHostMallocDefault));
+    }
+    HIPCHK(hipMemsetAsync(c->rbase, 0, 2 * sizeof(unsigned long long), c->nstream));
     c->strm = s;
     c->strm_ovf = false;
     // everything already logged is streamed too (from the first entry)
     c->strm_s = c->strm_l = 0;
-    s->n_facts = s->n_links = 0;
+    s->n_facts = s->n_links = s->n_s_runs = s->n_l_runs = 0;
     return EL_OK;
   });
 }
@@ -5052,10 +5143,17 @@ void el_destroy(el_ctx* c) {
   if (c->cstream) (void)hipStreamSynchronize(c->cstream);
   if (c->rstream) (void)hipStreamSynchronize(c->rstream);
   if (c->dstream) (void)hipStreamSynchronize(c->dstream);  // (an async copy-back's last DMAs)
+  if (c->nstream) (void)hipStreamSynchronize(c->nstream);
   if (c->ostream) (void)hipStreamSynchronize(c->ostream);
   c->copy_pending = false;
   c->free_state();
   c->free_index();
+  dfree(c->rcnt);
+  dfree(c->roff);
+  dfree(c->rscan_tmp);
+  dfree(c->rbase);
+  if (c->rbase_h) (void)hipHostFree(c->rbase_h);
+  if (c->nstream) (void)hipStreamDestroy(c->nstream);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   if (c->cstream) (void)hipStreamDestroy(c->cstream);
   if (c->rstream) (void)hipStreamDestroy(c->rstream);

@@ -83,7 +83,8 @@ class _ElConfig(C.Structure):
 class _ElStats(C.Structure):
     _fields_ = [("supersteps", C.c_uint32), ("s_facts", C.c_uint64), ("s_init", C.c_uint64),
                 ("links", C.c_uint64), ("derived", C.c_uint64), ("activations", C.c_uint64),
-                ("propagations", C.c_uint64), ("bytes", C.c_uint64), ("ms", C.c_double)]
+                ("propagations", C.c_uint64), ("bytes", C.c_uint64), ("ms", C.c_double),
+                ("exchange_bytes", C.c_uint64)]
 
 
 class _ElKernelStat(C.Structure):
@@ -98,8 +99,10 @@ class _ElResult(C.Structure):
 
 
 class _ElStream(C.Structure):
-    _fields_ = [("flags", C.c_uint32), ("s_x", _u32p), ("s_b", _u32p), ("s_cap", C.c_uint64), ("l_x", _u32p),
-                ("l_p", _u32p), ("l_cap", C.c_uint64), ("n_facts", C.c_uint64), ("n_links", C.c_uint64)]
+    _fields_ = [("flags", C.c_uint32), ("s_b", _u32p), ("s_cap", C.c_uint64), ("s_run", _u32p),
+                ("s_run_cap", C.c_uint64), ("l_p", _u32p), ("l_cap", C.c_uint64), ("l_run", _u32p),
+                ("l_run_cap", C.c_uint64), ("n_facts", C.c_uint64), ("n_links", C.c_uint64),
+                ("n_s_runs", C.c_uint64), ("n_l_runs", C.c_uint64)]
 
 
 _SINK = C.CFUNCTYPE(C.c_int, C.c_void_p, _u32p, _u32p, C.c_size_t)
@@ -257,26 +260,48 @@ class Result:
 
 class Stream:
     """Streamed result (el_stream_result): the result node's writes in commit order, as they are
-    committed — S facts (s_x[i], s_b[i]) meaning s_b[i] ∈ S(s_x[i]), links (l_x[i], l_p[i]) with
-    pair id l_p[i] (Engine.pid_table()).  Page-locked buffers, reused across classifications;
-    complete after Engine.result_wait()."""
+    committed, row-run encoded — S facts s_b[i] with the runs (x, end) of s_run, links l_p[i]
+    (pair ids, Engine.pid_table()) with the runs of l_run.  Page-locked buffers, reused across
+    classifications; complete after Engine.result_wait()."""
 
     def __init__(self):
-        self.n_facts = self.n_links = 0
-        self.s_x = self.s_b = self.l_x = self.l_p = None
+        self.n_facts = self.n_links = self.n_s_runs = self.n_l_runs = 0
+        self.s_b = self.l_p = self.s_run = self.l_run = None
         self._st = _ElStream()
 
-    def fit(self, n_facts: int, n_links: int) -> None:
-        if self.s_x is None or self.s_x.size < n_facts:
-            n = n_facts + n_facts // 8 + 1024
-            self.s_x, self.s_b = pinned_array(n, np.uint32), pinned_array(n, np.uint32)
-        if self.l_x is None or self.l_x.size < n_links:
-            n = n_links + n_links // 8 + 1024
-            self.l_x, self.l_p = pinned_array(n, np.uint32), pinned_array(n, np.uint32)
+    def fit(self, n_facts: int, n_links: int, n_s_runs: int = 0, n_l_runs: int = 0) -> None:
+        """Buffers for at least these counts (runs: a quarter of the entries unless known)."""
+        grow = lambda n: n + n // 8 + 1024
+        if self.s_b is None or self.s_b.size < n_facts:
+            self.s_b = pinned_array(grow(n_facts), np.uint32)
+        if self.l_p is None or self.l_p.size < n_links:
+            self.l_p = pinned_array(grow(n_links), np.uint32)
+        rs, rl = n_s_runs or n_facts // 4, n_l_runs or n_links // 4
+        if self.s_run is None or self.s_run.shape[0] < rs:
+            self.s_run = pinned_array(2 * grow(rs), np.uint32).reshape(-1, 2)
+        if self.l_run is None or self.l_run.shape[0] < rl:
+            self.l_run = pinned_array(2 * grow(rl), np.uint32).reshape(-1, 2)
+
+    @staticmethod
+    def _rows(runs: np.ndarray, n_runs: int, n: int) -> np.ndarray:
+        """Per-entry x from the runs (x, end)."""
+        r = runs[:n_runs]
+        ends = r[:, 1].astype(np.int64)
+        lens = np.diff(np.concatenate(([0], ends)))
+        assert n_runs == 0 or (ends[-1] == n and (lens > 0).all()), "malformed runs"
+        return np.repeat(r[:, 0], lens)
+
+    def fact_rows(self) -> Tuple[np.ndarray, np.ndarray]:
+        """(x, b) per fact, in commit order."""
+        return self._rows(self.s_run, self.n_s_runs, self.n_facts), self.s_b[:self.n_facts].copy()
+
+    def link_rows(self) -> Tuple[np.ndarray, np.ndarray]:
+        """(x, pid) per link, in commit order."""
+        return self._rows(self.l_run, self.n_l_runs, self.n_links), self.l_p[:self.n_links].copy()
 
     def facts(self, n_user: Optional[int] = None) -> Tuple[np.ndarray, np.ndarray]:
         """(x, a) pairs sorted by (x, a); rows >= n_user (ELK range fillers) dropped when given."""
-        x, a = self.s_x[:self.n_facts].copy(), self.s_b[:self.n_facts].copy()
+        x, a = self.fact_rows()
         if n_user is not None:
             keep = x < n_user
             x, a = x[keep], a[keep]
@@ -288,7 +313,8 @@ class Stats(dict):
     @staticmethod
     def from_c(s: _ElStats) -> "Stats":
         return Stats(supersteps=s.supersteps, s_facts=s.s_facts, s_init=s.s_init, links=s.links, derived=s.derived,
-                     activations=s.activations, propagations=s.propagations, bytes=s.bytes, ms=s.ms)
+                     activations=s.activations, propagations=s.propagations, bytes=s.bytes, ms=s.ms,
+                     exchange_bytes=s.exchange_bytes)
 
 
 class Partition:
@@ -445,7 +471,9 @@ class Engine:
         self._check(self._lib.el_saturate(self._ctx, C.byref(s)), "el_saturate")
         self._last = Stats.from_c(s)
         if self._stream is not None:  # (a streamed result: its counts are known now)
-            self._stream.n_facts, self._stream.n_links = int(self._stream._st.n_facts), int(self._stream._st.n_links)
+            st = self._stream._st
+            self._stream.n_facts, self._stream.n_links = int(st.n_facts), int(st.n_links)
+            self._stream.n_s_runs, self._stream.n_l_runs = int(st.n_s_runs), int(st.n_l_runs)
             self._stream = None
         return self._last
 
@@ -553,15 +581,17 @@ class Engine:
         last = self._last
         nf = max(n_facts, last["s_facts"] if last else 0) or 64 * max(self.ax.n_concepts if self.ax else 1, 1)
         nl = max(n_links, last["links"] if last else 0) or 64 * max(self.ax.n_concepts if self.ax else 1, 1)
-        out.fit(nf, nl)
+        out.fit(nf, nl, out.n_s_runs, out.n_l_runs)
         s = out._st
         s.flags = EL_RESULT_RELEASE if release else 0
-        s.s_x = out.s_x.ctypes.data_as(_u32p)
         s.s_b = out.s_b.ctypes.data_as(_u32p)
-        s.s_cap = out.s_x.size
-        s.l_x = out.l_x.ctypes.data_as(_u32p)
+        s.s_cap = out.s_b.size
+        s.s_run = out.s_run.ctypes.data_as(_u32p)
+        s.s_run_cap = out.s_run.shape[0]
         s.l_p = out.l_p.ctypes.data_as(_u32p)
-        s.l_cap = out.l_x.size
+        s.l_cap = out.l_p.size
+        s.l_run = out.l_run.ctypes.data_as(_u32p)
+        s.l_run_cap = out.l_run.shape[0]
         self._check(self._lib.el_stream_result(self._ctx, C.byref(s)), "el_stream_result")
         self._stream = out
         self._streamed = (out, release)

@@ -245,6 +245,7 @@ typedef struct el_stats {
   uint64_t propagations;       /* CR4 propagations ((r, Y), B): B for every X with (X, Y) ∈ R(r) */
   uint64_t bytes;              /* Σ algorithmic bytes over all kernels */
   double ms;                   /* wall ms of the call (device synchronised) */
+  uint64_t exchange_bytes;     /* partitioned: bytes this rank received from the delta all-gathers */
 } el_stats;
 
 typedef struct el_ctx el_ctx;
@@ -320,28 +321,38 @@ typedef struct el_result {
  * classification output is result-node DB0, sets filled by ZADD as facts are derived; the
  * X -> {B} flip is ResultRearranger's post-pass, ResultRearranger.java:57-105).  Armed after
  * el_init, before el_saturate: while the saturation runs, every committed segment of the fact
- * log and of the link log crosses PCIe into the caller's page-locked buffers (DMA beside the
- * next supersteps; a fact once derived never changes), so little is left to copy at the fixpoint.
- *   S facts  b ∈ S(x) as (s_x[i], s_b[i]), i < n_facts, in commit order (no duplicates)
- *   links    (x, y) ∈ R(r) as (l_x[i], l_p[i]), i < n_links, (r, y) = el_pid_table()[l_p[i]]
+ * log and of the link log crosses PCIe into the caller's page-locked buffers (beside the next
+ * supersteps; a fact once derived never changes), so little is left to copy at the fixpoint.
+ * Commit order, row-run encoded (the log's x comes in long runs: init facts and base links in
+ * x order, the commit's staged batches):
+ *   S facts  s_b[i], i < n_facts: the B of every fact, in commit order (no duplicates);
+ *            s_run[2k], s_run[2k + 1] = (x, end), k < n_s_runs: s_b[i] ∈ S(x) for
+ *            i in [end of run k - 1 (0 for k = 0), end)
+ *   links    l_p[i], i < n_links: pair ids ((r, y) = el_pid_table()[l_p[i]]); l_run likewise
+ *            gives their x: (x, y) ∈ R(r)
+ * 4 B per entry plus 8 B per run instead of 8 B per entry.  The run buffers are written by the
+ * device and must be page-locked host memory (el_host_alloc): EL_EINVAL otherwise.
  * Rows x ≥ n_concepts are the ELK range fillers (el_fresh_fillers), internal concepts.
- * n_facts / n_links are set when el_saturate returns; the buffers are complete when
+ * The n_* counts are set when el_saturate returns; the buffers are complete when
  * el_result_wait returns (every other call on the context waits for them first).  A buffer
- * smaller than its part: the first s_cap / l_cap entries arrive, el_result_wait returns
- * EL_ERANGE and the state is kept (not released): arm again with buffers of n_facts / n_links
- * entries and call el_saturate, which at the fixpoint runs no superstep and streams the whole
- * logs.  flags EL_RESULT_RELEASE: the state is released behind the saturation (no state until
- * el_init), as for el_copy_result. */
+ * smaller than its part: what fits arrives, el_result_wait returns EL_ERANGE and the state is
+ * kept (not released): arm again with buffers of the n_* counts and call el_saturate, which at
+ * the fixpoint runs no superstep and streams the whole logs.  flags EL_RESULT_RELEASE: the state
+ * is released behind the saturation (no state until el_init), as for el_copy_result. */
 typedef struct el_stream {
   uint32_t flags;           /* in: EL_RESULT_* (RELEASE) */
-  uint32_t* s_x;            /* in: s_cap entries each, or NULL */
-  uint32_t* s_b;
+  uint32_t* s_b;            /* in: s_cap entries, or NULL */
   uint64_t s_cap;
-  uint32_t* l_x;            /* in: l_cap entries each, or NULL */
-  uint32_t* l_p;
+  uint32_t* s_run;          /* in: 2 × s_run_cap words (page-locked), or NULL */
+  uint64_t s_run_cap;
+  uint32_t* l_p;            /* in: l_cap entries, or NULL */
   uint64_t l_cap;
+  uint32_t* l_run;          /* in: 2 × l_run_cap words (page-locked), or NULL */
+  uint64_t l_run_cap;
   uint64_t n_facts;         /* out */
   uint64_t n_links;         /* out */
+  uint64_t n_s_runs;        /* out */
+  uint64_t n_l_runs;        /* out */
 } el_stream;
 int el_stream_result(el_ctx* ctx, el_stream* s);  /* arms the next el_saturate; s stays valid until then */
 /* pair id -> (role, filler) in pid order (the ids the streamed links carry) */

@@ -359,7 +359,7 @@ def _stream_sets(eng, strm, n_user):
     """S facts sorted by (x, a) and links (x, r, y) sorted, from a streamed result."""
     x, a = strm.facts(n_user)
     role, filler = eng.pid_table()
-    lx, lp = strm.l_x[:strm.n_links], strm.l_p[:strm.n_links]
+    lx, lp = strm.link_rows()
     keep = lx < n_user
     lx, lr, ly = lx[keep], role[lp[keep]], filler[lp[keep]]
     o = np.lexsort((ly, lr, lx))
@@ -412,21 +412,42 @@ def test_stream_result_small_buffers_erange():
     st = eng.saturate()
     eng.init()
     strm = engine.Stream()
-    strm.fit(16, 16)
-    strm_sz = strm.s_x.size
+    strm.fit(16, 16, 16, 16)
     eng._last = None
-    s = engine._ElStream()  # arm by hand with buffers far too small
-    s.s_x = strm.s_x.ctypes.data_as(engine._u32p)
-    s.s_b = strm.s_b.ctypes.data_as(engine._u32p)
-    s.s_cap = 16
-    s.l_x = strm.l_x.ctypes.data_as(engine._u32p)
-    s.l_p = strm.l_p.ctypes.data_as(engine._u32p)
-    s.l_cap = 16
-    assert eng._lib.el_stream_result(eng._ctx, engine.C.byref(s)) == engine.EL_OK
-    eng._lib.el_saturate(eng._ctx, None)
-    assert s.n_facts == st["s_facts"] and strm_sz >= 16
-    with pytest.raises(engine.ElError):
+    for short in ("values", "runs"):
+        eng.init()
+        s = engine._ElStream()  # arm by hand with buffers far too small
+        s.s_b = strm.s_b.ctypes.data_as(engine._u32p)
+        s.s_cap = 16 if short == "values" else strm.s_b.size
+        s.s_run = strm.s_run.ctypes.data_as(engine._u32p)
+        s.s_run_cap = 16 if short == "runs" else strm.s_run.shape[0]
+        s.l_p = strm.l_p.ctypes.data_as(engine._u32p)
+        s.l_cap = 16 if short == "values" else strm.l_p.size
+        s.l_run = strm.l_run.ctypes.data_as(engine._u32p)
+        s.l_run_cap = 16 if short == "runs" else strm.l_run.shape[0]
+        s.flags = engine.EL_RESULT_RELEASE  # (a short buffer keeps the state all the same)
+        if short == "runs":  # values fit, only the runs are short
+            strm.fit(st["s_facts"], st["links"], 16, 16)
+            s.s_b, s.s_cap = strm.s_b.ctypes.data_as(engine._u32p), strm.s_b.size
+            s.l_p, s.l_cap = strm.l_p.ctypes.data_as(engine._u32p), strm.l_p.size
+        assert eng._lib.el_stream_result(eng._ctx, engine.C.byref(s)) == engine.EL_OK
+        eng._lib.el_saturate(eng._ctx, None)
+        assert s.n_facts == st["s_facts"] and s.n_links == st["links"]
+        assert s.n_s_runs > 16 and s.n_l_runs > 16
+        assert eng._lib.el_result_wait(eng._ctx) == engine.EL_ERANGE
+        # the state was kept: streamed again at the fixpoint into buffers of the counts
+        strm.n_facts, strm.n_links, strm.n_s_runs, strm.n_l_runs = s.n_facts, s.n_links, s.n_s_runs, s.n_l_runs
+        eng.stream_result(strm, release=True, n_facts=s.n_facts, n_links=s.n_links)
+        st2 = eng.saturate()
         eng.result_wait()
+        assert st2["supersteps"] == 0 or st2["derived"] == st["derived"]
+        assert (strm.n_facts, strm.n_links) == (st["s_facts"], st["links"])
+    # pageable run buffers are refused (the device writes them)
+    eng.init()
+    s = engine._ElStream()
+    pageable = np.zeros(64, np.uint32)
+    s.s_run, s.s_run_cap = pageable.ctypes.data_as(engine._u32p), 32
+    assert eng._lib.el_stream_result(eng._ctx, engine.C.byref(s)) == engine.EL_EINVAL
     eng.close()
 
 
