@@ -1848,6 +1848,40 @@ __global__ void k_rehash(unsigned long long* t, unsigned long long mask, const u
 
 // el_init after a classification: only the words the fact log names can be non-zero, and
 // when the log is small next to the matrix, clearing those words beats streaming it all
+// Clear the bit matrix by its block summary: every marked 512-B block is zeroed by one wave
+// (8 B per lane, one coalesced store), its summary byte with it.  Reads the summary (1/512 of
+// the matrix) and writes only the blocks that hold a bit: G3's 104 M facts lie in ~10 M of 37 M
+// blocks, so ~5 GB of streaming stores instead of 104 M scattered ones (k_clear_logged) or a
+// 19 GB memset.  rows: the summary's rows (relative to the matrix base), SB bytes each.
+__global__ void k_clear_summ(uint32_t* __restrict__ bits, uint64_t W, uint8_t* __restrict__ summ, uint32_t SB,
+                             uint64_t rows) {
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint64_t dwords = rows * SB / 4;  // (SB is a multiple of 16)
+  const uint64_t wave = (blockIdx.x * (uint64_t)blockDim.x + threadIdx.x) >> 6;
+  const uint64_t waves = ((uint64_t)gridDim.x * blockDim.x) >> 6;
+  uint32_t* sw = reinterpret_cast<uint32_t*>(summ);
+  for (uint64_t base = wave * 64; base < dwords; base += waves * 64) {  // (wave-uniform)
+    const uint64_t d = base + lane;
+    const uint32_t v = d < dwords ? sw[d] : 0u;
+    for (uint32_t j = 0; j < 4; ++j) {
+      unsigned long long m = __ballot(((v >> (8 * j)) & 0xffu) != 0u);
+      while (m) {
+        const uint32_t L = (uint32_t)__ffsll((long long)m) - 1u;
+        m &= m - 1ull;
+        const uint64_t sb = (base + L) * 4 + j;  // summary byte: row sb / SB, block sb % SB
+        const uint64_t row = sb / SB, w0 = (sb - row * SB) * 128 + 2 * lane;
+        uint32_t* p = bits + row * W + w0;
+        if (w0 + 1 < W) {
+          *reinterpret_cast<uint2*>(p) = make_uint2(0u, 0u);
+        } else if (w0 < W) {
+          *p = 0u;
+        }
+      }
+    }
+    if (d < dwords && v) sw[d] = 0u;
+  }
+}
+
 __global__ void k_clear_logged(DIndex ix, uint32_t* bits_base, const uint32_t* __restrict__ lx,
                                const uint32_t* __restrict__ la, uint32_t n, uint32_t row_from) {
   const uint32_t stride = gridDim.x * blockDim.x;
@@ -2237,6 +2271,10 @@ struct LocalExchange : Exchange {
 };
 }  // namespace
 
+namespace {
+uint32_t* mapped_for_device(void* h);
+}
+
 struct el_ctx {
   int device = 0;
   int profile = 0;
@@ -2603,19 +2641,28 @@ struct el_ctx {
   }
   // Streamed result (el_stream_result): the committed segments of the fact and link logs cross
   // PCIe while the saturation goes on: their values (b, pid) by DMA on dstream, their runs of x
-  // (el_stream.h) encoded on nstream straight into the caller's mapped run buffers
+  // (el_stream.h) encoded on nstream into device run buffers, which follow by DMA once a later
+  // stream_out finds the encoding done (an event query: the host never waits for it there)
   el_stream* strm = nullptr;      // armed for the next el_saturate
   uint64_t strm_s = 0, strm_l = 0;  // log entries already enqueued
   bool strm_ovf = false;          // a buffer was too small (el_result_wait: EL_ERANGE)
   hipEvent_t ev_strm = nullptr;
   hipStream_t nstream = nullptr;  // run encoding (never queued behind the DMAs)
   uint2 *s_run_dev = nullptr, *l_run_dev = nullptr;  // device addresses of the caller's run buffers
+  uint32_t *s_b_dev = nullptr, *l_p_dev = nullptr;     // ... and of its value buffers (null: pageable)
+  uint2 *srun = nullptr, *lrun = nullptr;              // the runs, encoded in device memory
+  uint64_t srun_cap = 0, lrun_cap = 0;
+  uint64_t run_sent[2] = {0, 0};                       // runs DMA'd so far: S, links
+  unsigned long long* rtot_h = nullptr;                // runs encoded so far (mapped, written by the device)
+  unsigned long long* rtot_d = nullptr;                // its device address
+  hipEvent_t ev_run = nullptr;                         // after the last encoding enqueued
+  bool run_pending = false;
+  void runs_out(bool wait);
   uint32_t *rcnt = nullptr, *roff = nullptr;  // per-tile run counts / their scan
   uint64_t rtiles_cap = 0;
   void* rscan_tmp = nullptr;
   size_t rscan_bytes = 0;
   unsigned long long* rbase = nullptr;    // runs written so far: S, links (device)
-  unsigned long long* rbase_h = nullptr;  // their page-locked copy at the fixpoint
   void stream_runs(const uint32_t* keys, uint64_t a, uint64_t b, uint2* out, uint64_t cap, int which);
   void stream_out();
   void stream_end(bool release);
@@ -3041,6 +3088,14 @@ void el_ctx::reset_device(hipStream_t stream, uint32_t clear_from, uint32_t summ
   const uint64_t matrix_bytes = (uint64_t)(hi - lo) * W * sizeof(uint32_t);
   if (clear_from >= hi) {
     // the releasing copy-back zeroed the matrix as it read the rows
+  } else if (summ && summ_from == clear_from && !getenv("EL_CLEAR_LOGGED")) {
+    // by the block summary (it marks every block holding a bit, whoever set it); clears the
+    // summary of those rows too
+    const uint64_t r0 = clear_from - lo;
+    hipLaunchKernelGGL(k_clear_summ, dim3(2048), dim3(BLOCK), 0, stream, bits + r0 * W, (uint64_t)W, summ + r0 * SB,
+                       SB, (uint64_t)(hi - clear_from));
+    HIPCHK(hipGetLastError());
+    summ_from = hi;
   } else if (bits_logged && (clear_from > lo || s_count * 64 < matrix_bytes)) {
     // one 64-B line per logged fact (of the rows still set) vs. the whole matrix
     hipLaunchKernelGGL(k_clear_logged, dim3(grid_for(s_count)), dim3(BLOCK), 0, stream, ix, dstate().bits, slog_x,
@@ -4151,18 +4206,54 @@ void el_ctx::stream_out() {
   HIPCHK(hipEventRecord(ev_strm, stream));
   HIPCHK(hipStreamWaitEvent(dstream, ev_strm, 0));
   HIPCHK(hipStreamWaitEvent(nstream, ev_strm, 0));
-  auto dma = [&](uint32_t* dst, const uint32_t* src, uint64_t a, uint64_t b, uint64_t cap) {
+  // Page-locked caller buffers are device-addressable: the runtime would copy into them with a
+  // shader blit (a device-to-device copy, kernels on the CUs beside the saturation); the NoCU
+  // kind puts the copy on a DMA engine (SDMA) instead.  Pageable buffers: a plain D2H copy.
+  auto dma = [&](uint32_t* dst, uint32_t* dst_dev, const uint32_t* src, uint64_t a, uint64_t b, uint64_t cap) {
     b = std::min(b, cap);
-    if (dst && b > a)
+    if (!dst || b <= a) return;
+    if (dst_dev)
+      HIPCHK(hipMemcpyAsync(dst_dev + a, src + a, (b - a) * sizeof(uint32_t), hipMemcpyDeviceToDeviceNoCU, dstream));
+    else
       HIPCHK(hipMemcpyAsync(dst + a, src + a, (b - a) * sizeof(uint32_t), hipMemcpyDeviceToHost, dstream));
   };
-  dma(strm->s_b, slog_a, strm_s, s1, strm->s_cap);
-  dma(strm->l_p, llog_p, strm_l, l1, strm->l_cap);
+  dma(strm->s_b, s_b_dev, slog_a, strm_s, s1, strm->s_cap);
+  dma(strm->l_p, l_p_dev, llog_p, strm_l, l1, strm->l_cap);
   if ((strm->s_b && s1 > strm->s_cap) || (strm->l_p && l1 > strm->l_cap)) strm_ovf = true;
-  if (s_run_dev) stream_runs(slog_x, strm_s, s1, s_run_dev, strm->s_run_cap, 0);
-  if (l_run_dev) stream_runs(llog_x, strm_l, l1, l_run_dev, strm->l_run_cap, 1);
+  runs_out(false);  // (the runs of the earlier segments whose encoding is done)
+  if (s_run_dev) stream_runs(slog_x, strm_s, s1, srun, strm->s_run_cap, 0);
+  if (l_run_dev) stream_runs(llog_x, strm_l, l1, lrun, strm->l_run_cap, 1);
+  HIPCHK(hipEventRecord(ev_run, nstream));
+  run_pending = true;
   strm_s = s1;
   strm_l = l1;
+}
+
+// DMA the runs encoded so far (wait: block until the encodings enqueued are done; else only if
+// they are).  rtot_h was written by the last encoding before ev_run, so it is read only after it.
+void el_ctx::runs_out(bool wait) {
+  if (!run_pending) return;
+  if (wait) {
+    HIPCHK(hipEventSynchronize(ev_run));
+  } else {
+    const hipError_t q = hipEventQuery(ev_run);
+    if (q == hipErrorNotReady) {
+      (void)hipGetLastError();
+      return;
+    }
+    HIPCHK(q);
+  }
+  run_pending = false;
+  const uint64_t caps[2] = {strm->s_run_cap, strm->l_run_cap};
+  uint2* devs[2] = {s_run_dev, l_run_dev};
+  const uint2* srcs[2] = {srun, lrun};
+  for (int w = 0; w < 2; ++w) {
+    const uint64_t n = std::min<uint64_t>(rtot_h[w], caps[w]);
+    if (!devs[w] || n <= run_sent[w]) continue;
+    HIPCHK(hipMemcpyAsync(devs[w] + run_sent[w], srcs[w] + run_sent[w], (n - run_sent[w]) * sizeof(uint2),
+                          hipMemcpyDeviceToDeviceNoCU, dstream));
+    run_sent[w] = n;
+  }
 }
 
 // The runs of x over keys[a, b) (a log segment) into the caller's run buffer, numbered on from
@@ -4184,7 +4275,7 @@ void el_ctx::stream_runs(const uint32_t* keys, uint64_t a, uint64_t b, uint2* ou
   }
   elst::count(nstream, keys, a, b, rcnt);
   elcl::scan(nstream, rscan_tmp, rscan_bytes, rcnt, roff, (uint32_t)nt);
-  elst::emit(nstream, keys, a, b, roff, rcnt, out, cap, rbase + which);
+  elst::emit(nstream, keys, a, b, roff, rcnt, out, cap, rbase + which, rtot_d + which);
 }
 
 // The fixpoint: the last segments, the counts, and (release) the next classification's reset on
@@ -4195,12 +4286,11 @@ void el_ctx::stream_end(bool release) {
   stream_out();
   strm->n_facts = s_count;
   strm->n_links = l_count;
-  // the run counts (the encoding is short work on its own stream: a short run buffer is known
+  // the last runs (the encoding is short work on its own stream: a short run buffer is known
   // here, before the release decision)
-  HIPCHK(hipMemcpyAsync(rbase_h, rbase, 2 * sizeof(unsigned long long), hipMemcpyDeviceToHost, nstream));
-  HIPCHK(hipStreamSynchronize(nstream));
-  strm->n_s_runs = s_run_dev ? rbase_h[0] : 0;
-  strm->n_l_runs = l_run_dev ? rbase_h[1] : 0;
+  runs_out(true);
+  strm->n_s_runs = s_run_dev ? rtot_h[0] : 0;
+  strm->n_l_runs = l_run_dev ? rtot_h[1] : 0;
   if (strm->n_s_runs > strm->s_run_cap || strm->n_l_runs > strm->l_run_cap) strm_ovf = true;
   strm = nullptr;
   HIPCHK(hipEventRecord(ev_copied[0], cstream));
@@ -5018,13 +5108,31 @@ int el_stream_result(el_ctx* c, el_stream* s) {
     // the run buffers are written by the device: page-locked and mapped (el_host_alloc)
     c->s_run_dev = reinterpret_cast<uint2*>(mapped_for_device(s->s_run));
     c->l_run_dev = reinterpret_cast<uint2*>(mapped_for_device(s->l_run));
+    c->s_b_dev = mapped_for_device(s->s_b);
+    c->l_p_dev = mapped_for_device(s->l_p);
     if ((s->s_run && !c->s_run_dev) || (s->l_run && !c->l_run_dev))
       return fail(c, EL_EINVAL, "el_stream run buffers must be page-locked host memory (el_host_alloc)");
     if (!c->rbase) {
       c->rbase = dalloc<unsigned long long>(2);
-      HIPCHK(hipHostMalloc((void**)&c->rbase_h, 2 * sizeof(unsigned long long), hipHostMallocDefault));
+      HIPCHK(hipHostMalloc((void**)&c->rtot_h, 2 * sizeof(unsigned long long), hipHostMallocMapped));
+      HIPCHK(hipHostGetDevicePointer((void**)&c->rtot_d, c->rtot_h, 0));
+      HIPCHK(hipEventCreateWithFlags(&c->ev_run, hipEventDisableTiming));
     }
+    // device run buffers of the caller's capacities (grow-only; nothing of a last stream reads them)
+    auto fit = [&](uint2*& d, uint64_t& cap, uint64_t want) {
+      if (want <= cap) return;
+      HIPCHK(hipStreamSynchronize(c->nstream));
+      HIPCHK(hipStreamSynchronize(c->dstream));
+      dfree(d);
+      d = dalloc<uint2>(want);
+      cap = want;
+    };
+    if (c->s_run_dev) fit(c->srun, c->srun_cap, s->s_run_cap);
+    if (c->l_run_dev) fit(c->lrun, c->lrun_cap, s->l_run_cap);
     HIPCHK(hipMemsetAsync(c->rbase, 0, 2 * sizeof(unsigned long long), c->nstream));
+    c->rtot_h[0] = c->rtot_h[1] = 0;
+    c->run_sent[0] = c->run_sent[1] = 0;
+    c->run_pending = false;
     c->strm = s;
     c->strm_ovf = false;
     // everything already logged is streamed too (from the first entry)
@@ -5152,7 +5260,10 @@ void el_destroy(el_ctx* c) {
   dfree(c->roff);
   dfree(c->rscan_tmp);
   dfree(c->rbase);
-  if (c->rbase_h) (void)hipHostFree(c->rbase_h);
+  dfree(c->srun);
+  dfree(c->lrun);
+  if (c->rtot_h) (void)hipHostFree(c->rtot_h);
+  if (c->ev_run) (void)hipEventDestroy(c->ev_run);
   if (c->nstream) (void)hipStreamDestroy(c->nstream);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   if (c->cstream) (void)hipStreamDestroy(c->cstream);

@@ -5,8 +5,8 @@
 // comes in long runs.  Each committed segment of a log crosses PCIe as its values (b, or pid:
 // one DMA) plus its runs (x, end): entries [end of the previous run, end) belong to row x.  The
 // runs are found on the device (a tile count, a scan of the counts, an emit) and written in
-// log order straight into the caller's page-locked run buffer (mapped), so the host receives
-// 4 B per entry plus 8 B per run instead of 8 B per entry.  A tile start always starts a run,
+// log order into a device run buffer that follows the values by DMA, so the host receives 4 B
+// per entry plus 8 B per run instead of 8 B per entry.  A tile start always starts a run,
 // so both passes see the same runs without looking across tiles.
 #pragma once
 
@@ -25,8 +25,9 @@ __host__ __device__ inline uint64_t tiles(uint64_t n) { return (n + TILE - 1) / 
 // cnt[t] = runs starting in tile t of keys[a, b)
 void count(hipStream_t s, const uint32_t* keys, uint64_t a, uint64_t b, uint32_t* cnt);
 // the runs of keys[a, b) as (key, end) at out[*base + off[t] + i] (only those below cap; off =
-// exclusive scan of cnt), then *base += Σ cnt (a one-thread launch behind the emit)
+// exclusive scan of cnt), then *base += Σ cnt and *total = *base (a one-thread launch behind the
+// emit; total may be mapped host memory)
 void emit(hipStream_t s, const uint32_t* keys, uint64_t a, uint64_t b, const uint32_t* off, const uint32_t* cnt,
-          uint2* out, uint64_t cap, unsigned long long* base);
+          uint2* out, uint64_t cap, unsigned long long* base, unsigned long long* total);
 
 }  // namespace elst

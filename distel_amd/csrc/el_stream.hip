@@ -85,8 +85,11 @@ __global__ void __launch_bounds__(BLOCK) k_run_emit(const uint32_t* __restrict__
   }
 }
 
-__global__ void k_run_advance(unsigned long long* base, const uint32_t* off, const uint32_t* cnt, uint64_t last) {
-  *base += (unsigned long long)off[last] + cnt[last];
+__global__ void k_run_advance(unsigned long long* base, const uint32_t* off, const uint32_t* cnt, uint64_t last,
+                              unsigned long long* total) {
+  const unsigned long long v = *base + off[last] + cnt[last];
+  *base = v;
+  *total = v;
 }
 
 }  // namespace
@@ -98,12 +101,12 @@ void count(hipStream_t s, const uint32_t* keys, uint64_t a, uint64_t b, uint32_t
 }
 
 void emit(hipStream_t s, const uint32_t* keys, uint64_t a, uint64_t b, const uint32_t* off, const uint32_t* cnt,
-          uint2* out, uint64_t cap, unsigned long long* base) {
+          uint2* out, uint64_t cap, unsigned long long* base, unsigned long long* total) {
   if (b <= a) return;
   const uint64_t nt = tiles(b - a);
   hipLaunchKernelGGL(k_run_emit, dim3(grid(nt)), dim3(BLOCK), 0, s, keys, a, b, off, out, cap, base);
   SCHK(hipGetLastError());
-  hipLaunchKernelGGL(k_run_advance, dim3(1), dim3(1), 0, s, base, off, cnt, nt - 1);
+  hipLaunchKernelGGL(k_run_advance, dim3(1), dim3(1), 0, s, base, off, cnt, nt - 1, total);
   SCHK(hipGetLastError());
 }
 

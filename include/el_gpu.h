@@ -162,12 +162,16 @@ typedef int (*el_allgather_fn)(void* user, const void* send, void* recv, size_t 
  * {r∘s⊑t : s ∈ second(r), t ∈ third(r)}, which el_load builds in place of the told chains.
  * Default (0): the correct EL+ join on s. */
 #define EL_FLAG_COMPAT_DISTEL_CHAIN 0x1u
-/* Range axioms (parity hazard H1).  Default: ELK's reading, as the
- * normalizer's range elimination gives it (Normalizer.java:122-137, 455-497): a CR3 axiom
- * A ⊑ ∃r.B whose role has ranges ranges*(r) (of r and its super-roles) points its links at a
- * fresh internal filler F = B ⊓ ranges*(r) (ids n_concepts, n_concepts + 1, …; see
- * el_fresh_fillers); an individual filler b gets b ⊑ C; datatype fillers are untouched.  The
- * result rows cover the caller's concepts only; link fillers may be fresh ids.
+/* Range axioms (parity hazard H1).  Default: ELK's reading, by the range
+ * elimination of the normalizer (Normalizer.java:122-137, 455-497): a CR3 axiom A ⊑ ∃r.B whose
+ * role has ranges points its links at a fresh internal filler F = B ⊓ ranges*(r) (ids
+ * n_concepts, n_concepts + 1, …; see el_fresh_fillers); an individual filler b gets b ⊑ C;
+ * datatype fillers are untouched.  ranges*(r) holds the ranges of r AND of its super-roles: an
+ * r-successor is an s-successor for r ⊑ s, so ELK (the reference's diff oracle) puts it under
+ * range(s) too.  Deliberate deviation: the reference Normalizer looks up the existential's own
+ * property only (objPropRangeMap.get(ope), Normalizer.java:462-489), which misses those
+ * subsumptions (KAT tests/golden/kat_range.elax pins the complete reading).  The result rows
+ * cover the caller's concepts only; link fillers may be fresh ids.
  * EL_FLAG_COMPAT_DISTEL_RANGE: DistEL's reading instead (RolePairHandler.java:471-479, K10
  * ScriptsCollection.java:45-62): a link into Y activates Y ⊑ C, and C joins every S(X)
  * holding Y. */

@@ -14,3 +14,9 @@ cat $OUT/g3.json
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/prof -o g3 -- python $R/bench.py --workload g3 --no-cpu --no-profile --no-throughput2 --steps 3 --warmup 1 > $OUT/prof.log 2>&1 || { tail $OUT/prof.log; exit 1; }
 python3 $R/scripts/rpd_stats.py "$OUT/prof/**/*.db" | cut -c1-120 | head -25
+# FETCH_SIZE / WRITE_SIZE calibration of the saturation's access patterns (scripts/micro/pmc_cal.hip)
+timeout -k 10 60 $R/scripts/micro/pmc_cal > $OUT/cal.txt 2>&1 || { cat $OUT/cal.txt; exit 1; }
+cat $OUT/cal.txt
+timeout -s KILL 60 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/c1 -o c -- $R/scripts/micro/pmc_cal > $OUT/c1.log 2>&1 || { tail -3 $OUT/c1.log; exit 1; }
+timeout -s KILL 60 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/c2 -o c -- $R/scripts/micro/pmc_cal > $OUT/c2.log 2>&1 || { tail -3 $OUT/c2.log; exit 1; }
+python3 $R/scripts/pmc_cal_summary.py $OUT $OUT/pmc_calibration.json
