@@ -363,11 +363,16 @@ def main():
     roofline = None
     kernels = None
     if rank == 0 and not args.no_profile:
-        # profiled classification: HIP events bracket every launch on the engine stream
+        # profiled classification in the timed step's schedule (the streamed copy-back beside the
+        # supersteps): HIP events bracket every launch on the engine stream
         peng = engine.Engine(device=dev, profile=True)
         peng.load(ax)
         peng.init()
+        if args.copyback == "stream":
+            peng.stream_result(engine.Stream())  # (not released: the event counters are read after)
         pst = peng.saturate()
+        if args.copyback == "stream":
+            peng.result_wait()
         ks = peng.kernel_stats()
         peng.close()
         # one row per launch: phases that share a launch (el_kernel_stat.group) add their bytes

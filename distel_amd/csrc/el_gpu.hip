@@ -3088,9 +3088,9 @@ void el_ctx::reset_device(hipStream_t stream, uint32_t clear_from, uint32_t summ
   const uint64_t matrix_bytes = (uint64_t)(hi - lo) * W * sizeof(uint32_t);
   if (clear_from >= hi) {
     // the releasing copy-back zeroed the matrix as it read the rows
-  } else if (summ && summ_from == clear_from && !getenv("EL_CLEAR_LOGGED")) {
-    // by the block summary (it marks every block holding a bit, whoever set it); clears the
-    // summary of those rows too
+  } else if (bits_logged && summ && summ_from == clear_from && !getenv("EL_CLEAR_LOGGED")) {
+    // by the block summary (it marks every block holding a bit, whoever set it, once the matrix
+    // was cleared whole: bits_logged); clears the summary of those rows too
     const uint64_t r0 = clear_from - lo;
     hipLaunchKernelGGL(k_clear_summ, dim3(2048), dim3(BLOCK), 0, stream, bits + r0 * W, (uint64_t)W, summ + r0 * SB,
                        SB, (uint64_t)(hi - clear_from));

@@ -1,5 +1,6 @@
 #!/bin/bash
-# PMC passes (one counter group per pass, --pmc only, no tracing domains) on one G2 classification.
+# PMC passes (one counter group per pass, --pmc only, no tracing domains) on one classification
+# of the bench workload (G3 by default; extra arguments go to bench.py).
 set -o pipefail
 TAG=${1:-pmc}; shift
 R=${GRAFT_REPO_ROOT:-$(pwd)}
@@ -9,7 +10,7 @@ cd /tmp && export TMPDIR=/tmp
 i=0
 for grp in "FETCH_SIZE" "WRITE_SIZE" "TCC_HIT_sum TCC_MISS_sum" "SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_VMEM_RD" "GRBM_GUI_ACTIVE GRBM_COUNT"; do
   i=$((i+1))
-  timeout -k 10 300 rocprofv3 --pmc $grp --output-format csv -d $OUT/p$i -o run -- python3 $R/bench.py --no-cpu --no-profile --steps 1 --warmup 0 "$@" > $OUT/p$i.log 2>&1
+  timeout -k 10 300 rocprofv3 --pmc $grp --output-format csv -d $OUT/p$i -o run -- python3 $R/bench.py --no-cpu --no-profile --no-throughput2 --steps 1 --warmup 0 "$@" > $OUT/p$i.log 2>&1
   rc=$?; echo "pass $i ($grp) rc=$rc"
   [ $rc -eq 0 ] || { tail -5 $OUT/p$i.log; exit $rc; }
 done

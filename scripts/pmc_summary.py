@@ -4,12 +4,20 @@
 Usage: scripts/pmc_summary.py gpurun_out/TAG OUT.json WORKLOAD
 
 Per kernel: dispatches, Σ FETCH_SIZE / WRITE_SIZE (KB, as rocprofv3 reports them) and the
-HBM bytes per dispatch, corrected as MI355X_MICROARCH.md prescribes for gfx950: FETCH_SIZE
-reports half the bytes of a wide streaming read (×2), WRITE_SIZE is exact.  The fetch side
-of 4–8-byte random accesses is uncalibrated (the guide says so); the doubled figure is
-reported and the raw one kept beside it.  The source digest of the HIP file ties the numbers
-to the build that produced them (bench.py uses them only for that build).
+HBM bytes per dispatch, corrected by the calibration of this engine's access patterns
+(profiles/pmc/r03_pmc_calibration.json, scripts/micro/pmc_cal.hip): FETCH_SIZE reports half the
+bytes of a coalesced streaming read (×2, as MI355X_MICROARCH.md has it for gfx950) but one 64-B
+unit per random 4–8-B load, i.e. per line request (×1); WRITE_SIZE counts 32 B per scattered
+4-B store or atomic, 64 B per 64-bit CAS (×1).  Kernels whose reads are random gathers (the
+saturation, the set inserts, the told-closure merges) take ×1, streaming kernels ×2; both the
+calibrated and the doubled figure are reported, with the raw one.  The source digest of the HIP
+file ties the numbers to the build that produced them (bench.py uses them only for that build).
 """
+
+# read pattern per kernel: random gathers (FETCH_SIZE = bytes of the line requests) or
+# coalesced streaming (FETCH_SIZE = half the bytes); calibration: r03_pmc_calibration.json
+RANDOM_READ = {"k_expand", "k_jobs", "k_commit", "k_commit_told", "k_rehash", "k_level", "k_relax", "k_gap_move_e",
+               "k_gap_ovf", "k_ximport", "k_clear_logged", "k_init_facts", "k_stats", "k_succ_fill", "k_group_fill"}
 import csv
 import glob
 import hashlib
@@ -51,8 +59,9 @@ def main():
     src = open(os.path.join(ROOT, "distel_amd", "csrc", "el_gpu.hip"), "rb").read()
     res = {"workload": workload, "source_sha256": hashlib.sha256(src).hexdigest(),
            "method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes over one classification "
-                     "(bench.py --steps 1 --warmup 0); hbm_bytes_per_dispatch = (2*FETCH_SIZE + WRITE_SIZE)*1024 "
-                     "/ dispatches (gfx950 FETCH_SIZE correction, MI355X_MICROARCH.md 'HBM')",
+                     "(bench.py --steps 1 --warmup 0); hbm_bytes_per_dispatch = (f*FETCH_SIZE + WRITE_SIZE)*1024 "
+                     "/ dispatches with f = 1 for random-gather kernels and 2 for streaming ones, as calibrated in "
+                     "profiles/pmc/r03_pmc_calibration.json (scripts/micro/pmc_cal.hip)",
            "kernels": {}}
     # informational passes (p3: L2 hit/miss, p4: SQ wave/issue cycles), when present
     extra = {c: load(os.path.join(tag, d), c) for d, c in
@@ -61,8 +70,11 @@ def main():
     for k in sorted(set(fetch) | set(write)):
         nd = max(fetch.get(k, [0, 0])[0], write.get(k, [0, 0])[0])
         fk, wk = fetch.get(k, [0, 0.0])[1], write.get(k, [0, 0.0])[1]
-        row = {"dispatches": nd, "fetch_kb": round(fk, 3), "write_kb": round(wk, 3),
-               "hbm_bytes_per_dispatch": round((2 * fk + wk) * 1024 / nd, 1) if nd else None,
+        ff = 1 if k.split("::")[-1] in RANDOM_READ else 2
+        row = {"dispatches": nd, "fetch_kb": round(fk, 3), "write_kb": round(wk, 3), "read_pattern":
+               "random (FETCH ×1)" if ff == 1 else "streaming (FETCH ×2)",
+               "hbm_bytes_per_dispatch": round((ff * fk + wk) * 1024 / nd, 1) if nd else None,
+               "doubled_bytes_per_dispatch": round((2 * fk + wk) * 1024 / nd, 1) if nd else None,
                "raw_bytes_per_dispatch": round((fk + wk) * 1024 / nd, 1) if nd else None}
         hit, miss = extra["TCC_HIT_sum"].get(k, [0, 0.0])[1], extra["TCC_MISS_sum"].get(k, [0, 0.0])[1]
         if hit + miss:
