@@ -2647,6 +2647,7 @@ struct el_ctx {
   uint64_t strm_s = 0, strm_l = 0;  // log entries already enqueued
   bool strm_ovf = false;          // a buffer was too small (el_result_wait: EL_ERANGE)
   hipEvent_t ev_strm = nullptr;
+  bool strm_marked = false;       // ev_strm was recorded right behind this step's commit
   hipStream_t nstream = nullptr;  // run encoding (never queued behind the DMAs)
   uint2 *s_run_dev = nullptr, *l_run_dev = nullptr;  // device addresses of the caller's run buffers
   uint32_t *s_b_dev = nullptr, *l_p_dev = nullptr;     // ... and of its value buffers (null: pageable)
@@ -3465,6 +3466,10 @@ bool el_ctx::superstep(uint32_t mask, uint64_t sb, uint64_t se, uint64_t lb, uin
     launch(EL_K_COMMIT_S, [&] {
       hipLaunchKernelGGL(k_commit, dim3(ca.gs + ca.gl + ca.ga + ca.gp), dim3(BLOCK), 0, stream, ix, st, ca);
     });
+    if (strm) {  // the step's log entries are final here (stream_out DMAs them behind this event)
+      HIPCHK(hipEventRecord(ev_strm, stream));
+      strm_marked = true;
+    }
     // the new links / propagations are already in their (gapped) CSR rows; S rows are
     // built lazily, for export only
     wait_commit(ca.pub.seq);
@@ -4203,7 +4208,20 @@ void el_ctx::stream_out() {
   if (!strm) return;
   const uint64_t s1 = s_count, l1 = l_count;
   if (s1 == strm_s && l1 == strm_l) return;
-  HIPCHK(hipEventRecord(ev_strm, stream));
+  // The DMAs wait for the commit that wrote the segment.  The host saw that commit publish, so
+  // the event is about to complete: wait for it here, so that the copy is enqueued without a
+  // pending dependency (the runtime then puts it on a DMA engine; with a dependency on the
+  // running engine stream it would run it as a blit kernel on the CUs).
+  const bool marked = strm_marked;
+  strm_marked = false;
+  if (marked) {
+    for (hipError_t q; (q = hipEventQuery(ev_strm)) != hipSuccess;) {
+      if (q != hipErrorNotReady) HIPCHK(q);
+      (void)hipGetLastError();
+    }
+  } else {  // (no commit of this call to wait for: behind everything enqueued, on the device)
+    HIPCHK(hipEventRecord(ev_strm, stream));
+  }
   HIPCHK(hipStreamWaitEvent(dstream, ev_strm, 0));
   HIPCHK(hipStreamWaitEvent(nstream, ev_strm, 0));
   // Page-locked caller buffers are device-addressable: the runtime would copy into them with a

@@ -7,7 +7,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch  # noqa: F401,E402  (as bench.py: the runtime torch loads)
 from distel_amd import engine, generators  # noqa: E402
 
-ax = generators.workload("g1", 0.2)
+ax = generators.workload(sys.argv[1] if len(sys.argv) > 1 else "g1", float(sys.argv[2]) if len(sys.argv) > 2 else 0.2)
 eng = engine.Engine(device=0)
 eng.load(ax)
 s = engine.Stream()
