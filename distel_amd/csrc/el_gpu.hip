@@ -2637,6 +2637,7 @@ struct el_ctx {
   void wait_copy() {
     if (!copy_pending) return;
     for (hipEvent_t e : ev_copied) HIPCHK(hipEventSynchronize(e));
+    if (sdma) sdma->wait();
     copy_pending = false;
   }
   // Streamed result (el_stream_result): the committed segments of the fact and link logs cross
@@ -2646,8 +2647,9 @@ struct el_ctx {
   el_stream* strm = nullptr;      // armed for the next el_saturate
   uint64_t strm_s = 0, strm_l = 0;  // log entries already enqueued
   bool strm_ovf = false;          // a buffer was too small (el_result_wait: EL_ERANGE)
-  hipEvent_t ev_strm = nullptr;
+  hipEvent_t ev_strm = nullptr;   // (release to system scope: an SDMA copy reads behind it)
   bool strm_marked = false;       // ev_strm was recorded right behind this step's commit
+  std::unique_ptr<elst::Sdma> sdma;  // the stream's copies on a DMA engine (null / !ok: hipMemcpyAsync)
   hipStream_t nstream = nullptr;  // run encoding (never queued behind the DMAs)
   uint2 *s_run_dev = nullptr, *l_run_dev = nullptr;  // device addresses of the caller's run buffers
   uint32_t *s_b_dev = nullptr, *l_p_dev = nullptr;     // ... and of its value buffers (null: pageable)
@@ -4213,24 +4215,28 @@ void el_ctx::stream_out() {
   // pending dependency (the runtime then puts it on a DMA engine; with a dependency on the
   // running engine stream it would run it as a blit kernel on the CUs).
   const bool marked = strm_marked;
+  const bool dma_engine = sdma && sdma->ok();
   strm_marked = false;
   if (marked) {
     for (hipError_t q; (q = hipEventQuery(ev_strm)) != hipSuccess;) {
       if (q != hipErrorNotReady) HIPCHK(q);
       (void)hipGetLastError();
     }
-  } else {  // (no commit of this call to wait for: behind everything enqueued, on the device)
+  } else {  // (no commit of this call to wait for: behind everything enqueued)
     HIPCHK(hipEventRecord(ev_strm, stream));
+    if (dma_engine) HIPCHK(hipEventSynchronize(ev_strm));
   }
   HIPCHK(hipStreamWaitEvent(dstream, ev_strm, 0));
   HIPCHK(hipStreamWaitEvent(nstream, ev_strm, 0));
-  // Page-locked caller buffers are device-addressable: the runtime would copy into them with a
-  // shader blit (a device-to-device copy, kernels on the CUs beside the saturation); the NoCU
-  // kind puts the copy on a DMA engine (SDMA) instead.  Pageable buffers: a plain D2H copy.
+  // The segment is final and visible (ev_strm completed, released to system scope): its values
+  // go by SDMA (elst::Sdma); without one, by hipMemcpyAsync on dstream (into page-locked buffers
+  // the runtime runs that as a blit kernel; the NoCU kind is the copy-engine request).
   auto dma = [&](uint32_t* dst, uint32_t* dst_dev, const uint32_t* src, uint64_t a, uint64_t b, uint64_t cap) {
     b = std::min(b, cap);
     if (!dst || b <= a) return;
-    if (dst_dev)
+    if (dma_engine)
+      sdma->copy(dst + a, src + a, (b - a) * sizeof(uint32_t));
+    else if (dst_dev)
       HIPCHK(hipMemcpyAsync(dst_dev + a, src + a, (b - a) * sizeof(uint32_t), hipMemcpyDeviceToDeviceNoCU, dstream));
     else
       HIPCHK(hipMemcpyAsync(dst + a, src + a, (b - a) * sizeof(uint32_t), hipMemcpyDeviceToHost, dstream));
@@ -4265,11 +4271,15 @@ void el_ctx::runs_out(bool wait) {
   const uint64_t caps[2] = {strm->s_run_cap, strm->l_run_cap};
   uint2* devs[2] = {s_run_dev, l_run_dev};
   const uint2* srcs[2] = {srun, lrun};
+  uint2* hosts[2] = {reinterpret_cast<uint2*>(strm->s_run), reinterpret_cast<uint2*>(strm->l_run)};
   for (int w = 0; w < 2; ++w) {
     const uint64_t n = std::min<uint64_t>(rtot_h[w], caps[w]);
     if (!devs[w] || n <= run_sent[w]) continue;
-    HIPCHK(hipMemcpyAsync(devs[w] + run_sent[w], srcs[w] + run_sent[w], (n - run_sent[w]) * sizeof(uint2),
-                          hipMemcpyDeviceToDeviceNoCU, dstream));
+    if (sdma && sdma->ok())
+      sdma->copy(hosts[w] + run_sent[w], srcs[w] + run_sent[w], (n - run_sent[w]) * sizeof(uint2));
+    else
+      HIPCHK(hipMemcpyAsync(devs[w] + run_sent[w], srcs[w] + run_sent[w], (n - run_sent[w]) * sizeof(uint2),
+                            hipMemcpyDeviceToDeviceNoCU, dstream));
     run_sent[w] = n;
   }
 }
@@ -4591,7 +4601,7 @@ int el_create(el_ctx** out, const el_config* cfg) {
     HIPCHK(hipEventCreateWithFlags(&c->ev_reset, hipEventDisableTiming));
     for (hipEvent_t& e : c->ev_copied) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     for (hipEvent_t& e : c->ev_base) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-    HIPCHK(hipEventCreateWithFlags(&c->ev_strm, hipEventDisableTiming));
+    HIPCHK(hipEventCreateWithFlags(&c->ev_strm, hipEventDisableTiming | hipEventReleaseToSystem));
     if (c->xmode == EL_XCHG_LOCAL) c->xchg.reset(new LocalExchange(cfg->group, (int)c->part_rank));
     if (c->xmode == EL_XCHG_RCCL)  // collective: every rank of the group calls el_create
       c->xchg.reset(new RcclExchange((int)c->part_rank, (int)c->part_count, cfg->rccl_id));
@@ -5128,13 +5138,14 @@ int el_stream_result(el_ctx* c, el_stream* s) {
     c->l_run_dev = reinterpret_cast<uint2*>(mapped_for_device(s->l_run));
     c->s_b_dev = mapped_for_device(s->s_b);
     c->l_p_dev = mapped_for_device(s->l_p);
+    if (!c->sdma && !(getenv("EL_SDMA") && !strcmp(getenv("EL_SDMA"), "0"))) c->sdma.reset(new elst::Sdma(c->device));
     if ((s->s_run && !c->s_run_dev) || (s->l_run && !c->l_run_dev))
       return fail(c, EL_EINVAL, "el_stream run buffers must be page-locked host memory (el_host_alloc)");
     if (!c->rbase) {
       c->rbase = dalloc<unsigned long long>(2);
       HIPCHK(hipHostMalloc((void**)&c->rtot_h, 2 * sizeof(unsigned long long), hipHostMallocMapped));
       HIPCHK(hipHostGetDevicePointer((void**)&c->rtot_d, c->rtot_h, 0));
-      HIPCHK(hipEventCreateWithFlags(&c->ev_run, hipEventDisableTiming));
+      HIPCHK(hipEventCreateWithFlags(&c->ev_run, hipEventDisableTiming | hipEventReleaseToSystem));
     }
     // device run buffers of the caller's capacities (grow-only; nothing of a last stream reads them)
     auto fit = [&](uint2*& d, uint64_t& cap, uint64_t want) {
@@ -5271,12 +5282,19 @@ void el_destroy(el_ctx* c) {
   if (c->dstream) (void)hipStreamSynchronize(c->dstream);  // (an async copy-back's last DMAs)
   if (c->nstream) (void)hipStreamSynchronize(c->nstream);
   if (c->ostream) (void)hipStreamSynchronize(c->ostream);
+  if (c->sdma) {
+    try {
+      c->sdma->wait();  // (an SDMA copy still reading the logs)
+    } catch (...) {
+    }
+  }
   c->copy_pending = false;
   c->free_state();
   c->free_index();
   dfree(c->rcnt);
   dfree(c->roff);
   dfree(c->rscan_tmp);
+  c->sdma.reset();
   dfree(c->rbase);
   dfree(c->srun);
   dfree(c->lrun);
