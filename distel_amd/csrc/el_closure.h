@@ -44,6 +44,10 @@ struct Axioms {
   const uint32_t* sc_w = nullptr;                       // pid -> sc_self + Σ sc_self of its lifts
   const uint32_t *fp_ptr = nullptr, *pair_role = nullptr;  // Y -> pairs (r, Y), sorted by r
   const uint8_t* kind = nullptr;
+  // the concepts whose rows are built: ⊥, ⊤ and [w_lo, w_hi) (a partitioned context: its column
+  // window, which holds every concept its rows can reach and is closed under told supers); the
+  // others keep empty rows and cost nothing
+  uint32_t w_lo = 2, w_hi = 0xffffffffu;
 };
 
 // per-node statistics (Out::nd + k * N)

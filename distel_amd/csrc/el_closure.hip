@@ -433,14 +433,19 @@ __device__ __forceinline__ void for_tasks(uint32_t N, Sel&& sel, Run&& run) {
   }
 }
 
+// a concept outside the built set (Axioms::w_lo/w_hi): never ready, never stuck
+constexpr uint32_t SKIP = NONE - 1u;
+__device__ __forceinline__ bool built(const Axioms& ax, uint32_t A) { return A < 2u || (A >= ax.w_lo && A < ax.w_hi); }
+
 __global__ void __launch_bounds__(BLOCK) k_start(Axioms ax, Out o) {
   const uint32_t stride = gridDim.x * blockDim.x;
   bool root = false;
   for (uint32_t A = blockIdx.x * blockDim.x + threadIdx.x; A < ax.N; A += stride) {
     const uint32_t d = ax.par_ptr[A + 1] - ax.par_ptr[A];
+    const bool in = built(ax, A);
     o.indeg[A] = d;
-    o.level[A] = d ? NONE : 0u;
-    root |= d == 0;
+    o.level[A] = !in ? SKIP : d ? NONE : 0u;
+    root |= in && d == 0;
     o.meta[2 * A] = make_uint4(0u, ax.cidx_ptr[A], 0u, 0u);
     o.meta[2 * A + 1] = make_uint4(0u, ax.cidx_ptr[A + 1], 0u, 0u);
   }
@@ -468,7 +473,7 @@ __global__ void __launch_bounds__(BLOCK) k_level(Axioms ax, Out o, uint32_t L) {
       const uint32_t cb = ax.chi_ptr[A], ce = ax.chi_ptr[A + 1];
       for (uint32_t q = cb + lane(); q < ce; q += 64) {
         const uint32_t c = ax.chi[q];
-        if (atomicSub(o.indeg + c, 1u) == 1u) {
+        if (o.level[c] != SKIP && atomicSub(o.indeg + c, 1u) == 1u) {
           o.level[c] = L + 1;
           any = true;
         }
@@ -618,6 +623,7 @@ __global__ void __launch_bounds__(BLOCK) k_totals(Axioms ax, Out o, uint32_t lo,
   unsigned long long t[T_NUM - 1] = {}, e[E_NUM] = {};
   const uint32_t N1 = ax.N + 1;
   for (uint32_t A = blockIdx.x * blockDim.x + threadIdx.x; A < ax.N; A += gridDim.x * blockDim.x) {
+    if (!built(ax, A)) continue;
     const uint4 b = o.meta[2 * A], f = o.meta[2 * A + 1];
     const uint32_t tl = f.x - b.x, el = f.z - b.z, ll = f.w - b.w;
     const uint32_t pb = ax.par_ptr[A], pe = ax.par_ptr[A + 1], nch = ax.chi_ptr[A + 1] - ax.chi_ptr[A];

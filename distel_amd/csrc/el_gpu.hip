@@ -3953,6 +3953,10 @@ void el_ctx::closure_tail(uint32_t a, uint32_t b, uint32_t L) {
 // up front), one per relaxation round.
 void el_ctx::closure_rows(uint32_t a, uint32_t b) {
   const uint32_t N = hx.N;
+  // a partitioned context builds the rows of its column window only (×N of G3 on N ranks: each
+  // builds its own copy's closure, not the N copies')
+  cax.w_lo = part() ? ix.c_lo : 2u;
+  cax.w_hi = part() ? ix.c_hi : 0xffffffffu;
   for (int attempt = 0;; ++attempt) {
     if (attempt > 32) throw ElError{EL_EHIP, "told closure: the build did not fit its buffers"};
     launch(EL_K_CLOSURE, [&] { elcl::start(stream, cax, cl); });
