@@ -5142,7 +5142,9 @@ int el_stream_result(el_ctx* c, el_stream* s) {
     c->l_run_dev = reinterpret_cast<uint2*>(mapped_for_device(s->l_run));
     c->s_b_dev = mapped_for_device(s->s_b);
     c->l_p_dev = mapped_for_device(s->l_p);
-    if (!c->sdma && !(getenv("EL_SDMA") && !strcmp(getenv("EL_SDMA"), "0"))) c->sdma.reset(new elst::Sdma(c->device));
+    // EL_SDMA=1: the copies through HSA on an SDMA engine (A/B: G3 27.37 vs 27.56 ms, within noise;
+    // and a rocprofv3-traced run of it stalled), default the runtime's copies
+    if (!c->sdma && getenv("EL_SDMA") && !strcmp(getenv("EL_SDMA"), "1")) c->sdma.reset(new elst::Sdma(c->device));
     if ((s->s_run && !c->s_run_dev) || (s->l_run && !c->l_run_dev))
       return fail(c, EL_EINVAL, "el_stream run buffers must be page-locked host memory (el_host_alloc)");
     if (!c->rbase) {
