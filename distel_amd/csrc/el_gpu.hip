@@ -2667,7 +2667,11 @@ struct el_ctx {
   size_t rscan_bytes = 0;
   unsigned long long* rbase = nullptr;    // runs written so far: S, links (device)
   void stream_runs(const uint32_t* keys, uint64_t a, uint64_t b, uint2* out, uint64_t cap, int which);
-  void stream_out();
+  void stream_out();    // stream_mark + stream_flush
+  void stream_mark();
+  void stream_flush();
+  uint64_t mark_s = 0, mark_l = 0;  // the marked segment ends [strm_s, mark_s), [strm_l, mark_l)
+  bool mark_pending = false;
   void stream_end(bool release);
   hipEvent_t ev_base[2] = {nullptr, nullptr};  // base links logged (stream) / in the link set (rstream)
   bool base_filling = false;                   // the set fill runs beside the first superstep
@@ -3468,7 +3472,9 @@ bool el_ctx::superstep(uint32_t mask, uint64_t sb, uint64_t se, uint64_t lb, uin
     launch(EL_K_COMMIT_S, [&] {
       hipLaunchKernelGGL(k_commit, dim3(ca.gs + ca.gl + ca.ga + ca.gp), dim3(BLOCK), 0, stream, ix, st, ca);
     });
-    if (strm) {  // the step's log entries are final here (stream_out DMAs them behind this event)
+    if (strm) {  // the last step's segment goes now, beside this step's kernels; this step's
+                 // entries are final behind the event recorded here (stream_mark picks it up)
+      stream_flush();
       HIPCHK(hipEventRecord(ev_strm, stream));
       strm_marked = true;
     }
@@ -4208,33 +4214,32 @@ void el_ctx::install_base() {
   host_ev[EL_K_INIT][EL_EV_EMIT] += nb;
 }
 
-// Streamed result: enqueue the DMAs of the log entries committed since the last call (behind
-// the work enqueued on the engine stream so far: the entries below s_count / l_count are final).
-void el_ctx::stream_out() {
+// Streamed result, in two halves so that no copy work sits between two supersteps:
+// stream_mark() (after a superstep) notes the log entries committed so far, behind ev_strm (the
+// event the superstep recorded right after its commit, or one recorded now behind everything);
+// stream_flush() enqueues their copies and run encoding — called by the NEXT superstep once its
+// own kernels are enqueued (the host's enqueue work then overlaps them), or at the fixpoint.
+void el_ctx::stream_mark() {
   if (!strm) return;
   const uint64_t s1 = s_count, l1 = l_count;
-  if (s1 == strm_s && l1 == strm_l) return;
-  // The DMAs wait for the commit that wrote the segment.  The host saw that commit publish, so
-  // the event is about to complete: wait for it here, so that the copy is enqueued without a
-  // pending dependency (the runtime then puts it on a DMA engine; with a dependency on the
-  // running engine stream it would run it as a blit kernel on the CUs).
-  const bool marked = strm_marked;
-  const bool dma_engine = sdma && sdma->ok();
+  if (s1 == (mark_pending ? mark_s : strm_s) && l1 == (mark_pending ? mark_l : strm_l)) return;
+  if (!strm_marked) HIPCHK(hipEventRecord(ev_strm, stream));  // (no commit of this step marked it)
   strm_marked = false;
-  if (marked) {
-    for (hipError_t q; (q = hipEventQuery(ev_strm)) != hipSuccess;) {
-      if (q != hipErrorNotReady) HIPCHK(q);
-      (void)hipGetLastError();
-    }
-  } else {  // (no commit of this call to wait for: behind everything enqueued)
-    HIPCHK(hipEventRecord(ev_strm, stream));
-    if (dma_engine) HIPCHK(hipEventSynchronize(ev_strm));
-  }
+  mark_s = s1;
+  mark_l = l1;
+  mark_pending = true;
+}
+
+void el_ctx::stream_flush() {
+  if (!strm || !mark_pending) return;
+  mark_pending = false;
+  const uint64_t s1 = mark_s, l1 = mark_l;
+  const bool dma_engine = sdma && sdma->ok();
+  if (dma_engine) HIPCHK(hipEventSynchronize(ev_strm));  // (an SDMA copy carries no dependency)
   HIPCHK(hipStreamWaitEvent(dstream, ev_strm, 0));
   HIPCHK(hipStreamWaitEvent(nstream, ev_strm, 0));
-  // The segment is final and visible (ev_strm completed, released to system scope): its values
-  // go by SDMA (elst::Sdma); without one, by hipMemcpyAsync on dstream (into page-locked buffers
-  // the runtime runs that as a blit kernel; the NoCU kind is the copy-engine request).
+  // the values by hipMemcpyAsync on dstream (NoCU: the copy-engine request for page-locked
+  // buffers the device has mapped) or, with EL_SDMA=1, through HSA on an SDMA engine
   auto dma = [&](uint32_t* dst, uint32_t* dst_dev, const uint32_t* src, uint64_t a, uint64_t b, uint64_t cap) {
     b = std::min(b, cap);
     if (!dst || b <= a) return;
@@ -4255,6 +4260,11 @@ void el_ctx::stream_out() {
   run_pending = true;
   strm_s = s1;
   strm_l = l1;
+}
+
+void el_ctx::stream_out() {
+  stream_mark();
+  stream_flush();
 }
 
 // DMA the runs encoded so far (wait: block until the encodings enqueued are done; else only if
@@ -4784,7 +4794,7 @@ int el_saturate(el_ctx* c, el_stats* stats) {
     auto t0 = std::chrono::steady_clock::now();
     if (c->fresh && !c->part()) c->install_base();
     c->fresh = false;
-    c->stream_out();  // (a streamed result: the init facts and base links cross PCIe already)
+    c->stream_mark();  // (a streamed result: the init facts and base links go beside the first superstep)
     // all rule types share one frontier: start at the oldest watermark
     uint64_t sb = c->s_count, lb = c->l_count, ab = c->a_count, pb = c->p_count;
     for (int r = 0; r < EL_NUM_RULE_TYPES; ++r) {
@@ -4825,7 +4835,7 @@ int el_saturate(el_ctx* c, el_stats* stats) {
       c->tr_a.push_back(ae - ab);
       c->superstep(pb < pe ? (M_ALL | M_R4P) : M_ALL, sb, se, lb, le, ab, ae, pb, pe);
       c->join_base();
-      c->stream_out();
+      c->stream_mark();
       sb = se;
       lb = le;
       ab = ae;
@@ -5172,6 +5182,7 @@ int el_stream_result(el_ctx* c, el_stream* s) {
     c->strm_ovf = false;
     // everything already logged is streamed too (from the first entry)
     c->strm_s = c->strm_l = 0;
+    c->mark_pending = c->strm_marked = false;
     s->n_facts = s->n_links = s->n_s_runs = s->n_l_runs = 0;
     return EL_OK;
   });
