@@ -1384,18 +1384,10 @@ static void base_links(elo_ctx* c) {
   }
 }
 
-/* after the first superstep the link set holds the base links (the GPU fills it beside that
- * superstep, EL_K_REHASH): later probes go to the set alone */
-static void base_join(elo_ctx* c) {
-  uint64_t i;
-  if (!c->base) return;
-  for (i = 0; i < c->l_base; ++i) hs_add(&c->links, lkey(c->llog_p.v[i], c->llog_x.v[i]));
-  for (i = 0; i < c->p_base; ++i) hs_add(&c->props, lkey(c->plog_p.v[i], c->plog_b.v[i]));
-  EVN(EL_K_REHASH, EL_EV_HASH, c->l_base + c->p_base);
-  c->base = 0;
-  c->l_base = 0;
-  c->p_base = 0;
-}
+/* The base links / propagations stay out of the sets for the whole saturation (as on the GPU,
+ * el_ctx::install_base): a membership test is base_has / the bpp binary search, then the set
+ * probe.  (Round 2 filled the sets after the first superstep, EL_K_REHASH.) */
+static void base_join(elo_ctx* c) { (void)c; }
 
 int elo_step(elo_ctx* c, int rule, int* changed) {
   uint64_t se, le, ae, pe;
