@@ -351,6 +351,94 @@ __device__ void gather(const Axioms& ax, const Out& o, uint32_t A, uint32_t pb, 
   }
 }
 
+// A concept with at most one told super P (in the Kahn levels: no cycle through A, so A is not in
+// P's rows): its row of type T is P's row merged with a short sorted list — {P} for told*, A's own
+// axioms xr(A) / xl(A) (sorted, unique) for exr* / exl*.  A merge, not a sort: each list entry
+// finds its place in P's row by a binary search (and drops out if P's row holds it), each entry
+// of P's row moves up by the list entries below it, and the row is written straight into its
+// reservation (coalesced).  Returns false when the list has more than 64 entries (the caller
+// sorts).  Writes meta like task().
+template <uint32_t T>
+__device__ bool task_merge1(const Axioms& ax, const Out& o, uint32_t A, uint32_t pb, uint32_t pe, Rsv& rs) {
+  using K = typename RowT<T>::K;
+  uint32_t s = 0;
+  K sv = 0;
+  if (T == R_TOLD) {
+    s = pe > pb ? 1u : 0u;
+    if (s && lane() == 0) sv = (K)ax.par[pb];
+  } else if (T == R_EXR) {
+    const uint32_t b0 = ax.xr_ptr[A];
+    s = ax.xr_ptr[A + 1] - b0;
+    if (s > 64) return false;
+    if (lane() < s) sv = (K)ax.xr[b0 + lane()];
+  } else {
+    const uint32_t b0 = ax.xl_ptr[A];
+    s = ax.xl_ptr[A + 1] - b0;
+    if (s > 64) return false;
+    if (lane() < s) sv = ((K)ax.xl_r[b0 + lane()] << 32) | ax.xl_b[b0 + lane()];
+  }
+  uint32_t lb = 0, n = 0;
+  if (pe > pb) {
+    const uint32_t P = ax.par[pb];
+    lb = meta_word(o.meta, P, 0, RowT<T>::comp);
+    n = meta_word(o.meta, P, 1, RowT<T>::comp) - lb;
+  }
+  auto at = [&](uint32_t j) -> K {
+    if (T == R_TOLD) return (K)o.t_val[lb + j];
+    if (T == R_EXR) return (K)o.e_val[lb + j];
+    return ((K)o.l_r[lb + j] << 32) | o.l_b[lb + j];
+  };
+  // the list entries: rank in P's row, dropped when P's row holds them
+  uint32_t rank = 0;
+  bool kept = false;
+  if (lane() < s) {
+    uint32_t lo = 0, hi = n;
+    while (lo < hi) {
+      const uint32_t mid = (lo + hi) >> 1;
+      if (at(mid) < sv)
+        lo = mid + 1;
+      else
+        hi = mid;
+    }
+    rank = lo;
+    kept = !(lo < n && at(lo) == sv);
+  }
+  const unsigned long long km = __ballot(kept);
+  const uint32_t nk = (uint32_t)__popcll(km), nout = n + nk;
+  const uint32_t cap = T == R_TOLD ? o.t_cap : T == R_EXR ? o.e_cap : o.l_cap;
+  uint32_t* tail = T == R_TOLD ? &o.ctr->t_tail : T == R_EXR ? &o.ctr->e_tail : &o.ctr->l_tail;
+  const uint32_t r = reserve(o, rs, T, nout, cap, tail);
+  if (r == NONE) return true;  // (overflow flagged: the build is redone larger)
+  auto put = [&](uint32_t i, K v) {
+    if (T == R_TOLD) {
+      o.t_val[r + i] = (uint32_t)v;
+    } else if (T == R_EXR) {
+      o.e_val[r + i] = (uint32_t)v;
+    } else {
+      o.l_r[r + i] = (uint32_t)((unsigned long long)v >> 32);
+      o.l_b[r + i] = (uint32_t)v;
+    }
+  };
+  if (kept) put(rank + (uint32_t)__popcll(km & ((1ull << lane()) - 1ull)), sv);
+  for (uint32_t j0 = 0; j0 < n; j0 += 64) {  // (wave-uniform)
+    const uint32_t j = j0 + lane();
+    K v = 0;
+    if (j < n) v = at(j);
+    uint32_t below = 0;  // kept list entries below v
+    for (unsigned long long m = km; m;) {
+      const uint32_t i = (uint32_t)__ffsll((long long)m) - 1u;
+      m &= m - 1ull;
+      below += __shfl(sv, (int)i) < v ? 1u : 0u;
+    }
+    if (j < n) put(j + below, v);
+  }
+  if (lane() == 0) {
+    reinterpret_cast<uint32_t*>(o.meta + 2 * A)[RowT<T>::comp] = r;
+    reinterpret_cast<uint32_t*>(o.meta + 2 * A + 1)[RowT<T>::comp] = r + nout;
+  }
+  return true;
+}
+
 // Row type T of concept A (a wave; A wave-uniform): gather, sort, drop duplicates (and A itself
 // from told*: a told cycle would put it there), append, record the range.  RELAX: a row is only
 // appended when it grew; its range goes to meta2 (committed after the round).  Returns whether
@@ -359,6 +447,7 @@ template <uint32_t T, bool RELAX>
 __device__ bool task(const Axioms& ax, const Out& o, uint32_t A, uint32_t* lbuf, Rsv& rs) {
   using K = typename RowT<T>::K;
   const uint32_t pb = ax.par_ptr[A], pe = ax.par_ptr[A + 1];
+  if (!RELAX && pe - pb <= 1 && task_merge1<T>(ax, o, A, pb, pe, rs)) return true;
   unsigned long long raw = 0;
   for (uint32_t q = pb + lane(); q < pe; q += 64) {
     const uint32_t p = ax.par[q];
