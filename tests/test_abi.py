@@ -99,3 +99,26 @@ def test_no_oracle_in_product():
                 src = open(os.path.join(dirpath, f), encoding="utf-8").read()
                 for bad in ('#include "el_oracle', "libel_oracle", "import oracle", "from oracle"):
                     assert bad not in src, (f, bad)
+
+
+def test_stream_run_decode():
+    """The streamed result's row-run encoding (el_stream: values + (x, end) runs) decodes to the
+    per-entry rows; a run table that does not end at the entry count is refused."""
+    import numpy as np
+    from distel_amd import engine
+    s = engine.Stream()
+    s.s_b = np.array([5, 7, 9, 1, 2, 3, 4], np.uint32)
+    s.s_run = np.array([[10, 2], [11, 3], [10, 7]], np.uint32)  # x = 10, 10, 11, 10, 10, 10, 10
+    s.n_facts, s.n_s_runs = 7, 3
+    x, b = s.fact_rows()
+    assert x.tolist() == [10, 10, 11, 10, 10, 10, 10] and b.tolist() == [5, 7, 9, 1, 2, 3, 4]
+    fx, fb = s.facts()
+    assert fx.tolist() == [10] * 6 + [11] and fb.tolist() == [1, 2, 3, 4, 5, 7, 9]
+    s.s_run = np.array([[10, 2], [11, 6]], np.uint32)
+    s.n_s_runs = 2
+    with pytest.raises(AssertionError):
+        s.fact_rows()
+    empty = engine.Stream()
+    empty.s_b, empty.s_run = np.zeros(0, np.uint32), np.zeros((0, 2), np.uint32)
+    x, b = empty.fact_rows()
+    assert len(x) == 0 and len(b) == 0
