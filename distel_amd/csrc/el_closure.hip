@@ -439,6 +439,136 @@ __device__ bool task_merge1(const Axioms& ax, const Out& o, uint32_t A, uint32_t
   return true;
 }
 
+// Two told supers P1, P2: the row is the union of their rows (sorted, unique) and a short sorted
+// list ({P1, P2} for told*, A's own axioms for exr* / exl*), found by ranks instead of a sort.  An
+// entry's place in the row is the number of distinct values below it: those of P1's row, those of
+// P2's row not in P1's (a prefix count over P2's row, in the wave's LDS), and the list entries in
+// neither row below it.  An entry of P2's row or of the list that an earlier source holds drops
+// out.  Returns false (the caller sorts) when the list has more than 64 entries or P2's row does
+// not fit the LDS prefix.
+template <uint32_t T>
+__device__ bool task_merge2(const Axioms& ax, const Out& o, uint32_t A, uint32_t pb, uint32_t* lbuf, Rsv& rs) {
+  using K = typename RowT<T>::K;
+  const uint32_t P1 = ax.par[pb], P2 = ax.par[pb + 1];
+  const uint32_t b1 = meta_word(o.meta, P1, 0, RowT<T>::comp), n1 = meta_word(o.meta, P1, 1, RowT<T>::comp) - b1;
+  const uint32_t b2 = meta_word(o.meta, P2, 0, RowT<T>::comp), n2 = meta_word(o.meta, P2, 1, RowT<T>::comp) - b2;
+  if (n2 + 1 > CAPW) return false;
+  uint32_t s = 0;
+  K sv = 0;
+  if (T == R_TOLD) {
+    s = 2;
+    if (lane() < 2) sv = (K)(lane() ? P2 : P1);  // (par is sorted: P1 < P2)
+  } else if (T == R_EXR) {
+    const uint32_t b0 = ax.xr_ptr[A];
+    s = ax.xr_ptr[A + 1] - b0;
+    if (s > 64) return false;
+    if (lane() < s) sv = (K)ax.xr[b0 + lane()];
+  } else {
+    const uint32_t b0 = ax.xl_ptr[A];
+    s = ax.xl_ptr[A + 1] - b0;
+    if (s > 64) return false;
+    if (lane() < s) sv = ((K)ax.xl_r[b0 + lane()] << 32) | ax.xl_b[b0 + lane()];
+  }
+  auto at = [&](uint32_t b, uint32_t j) -> K {
+    if (T == R_TOLD) return (K)o.t_val[b + j];
+    if (T == R_EXR) return (K)o.e_val[b + j];
+    return ((K)o.l_r[b + j] << 32) | o.l_b[b + j];
+  };
+  auto lower = [&](uint32_t b, uint32_t n, K v) {  // entries of row [b, b + n) below v
+    uint32_t lo = 0, hi = n;
+    while (lo < hi) {
+      const uint32_t mid = (lo + hi) >> 1;
+      if (at(b, mid) < v)
+        lo = mid + 1;
+      else
+        hi = mid;
+    }
+    return lo;
+  };
+  // P2's row: which entries P1's row holds; pre[j] = entries of P2's row before j it does not
+  uint32_t* pre = lbuf;
+  uint32_t run = 0;
+  for (uint32_t j0 = 0; j0 < n2; j0 += 64) {  // (wave-uniform)
+    const uint32_t j = j0 + lane();
+    bool fresh = false;
+    if (j < n2) {
+      const K v = at(b2, j);
+      const uint32_t r = lower(b1, n1, v);
+      fresh = !(r < n1 && at(b1, r) == v);
+    }
+    const unsigned long long m = __ballot(fresh);
+    if (j < n2) pre[j] = run + (uint32_t)__popcll(m & ((1ull << lane()) - 1ull));
+    run += (uint32_t)__popcll(m);
+  }
+  if (lane() == 0) pre[n2] = run;
+  Lds::sync();
+  // the list entries in neither row
+  uint32_t r1 = 0, r2 = 0;
+  bool kept = false;
+  if (lane() < s) {
+    r1 = lower(b1, n1, sv);
+    r2 = lower(b2, n2, sv);
+    kept = !(r1 < n1 && at(b1, r1) == sv) && !(r2 < n2 && at(b2, r2) == sv);
+  }
+  const unsigned long long km = __ballot(kept);
+  const uint32_t nout = n1 + run + (uint32_t)__popcll(km);
+  const uint32_t cap = T == R_TOLD ? o.t_cap : T == R_EXR ? o.e_cap : o.l_cap;
+  uint32_t* tail = T == R_TOLD ? &o.ctr->t_tail : T == R_EXR ? &o.ctr->e_tail : &o.ctr->l_tail;
+  const uint32_t r = reserve(o, rs, T, nout, cap, tail);
+  if (r != NONE) {
+    auto put = [&](uint32_t i, K v) {
+      if (T == R_TOLD) {
+        o.t_val[r + i] = (uint32_t)v;
+      } else if (T == R_EXR) {
+        o.e_val[r + i] = (uint32_t)v;
+      } else {
+        o.l_r[r + i] = (uint32_t)((unsigned long long)v >> 32);
+        o.l_b[r + i] = (uint32_t)v;
+      }
+    };
+    auto list_below = [&](K v) {  // kept list entries below v
+      uint32_t c = 0;
+      for (unsigned long long m = km; m;) {
+        const uint32_t i = (uint32_t)__ffsll((long long)m) - 1u;
+        m &= m - 1ull;
+        c += __shfl(sv, (int)i) < v ? 1u : 0u;
+      }
+      return c;
+    };
+    if (kept) put(r1 + pre[r2] + (uint32_t)__popcll(km & ((1ull << lane()) - 1ull)), sv);
+    for (uint32_t j0 = 0; j0 < n1; j0 += 64) {  // P1's row (wave-uniform)
+      const uint32_t j = j0 + lane();
+      K v = 0;
+      uint32_t q = 0;
+      if (j < n1) {
+        v = at(b1, j);
+        q = pre[lower(b2, n2, v)];
+      }
+      const uint32_t lb = list_below(v);
+      if (j < n1) put(j + q + lb, v);
+    }
+    for (uint32_t j0 = 0; j0 < n2; j0 += 64) {  // P2's row: the entries P1's row does not hold
+      const uint32_t j = j0 + lane();
+      K v = 0;
+      bool fresh = false;
+      uint32_t q = 0;
+      if (j < n2) {
+        v = at(b2, j);
+        fresh = pre[j + 1] != pre[j];
+        if (fresh) q = lower(b1, n1, v);
+      }
+      const uint32_t lb = list_below(v);
+      if (fresh) put(q + pre[j] + lb, v);
+    }
+    if (lane() == 0) {
+      reinterpret_cast<uint32_t*>(o.meta + 2 * A)[RowT<T>::comp] = r;
+      reinterpret_cast<uint32_t*>(o.meta + 2 * A + 1)[RowT<T>::comp] = r + nout;
+    }
+  }
+  Lds::sync();  // (lbuf is reused by the wave's next task)
+  return true;
+}
+
 // Row type T of concept A (a wave; A wave-uniform): gather, sort, drop duplicates (and A itself
 // from told*: a told cycle would put it there), append, record the range.  RELAX: a row is only
 // appended when it grew; its range goes to meta2 (committed after the round).  Returns whether
@@ -448,6 +578,7 @@ __device__ bool task(const Axioms& ax, const Out& o, uint32_t A, uint32_t* lbuf,
   using K = typename RowT<T>::K;
   const uint32_t pb = ax.par_ptr[A], pe = ax.par_ptr[A + 1];
   if (!RELAX && pe - pb <= 1 && task_merge1<T>(ax, o, A, pb, pe, rs)) return true;
+  if (!RELAX && pe - pb == 2 && task_merge2<T>(ax, o, A, pb, lbuf, rs)) return true;
   unsigned long long raw = 0;
   for (uint32_t q = pb + lane(); q < pe; q += 64) {
     const uint32_t p = ax.par[q];
