@@ -142,3 +142,55 @@ def test_g4_shape_eight_partitions(name, oracle_lib):
     assert sum(s["derived"] for s in st) == o.stats()["derived"]
     assert len({s["supersteps"] for s in st}) == 1
     _close(engs)
+
+
+def test_partitioned_stream_result(oracle_lib):
+    """Every rank of a row partition streams its own rows while the collective supersteps run
+    (el_stream_result with release, as bench.py's exchange leg does); the union of the streamed
+    rows is the oracle's closure."""
+    import threading
+    ax = generators.workload("g3", scale=0.02)
+    parts = 3
+    group = engine.LocalGroup(parts)
+    engs = [engine.Engine(device=0, partition=engine.Partition(q, parts, engine.XCHG_LOCAL, group=group))
+            for q in range(parts)]
+    for e in engs:
+        e.load(ax)
+    strms = [engine.Stream() for _ in range(parts)]
+    errs = []
+
+    def run(q):
+        try:
+            engs[q].init()
+            engs[q].stream_result(strms[q], release=True)
+            engs[q].saturate()
+            engs[q].result_wait()
+        except BaseException as exc:  # noqa: BLE001 — re-raised below
+            errs.append(exc)
+            group_fail = getattr(group, "fail", None)
+            if group_fail:
+                group_fail()
+    ts = [threading.Thread(target=run, args=(q,)) for q in range(parts)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(timeout=300)
+    assert not errs, errs
+    fx = np.concatenate([s.facts(ax.n_concepts)[0] for s in strms])
+    fa = np.concatenate([s.facts(ax.n_concepts)[1] for s in strms])
+    o = np.lexsort((fa, fx))
+    orc = oracle_lib.saturate(ax, 0)
+    ox, oa = orc.facts()
+    assert np.array_equal(fx[o], ox) and np.array_equal(fa[o], oa), "streamed S(X) differs from the oracle"
+    lx, lr, ly = [], [], []
+    for e, s in zip(engs, strms):
+        x, p = s.link_rows()
+        role, filler = e.pid_table()
+        keep = x < ax.n_concepts
+        lx.append(x[keep]), lr.append(role[p[keep]]), ly.append(filler[p[keep]])
+    lx, lr, ly = (np.concatenate(v) for v in (lx, lr, ly))
+    o = np.lexsort((ly, lr, lx))
+    for g, c in zip((lx[o], lr[o], ly[o]), orc.links()):
+        assert np.array_equal(g, c), "streamed R(r) differs from the oracle"
+    _close(engs)
+    group.close()
