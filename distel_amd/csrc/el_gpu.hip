@@ -2464,6 +2464,7 @@ struct el_ctx {
   uint64_t xcap = 0;                              // records per rank per exchange (grows on overflow)
   uint64_t xrounds_bytes = 0;                     // bytes all-gathered (received) since el_init
   bool part() const { return xmode != EL_XCHG_NONE; }
+  bool part_fixpoint = false;  // partitioned: the last el_saturate reached the global fixpoint (el_init clears)
   bool bits_logged = false;
   bool trace_cands = getenv("EL_TRACE_CANDS") != nullptr;  // every set bit of the matrix is in the fact log (not after el_load)
 
@@ -2637,7 +2638,6 @@ struct el_ctx {
   void wait_copy() {
     if (!copy_pending) return;
     for (hipEvent_t e : ev_copied) HIPCHK(hipEventSynchronize(e));
-    if (sdma) sdma->wait();
     copy_pending = false;
   }
   // Streamed result (el_stream_result): the committed segments of the fact and link logs cross
@@ -2647,9 +2647,8 @@ struct el_ctx {
   el_stream* strm = nullptr;      // armed for the next el_saturate
   uint64_t strm_s = 0, strm_l = 0;  // log entries already enqueued
   bool strm_ovf = false;          // a buffer was too small (el_result_wait: EL_ERANGE)
-  hipEvent_t ev_strm = nullptr;   // (release to system scope: an SDMA copy reads behind it)
+  hipEvent_t ev_strm = nullptr;   // recorded right behind a superstep's commit
   bool strm_marked = false;       // ev_strm was recorded right behind this step's commit
-  std::unique_ptr<elst::Sdma> sdma;  // the stream's copies on a DMA engine (null / !ok: hipMemcpyAsync)
   hipStream_t nstream = nullptr;  // run encoding (never queued behind the DMAs)
   uint2 *s_run_dev = nullptr, *l_run_dev = nullptr;  // device addresses of the caller's run buffers
   uint32_t *s_b_dev = nullptr, *l_p_dev = nullptr;     // ... and of its value buffers (null: pageable)
@@ -3143,6 +3142,7 @@ void el_ctx::reset_state() {
   bits_logged = true;  // from here on every set bit is in the fact log (the init facts and k_commit append)
   uc_s_n = uc_l_n = ~0ull;
   s_count = l_count = a_count = p_count = s_init = x_count = 0;
+  part_fixpoint = false;
   if (base_filling) HIPCHK(hipStreamWaitEvent(stream, ev_base[1], 0));  // (an interrupted saturation)
   base_filling = false;
   l_base = p_base = 0;
@@ -4238,18 +4238,14 @@ void el_ctx::stream_flush() {
   if (!strm || !mark_pending) return;
   mark_pending = false;
   const uint64_t s1 = mark_s, l1 = mark_l;
-  const bool dma_engine = sdma && sdma->ok();
-  if (dma_engine) HIPCHK(hipEventSynchronize(ev_strm));  // (an SDMA copy carries no dependency)
   HIPCHK(hipStreamWaitEvent(dstream, ev_strm, 0));
   HIPCHK(hipStreamWaitEvent(nstream, ev_strm, 0));
   // the values by hipMemcpyAsync on dstream (NoCU: the copy-engine request for page-locked
-  // buffers the device has mapped) or, with EL_SDMA=1, through HSA on an SDMA engine
+  // buffers the device has mapped)
   auto dma = [&](uint32_t* dst, uint32_t* dst_dev, const uint32_t* src, uint64_t a, uint64_t b, uint64_t cap) {
     b = std::min(b, cap);
     if (!dst || b <= a) return;
-    if (dma_engine)
-      sdma->copy(dst + a, src + a, (b - a) * sizeof(uint32_t));
-    else if (dst_dev)
+    if (dst_dev)
       HIPCHK(hipMemcpyAsync(dst_dev + a, src + a, (b - a) * sizeof(uint32_t), hipMemcpyDeviceToDeviceNoCU, dstream));
     else
       HIPCHK(hipMemcpyAsync(dst + a, src + a, (b - a) * sizeof(uint32_t), hipMemcpyDeviceToHost, dstream));
@@ -4289,14 +4285,10 @@ void el_ctx::runs_out(bool wait) {
   const uint64_t caps[2] = {strm->s_run_cap, strm->l_run_cap};
   uint2* devs[2] = {s_run_dev, l_run_dev};
   const uint2* srcs[2] = {srun, lrun};
-  uint2* hosts[2] = {reinterpret_cast<uint2*>(strm->s_run), reinterpret_cast<uint2*>(strm->l_run)};
   for (int w = 0; w < 2; ++w) {
     const uint64_t n = std::min<uint64_t>(rtot_h[w], caps[w]);
     if (!devs[w] || n <= run_sent[w]) continue;
-    if (sdma && sdma->ok())
-      sdma->copy(hosts[w] + run_sent[w], srcs[w] + run_sent[w], (n - run_sent[w]) * sizeof(uint2));
-    else
-      HIPCHK(hipMemcpyAsync(devs[w] + run_sent[w], srcs[w] + run_sent[w], (n - run_sent[w]) * sizeof(uint2),
+    HIPCHK(hipMemcpyAsync(devs[w] + run_sent[w], srcs[w] + run_sent[w], (n - run_sent[w]) * sizeof(uint2),
                             hipMemcpyDeviceToDeviceNoCU, dstream));
     run_sent[w] = n;
   }
@@ -4813,7 +4805,10 @@ int el_saturate(el_ctx* c, el_stats* stats) {
     c->tr_s.clear();
     c->tr_l.clear();
     c->tr_a.clear();
-    if (c->part()) {  // collective: every rank runs the same supersteps (global delta)
+    // A partitioned context at its global fixpoint (an el_saturate that returned since the last
+    // el_init: a re-stream into fitted buffers after EL_ERANGE, which one rank may do alone) runs
+    // no collective superstep: its peers have left the exchange.
+    if (c->part() && !c->part_fixpoint) {  // collective: every rank runs the same supersteps (global delta)
       constexpr uint32_t mask = (M_ALL & ~M_R4D) | M_R4P;
       uint64_t xb = 0;
       for (int r = 0; r < EL_NUM_RULE_TYPES; ++r) pb = std::min(pb, c->wm_p[r]);
@@ -4829,6 +4824,7 @@ int el_saturate(el_ctx* c, el_stats* stats) {
         if (g == 0) break;
       }
       c->wm_x = c->x_count;
+      c->part_fixpoint = true;
     }
     for (;;) {
       if (c->part()) break;
@@ -5156,9 +5152,6 @@ int el_stream_result(el_ctx* c, el_stream* s) {
     c->l_run_dev = reinterpret_cast<uint2*>(mapped_for_device(s->l_run));
     c->s_b_dev = mapped_for_device(s->s_b);
     c->l_p_dev = mapped_for_device(s->l_p);
-    // EL_SDMA=1: the copies through HSA on an SDMA engine (A/B: G3 27.37 vs 27.56 ms, within noise;
-    // and a rocprofv3-traced run of it stalled), default the runtime's copies
-    if (!c->sdma && getenv("EL_SDMA") && !strcmp(getenv("EL_SDMA"), "1")) c->sdma.reset(new elst::Sdma(c->device));
     if ((s->s_run && !c->s_run_dev) || (s->l_run && !c->l_run_dev))
       return fail(c, EL_EINVAL, "el_stream run buffers must be page-locked host memory (el_host_alloc)");
     if (!c->rbase) {
@@ -5303,19 +5296,12 @@ void el_destroy(el_ctx* c) {
   if (c->dstream) (void)hipStreamSynchronize(c->dstream);  // (an async copy-back's last DMAs)
   if (c->nstream) (void)hipStreamSynchronize(c->nstream);
   if (c->ostream) (void)hipStreamSynchronize(c->ostream);
-  if (c->sdma) {
-    try {
-      c->sdma->wait();  // (an SDMA copy still reading the logs)
-    } catch (...) {
-    }
-  }
   c->copy_pending = false;
   c->free_state();
   c->free_index();
   dfree(c->rcnt);
   dfree(c->roff);
   dfree(c->rscan_tmp);
-  c->sdma.reset();
   dfree(c->rbase);
   dfree(c->srun);
   dfree(c->lrun);

@@ -30,30 +30,4 @@ void count(hipStream_t s, const uint32_t* keys, uint64_t a, uint64_t b, uint32_t
 void emit(hipStream_t s, const uint32_t* keys, uint64_t a, uint64_t b, const uint32_t* off, const uint32_t* cnt,
           uint2* out, uint64_t cap, unsigned long long* base, unsigned long long* total);
 
-// Device-to-host copies on an SDMA engine, issued through the HSA runtime.  hipMemcpyAsync into
-// page-locked memory that the device has mapped is a device-to-device copy to the HIP runtime,
-// which it runs as a blit kernel on the CUs (beside the saturation: the copies of a G3
-// classification took 13 ms of CU time and slowed the supersteps they overlapped).  Here the
-// copy goes to a DMA engine with force_copy_on_sdma.  The caller makes sure the source is final
-// and visible (a host-completed event recorded with hipEventReleaseToSystem), so no copy has a
-// device-side dependency.  ok() is false when HSA offers no SDMA path (the caller falls back to
-// hipMemcpyAsync).
-class Sdma {
- public:
-  explicit Sdma(int hip_device);
-  ~Sdma();
-  Sdma(const Sdma&) = delete;
-  Sdma& operator=(const Sdma&) = delete;
-  bool ok() const { return ok_; }
-  void copy(void* dst_host, const void* src_dev, size_t bytes);  // asynchronous
-  void wait();                                                    // every copy issued so far
-  bool idle() const { return pending_n_ == 0; }
-
- private:
-  struct Impl;
-  Impl* impl_ = nullptr;
-  bool ok_ = false;
-  size_t pending_n_ = 0;
-};
-
 }  // namespace elst

@@ -1,8 +1,6 @@
 // el_stream.hip — run encoding of the streamed result's log segments (el_stream.h).
 #include "el_stream.h"
 
-#include <hsa/hsa.h>
-#include <hsa/hsa_ext_amd.h>
 
 #include <stdexcept>
 #include <string>
@@ -112,106 +110,6 @@ void emit(hipStream_t s, const uint32_t* keys, uint64_t a, uint64_t b, const uin
   SCHK(hipGetLastError());
   hipLaunchKernelGGL(k_run_advance, dim3(1), dim3(1), 0, s, base, off, cnt, nt - 1, total);
   SCHK(hipGetLastError());
-}
-
-// ---- SDMA copies through HSA
-
-struct Sdma::Impl {
-  hsa_agent_t gpu{}, cpu{};
-  uint32_t engine = 0;  // an HSA_AMD_SDMA_ENGINE_* bit
-  std::vector<hsa_signal_t> pool, pending;
-  bool hsa_up = false;
-};
-
-namespace {
-struct Found {
-  uint32_t domain = 0, bdf = 0;
-  bool have_gpu = false, have_cpu = false;
-  hsa_agent_t gpu{}, cpu{};
-};
-hsa_status_t find_agents(hsa_agent_t a, void* data) {
-  Found* f = static_cast<Found*>(data);
-  hsa_device_type_t t;
-  if (hsa_agent_get_info(a, HSA_AGENT_INFO_DEVICE, &t) != HSA_STATUS_SUCCESS) return HSA_STATUS_SUCCESS;
-  if (t == HSA_DEVICE_TYPE_CPU && !f->have_cpu) {
-    f->cpu = a;
-    f->have_cpu = true;
-  } else if (t == HSA_DEVICE_TYPE_GPU && !f->have_gpu) {
-    uint32_t bdf = 0, dom = 0;
-    if (hsa_agent_get_info(a, (hsa_agent_info_t)HSA_AMD_AGENT_INFO_BDFID, &bdf) == HSA_STATUS_SUCCESS &&
-        hsa_agent_get_info(a, (hsa_agent_info_t)HSA_AMD_AGENT_INFO_DOMAIN, &dom) == HSA_STATUS_SUCCESS &&
-        bdf == f->bdf && dom == f->domain) {
-      f->gpu = a;
-      f->have_gpu = true;
-    }
-  }
-  return HSA_STATUS_SUCCESS;
-}
-}  // namespace
-
-Sdma::Sdma(int hip_device) : impl_(new Impl) {
-  int bus = 0, dev = 0, dom = 0;
-  if (hipDeviceGetAttribute(&bus, hipDeviceAttributePciBusId, hip_device) != hipSuccess ||
-      hipDeviceGetAttribute(&dev, hipDeviceAttributePciDeviceId, hip_device) != hipSuccess ||
-      hipDeviceGetAttribute(&dom, hipDeviceAttributePciDomainID, hip_device) != hipSuccess) {
-    (void)hipGetLastError();
-    return;
-  }
-  if (hsa_init() != HSA_STATUS_SUCCESS) return;  // (reference-counted: HIP initialised it already)
-  impl_->hsa_up = true;
-  Found f;
-  f.domain = (uint32_t)dom;
-  f.bdf = ((uint32_t)bus << 8) | ((uint32_t)dev << 3);  // function 0
-  if (hsa_iterate_agents(find_agents, &f) != HSA_STATUS_SUCCESS || !f.have_gpu || !f.have_cpu) return;
-  impl_->gpu = f.gpu;
-  impl_->cpu = f.cpu;
-  uint32_t mask = 0;
-  if (hsa_amd_memory_get_preferred_copy_engine(f.cpu, f.gpu, &mask) != HSA_STATUS_SUCCESS || mask == 0)
-    if (hsa_amd_memory_copy_engine_status(f.cpu, f.gpu, &mask) != HSA_STATUS_SUCCESS) mask = 0;
-  if (mask == 0) return;
-  impl_->engine = mask & (~mask + 1u);  // the lowest engine offered
-  ok_ = true;
-}
-
-Sdma::~Sdma() {
-  if (!impl_) return;
-  try {
-    wait();
-  } catch (...) {
-  }
-  for (hsa_signal_t s : impl_->pool) (void)hsa_signal_destroy(s);
-  if (impl_->hsa_up) (void)hsa_shut_down();
-  delete impl_;
-}
-
-void Sdma::copy(void* dst_host, const void* src_dev, size_t bytes) {
-  if (!bytes) return;
-  hsa_signal_t sig;
-  if (!impl_->pool.empty()) {
-    sig = impl_->pool.back();
-    impl_->pool.pop_back();
-    hsa_signal_store_screlease(sig, 1);
-  } else if (hsa_signal_create(1, 0, nullptr, &sig) != HSA_STATUS_SUCCESS) {
-    throw std::runtime_error("hsa_signal_create failed");
-  }
-  const hsa_status_t st = hsa_amd_memory_async_copy_on_engine(
-      dst_host, impl_->cpu, src_dev, impl_->gpu, bytes, 0, nullptr, sig, (hsa_amd_sdma_engine_id_t)impl_->engine, true);
-  if (st != HSA_STATUS_SUCCESS) {
-    impl_->pool.push_back(sig);
-    throw std::runtime_error("hsa_amd_memory_async_copy_on_engine failed (" + std::to_string((int)st) + ")");
-  }
-  impl_->pending.push_back(sig);
-  pending_n_ = impl_->pending.size();
-}
-
-void Sdma::wait() {
-  for (hsa_signal_t s : impl_->pending) {
-    while (hsa_signal_wait_scacquire(s, HSA_SIGNAL_CONDITION_LT, 1, UINT64_MAX, HSA_WAIT_STATE_BLOCKED) >= 1) {
-    }
-    impl_->pool.push_back(s);
-  }
-  impl_->pending.clear();
-  pending_n_ = 0;
 }
 
 }  // namespace elst

@@ -285,10 +285,15 @@ class Stream:
     @staticmethod
     def _rows(runs: np.ndarray, n_runs: int, n: int) -> np.ndarray:
         """Per-entry x from the runs (x, end)."""
+        if n_runs == 0:
+            if n:
+                raise ValueError(f"malformed runs: {n} entries but no run")
+            return np.zeros(0, np.uint32)
         r = runs[:n_runs]
         ends = r[:, 1].astype(np.int64)
         lens = np.diff(np.concatenate(([0], ends)))
-        assert n_runs == 0 or (ends[-1] == n and (lens > 0).all()), "malformed runs"
+        if ends[-1] != n or not (lens > 0).all():
+            raise ValueError("malformed runs: the run ends do not cover the entries in ascending order")
         return np.repeat(r[:, 0], lens)
 
     def fact_rows(self) -> Tuple[np.ndarray, np.ndarray]:
@@ -307,6 +312,19 @@ class Stream:
             x, a = x[keep], a[keep]
         o = np.lexsort((a, x))
         return x[o], a[o]
+
+    def digest(self, pid_role: np.ndarray, pid_filler: np.ndarray, n_user: int) -> str:
+        """Order-independent digest (distel_amd.result.set_digest) of the streamed closure over
+        the caller's rows (< n_user): decoded from the runs and hashed per entry, no sort."""
+        from .result import set_digest
+        x, b = self.fact_rows()
+        lx, lp = self.link_rows()
+        if n_user is not None:
+            k = x < n_user
+            x, b = x[k], b[k]
+            k = lx < n_user
+            lx, lp = lx[k], lp[k]
+        return set_digest(x, b, lx, pid_role[lp], pid_filler[lp])
 
 
 class Stats(dict):
@@ -421,9 +439,11 @@ class Engine:
         self._stream: Optional[Stream] = None  # a streamed result armed for the next saturate()
 
     def _check(self, rc: int, what: str) -> None:
+        cause = None
+        if self.partition is not None:  # the transport's exception of THIS call, if any
+            cause, self.partition.error = self.partition.error, None
         if rc != EL_OK:
             msg = self._lib.el_last_error(self._ctx)
-            cause = self.partition.error if self.partition is not None else None
             raise ElError(rc, f"{what}: {msg.decode() if msg else ''}") from cause
 
     def close(self) -> None:

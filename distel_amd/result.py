@@ -176,3 +176,30 @@ def diff_results(expected: Dict[str, set], got: Dict[str, set], bottom: Optional
                           "".join(f"\n\t -- {b}" for b in extra))
     report.append(f"No of classes not equal: {misses}")
     return misses, report
+
+
+def _mix64(k: np.ndarray) -> np.ndarray:
+    """splitmix64 finaliser over a uint64 array (wrapping arithmetic)."""
+    k = k ^ (k >> np.uint64(33))
+    k = k * np.uint64(0xFF51AFD7ED558CCD)
+    k = k ^ (k >> np.uint64(33))
+    k = k * np.uint64(0xC4CEB9FE1A85EC53)
+    return k ^ (k >> np.uint64(33))
+
+
+def set_digest(fx: np.ndarray, fa: np.ndarray, lx: np.ndarray, lr: np.ndarray, ly: np.ndarray) -> str:
+    """Order-independent digest of a closure: the S facts (x, a) and the links (x, r, y) as sets.
+    Each entry is hashed on its own (two independent 64-bit mixes) and the hashes are summed mod
+    2^64, so the facts and links may come in any order (a streamed result's commit order, several
+    partitions' rows) and nothing is sorted: O(entries), vectorised.  Duplicates are not removed
+    (a closure has none).  Returns "<n_facts>:<n_links>:<16 hex digits> x 4"."""
+    with np.errstate(over="ignore"):
+        kf = (fx.astype(np.uint64) << np.uint64(32)) | fa.astype(np.uint64)
+        kl = (lx.astype(np.uint64) << np.uint64(32)) | ly.astype(np.uint64)
+        kl = _mix64(kl) ^ (lr.astype(np.uint64) * np.uint64(0x9E3779B97F4A7C15))
+        parts = []
+        for k, salt in ((kf, 0x243F6A8885A308D3), (kl, 0x13198A2E03707344)):
+            for s2 in (0, 0xA4093822299F31D0):
+                h = _mix64(k ^ np.uint64(salt ^ s2))
+                parts.append(int(h.sum(dtype=np.uint64)))
+    return f"{fx.size}:{lx.size}:" + "".join(f"{p:016x}" for p in parts)

@@ -341,7 +341,8 @@ typedef struct el_result {
  * el_result_wait returns (every other call on the context waits for them first).  A buffer
  * smaller than its part: what fits arrives, el_result_wait returns EL_ERANGE and the state is
  * kept (not released): arm again with buffers of the n_* counts and call el_saturate, which at
- * the fixpoint runs no superstep and streams the whole logs.  flags EL_RESULT_RELEASE: the state
+ * the fixpoint runs no superstep and streams the whole logs (a row partition too: that call is
+ * not collective, so one rank may re-stream alone).  flags EL_RESULT_RELEASE: the state
  * is released behind the saturation (no state until el_init), as for el_copy_result. */
 typedef struct el_stream {
   uint32_t flags;           /* in: EL_RESULT_* (RELEASE) */

@@ -81,3 +81,50 @@ def test_cli_normalize(tmp_path):
     a = owl.to_axioms(n)                               # already normal: types without normalizing
     b = owl.to_axioms(owl.normalize(owl.parse_functional(open(src).read())))
     assert a.counts() == b.counts()
+
+
+def test_set_digest_order_independent_and_pinned(oracle_lib):
+    """set_digest ignores order, sees every entry, and reproduces the pinned set digest of a
+    pinned workload from the oracle's closure (tests/golden/set_digests.txt)."""
+    from distel_amd import generators
+    rng = np.random.default_rng(7)
+    fx, fa = rng.integers(0, 1000, 500).astype(np.uint32), rng.integers(0, 1000, 500).astype(np.uint32)
+    lx, lr, ly = (rng.integers(0, 50, 300).astype(np.uint32) for _ in range(3))
+    d = result.set_digest(fx, fa, lx, lr, ly)
+    p, q = rng.permutation(500), rng.permutation(300)
+    assert result.set_digest(fx[p], fa[p], lx[q], lr[q], ly[q]) == d
+    fa2 = fa.copy()
+    fa2[17] ^= 1
+    assert result.set_digest(fx, fa2, lx, lr, ly) != d
+    lr2 = lr.copy()
+    lr2[3] += 1
+    assert result.set_digest(fx, fa, lx, lr2, ly) != d
+    pins = {}
+    for line in open(os.path.join(os.path.dirname(__file__), "golden", "set_digests.txt")):
+        f = line.split()
+        if len(f) == 4 and not line.startswith("#"):
+            pins[(f[0], float(f[1]))] = (f[2], f[3])
+    ax = generators.workload("g1", 0.1)
+    assert ax.digest() == pins[("g1", 0.1)][0]
+    o = oracle_lib.saturate(ax, 0)
+    assert result.set_digest(*o.facts(), *o.links()) == pins[("g1", 0.1)][1]
+
+
+def test_stream_runs_malformed_raise():
+    """A streamed result's run table that does not cover its entries is an error, not an assert
+    (python -O keeps the check)."""
+    from distel_amd.engine import Stream
+    runs = np.array([[5, 3], [6, 7]], np.uint32)
+    assert Stream._rows(runs, 2, 7).tolist() == [5, 5, 5, 6, 6, 6, 6]
+    for n_runs, n in ((2, 8), (0, 4)):
+        try:
+            Stream._rows(runs, n_runs, n)
+        except ValueError:
+            continue
+        raise AssertionError("malformed runs accepted")
+    bad = np.array([[5, 3], [6, 3]], np.uint32)
+    try:
+        Stream._rows(bad, 2, 3)
+    except ValueError:
+        return
+    raise AssertionError("empty run accepted")
