@@ -78,6 +78,16 @@ class _stdout_to_stderr:
         os.close(self.saved)
 
 
+def source_sha256() -> str:
+    """SHA-256 over the engine's sources (the kernel table and the PMC summaries name it)."""
+    import hashlib
+    h = hashlib.sha256()
+    for f in ("el_gpu.hip", "el_closure.hip", "el_rows.hip", "el_stream.hip", "el_index.cpp"):
+        with open(os.path.join(ROOT, "distel_amd", "csrc", f), "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()
+
+
 def pmc_traffic(workload: str, kernel: str):
     """HBM bytes per launch of `kernel` from the committed PMC summary of this workload
     (profiles/pmc/rNN_pmc_<workload>.json, written by scripts/pmc_summary.py from separate
@@ -393,7 +403,10 @@ def main():
                     "traffic": pmc_traffic(args.workload, dom["kernel"]),
                     "kernel": dom["kernel"], "bytes_per_launch": int(per_launch_bytes),
                     "avg_launch_us": round(avg_ms * 1e3, 3), "launches": dom["launches"],
-                    "profiled_ms": round(pst["ms"], 3)}
+                    "profiled_ms": round(pst["ms"], 3),
+                    "source": "HIP events around every launch on the engine stream of one profiled classification "
+                              "in the timed schedule; the whole table is this line's `kernels` "
+                              "(launches, ms, algorithmic bytes per kernel)"}
         kernels = {g["kernel"]: {"launches": g["launches"], "ms": round(g["ms"], 4), "bytes": g["bytes"]}
                    for g in launches.values() if g["launches"]}
 
@@ -437,8 +450,9 @@ def main():
         extra["roofline"] = roofline
         extra["cpu_baseline"] = cpu
         line = build_line(head, head_name, extra)
-        if args.verbose and kernels:
+        if kernels:  # the record roofline is computed from (HIP events, the profiled classification)
             line["kernels"] = kernels
+            line["source_sha256"] = source_sha256()
         print(json.dumps(line), flush=True)
     D.shutdown(rk)
 

@@ -20,7 +20,8 @@
 //   commit      k_commit (roles: S, links, activations, propagations) dedups the
 //               candidates against the bit rows / hash sets, appends the new ones
 //               to the logs and publishes the counters to pinned host memory;
-//   (re-layout) only when a gapped CSR row overflowed: k_gap_scan, k_gap_move_e, k_gap_ovf.
+//   (relocation) only when a gapped CSR row overflowed: k_reloc_claim / _move / _commit move
+//               that row alone to the end of the CSR's slot array.
 // Result rows (export, copy-back) are built from the logs on demand (el_rows.hip).
 // Generation never writes state, so a step can be re-run after growing a buffer,
 // and the delta of every step is exactly {candidates} \ S_{t-1}: the same sets
@@ -143,7 +144,20 @@ struct DIndex {
   // base propagations of pid: the propagation log's [bpp_s[pid], bpp_e[pid]) (B ascending)
   const uint32_t *bpp_s, *bpp_e;
   const uint8_t* role_chs;     // r -> r is the second role of some chain (its links are exchanged)
+  // partitioned: every rank's column window [x, y) (el_ctx::exchange_windows); a record keyed by
+  // concept Y is sent only when some OTHER rank's window holds Y (its rows can reach Y)
+  const uint2* xwin;
+  uint32_t nranks, me;
 };
+
+// some other rank's rows can reach concept y (⊥ and ⊤ are in every window)
+__device__ __forceinline__ bool remote(const DIndex& ix, uint32_t y) {
+  if (ix.nranks < 2) return false;
+  if (y < 2u) return true;
+  for (uint32_t q = 0; q < ix.nranks; ++q)
+    if (q != ix.me && y >= ix.xwin[q].x && y < ix.xwin[q].y) return true;
+  return false;
+}
 
 // Event counters: one partial row per block index, updated with plain read-modify-writes
 // (a block index is unique within a launch and launches on the stream do not overlap), so
@@ -158,12 +172,14 @@ constexpr size_t EV_WORDS = (EV_BLOCKS + 1) * EV_TOTAL;
 // ≈12 ns per atomic on one line).  The host copy (HCounters) is compact.
 constexpr uint32_t CTR_STRIDE = 64;  // words
 // Counters [0, CTR_KEEP) persist across steps; the rest are per-step (zeroed by k_commit).
-// x_log / x_send / g_delta / g_max belong to the partitioned exchange (k_ximport).
+// x_log / x_send / x_sp / x_sa / g_delta / g_max belong to the partitioned exchange (k_ximport):
+// x_send, x_sp, x_sa count this step's records routed to other ranks (chain links, propagations,
+// activations; k_commit appends, the import zeroes them once they went out).
 // ov_* count the entries of this step that did not fit their slack row (gapped CSRs below).
 // cand_t counts the CR1 told-closure candidates (committed first, by k_commit_told).
-#define EL_COUNTERS(X) X(s_log) X(l_log) X(a_log) X(p_log) X(x_log) X(x_send) X(ov_pr) X(ov_sc) X(ov_pp) \
+#define EL_COUNTERS(X) X(s_log) X(l_log) X(a_log) X(p_log) X(x_log) X(x_send) X(x_sp) X(x_sa) X(ov_pr) X(ov_sc) X(ov_pp) \
   X(cand_s) X(cand_l) X(cand_a) X(jobs) X(cand_p) X(cand_t) X(g_delta) X(g_max) X(g_ovf) X(ticket) X(seq)
-constexpr uint32_t CTR_KEEP = 9;
+constexpr uint32_t CTR_KEEP = 11;
 #define EL_CTR_DEV(n) uint32_t n; uint32_t n##_pad[CTR_STRIDE - 1];
 #define EL_CTR_HOST(n) uint32_t n;
 struct DCounters {
@@ -175,14 +191,17 @@ struct HCounters {  // ticket: k_gap_scan tile dispenser; seq: host copy only
 constexpr uint32_t NUM_CTRS = sizeof(HCounters) / 4;
 static_assert(sizeof(DCounters) == NUM_CTRS * CTR_STRIDE * 4, "counter layout");
 
-// Gapped ("slack") CSR: row r owns the slots [start[r], start[r+1]) and holds len[r]
-// entries.  An entry is appended where its row's keyed atomic on len places it, so a
-// superstep needs no CSR merge; an entry past its row's capacity goes to the overflow
-// queue (row, value, rank) and the host re-lays out the rows (gap_cap) before the next
-// step reads them.  Readers of step t see len at the end of step t-1 (appends happen only
-// in commit / import launches, which no reader shares).
+// Gapped ("slack") CSR: row r owns the slots [start[r], end[r]) and holds len[r] entries.
+// An entry is appended where its row's keyed atomic on len places it, so a superstep needs no
+// CSR merge; an entry past its row's capacity goes to the overflow queue (row, value, rank)
+// and the host relocates the rows that overflowed — each to gap_cap(len) fresh slots at the
+// end of the slot array, its in-place entries moved and the overflow entries placed by rank —
+// before the next step reads them; every other row stays where it is.  Readers of step t see
+// len at the end of step t-1 (appends happen only in commit / import launches, which no reader
+// shares).
 struct DGap {
-  const uint32_t* start;  // rows + 1
+  const uint32_t* start;  // rows + 1 (the initial layout's scan; start[rows] is its end)
+  const uint32_t* end;    // rows: end of row r's slots
   uint32_t* len;          // rows
   uint32_t* val;
   uint32_t* ovq;          // 3 words per overflowing entry
@@ -228,9 +247,12 @@ struct DState {
   uint32_t need_pred, need_succ;  // CSRs with readers: only those get delta counts
   uint32_t dedup;                 // in-wave S-candidate filter on (EL_DEDUP_OFF: off)
   uint32_t succ_at_commit;        // successor counts taken by k_commit (whole-ontology mode)
-  // partitioned exchange: replicated chain-second link log, local send queue, import ranks
+  // partitioned exchange: replicated chain-second link log; this step's records for other ranks:
+  // chain-second links (xs), propagations (xp), activations (xa)
   uint32_t *xlog_x, *xlog_p;
-  uint32_t *xs_x, *xs_p;
+  uint32_t *xs_x, *xs_p, xs_cap;
+  uint32_t *xp_p, *xp_b, xp_cap;
+  uint32_t *xa_y, *xa_c, xa_cap;
   uint32_t *cs_x, *cs_a, cs_cap;
   uint32_t cs_chunk;  // S-queue reservation per wave (wq_publish_s; 0: one atomic per publish)
   uint32_t *ct_x, *ct_a, ct_cap;  // CR1 told-closure candidates
@@ -361,7 +383,7 @@ __device__ __forceinline__ void gap_append(const DGap& g, uint32_t row, uint32_t
     ev[EL_EV_ROW]++;
     ev[EL_EV_ENT]++;
     const uint32_t s = g.start[row] + rank;
-    ovf = s >= g.start[row + 1];
+    ovf = s >= g.end[row];
     if (!ovf) g.val[s] = v;
   }
   const uint32_t q = wave_append(g.ov_count, ovf);
@@ -1358,10 +1380,20 @@ __device__ void commit_l(const DIndex& ix, const DState& st, CommitLds& sm, uint
     if (st.need_pred) gap_append(st.pr, p, x, nw, ev.v);
     // successor rows are read only by CR6 with the row's role second: other links stay out
     if (st.succ_at_commit) gap_append(st.sc, x, p, nw && ix.role_chs[ix.pair_role[p]], ev.v);
-    if (ix.part) {  // partitioned: a new link of a chain-second role goes to every rank
-      const bool xs = nw && ix.role_chs[ix.pair_role[p]];
+    if (ix.part) {
+      // partitioned: a new link (x, s, z) of a chain-second role joins this rank's replicated
+      // chain-link log and successor rows now (CR6 with s second, expand_x), and goes to the ranks
+      // whose rows can reach x (a link (x', r, x) of theirs) in the exchange
+      const bool ch = nw && ix.role_chs[ix.pair_role[p]];
+      const uint32_t xsl = wave_append(&st.ctr->x_log, ch);
+      if (st.need_succ) gap_append(st.sc, x, p, ch, ev.v);
+      if (ch) {
+        st.xlog_x[xsl] = x;
+        st.xlog_p[xsl] = p;
+      }
+      const bool xs = ch && remote(ix, x);
       const uint32_t slot = wave_append(&st.ctr->x_send, xs);
-      if (xs) {
+      if (xs && slot < st.xs_cap) {
         st.xs_x[slot] = x;
         st.xs_p[slot] = p;
       }
@@ -1402,6 +1434,14 @@ __device__ void commit_a(const DIndex& ix, const DState& st, uint32_t bid, uint3
       st.alog_y[slot] = y;
       st.alog_c[slot] = c;
       st.has_act[y] = 1;
+    }
+    if (ix.part) {  // to the ranks whose rows can hold y
+      const bool xs = nw && remote(ix, y);
+      const uint32_t q = wave_append(&st.ctr->x_sa, xs);
+      if (xs && q < st.xa_cap) {
+        st.xa_y[q] = y;
+        st.xa_c[q] = c;
+      }
     }
   }
   ev_flush(st.ev, EL_K_COMMIT_A, ev);
@@ -1444,6 +1484,14 @@ __device__ void commit_p(const DIndex& ix, const DState& st, uint32_t bid, uint3
       ev.v[EL_EV_EMIT]++;
       st.plog_p[slot] = pid;
       st.plog_b[slot] = b;
+    }
+    if (ix.part) {  // ((r, Y), B) to the ranks whose rows can link to Y
+      const bool xs = nw && remote(ix, ix.pair_y[pid]);
+      const uint32_t q = wave_append(&st.ctr->x_sp, xs);
+      if (xs && q < st.xp_cap) {
+        st.xp_p[q] = pid;
+        st.xp_b[q] = b;
+      }
     }
   }
   ev_flush(st.ev, EL_K_COMMIT_P, ev);
@@ -1611,24 +1659,31 @@ __global__ void k_commit(DIndex ix, DState st, CommitArgs a) {
 // ---- partitioned exchange (protocol: oracle/partition_model.py)
 // Each rank's slot of the all-gather: XH header words, then up to cap records (a, b):
 // its new propagations (pid, B), then new activations (Y, C), then new chain-second
-// links (X, pid).  Records past cap wait for a larger exchange (the host redoes it).
+// links (X, pid) — only those some other rank's rows can reach (remote(), routed by the commit).
+// Records past cap wait for a larger exchange (the host redoes it).
 constexpr uint32_t XH = 16;
-enum : uint32_t { XH_NP = 0, XH_NA = 1, XH_NX = 2, XH_DS = 3, XH_DL = 4, XH_OVF = 5 };
+// header words: records sent (NP, NA, NX); this step's local deltas — facts, links, propagations,
+// activations, chain links (DS, DL, DP, DA, DX: their sum over ranks, with the records sent, is
+// the termination test); a candidate queue overflowed (OVF: redo); a send queue overflowed (QOVF)
+enum : uint32_t { XH_NP = 0, XH_NA = 1, XH_NX = 2, XH_DS = 3, XH_DL = 4, XH_OVF = 5, XH_QOVF = 6, XH_DP = 7, XH_DA = 8,
+                  XH_DX = 9 };
 struct XchgArgs {
   uint32_t* send;        // this rank's slot: XH + 2 * cap words
   const uint32_t* recv;  // nranks slots
   uint32_t cap, nranks, me;
-  uint32_t s0, l0, a0, p0;  // log counts at the start of the attempt
+  uint32_t s0, l0, a0, p0, x0;  // log counts at the start of the attempt
   uint32_t cs_cap, cl_cap, ca_cap, cp_cap, job_cap, ct_cap;  // a candidate queue past its cap = redo
 };
-// per-step counters the import zeroes once the exchange went through: x_send, cand_*, jobs
-constexpr uint32_t XCHG_ZERO = (1u << 5) | (1u << 9) | (1u << 10) | (1u << 11) | (1u << 12) | (1u << 13) | (1u << 14);
-static_assert(offsetof(DCounters, x_send) == 5 * CTR_STRIDE * 4 && offsetof(DCounters, cand_s) == 9 * CTR_STRIDE * 4 &&
-                  offsetof(DCounters, cand_t) == 14 * CTR_STRIDE * 4,
+// per-step counters the import zeroes once the exchange went through: x_send, x_sp, x_sa,
+// cand_*, jobs
+constexpr uint32_t XCHG_ZERO = (1u << 5) | (1u << 6) | (1u << 7) | (1u << 11) | (1u << 12) | (1u << 13) | (1u << 14) |
+                               (1u << 15) | (1u << 16);
+static_assert(offsetof(DCounters, x_send) == 5 * CTR_STRIDE * 4 && offsetof(DCounters, x_sa) == 7 * CTR_STRIDE * 4 &&
+                  offsetof(DCounters, cand_s) == 11 * CTR_STRIDE * 4 && offsetof(DCounters, cand_t) == 16 * CTR_STRIDE * 4,
               "XCHG_ZERO bits");
 
 __global__ void k_xpack(DState st, XchgArgs x) {
-  const uint32_t np = st.ctr->p_log - x.p0, na = st.ctr->a_log - x.a0, nx = st.ctr->x_send;
+  const uint32_t np = st.ctr->x_sp, na = st.ctr->x_sa, nx = st.ctr->x_send;
   const uint32_t tot = np + na + nx, n = min(tot, x.cap);
   if (blockIdx.x == 0 && threadIdx.x < XH) {
     uint32_t v = 0;
@@ -1637,24 +1692,29 @@ __global__ void k_xpack(DState st, XchgArgs x) {
     if (threadIdx.x == XH_NX) v = nx;
     if (threadIdx.x == XH_DS) v = st.ctr->s_log - x.s0;
     if (threadIdx.x == XH_DL) v = st.ctr->l_log - x.l0;
+    if (threadIdx.x == XH_DP) v = st.ctr->p_log - x.p0;
+    if (threadIdx.x == XH_DA) v = st.ctr->a_log - x.a0;
+    if (threadIdx.x == XH_DX) v = st.ctr->x_log - x.x0;
     if (threadIdx.x == XH_OVF)
       v = st.ctr->cand_s > x.cs_cap || st.ctr->cand_l > x.cl_cap || st.ctr->cand_a > x.ca_cap ||
           st.ctr->cand_p > x.cp_cap || st.ctr->jobs > x.job_cap || st.ctr->cand_t > x.ct_cap;
+    if (threadIdx.x == XH_QOVF)  // a send queue lost records (sized to never do so): fatal
+      v = np > st.xp_cap || na > st.xa_cap || nx > st.xs_cap;
     x.send[threadIdx.x] = v;
   }
   uint2* rec = reinterpret_cast<uint2*>(x.send + XH);
   for (uint32_t g = blockIdx.x * blockDim.x + threadIdx.x; g < n; g += gridDim.x * blockDim.x) {
     uint2 r;
-    if (g < np) r = make_uint2(st.plog_p[x.p0 + g], st.plog_b[x.p0 + g]);
-    else if (g < np + na) r = make_uint2(st.alog_y[x.a0 + g - np], st.alog_c[x.a0 + g - np]);
+    if (g < np) r = make_uint2(st.xp_p[g], st.xp_b[g]);
+    else if (g < np + na) r = make_uint2(st.xa_y[g - np], st.xa_c[g - np]);
     else r = make_uint2(st.xs_x[g - np - na], st.xs_p[g - np - na]);
     rec[g] = r;
   }
 }
 
-// Import every rank's records: other ranks' propagations and activations into the
-// replicated sets (dedup), every rank's chain links (own included) into the replicated
-// chain-link log with their successor-CSR ranks.  If any rank's records exceeded the cap
+// Import the other ranks' records: propagations and activations into the replicated sets
+// (dedup), chain links into the replicated chain-link log and the successor rows (this rank's
+// own went there at its commit).  If any rank's records exceeded the cap
 // nothing is imported (g_max tells the host; it re-runs the exchange with a larger cap).
 // The last block publishes: g_delta = Σ over ranks of all deltas (0 = global fixpoint).
 __global__ void k_ximport(DIndex ix, DState st, XchgArgs x, PubArgs pub) {
@@ -1682,7 +1742,7 @@ __global__ void k_ximport(DIndex ix, DState st, XchgArgs x, PubArgs pub) {
     const bool live = i < total && j < np + na + nx;
     const bool is_p = live && j < np && q != x.me;
     const bool is_a = live && j >= np && j < np + na && q != x.me;
-    const bool is_x = live && j >= np + na;
+    const bool is_x = live && j >= np + na && q != x.me;
     // propagations (unique per owner of Y, so a remote one is new unless re-imported)
     const bool nwp = is_p && hash_insert(st.phash, st.pmask, link_key(r.x, r.y));
     const uint32_t ps = wave_append(&st.ctr->p_log, nwp);
@@ -1712,7 +1772,7 @@ __global__ void k_ximport(DIndex ix, DState st, XchgArgs x, PubArgs pub) {
       uint32_t gd = 0, go = 0;
       for (uint32_t q = 0; q < x.nranks; ++q) {
         const uint32_t* h = x.recv + (size_t)q * stride;
-        gd += h[XH_NP] + h[XH_NA] + h[XH_NX] + h[XH_DS] + h[XH_DL];
+        gd += h[XH_NP] + h[XH_NA] + h[XH_NX] + h[XH_DS] + h[XH_DL] + h[XH_DP] + h[XH_DA] + h[XH_DX];
         go += h[XH_OVF];
       }
       auto put = [](uint32_t* w, uint32_t v) { __hip_atomic_store(w, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); };
@@ -1727,6 +1787,51 @@ __global__ void k_ximport(DIndex ix, DState st, XchgArgs x, PubArgs pub) {
   });
 }
 
+// Partitioned install of the base links / propagations (el_ctx::install_base): what the commit
+// routes for a new link or propagation (commit_l, commit_p), done for the base ones.  The
+// chain-second base links join the replicated chain-link log (the successor rows already hold
+// them: succ_fill) and, when another rank's rows can reach their x, the send queue; a base
+// propagation ((r, Y), B) goes to the send queue when another rank's rows can link to Y.
+__global__ void k_base_route(DIndex ix, DState st, uint32_t nb, uint32_t nbp) {
+  const uint32_t stride = gridDim.x * blockDim.x;
+  for (uint32_t base = blockIdx.x * blockDim.x; base < nb; base += stride) {  // (uniform trip count)
+    const uint32_t i = base + threadIdx.x;
+    uint32_t x = 0, p = 0;
+    bool ch = false;
+    if (i < nb) {
+      x = st.llog_x[i];
+      p = st.llog_p[i];
+      ch = ix.role_chs[ix.pair_role[p]];
+    }
+    const uint32_t xsl = wave_append(&st.ctr->x_log, ch);
+    if (ch) {
+      st.xlog_x[xsl] = x;
+      st.xlog_p[xsl] = p;
+    }
+    const bool xs = ch && remote(ix, x);
+    const uint32_t q = wave_append(&st.ctr->x_send, xs);
+    if (xs && q < st.xs_cap) {
+      st.xs_x[q] = x;
+      st.xs_p[q] = p;
+    }
+  }
+  for (uint32_t base = blockIdx.x * blockDim.x; base < nbp; base += stride) {
+    const uint32_t i = base + threadIdx.x;
+    bool xs = false;
+    uint32_t pid = 0, b = 0;
+    if (i < nbp) {
+      pid = st.plog_p[i];
+      b = st.plog_b[i];
+      xs = remote(ix, ix.pair_y[pid]);
+    }
+    const uint32_t q = wave_append(&st.ctr->x_sp, xs);
+    if (xs && q < st.xp_cap) {
+      st.xp_p[q] = pid;
+      st.xp_b[q] = b;
+    }
+  }
+}
+
 // Re-layout scan of a gapped CSR: new row starts = exclusive scan of gap_cap(len[r]).
 // Single pass with decoupled look-back: tiles are handed out by an atomic ticket, so every
 // predecessor tile of a block is owned by a block that is already running (look-back cannot
@@ -1736,8 +1841,7 @@ constexpr uint32_t SCAN_ITEMS = 8;
 constexpr uint32_t SCAN_TILE = 256 * SCAN_ITEMS;
 constexpr uint32_t FLAG_AGG = 1, FLAG_INC = 2;
 struct ScanArgs {
-  const uint32_t* len;  // rows
-  const uint32_t* s_old;  // null: scan gap_cap(len) (new row starts); else min(len, row capacity): in-place entries
+  const uint32_t* len;  // rows: start_out = exclusive scan of gap_cap(len[r])
   uint32_t* start_out;  // rows + 1
   uint32_t n1;          // rows + 1
   uint32_t tiles;
@@ -1763,9 +1867,7 @@ __global__ void __launch_bounds__(256) k_gap_scan(ScanArgs sa) {
 #pragma unroll
   for (uint32_t i = 0; i < SCAN_ITEMS; ++i) {
     const uint32_t idx = r0 + i * 256 + tid;
-    buf[i * 256 + tid] = idx + 1 >= sa.n1 ? 0u
-                         : sa.s_old   ? min(sa.len[idx], sa.s_old[idx + 1] - sa.s_old[idx])  // in-place entries
-                                      : gap_cap(sa.len[idx]);                                // new row capacities
+    buf[i * 256 + tid] = idx + 1 >= sa.n1 ? 0u : gap_cap(sa.len[idx]);  // row capacities
   }
   __syncthreads();
   uint32_t v[SCAN_ITEMS], run = 0;
@@ -1893,51 +1995,99 @@ __global__ void k_clear_logged(DIndex ix, uint32_t* bits_base, const uint32_t* _
 }
 
 // ---- gapped-CSR layout kernels (rare: initial layout, re-layout after an overflow)
-__global__ void k_gap_init(uint32_t* start, uint32_t* len, uint32_t rows, const uint32_t* __restrict__ start0) {
+__global__ void k_gap_init(uint32_t* start, uint32_t* end, uint32_t* len, uint32_t rows,
+                           const uint32_t* __restrict__ start0) {
   const uint32_t stride = gridDim.x * blockDim.x;
   for (uint32_t r = blockIdx.x * blockDim.x + threadIdx.x; r <= rows; r += stride) {
-    start[r] = start0 ? start0[r] : r * gap_cap(0);
+    const uint32_t v = start0 ? start0[r] : r * gap_cap(0);
+    start[r] = v;
+    if (r > 0) end[r - 1] = v;
     if (r < rows) len[r] = 0;
   }
 }
 
-// the largest r in [lo, hi] with ptr[r] <= j (ptr[lo] <= j)
-__device__ __forceinline__ uint32_t csr_row_of(const uint32_t* __restrict__ ptr, uint32_t lo, uint32_t hi, uint32_t j) {
-  while (lo < hi) {
-    const uint32_t mid = (lo + hi + 1) >> 1;
-    if (ptr[mid] <= j)
-      lo = mid;
-    else
-      hi = mid - 1;
-  }
-  return lo;
+// end[r] = start[r + 1]: the slots of a layout made by a scan (gap_build_from_log)
+__global__ void k_gap_ends(const uint32_t* __restrict__ start, uint32_t* __restrict__ end, uint32_t rows) {
+  const uint32_t stride = gridDim.x * blockDim.x;
+  for (uint32_t r = blockIdx.x * blockDim.x + threadIdx.x; r < rows; r += stride) end[r] = start[r + 1];
 }
 
-// Re-layout move, one in-place entry per lane: entry e of the dense order (rows ascending,
-// pre = exclusive scan of the rows' in-place counts) goes from its old slot to its new one.
-// A block takes 256·items entries a round; two lanes find the rows of its first and last entry,
-// then each entry's row is searched within that span only (a hub row spreads over many blocks);
-// a row-per-lane move (64 rows per wave) ran at 0.65 TB/s
-// (G3: 28.6 M predecessors, 0.35 ms per re-layout).
-__global__ void __launch_bounds__(256) k_gap_move_e(const uint32_t* __restrict__ pre, uint32_t rows, uint32_t n,
-                                                    const uint32_t* __restrict__ s_old,
-                                                    const uint32_t* __restrict__ v_old,
-                                                    const uint32_t* __restrict__ s_new, uint32_t* __restrict__ v_new,
-                                                    uint32_t items) {
-  __shared__ uint32_t span[2];
-  const uint32_t TILE = 256 * items;
-  for (uint32_t base = blockIdx.x * TILE; base < n; base += gridDim.x * TILE) {
-    if (threadIdx.x < 2) span[threadIdx.x] = csr_row_of(pre, 0, rows - 1, threadIdx.x ? min(base + TILE - 1, n - 1) : base);
-    __syncthreads();
-    const uint32_t a0 = span[0], a1 = span[1];
-    for (uint32_t k = 0; k < items; ++k) {
-      const uint32_t e = base + k * 256 + threadIdx.x;
-      if (e < n) {
-        const uint32_t r = csr_row_of(pre, a0, a1, e), o = e - pre[r];
-        v_new[s_new[r] + o] = v_old[s_old[r] + o];
+// ---- relocation of the rows that overflowed in a step (el_ctx::gap_relocate).  rc[0] = the
+// slot array's next free slot (64-bit), rc[1] = rows claimed, rc[2] = their in-place entries.
+struct Reloc {
+  uint32_t* start;
+  uint32_t* end;
+  const uint32_t* len;
+  uint32_t* val;
+  const uint32_t* ovq;  // (row, value, rank) per overflowing entry
+  uint32_t n_ovf;
+  uint32_t* flag;    // rows: 1 while claimed (zero otherwise)
+  uint32_t* nstart;  // rows: new start of a claimed row
+  uint32_t* rlist;   // claimed rows (≤ n_ovf)
+  unsigned long long* rc;
+};
+
+// The first overflow record of each row claims the row and reserves gap_cap(len) slots for it:
+// one atomic per wave on the tail (a prefix sum of the wave's claims), not one per row.
+__global__ void k_reloc_claim(Reloc a) {
+  const uint32_t stride = gridDim.x * blockDim.x;
+  for (uint32_t base = blockIdx.x * blockDim.x; base < a.n_ovf; base += stride) {  // (uniform trip count)
+    const uint32_t i = base + threadIdx.x;
+    uint32_t row = 0, sz = 0, old = 0;
+    bool won = false;
+    if (i < a.n_ovf) {
+      row = a.ovq[3 * (size_t)i];
+      won = atomicExch(a.flag + row, 1u) == 0u;
+      if (won) {
+        sz = gap_cap(a.len[row]);
+        old = a.end[row] - a.start[row];  // (an overflowing row is full: every slot holds an entry)
       }
     }
-    __syncthreads();
+    uint32_t inc = sz;
+#pragma unroll
+    for (uint32_t o = 1; o < 64; o <<= 1) {
+      const uint32_t v = __shfl_up(inc, o);
+      if (lane_id() >= o) inc += v;
+    }
+    const uint32_t total = __shfl(inc, 63);
+    const unsigned long long moved = wave_sum(old);
+    unsigned long long b = 0;
+    if (lane_id() == 0 && total) b = atomicAdd(a.rc, (unsigned long long)total);
+    if (lane_id() == 0 && moved) atomicAdd(a.rc + 2, moved);
+    b = __shfl(b, 0);
+    const uint32_t k = wave_append(reinterpret_cast<uint32_t*>(a.rc + 1), won);
+    if (won) {
+      a.nstart[row] = (uint32_t)(b + inc - sz);  // (the host checked the tail fits 32 bits first)
+      a.rlist[k] = row;
+    }
+  }
+}
+
+// Claimed rows: the in-place entries to the new slots (a block per row), then the overflow
+// entries by rank (roles: blocks [0, nb) rows, the rest overflow records).
+__global__ void k_reloc_move(Reloc a, uint32_t nb) {
+  const uint32_t nrows = (uint32_t)a.rc[1];
+  if (blockIdx.x < nb) {
+    for (uint32_t k = blockIdx.x; k < nrows; k += nb) {
+      const uint32_t row = a.rlist[k], s0 = a.start[row], n = a.end[row] - s0, d = a.nstart[row];
+      for (uint32_t j = threadIdx.x; j < n; j += blockDim.x) a.val[d + j] = a.val[s0 + j];
+    }
+    return;
+  }
+  const uint32_t stride = (gridDim.x - nb) * blockDim.x;
+  for (uint32_t i = (blockIdx.x - nb) * blockDim.x + threadIdx.x; i < a.n_ovf; i += stride) {
+    const uint32_t row = a.ovq[3 * (size_t)i];
+    a.val[a.nstart[row] + a.ovq[3 * (size_t)i + 2]] = a.ovq[3 * (size_t)i + 1];
+  }
+}
+
+__global__ void k_reloc_commit(Reloc a) {
+  const uint32_t nrows = (uint32_t)a.rc[1], stride = gridDim.x * blockDim.x;
+  for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < nrows; k += stride) {
+    const uint32_t row = a.rlist[k];
+    a.start[row] = a.nstart[row];
+    a.end[row] = a.nstart[row] + gap_cap(a.len[row]);
+    a.flag[row] = 0u;
   }
 }
 
@@ -1971,14 +2121,6 @@ __global__ void k_gap_fill(DGap g, const uint32_t* __restrict__ rows, const uint
     const bool p = i < n && keep(vals[i]);
     gap_append(g, p ? rows[i] : 0u, p ? vals[i] : 0u, p, ev);
   }
-}
-
-// overflow records (row, value, rank) land at their rank in the new layout
-__global__ void k_gap_ovf(const uint32_t* __restrict__ q, uint32_t n, const uint32_t* __restrict__ s_new,
-                          uint32_t* __restrict__ v_new) {
-  const uint32_t stride = gridDim.x * blockDim.x;
-  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
-    v_new[s_new[q[3 * (size_t)i]] + q[3 * (size_t)i + 2]] = q[3 * (size_t)i + 1];
 }
 
 // ---------------------------------------------------------------- host side
@@ -2057,32 +2199,37 @@ static void wave_triggers(uint64_t n, uint32_t maxb, uint32_t& grid, uint32_t& t
   grid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(maxb, (n + per_block - 1) / per_block));
 }
 
-// Gapped CSR (DGap) on the host side: the layout buffers, the overflow queue, scan scratch.
+// Gapped CSR (DGap) on the host side: the layout buffers, the overflow queue, relocation scratch.
 struct GapCsr {
   uint32_t rows = 0;
-  uint32_t *start = nullptr, *start2 = nullptr, *len = nullptr;
-  uint32_t* pre = nullptr;  // re-layout scratch: exclusive scan of the in-place entries (rows + 1)
-  uint32_t *val = nullptr, *val2 = nullptr;
-  uint64_t val_cap = 0, val2_cap = 0;
+  uint32_t *start = nullptr, *end = nullptr, *len = nullptr;
+  uint32_t* val = nullptr;
+  uint64_t val_cap = 0;
+  uint64_t used = 0;  // slots in use: the layout's, then every relocated row's (val[used, val_cap) is free)
   uint32_t* ovq = nullptr;
   uint64_t ovq_cap = 0;
+  uint32_t *flag = nullptr, *nstart = nullptr;  // relocation: per row (flag zero between relocations)
+  uint32_t* rlist = nullptr;                    // relocation: claimed rows (ovq_cap)
   bool live = false;  // maintained for this ontology (it has readers)
   // The classification's initial layout (el_init: a device scan of the row capacities the
   // first supersteps ask for — the base links and their CR5 lifts; el_ctx::closure_state), or
-  // r · gap_cap(0) when `laid` is false.  undo / reset restore it (k_gap_init).
+  // r · gap_cap(0) when `laid` is false.  Reset restores it (k_gap_init).
   uint32_t* start0 = nullptr;
   bool laid = false;
   uint64_t total0 = 0;  // slots of the initial layout
   void alloc(uint32_t n, uint64_t ovq_entries) {
     rows = n;
     start = dalloc<uint32_t>(n + 1);
-    start2 = dalloc<uint32_t>(n + 1);
-    pre = dalloc<uint32_t>(n + 1);
+    end = dalloc<uint32_t>(n);
     len = dalloc<uint32_t>(n);
     start0 = dalloc<uint32_t>(n + 1);
+    flag = dalloc<uint32_t>(n);
+    HIPCHK(hipMemset(flag, 0, (uint64_t)n * sizeof(uint32_t)));
+    nstart = dalloc<uint32_t>(n);
     laid = false;
     total0 = (uint64_t)gap_cap(0) * n;
     val_cap = total0;
+    used = total0;
     val = dalloc<uint32_t>(val_cap);
     live = true;
     set_ovq(ovq_entries);
@@ -2090,23 +2237,26 @@ struct GapCsr {
   void set_ovq(uint64_t entries) {
     if (!live || entries <= ovq_cap) return;
     dfree(ovq);
+    dfree(rlist);
     ovq_cap = entries;
     ovq = dalloc<uint32_t>(3 * entries);
+    rlist = dalloc<uint32_t>(entries);
   }
   void release() {
     dfree(start);
-    dfree(start2);
-    dfree(pre);
+    dfree(end);
     dfree(len);
     dfree(val);
-    dfree(val2);
     dfree(ovq);
+    dfree(rlist);
+    dfree(flag);
+    dfree(nstart);
     dfree(start0);
-    val_cap = val2_cap = ovq_cap = total0 = 0;
+    val_cap = ovq_cap = total0 = used = 0;
     live = laid = false;
   }
   DGap view(uint32_t* ov_count) const {
-    return DGap{start, len, val, ovq, (uint32_t)ovq_cap, ov_count};
+    return DGap{start, end, len, val, ovq, (uint32_t)ovq_cap, ov_count};
   }
 };
 
@@ -2456,7 +2606,14 @@ struct el_ctx {
   bool use_props = false;   // propagation set in use (CR4 axioms, or ⊥ in partitioned mode)
   uint32_t *xlog_x = nullptr, *xlog_p = nullptr;  // replicated chain-second links
   uint64_t xlog_cap = 0, x_count = 0;
-  uint32_t *xs_x = nullptr, *xs_p = nullptr;      // this step's local chain links to send (cl_cap)
+  // this step's records for other ranks (routed by the commit, remote()): chain-second links,
+  // propagations, activations; sized for a step's candidates (+ the base ones, el_init)
+  uint32_t *xs_x = nullptr, *xs_p = nullptr, *xp_p = nullptr, *xp_b = nullptr, *xa_y = nullptr, *xa_c = nullptr;
+  uint64_t xs_cap = 0, xp_cap = 0, xa_cap = 0;
+  void fit_xqueues(uint64_t xs, uint64_t xp, uint64_t xa);  // (only while they are empty)
+  uint2* xwin = nullptr;       // every rank's column window (device; exchange_windows)
+  void exchange_windows();     // collective, once per el_load
+  uint32_t* sc_own = nullptr;  // partitioned: successor-row capacities of the own rows only (layout)
   uint32_t* xsend = nullptr;                      // exchange slot: XH + 2 * xcap words
   uint32_t* xrecv = nullptr;                      // part_count slots
   uint32_t* xhdr = nullptr;                       // part_count headers (the header round)
@@ -2522,6 +2679,13 @@ struct el_ctx {
     s.xlog_p = xlog_p;
     s.xs_x = xs_x;
     s.xs_p = xs_p;
+    s.xs_cap = (uint32_t)std::min<uint64_t>(xs_cap, 0xffffffffu);
+    s.xp_p = xp_p;
+    s.xp_b = xp_b;
+    s.xp_cap = (uint32_t)std::min<uint64_t>(xp_cap, 0xffffffffu);
+    s.xa_y = xa_y;
+    s.xa_c = xa_c;
+    s.xa_cap = (uint32_t)std::min<uint64_t>(xa_cap, 0xffffffffu);
 
     s.cs_x = cs_x;
     s.cs_a = cs_a;
@@ -2648,6 +2812,7 @@ struct el_ctx {
   uint64_t strm_s = 0, strm_l = 0;  // log entries already enqueued
   bool strm_ovf = false;          // a buffer was too small (el_result_wait: EL_ERANGE)
   hipEvent_t ev_strm = nullptr;   // recorded right behind a superstep's commit
+  bool dma_hostptr = getenv("EL_DMA_HOSTPTR") != nullptr;  // A/B: copies to the host pointers, kind DeviceToHost
   bool strm_marked = false;       // ev_strm was recorded right behind this step's commit
   hipStream_t nstream = nullptr;  // run encoding (never queued behind the DMAs)
   uint2 *s_run_dev = nullptr, *l_run_dev = nullptr;  // device addresses of the caller's run buffers
@@ -2693,14 +2858,16 @@ struct el_ctx {
   uint64_t superstep_part(uint32_t mask, uint64_t sb, uint64_t se, uint64_t lb, uint64_t le, uint64_t ab,
                           uint64_t ae, uint64_t pb, uint64_t pe, uint64_t xb, uint64_t xe);
   void grow_part(uint64_t new_xcap);
-  uint32_t exchange_round(uint32_t s0, uint32_t l0, uint32_t a0, uint32_t p0);
+  uint32_t exchange_round(uint32_t s0, uint32_t l0, uint32_t a0, uint32_t p0, uint32_t x0);
   uint64_t remote_bound() const { return part() ? (uint64_t)(part_count - 1) * xcap : 0u; }
+  // successor-row appends of one step: the own new chain links (+ the imported ones)
+  uint64_t sc_ovq() const { return cl_cap + (part() ? (uint64_t)part_count * xcap : 0u); }
   void fill_stats(el_stats* st, double ms);
-  void gap_rebuild(GapCsr& g, uint32_t n_ovf, uint64_t entries);
-  void gap_rebuild_all();
+  void gap_relocate_all();
+  unsigned long long *reloc_rc = nullptr, *reloc_h = nullptr;  // relocation counters (device / pinned), 3 per CSR
   void gap_build_from_log(GapCsr& g, const uint32_t* rows, const uint32_t* vals, uint64_t n,
                           const uint8_t* keep = nullptr);
-  void launch_gap_scan(const uint32_t* len, uint32_t R, uint32_t* start_out, const uint32_t* s_old = nullptr);
+  void launch_gap_scan(const uint32_t* len, uint32_t R, uint32_t* start_out);
   std::string install_index(el::HostIndex&& h);
   void column_window();
   void migrate_state(uint32_t N0, const std::vector<uint32_t>& pmap);
@@ -2844,7 +3011,53 @@ std::string el_ctx::install_index(el::HostIndex&& hnew) {
   d.hi = hi;
   column_window();
   d.part = part() ? 1u : 0u;
+  d.xwin = nullptr;  // (the windows of the other ranks: exchange_windows, at the first el_saturate)
+  d.nranks = part() ? part_count : 1u;
+  d.me = part_rank;
   return "";
+}
+
+// Every rank's column window, all-gathered once per el_load (the first el_saturate: collective).
+// A record keyed by concept y (a propagation ((r, y), B), an activation (y, C), a chain-second
+// link (y, s, z)) can only matter to a rank whose rows can reach y — y in its window — so the
+// commit routes to the exchange only those some other rank's window holds (remote()).  For
+// OntologyMultiplier copies aligned with the partition nothing crosses but the header words.
+void el_ctx::exchange_windows() {
+  if (ix.xwin || part_count < 2) {
+    if (!ix.xwin) ix.nranks = 1;
+    return;
+  }
+  uint32_t* buf = dalloc<uint32_t>(4 + 4 * (uint64_t)part_count);
+  index_bufs.push_back(buf);
+  const uint32_t mine[4] = {ix.c_lo, ix.c_hi, lo, hi};
+  HIPCHK(hipMemcpyAsync(buf, mine, sizeof mine, hipMemcpyHostToDevice, stream));
+  xchg->allgather(buf, buf + 4, 4 * sizeof(uint32_t), stream);
+  std::vector<uint32_t> all(4 * (uint64_t)part_count);
+  HIPCHK(hipMemcpyAsync(all.data(), buf + 4, all.size() * sizeof(uint32_t), hipMemcpyDeviceToHost, stream));
+  HIPCHK(hipStreamSynchronize(stream));
+  std::vector<uint32_t> win(2 * (uint64_t)part_count);
+  for (uint32_t q = 0; q < part_count; ++q) {
+    win[2 * q] = all[4 * q];
+    win[2 * q + 1] = all[4 * q + 1];
+  }
+  uint32_t* d = dupload(win);
+  index_bufs.push_back(d);
+  ix.xwin = reinterpret_cast<const uint2*>(d);
+}
+
+void el_ctx::fit_xqueues(uint64_t xs, uint64_t xp, uint64_t xa) {
+  auto fit = [&](uint64_t want, uint64_t& cap, uint32_t*& a, uint32_t*& b) {
+    if (want <= cap && a) return;
+    HIPCHK(hipStreamSynchronize(stream));
+    dfree(a);
+    dfree(b);
+    cap = std::max<uint64_t>(want, 1024);
+    a = dalloc<uint32_t>(cap);
+    b = dalloc<uint32_t>(cap);
+  };
+  fit(xs, xs_cap, xs_x, xs_p);
+  fit(xp, xp_cap, xp_p, xp_b);
+  fit(xa, xa_cap, xa_y, xa_c);
 }
 
 // Bit-row columns of this context (SURVEY.md §7 "hard parts": columns compacted per
@@ -2977,6 +3190,12 @@ void el_ctx::free_state() {
   dfree(xlog_p);
   dfree(xs_x);
   dfree(xs_p);
+  dfree(xp_p);
+  dfree(xp_b);
+  dfree(xa_y);
+  dfree(xa_c);
+  xs_cap = xp_cap = xa_cap = 0;
+  dfree(sc_own);
   dfree(xsend);
   dfree(xrecv);
   dfree(xhdr);
@@ -3036,7 +3255,7 @@ void el_ctx::alloc_state() {
   // supersteps' links (the base links and their CR5 lifts, the base propagations), as the oracle
   // sizes its rows (el_oracle.c, elo_create), so no early re-layout is needed
   if (P && need_pred) PR.alloc((uint32_t)P, cl_cap);
-  if (need_succ) SC.alloc((uint32_t)N, part() ? (uint64_t)part_count * xcap : cl_cap);
+  if (need_succ) SC.alloc((uint32_t)N, cl_cap + (part() ? (uint64_t)part_count * xcap : 0));
   if (use_props) PP.alloc((uint32_t)P, cp_cap + remote_bound());
   HIPCHK(hipHostMalloc((void**)&pin_word, sizeof(uint32_t), hipHostMallocDefault));
   // range activation candidates: a new link (X, r, Y) emits one (Y, C) per C ∈ rng(r), so a
@@ -3075,8 +3294,7 @@ void el_ctx::alloc_state() {
     xlog_cap = std::max<uint64_t>(1u << 16, (uint64_t)part_count * xcap);
     xlog_x = dalloc<uint32_t>(xlog_cap);
     xlog_p = dalloc<uint32_t>(xlog_cap);
-    xs_x = dalloc<uint32_t>(cl_cap);
-    xs_p = dalloc<uint32_t>(cl_cap);
+    fit_xqueues(cl_cap, cp_cap, ca_cap);
     xsend = dalloc<uint32_t>(XH + 2 * xcap);
     xrecv = dalloc<uint32_t>((uint64_t)part_count * (XH + 2 * xcap));
     xhdr = dalloc<uint32_t>((uint64_t)part_count * XH);
@@ -3490,7 +3708,7 @@ bool el_ctx::superstep(uint32_t mask, uint64_t sb, uint64_t se, uint64_t lb, uin
     l_count = hc.l_log;
     a_count = hc.a_log;
     p_count = hc.p_log;
-    gap_rebuild_all();  // rows that outgrew their slack get a new layout before anyone reads them
+    gap_relocate_all();  // rows that outgrew their slack move to new slots before anyone reads them
     // ---- keep the buffers ahead of demand; complete the step if one overflowed
     bool overflow = false;
     // Each trigger of the next step fans out to a few S conclusions (G3 step 1: 25 M new links
@@ -3522,7 +3740,7 @@ bool el_ctx::superstep(uint32_t mask, uint64_t sb, uint64_t se, uint64_t lb, uin
     if (max_rng && cl_cap * max_rng > ca_cap)  // activation candidates follow the link queue
       regrow2((uint32_t)std::min<uint64_t>(cl_cap * max_rng / 2, 0xffffffffu), ca_cap, ca_y, ca_c);
     PR.set_ovq(cl_cap);  // overflow queues hold one step's appends
-    SC.set_ovq(part() ? (uint64_t)part_count * xcap : cl_cap);
+    SC.set_ovq(sc_ovq());
     PP.set_ovq(cp_cap + remote_bound());
     // fan-out jobs: about one per trigger at most (G5 step 1: 4.4 M new links -> 1.7 M jobs)
     if (const uint64_t want = std::min<uint64_t>(next_trig, 1ull << 26); want > job_cap && !small_queues) {
@@ -3554,7 +3772,7 @@ void el_ctx::grow_part(uint64_t new_xcap) {
     dfree(xrecv);
     xsend = dalloc<uint32_t>(XH + 2 * xcap);
     xrecv = dalloc<uint32_t>((uint64_t)part_count * (XH + 2 * xcap));
-    if (SC.live) SC.set_ovq((uint64_t)part_count * xcap);
+    if (SC.live) SC.set_ovq(sc_ovq());
     if (PP.live) PP.set_ovq(cp_cap + remote_bound());
   }
   const uint64_t rb = remote_bound(), xb = (uint64_t)part_count * xcap;
@@ -3569,7 +3787,7 @@ void el_ctx::grow_part(uint64_t new_xcap) {
   if (2 * (p_count + cp_cap + rb) > phash_cap) rehash_props(next_pow2(2 * (p_count + cp_cap + rb)));
   grow_log(a_count, a_count + ca_cap + rb, alog_cap, alog_y, alog_c);
   if (2 * (a_count + ca_cap + rb) > ahash_cap) rehash_acts(next_pow2(2 * (a_count + ca_cap + rb)));
-  grow_log(x_count, x_count + xb, xlog_cap, xlog_x, xlog_p);
+  grow_log(x_count, x_count + cl_cap + xb, xlog_cap, xlog_x, xlog_p);
 }
 
 // Pack this rank's new records, all-gather every rank's, import them, merge the CSRs.
@@ -3577,7 +3795,7 @@ void el_ctx::grow_part(uint64_t new_xcap) {
 // round to the largest rank's records this superstep (not the capacity: late supersteps send
 // almost nothing), then the records.  Returns the largest rank's record count after the import
 // published; hc then holds the global g_* words (g_max > xcap: nothing was imported).
-uint32_t el_ctx::exchange_round(uint32_t s0, uint32_t l0, uint32_t a0, uint32_t p0) {
+uint32_t el_ctx::exchange_round(uint32_t s0, uint32_t l0, uint32_t a0, uint32_t p0, uint32_t x0) {
   DState st = dstate();
   XchgArgs xa{};
   xa.send = xsend;
@@ -3585,7 +3803,7 @@ uint32_t el_ctx::exchange_round(uint32_t s0, uint32_t l0, uint32_t a0, uint32_t 
   xa.cap = (uint32_t)xcap;
   xa.nranks = part_count;
   xa.me = part_rank;
-  xa.s0 = s0, xa.l0 = l0, xa.a0 = a0, xa.p0 = p0;
+  xa.s0 = s0, xa.l0 = l0, xa.a0 = a0, xa.p0 = p0, xa.x0 = x0;
   xa.cs_cap = (uint32_t)cs_cap, xa.cl_cap = (uint32_t)cl_cap, xa.ca_cap = (uint32_t)ca_cap;
   xa.cp_cap = (uint32_t)cp_cap, xa.job_cap = (uint32_t)job_cap, xa.ct_cap = (uint32_t)ct_cap;
   hipLaunchKernelGGL(k_xpack, dim3(grid_for(xcap, 64)), dim3(BLOCK), 0, stream, st, xa);
@@ -3597,6 +3815,7 @@ uint32_t el_ctx::exchange_round(uint32_t s0, uint32_t l0, uint32_t a0, uint32_t 
   for (uint32_t q = 0; q < part_count; ++q) {
     const uint32_t* h = xhdr_h + (uint64_t)q * XH;
     m = std::max(m, h[XH_NP] + h[XH_NA] + h[XH_NX]);
+    if (h[XH_QOVF]) throw ElError{EL_EHIP, "exchange: a send queue overflowed on rank " + std::to_string(q)};
   }
   // this round's records per rank; a rank past xcap: headers only, the import takes nothing and
   // publishes g_max (the caller grows and redoes; the commit's gapped-row overflows are placed first)
@@ -3617,7 +3836,7 @@ uint32_t el_ctx::exchange_round(uint32_t s0, uint32_t l0, uint32_t a0, uint32_t 
   a_count = hc.a_log;
   p_count = hc.p_log;
   x_count = hc.x_log;
-  gap_rebuild_all();
+  gap_relocate_all();
   return hc.g_max;
 }
 
@@ -3632,9 +3851,10 @@ uint64_t el_ctx::superstep_part(uint32_t mask, uint64_t sb, uint64_t se, uint64_
     // ---- capacities for the local candidates (as in superstep) and the remote imports
     const uint64_t rb = remote_bound();
     const bool grow = s_count + cs_cap + ct_cap > slog_cap || l_count + cl_cap > llog_cap ||
-                      2 * (l_count - l_base + cl_cap) > lhash_cap || a_count + ca_cap + rb > alog_cap || 2 * (a_count + ca_cap + rb) > ahash_cap ||
-                      p_count + cp_cap + rb > plog_cap || 2 * (p_count + cp_cap + rb) > phash_cap ||
-                      x_count + part_count * xcap > xlog_cap;
+                      2 * (l_count - l_base + cl_cap) > lhash_cap || a_count + ca_cap + rb > alog_cap ||
+                      2 * (a_count + ca_cap + rb) > ahash_cap || p_count + cp_cap + rb > plog_cap ||
+                      2 * (p_count - p_base + cp_cap + rb) > phash_cap ||
+                      x_count + cl_cap + part_count * xcap > xlog_cap;
     if (grow) {
       sync();
       if (strm) HIPCHK(hipStreamSynchronize(dstream));
@@ -3654,7 +3874,8 @@ uint64_t el_ctx::superstep_part(uint32_t mask, uint64_t sb, uint64_t se, uint64_
       if (2 * (l_count - l_base + cl_cap) > lhash_cap) rehash_links(next_pow2(2 * (l_count - l_base + cl_cap)));
       grow_part(xcap);
     }
-    const uint32_t s0 = (uint32_t)s_count, l0 = (uint32_t)l_count, a0 = (uint32_t)a_count, p0 = (uint32_t)p_count;
+    const uint32_t s0 = (uint32_t)s_count, l0 = (uint32_t)l_count, a0 = (uint32_t)a_count, p0 = (uint32_t)p_count,
+                   x0 = (uint32_t)x_count;
 
     // ---- generation + local commit (no publish: the import publishes for the step)
     refresh_acts();
@@ -3670,34 +3891,44 @@ uint64_t el_ctx::superstep_part(uint32_t mask, uint64_t sb, uint64_t se, uint64_
     ea.sb = (uint32_t)sb, ea.se = (uint32_t)se, ea.lb = (uint32_t)lb, ea.le = (uint32_t)le;
     ea.ab = (uint32_t)ab, ea.ae = (uint32_t)ae, ea.pb = (uint32_t)pb, ea.pe = (uint32_t)pe;
     ea.xb = (uint32_t)xb, ea.xe = (uint32_t)xe;
-    ea.mask = mask;
+    // an empty link / propagation set (the first superstep over the base links): probes cannot
+    // hit (the imports of a superstep come after its generation)
+    ea.mask = mask | (l_count == l_base ? (uint32_t)M_LEMPTY : 0u) | (p_count == p_base ? (uint32_t)M_PEMPTY : 0u);
     ea.a_end = (uint32_t)ab;  // activations known at t-1 (the exchange appended this step's)
+    // S-queue reservations for a big step (wq_publish_s), as in superstep()
+    if (!small_queues && (se - sb) + (le - lb) >= (1u << 18)) {
+      const uint64_t waves = (uint64_t)(ea.gs + ea.gl + ea.ga + ea.gp + ea.gx + tune_jobs) * (BLOCK / 64);
+      for (uint32_t c = 4096; c >= 1024 && !st.cs_chunk; c >>= 1)
+        if (4 * waves * c <= cs_cap) st.cs_chunk = c;
+    }
     const uint32_t eg = ea.gs + ea.gl + ea.ga + ea.gp + ea.gx;
     if (eg) {
       launch(EL_K_EXPAND_S, [&] { hipLaunchKernelGGL(k_expand, dim3(eg), dim3(BLOCK), 0, stream, ix, st, ea); });
-      launch(EL_K_JOBS, [&] { hipLaunchKernelGGL(k_jobs, dim3(tune_jobs), dim3(BLOCK), 0, stream, ix, st, mask); });
+      launch(EL_K_JOBS, [&] { hipLaunchKernelGGL(k_jobs, dim3(tune_jobs), dim3(BLOCK), 0, stream, ix, st, ea.mask); });
     }
     CommitArgs ca{};
-    ca.gs = grid_for(cs_cap, tune_commit);
-    ca.gl = grid_for(cl_cap, tune_commit);
+    // grids from the step's triggers, as in superstep() (the roles loop grid-stride)
+    const uint64_t est = std::max<uint64_t>(2 * ((se - sb) + (le - lb) + (xe - xb) + (pe - pb)), 16384);
+    ca.gs = grid_for(std::min<uint64_t>(cs_cap, est), tune_commit);
+    ca.gl = grid_for(std::min<uint64_t>(cl_cap, est), tune_commit);
     ca.ga = hx.rng.a.size() ? grid_for(ca_cap, 64) : 0u;
     ca.gp = use_props ? grid_for(cp_cap, 256) : 0u;
     ca.cs_cap = (uint32_t)cs_cap, ca.cl_cap = (uint32_t)cl_cap;
     ca.ca_cap = (uint32_t)ca_cap, ca.cp_cap = (uint32_t)cp_cap;
     ca.publish = 0;
     launch(EL_K_COMMIT_T, [&] {
-      hipLaunchKernelGGL(k_commit_told, dim3(grid_for(ct_cap, tune_commit)), dim3(BLOCK), 0, stream, ix, st,
-                         (uint32_t)ct_cap);
+      hipLaunchKernelGGL(k_commit_told, dim3(grid_for(std::min<uint64_t>(ct_cap, 8 * est), tune_commit)), dim3(BLOCK),
+                         0, stream, ix, st, (uint32_t)ct_cap);
     });
     launch(EL_K_COMMIT_S, [&] {
       hipLaunchKernelGGL(k_commit, dim3(ca.gs + ca.gl + ca.ga + ca.gp), dim3(BLOCK), 0, stream, ix, st, ca);
     });
 
     // ---- delta exchange; a too-small exchange imports nothing and is redone larger
-    uint32_t gmax = exchange_round(s0, l0, a0, p0);
+    uint32_t gmax = exchange_round(s0, l0, a0, p0, x0);
     if (gmax > xcap) {
       grow_part(next_pow2(gmax));
-      gmax = exchange_round(s0, l0, a0, p0);
+      gmax = exchange_round(s0, l0, a0, p0, x0);
       if (gmax > xcap) throw std::runtime_error("exchange overflow after growth");
     }
     gdelta += hc.g_delta;
@@ -3716,14 +3947,12 @@ uint64_t el_ctx::superstep_part(uint32_t mask, uint64_t sb, uint64_t se, uint64_
     regrow2(hc.cand_s, cs_cap, cs_x, cs_a);
     regrow2(hc.cand_t, ct_cap, ct_x, ct_a);
     if (regrow2(hc.cand_l, cl_cap, cl_x, cl_p)) {
-      dfree(xs_x);
-      dfree(xs_p);
-      xs_x = dalloc<uint32_t>(cl_cap);
-      xs_p = dalloc<uint32_t>(cl_cap);
       PR.set_ovq(cl_cap);
+      SC.set_ovq(sc_ovq());
     }
     regrow2(hc.cand_a, ca_cap, ca_y, ca_c);
     if (regrow2(hc.cand_p, cp_cap, cp_p, cp_b)) PP.set_ovq(cp_cap + remote_bound());
+    fit_xqueues(cl_cap, cp_cap, ca_cap);  // (sent: the queues are empty)
     if (2ull * hc.jobs > job_cap) {
       sync();
       job_cap = next_pow2(2ull * hc.jobs + 1024);
@@ -3735,55 +3964,10 @@ uint64_t el_ctx::superstep_part(uint32_t mask, uint64_t sb, uint64_t se, uint64_
   return gdelta;
 }
 
-// Re-lay out a gapped CSR whose rows overflowed this step: every row gets gap_cap(len)
-// slots (exclusive scan), its in-place entries move, the overflow records land at their
-// rank.  Events mirror the CPU oracle (same formula as a CSR merge with `entries` - n_ovf
-// moved and n_ovf placed entries).
-void el_ctx::gap_rebuild(GapCsr& g, uint32_t n_ovf, uint64_t entries) {
-  if (n_ovf > g.ovq_cap) throw std::runtime_error("gapped-CSR overflow queue overrun");
-  const uint32_t R = g.rows;
-  // Σ_r gap_cap(len[r]) with Σ len = entries: the host sizes the new layout without a readback
-  const uint64_t total = (uint64_t)GAP_MUL * entries + (uint64_t)gap_cap(0) * R;
-  if (total > 0xffffffffull) throw ElError{EL_ENOMEM, "gapped CSR beyond 2^32 slots"};
-  if (total > g.val2_cap) {
-    sync();
-    dfree(g.val2);
-    g.val2_cap = total + total / 2;
-    g.val2 = dalloc<uint32_t>(g.val2_cap);
-  }
-  launch_gap_scan(g.len, R, g.start2);
-  const uint64_t moved_n = entries - n_ovf;  // every row's in-place entries
-  launch_gap_scan(g.len, R, g.pre, g.start);
-  if (moved_n)
-    launch(EL_K_SCATTER_OLD, [&] {
-      const uint32_t items = (uint32_t)std::min<uint64_t>(16, std::max<uint64_t>(1, moved_n / (2048 * 256)));
-      const uint64_t t = 256ull * items;
-      hipLaunchKernelGGL(k_gap_move_e, dim3((uint32_t)std::min<uint64_t>(2048, (moved_n + t - 1) / t)), dim3(256), 0,
-                         stream, g.pre, R, (uint32_t)moved_n, g.start, g.val, g.start2, g.val2, items);
-    });
-  if (n_ovf)
-    launch(EL_K_SCATTER_NEW, [&] {
-      hipLaunchKernelGGL(k_gap_ovf, dim3(grid_for(n_ovf)), dim3(BLOCK), 0, stream, g.ovq, n_ovf, g.start2, g.val2);
-    });
-  std::swap(g.start, g.start2);
-  std::swap(g.val, g.val2);
-  std::swap(g.val_cap, g.val2_cap);
-  const uint64_t n1 = (uint64_t)R + 1, moved = entries - n_ovf;
-  host_ev[EL_K_SCAN][EL_EV_ENT] += 3 * n1;        // read len, write caps, scan
-  host_ev[EL_K_MERGE_PTR][EL_EV_ENT] += 2 * n1;   // old and new row starts
-  host_ev[EL_K_SCATTER_OLD][EL_EV_TRIG] += moved;
-  host_ev[EL_K_SCATTER_OLD][EL_EV_ENT] += moved;
-  host_ev[EL_K_SCATTER_OLD][EL_EV_EMIT] += moved;
-  host_ev[EL_K_SCATTER_NEW][EL_EV_TRIG] += n_ovf;
-  host_ev[EL_K_SCATTER_NEW][EL_EV_ENT] += 3ull * n_ovf;
-  host_ev[EL_K_SCATTER_NEW][EL_EV_EMIT] += n_ovf;
-}
-
 // new row starts = exclusive scan of gap_cap(len[r]) (k_gap_scan)
-void el_ctx::launch_gap_scan(const uint32_t* len, uint32_t R, uint32_t* start_out, const uint32_t* s_old) {
+void el_ctx::launch_gap_scan(const uint32_t* len, uint32_t R, uint32_t* start_out) {
   ScanArgs sa{};
   sa.len = len;
-  sa.s_old = s_old;
   sa.start_out = start_out;
   sa.n1 = R + 1;
   sa.tiles = (R + 1 + SCAN_TILE - 1) / SCAN_TILE;
@@ -3809,13 +3993,17 @@ void el_ctx::gap_build_from_log(GapCsr& g, const uint32_t* rows, const uint32_t*
     HIPCHK(hipGetLastError());
   }
   launch_gap_scan(g.len, R, g.start);
+  hipLaunchKernelGGL(k_gap_ends, dim3(grid_for(R)), dim3(BLOCK), 0, stream, g.start, g.end, R);
+  HIPCHK(hipGetLastError());
   const uint64_t total = (uint64_t)GAP_MUL * n + (uint64_t)gap_cap(0) * R;
+  if (total > 0xffffffffull) throw ElError{EL_ENOMEM, "gapped CSR beyond 2^32 slots"};
   if (total > g.val_cap) {
     sync();
     dfree(g.val);
     g.val_cap = total + total / 2;
     g.val = dalloc<uint32_t>(g.val_cap);
   }
+  g.used = total;
   HIPCHK(hipMemsetAsync(g.len, 0, (uint64_t)R * sizeof(uint32_t), stream));
   if (n) {
     hipLaunchKernelGGL(k_gap_fill, dim3(grid_for(n)), dim3(BLOCK), 0, stream, g.view(&ctr->ov_pr), rows, vals, n, gk);
@@ -3939,7 +4127,7 @@ void el_ctx::closure_grow() {
 void el_ctx::closure_tail(uint32_t a, uint32_t b, uint32_t L) {
   HIPCHK(hipMemsetAsync(&cl.ctr->tot[elcl::T_STUCK], 0, sizeof(unsigned long long), stream));
   elcl::check(stream, cax, cl);
-  elcl::stats(stream, cax, cl, 0, hx.N, use_props && !part());  // (every row: the SC layout spans them)
+  elcl::stats(stream, cax, cl, 0, hx.N, use_props);  // (every row: the SC layout spans them)
   HIPCHK(hipMemsetAsync(cl.ctr->tot, 0, elcl::T_STUCK * sizeof(unsigned long long), stream));
   HIPCHK(hipMemsetAsync(cl.ctr->ev, 0, sizeof(cl.ctr->ev), stream));
   elcl::totals(stream, cax, cl, a, b);
@@ -4006,10 +4194,12 @@ void el_ctx::closure_rows(uint32_t a, uint32_t b) {
   host_ev[EL_K_CLOSURE][EL_EV_RMW] += clt.ev[elcl::E_RMW];
 }
 
-// The owned rows' init facts S(X) = {X, ⊤} ∪ told*(X) (fact log + bits), and for a whole-ontology
-// context the base links / propagations in the heads of their logs (installed by el_saturate),
-// the base links by pid (radix sort) and this classification's gapped-row layouts.  Buffers
-// grow first to what the closure asks for (grow-only).
+// The owned rows' init facts S(X) = {X, ⊤} ∪ told*(X) (fact log + bits), the base links /
+// propagations of the owned rows in the heads of their logs (installed by el_saturate), the base
+// links by pid (radix sort) and this classification's gapped-row layouts.  Buffers grow first to
+// what the closure asks for (grow-only).  A row partition does the same for its own rows (its
+// base links are local; el_saturate routes the chain-second ones and the propagations that other
+// ranks' rows can reach into the first exchange).
 void el_ctx::closure_state() {
   if (reset_wait) {
     HIPCHK(hipStreamWaitEvent(stream, ev_reset, 0));
@@ -4024,10 +4214,9 @@ void el_ctx::closure_state() {
   const uint64_t b_link = T[elcl::T_EXR] + two * (te.z - tb.z);
   const uint64_t b_conj = T[elcl::T_CIDX] + two * (te.y - tb.y) + T[elcl::T_CZ];
   const uint64_t b_prop = T[elcl::T_EXL] + two * (te.w - tb.w);
-  const bool base = !part();
-  nb = base ? T[elcl::T_EXR] : 0;
-  nbp = base && use_props ? T[elcl::T_PROPS] : 0;
-  nc = base && SC.live ? T[elcl::T_SC0] : 0;
+  nb = T[elcl::T_EXR];
+  nbp = use_props ? T[elcl::T_PROPS] : 0;
+  nc = SC.live ? T[elcl::T_SC0] : 0;
   if (n_init > 0xffffffffull || nb > 0xffffffffull || nbp > 0xffffffffull)
     throw ElError{EL_ENOMEM, "init facts or base links beyond 2^32 (uint32 device counters)"};
   auto realloc2 = [](uint64_t cap, uint32_t*& a, uint32_t*& b) {
@@ -4038,18 +4227,22 @@ void el_ctx::closure_state() {
   };
   if (!small_queues) {
     if (const uint64_t w = next_pow2(b_conj + b_conj / 4); w > cs_cap) realloc2(cs_cap = w, cs_x, cs_a);
-    if (const uint64_t w = next_pow2(b_link + b_link / 4); w > cl_cap) {
-      realloc2(cl_cap = w, cl_x, cl_p);
-      if (part()) realloc2(cl_cap, xs_x, xs_p);
-    }
+    if (const uint64_t w = next_pow2(b_link + b_link / 4); w > cl_cap) realloc2(cl_cap = w, cl_x, cl_p);
   }
   if (const uint64_t w = next_pow2(b_prop + b_prop / 4); w > cp_cap) realloc2(cp_cap = w, cp_p, cp_b);
   if (const uint64_t w = std::max<uint64_t>(cs_cap, next_pow2(2 * T[elcl::T_TOLD] + 1024)); w > ct_cap)
     realloc2(ct_cap = w, ct_x, ct_a);
   if (max_rng && next_pow2(cl_cap * max_rng) > ca_cap) realloc2(ca_cap = next_pow2(cl_cap * max_rng), ca_y, ca_c);
   PR.set_ovq(cl_cap);
-  SC.set_ovq(part() ? (uint64_t)part_count * xcap : cl_cap);
+  SC.set_ovq(sc_ovq());
   PP.set_ovq(cp_cap + remote_bound());
+  if (part()) {  // (the queues and the chain-link log are empty at el_init)
+    fit_xqueues(cl_cap + nc, cp_cap + nbp, ca_cap);
+    if (const uint64_t w = nc + cl_cap + (uint64_t)part_count * xcap; w > xlog_cap) {
+      xlog_cap = next_pow2(w);
+      realloc2(xlog_cap, xlog_x, xlog_p);
+    }
+  }
   if (n_init + cs_cap + ct_cap > slog_cap) {  // (s_count is 0: nothing to keep)
     slog_cap = next_pow2(n_init + cs_cap + ct_cap);
     realloc2(slog_cap, slog_x, slog_a);
@@ -4072,10 +4265,10 @@ void el_ctx::closure_state() {
     }
     g.laid = false;
   };
-  fit_gap(PR, base ? nb + T[elcl::T_LIFT] : 0);
-  fit_gap(SC, base ? T[elcl::T_SC] : 0);
+  fit_gap(PR, nb + T[elcl::T_LIFT]);
+  fit_gap(SC, T[elcl::T_SC]);
   fit_gap(PP, nbp);
-  if (base && PR.live && nb) {
+  if (PR.live && nb) {
     if (nb > sk_cap) {
       sk_cap = nb + nb / 8;
       realloc2(sk_cap, sk, sv);
@@ -4103,7 +4296,7 @@ void el_ctx::closure_state() {
   host_ev[EL_K_INIT][EL_EV_RMW] += n_init;
   host_ev[EL_K_INIT][EL_EV_EMIT] += n_init;
   // ---- base links / propagations and the layouts they ask for
-  if (base) {
+  {
     const uint32_t n32 = (uint32_t)N, p32 = (uint32_t)P;
     if (nb) elcl::base_links(stream, cax, cl, lo, hi, cpos[1], llog_x, llog_p);
     if (P) {
@@ -4125,7 +4318,16 @@ void el_ctx::closure_state() {
       PR.laid = true;
     }
     if (SC.live) {
-      launch_gap_scan(cl.nd + elcl::ND_SC * (N + 1), n32, SC.start0);
+      const uint32_t* sc_cap = cl.nd + elcl::ND_SC * (N + 1);
+      if (part()) {  // the own rows' capacities only (T_SC sized the slots): other rows grow on demand
+        if (!sc_own) sc_own = dalloc<uint32_t>(N + 1);
+        HIPCHK(hipMemsetAsync(sc_own, 0, (N + 1) * sizeof(uint32_t), stream));
+        if (hi > lo)
+          HIPCHK(hipMemcpyAsync(sc_own + lo, sc_cap + lo, (uint64_t)(hi - lo) * sizeof(uint32_t),
+                                hipMemcpyDeviceToDevice, stream));
+        sc_cap = sc_own;
+      }
+      launch_gap_scan(sc_cap, n32, SC.start0);
       SC.laid = true;
     }
     if (PP.live) {
@@ -4137,7 +4339,8 @@ void el_ctx::closure_state() {
   }
   for (GapCsr* g : {&PR, &SC, &PP}) {
     if (!g->live) continue;
-    hipLaunchKernelGGL(k_gap_init, dim3(grid_for(g->rows + 1)), dim3(BLOCK), 0, stream, g->start, g->len, g->rows,
+    g->used = g->laid ? g->total0 : (uint64_t)gap_cap(0) * g->rows;
+    hipLaunchKernelGGL(k_gap_init, dim3(grid_for(g->rows + 1)), dim3(BLOCK), 0, stream, g->start, g->end, g->len, g->rows,
                        g->laid ? g->start0 : nullptr);
     HIPCHK(hipGetLastError());
   }
@@ -4153,7 +4356,7 @@ void el_ctx::closure_state() {
 // the second did before; its queues start at what the second got.  The CPU oracle installs the
 // same links (el_oracle.c, base_links).
 void el_ctx::install_base() {
-  if (nb == 0 || l_count != 0 || part()) return;
+  if (nb == 0 || l_count != 0) return;
   const uint64_t trig = s_count + nb;
   if (!small_queues) {
     if (const uint64_t want = std::min<uint64_t>(4 * trig, 1ull << 28); want > cs_cap) {
@@ -4199,7 +4402,7 @@ void el_ctx::install_base() {
   // them instead costs 25 M + 2.6 M random CAS on G3 (k_rehash, ≈2.3 ms each beside the first
   // superstep).  EL_BASE_JOIN=1 restores that fill (A/B only: the CPU oracle counts the
   // binary searches, so the event parity holds without it).
-  if (getenv("EL_BASE_JOIN")) {
+  if (getenv("EL_BASE_JOIN") && !part()) {
     HIPCHK(hipEventRecord(ev_base[0], stream));
     HIPCHK(hipStreamWaitEvent(rstream, ev_base[0], 0));
     hipLaunchKernelGGL(k_rehash, dim3(grid_for(nb, 2048)), dim3(BLOCK), 0, rstream, lhash, lhash_cap - 1, llog_x,
@@ -4216,6 +4419,16 @@ void el_ctx::install_base() {
   // the log entries read and written, the rows' entries
   host_ev[EL_K_INIT][EL_EV_ENT] += nb + (PR.live ? nb : 0) + (SC.live ? nc : 0);
   host_ev[EL_K_INIT][EL_EV_EMIT] += nb;
+  if (part()) {
+    // the chain-second base links join the replicated chain-link log (the triggers of CR6 with
+    // their role second, expand_x); those and the base propagations that other ranks' rows can
+    // reach go into the send queues of the first exchange (the commit routes every later one)
+    DState st = dstate();
+    hipLaunchKernelGGL(k_base_route, dim3(grid_for(std::max(nb, nbp))), dim3(BLOCK), 0, stream, ix, st, (uint32_t)nb,
+                       props ? (uint32_t)nbp : 0u);
+    HIPCHK(hipGetLastError());
+    x_count = nc;
+  }
 }
 
 // Streamed result, in two halves so that no copy work sits between two supersteps:
@@ -4245,7 +4458,7 @@ void el_ctx::stream_flush() {
   auto dma = [&](uint32_t* dst, uint32_t* dst_dev, const uint32_t* src, uint64_t a, uint64_t b, uint64_t cap) {
     b = std::min(b, cap);
     if (!dst || b <= a) return;
-    if (dst_dev)
+    if (dst_dev && !dma_hostptr)
       HIPCHK(hipMemcpyAsync(dst_dev + a, src + a, (b - a) * sizeof(uint32_t), hipMemcpyDeviceToDeviceNoCU, dstream));
     else
       HIPCHK(hipMemcpyAsync(dst + a, src + a, (b - a) * sizeof(uint32_t), hipMemcpyDeviceToHost, dstream));
@@ -4288,7 +4501,11 @@ void el_ctx::runs_out(bool wait) {
   for (int w = 0; w < 2; ++w) {
     const uint64_t n = std::min<uint64_t>(rtot_h[w], caps[w]);
     if (!devs[w] || n <= run_sent[w]) continue;
-    HIPCHK(hipMemcpyAsync(devs[w] + run_sent[w], srcs[w] + run_sent[w], (n - run_sent[w]) * sizeof(uint2),
+    if (dma_hostptr)
+      HIPCHK(hipMemcpyAsync(reinterpret_cast<uint2*>(w ? strm->l_run : strm->s_run) + run_sent[w], srcs[w] + run_sent[w],
+                            (n - run_sent[w]) * sizeof(uint2), hipMemcpyDeviceToHost, dstream));
+    else
+      HIPCHK(hipMemcpyAsync(devs[w] + run_sent[w], srcs[w] + run_sent[w], (n - run_sent[w]) * sizeof(uint2),
                             hipMemcpyDeviceToDeviceNoCU, dstream));
     run_sent[w] = n;
   }
@@ -4473,14 +4690,68 @@ void el_ctx::migrate_state(uint32_t N0, const std::vector<uint32_t>& pmap) {
   stats_stale = true;
 }
 
-void el_ctx::gap_rebuild_all() {
+// The rows of the gapped CSRs that overflowed in this step move, each alone, to gap_cap(len)
+// fresh slots at the end of its CSR's slot array (the other rows stay where they are): the
+// first overflow record of a row claims it and reserves its slots (k_reloc_claim), one readback
+// of the slot tails grows an array that would not hold them, then the rows' in-place entries and
+// the overflow entries land in the new slots (k_reloc_move) and the rows' bounds switch
+// (k_reloc_commit).  Events (the CPU oracle counts the same, el_oracle.c gap_step_end): the
+// overflow records read and claimed, the rows relocated, their moved and placed entries.
+void el_ctx::gap_relocate_all() {
   const uint32_t ov[3] = {hc.ov_pr, hc.ov_sc, hc.ov_pp};
   if (!(ov[0] | ov[1] | ov[2])) return;
   GapCsr* gs[3] = {&PR, &SC, &PP};
-  const uint64_t entries[3] = {l_count, part() ? x_count : l_count, p_count};
-  for (int i = 0; i < 3; ++i)
-    if (ov[i]) gap_rebuild(*gs[i], ov[i], entries[i]);
-  // the overflow counters start over (stream-ordered after the re-layout kernels)
+  if (!reloc_rc) {
+    reloc_rc = dalloc<unsigned long long>(9);
+    HIPCHK(hipHostMalloc((void**)&reloc_h, 18 * sizeof(unsigned long long), hipHostMallocDefault));
+  }
+  unsigned long long* init_h = reloc_h + 9;  // (a separate pinned block: the readback lands in reloc_h)
+  auto args = [&](int i) {
+    GapCsr& g = *gs[i];
+    return Reloc{g.start, g.end, g.len, g.val, g.ovq, ov[i], g.flag, g.nstart, g.rlist, reloc_rc + 3 * i};
+  };
+  for (int i = 0; i < 3; ++i) {
+    init_h[3 * i] = gs[i]->used;
+    init_h[3 * i + 1] = init_h[3 * i + 2] = 0;
+  }
+  HIPCHK(hipMemcpyAsync(reloc_rc, init_h, 9 * sizeof(unsigned long long), hipMemcpyHostToDevice, stream));
+  for (int i = 0; i < 3; ++i) {
+    if (!ov[i]) continue;
+    if (ov[i] > gs[i]->ovq_cap) throw std::runtime_error("gapped-CSR overflow queue overrun");
+    launch(EL_K_SCAN, [&] { hipLaunchKernelGGL(k_reloc_claim, dim3(grid_for(ov[i])), dim3(BLOCK), 0, stream, args(i)); });
+  }
+  HIPCHK(hipMemcpyAsync(reloc_h, reloc_rc, 9 * sizeof(unsigned long long), hipMemcpyDeviceToHost, stream));
+  sync();
+  for (int i = 0; i < 3; ++i) {
+    if (!ov[i]) continue;
+    GapCsr& g = *gs[i];
+    const uint64_t tail = reloc_h[3 * i], nrows = reloc_h[3 * i + 1] & 0xffffffffull, moved = reloc_h[3 * i + 2];
+    if (tail > 0xffffffffull) throw ElError{EL_ENOMEM, "gapped CSR beyond 2^32 slots"};
+    if (tail > g.val_cap) {  // (the stream is idle: the readback synchronised it)
+      const uint64_t c = std::min<uint64_t>(tail + tail / 2, 0xffffffffull);
+      dgrow(g.val, g.used, c);
+      g.val_cap = c;
+    }
+    const uint32_t nb = (uint32_t)std::min<uint64_t>(nrows, 2048);
+    launch(EL_K_SCATTER_OLD, [&] {
+      hipLaunchKernelGGL(k_reloc_move, dim3(nb + grid_for(ov[i])), dim3(BLOCK), 0, stream, args(i), nb);
+    });
+    launch(EL_K_MERGE_PTR, [&] {
+      hipLaunchKernelGGL(k_reloc_commit, dim3(grid_for(nrows)), dim3(BLOCK), 0, stream, args(i));
+    });
+    g.used = tail;
+    host_ev[EL_K_SCAN][EL_EV_TRIG] += ov[i];
+    host_ev[EL_K_SCAN][EL_EV_RMW] += ov[i];
+    host_ev[EL_K_SCAN][EL_EV_ROW] += nrows;
+    host_ev[EL_K_MERGE_PTR][EL_EV_ENT] += 2 * nrows;
+    host_ev[EL_K_SCATTER_OLD][EL_EV_TRIG] += moved;
+    host_ev[EL_K_SCATTER_OLD][EL_EV_ENT] += moved;
+    host_ev[EL_K_SCATTER_OLD][EL_EV_EMIT] += moved;
+    host_ev[EL_K_SCATTER_NEW][EL_EV_TRIG] += ov[i];
+    host_ev[EL_K_SCATTER_NEW][EL_EV_ENT] += 3ull * ov[i];
+    host_ev[EL_K_SCATTER_NEW][EL_EV_EMIT] += ov[i];
+  }
+  // the overflow counters start over (stream-ordered after the relocation kernels)
   HIPCHK(hipMemsetAsync(&ctr->ov_pr, 0, 3 * CTR_STRIDE * sizeof(uint32_t), stream));
   hc.ov_pr = hc.ov_sc = hc.ov_pp = 0;
 }
@@ -4788,7 +5059,8 @@ int el_saturate(el_ctx* c, el_stats* stats) {
   if (!c->inited) return fail(c, EL_ESTATE, "el_saturate before el_init");
   return guarded(c, [&] {
     auto t0 = std::chrono::steady_clock::now();
-    if (c->fresh && !c->part()) c->install_base();
+    if (c->part() && !c->part_fixpoint) c->exchange_windows();  // (collective, once per el_load)
+    if (c->fresh) c->install_base();
     c->fresh = false;
     c->stream_mark();  // (a streamed result: the init facts and base links go beside the first superstep)
     // all rule types share one frontier: start at the oldest watermark
@@ -5299,6 +5571,8 @@ void el_destroy(el_ctx* c) {
   c->copy_pending = false;
   c->free_state();
   c->free_index();
+  dfree(c->reloc_rc);
+  if (c->reloc_h) (void)hipHostFree(c->reloc_h);
   dfree(c->rcnt);
   dfree(c->roff);
   dfree(c->rscan_tmp);

@@ -1071,29 +1071,33 @@ static void gap_append_ev(elo_ctx* c, int K, uint64_t n, uint32_t cap, uint64_t*
   }
 }
 
-/* analytic events of a re-layout (and formerly of a CSR merge) with old_n moved and nn
- * placed entries (same formula as the GPU host side): the row capacities and their scan,
- * old and new row starts, the moved entries, and the overflow entries placed by rank */
-static void merge_seg_events(elo_ctx* c, uint64_t nrows, uint64_t old_n, uint64_t nn) {
-  uint64_t n1 = nrows + 1;
-  EVN(EL_K_SCAN, EL_EV_ENT, 3 * n1);
-  EVN(EL_K_MERGE_PTR, EL_EV_ENT, 2 * n1);
-  EVN(EL_K_SCATTER_OLD, EL_EV_TRIG, old_n);
-  EVN(EL_K_SCATTER_OLD, EL_EV_ENT, old_n);
-  EVN(EL_K_SCATTER_OLD, EL_EV_EMIT, old_n);
-  EVN(EL_K_SCATTER_NEW, EL_EV_TRIG, nn);
-  EVN(EL_K_SCATTER_NEW, EL_EV_ENT, 3 * nn);
-  EVN(EL_K_SCATTER_NEW, EL_EV_EMIT, nn);
-}
-
+/* A step's overflowing rows are relocated, each alone, to GAP_CAP(n) fresh slots (the GPU's
+ * gap_relocate_all; every other row keeps its capacity).  Events: the overflow records read
+ * and claimed, the rows relocated (their bounds read and written), their in-place entries
+ * moved (a full row: its old capacity) and the overflow entries placed by rank. */
 static void gap_step_end(elo_ctx* c, const vec* rows, uint32_t R, uint32_t* cap, uint64_t* ov, uint64_t entries) {
   uint32_t r;
-  if (!*ov) return;
-  if (getenv("ELO_GAPTRACE")) /* diagnostic: which gapped CSR re-lays out after which step */
-    fprintf(stderr, "step %u relayout rows %u ovf %llu entries %llu\n", c->supersteps, R, (unsigned long long)*ov,
+  uint64_t nrows = 0, moved = 0, n = *ov;
+  if (!n) return;
+  if (getenv("ELO_GAPTRACE")) /* diagnostic: which gapped CSR relocates rows after which step */
+    fprintf(stderr, "step %u relocate rows %u ovf %llu entries %llu\n", c->supersteps, R, (unsigned long long)n,
             (unsigned long long)entries);
-  merge_seg_events(c, R, entries - *ov, *ov);
-  for (r = 0; r < R; ++r) cap[r] = GAP_CAP(rows[r].n);
+  for (r = 0; r < R; ++r)
+    if (rows[r].n > cap[r]) {
+      ++nrows;
+      moved += cap[r];
+      cap[r] = GAP_CAP(rows[r].n);
+    }
+  EVN(EL_K_SCAN, EL_EV_TRIG, n);
+  EVN(EL_K_SCAN, EL_EV_RMW, n);
+  EVN(EL_K_SCAN, EL_EV_ROW, nrows);
+  EVN(EL_K_MERGE_PTR, EL_EV_ENT, 2 * nrows);
+  EVN(EL_K_SCATTER_OLD, EL_EV_TRIG, moved);
+  EVN(EL_K_SCATTER_OLD, EL_EV_ENT, moved);
+  EVN(EL_K_SCATTER_OLD, EL_EV_EMIT, moved);
+  EVN(EL_K_SCATTER_NEW, EL_EV_TRIG, n);
+  EVN(EL_K_SCATTER_NEW, EL_EV_ENT, 3 * n);
+  EVN(EL_K_SCATTER_NEW, EL_EV_EMIT, n);
   *ov = 0;
 }
 

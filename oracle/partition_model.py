@@ -25,10 +25,13 @@ One Jacobi superstep reads only the state after step t-1 and the deltas of t-1:
   Δacts          owned X with Y ∈ S(X) get C          (K10, ScriptsCollection.java:45-62)
   Δchain links   (X, r, Y), r second of p ∘ r ⊑ t: preds[(p, X)] × (·, t, Y)
 
-then commits locally, and ALL-GATHERS its new props, new activations and new chain links
-(the delta exchange of SURVEY.md §8(e)); every rank imports them.  The fixpoint is
-reached when the sum over ranks of all deltas is zero (the all-gathered counts double as
-the termination reduction, CommunicationHandler.java:49-84).
+then commits locally — its own new props, activations and chain links join its replicated
+sets at once — and ALL-GATHERS those some OTHER rank can use (the delta exchange of SURVEY.md
+§8(e)): a record keyed by concept y (((r, y), B), (y, C), (y, s, z)) only matters to a rank whose
+rows can reach y, i.e. y in its column window (el_ctx::column_window: the span of every concept
+its rows can hold), so only those are sent; every rank imports the others'.  The fixpoint is
+reached when the sum over ranks of all local deltas (and records sent) is zero (the
+all-gathered counts double as the termination reduction, CommunicationHandler.java:49-84).
 """
 from __future__ import annotations
 
@@ -86,6 +89,8 @@ class Rank:
     def __init__(self, ax, lo: int, hi: int):
         self.k = _Static(ax)
         self.lo, self.hi = lo, hi
+        self.win = self._window()
+        self.others: List[Tuple[int, int]] = []  # the other ranks' windows (set_windows)
         self.S: Dict[int, Set[int]] = {}
         self.links: Set[Tuple[int, int, int]] = set()
         self.preds: Dict[Tuple[int, int], Set[int]] = defaultdict(set)
@@ -103,6 +108,58 @@ class Rank:
             if self.k.plain(x) and x != BOTTOM:
                 self.S[x].add(TOP)
                 self.dS.append((x, TOP))
+
+    def _window(self) -> Tuple[int, int]:
+        """[c_lo, c_hi): the span of every concept the owned rows can hold — closed under told
+        supers, conjunction conclusions, existential fillers and CR4 conclusions, and the domains
+        and ranges of every role their links can carry (an existential's role, its super-roles and
+        the chains' results), as el_ctx::column_window computes it."""
+        k = self.k
+        seen = set(range(self.lo, self.hi)) | {BOTTOM, TOP}
+        stack = sorted(seen)  # (⊥ and ⊤ are in every row: their closures too)
+        roles, rstack = set(), []
+
+        def add(c):
+            if c not in seen:
+                seen.add(c)
+                stack.append(c)
+
+        def add_role(r):
+            if r not in roles:
+                roles.add(r)
+                rstack.append(r)
+        while stack or rstack:
+            if stack:
+                a = stack.pop()
+                for b in k.told[a]:
+                    add(b)
+                for _, b in k.conj_of[a]:
+                    add(b)
+                for r, b in k.exr[a]:
+                    add(b)
+                    add_role(r)
+                for _, b in k.exl[a]:
+                    add(b)
+                continue
+            r = rstack.pop()
+            for s in k.sup[r]:
+                add_role(s)
+            for _, t in k.chf[r]:
+                add_role(t)
+            for _, t in k.chs[r]:
+                add_role(t)
+            for c in k.dom[r] + k.rng[r]:
+                add(c)
+        inner = [c for c in seen if c >= 2]
+        return (min(inner), max(inner) + 1) if inner else (2, 2)
+
+    def set_windows(self, wins: Sequence[Tuple[int, int, Tuple[int, int]]]) -> None:
+        """Every rank's (lo, hi, window), all-gathered once (el_ctx::exchange_windows)."""
+        self.others = [w for lo, hi, w in wins if (lo, hi) != (self.lo, self.hi)]
+
+    def remote(self, y: int) -> bool:
+        """Some other rank's rows can reach concept y (⊥ and ⊤ are in every window)."""
+        return any(y < 2 or lo <= y < hi for lo, hi in self.others)
 
     # -- generation + local commit; returns the records to all-gather
     def step(self):
@@ -164,12 +221,27 @@ class Rank:
         new_p = sorted(p for p in cp if p[1] not in self.props[p[0]])
         new_a = sorted(a for a in ca if a not in self.acts)
         new_x = [l for l in self.dL if k.chs[l[1]]]
-        return {"props": new_p, "acts": new_a, "xlinks": new_x, "ds": len(self.dS), "dl": len(self.dL)}
+        self._own = (new_p, new_a, new_x)
+        return {"props": [p for p in new_p if self.remote(p[0][1])], "acts": [a for a in new_a if self.remote(a[0])],
+                "xlinks": [l for l in new_x if self.remote(l[0])], "ds": len(self.dS), "dl": len(self.dL),
+                "dp": len(new_p), "da": len(new_a), "dx": len(new_x), "rows": (self.lo, self.hi)}
 
-    # -- import of every rank's records (own included)
+    # -- this rank's own new records, then the other ranks' records it was sent
     def absorb(self, gathered: Sequence[dict]) -> int:
         dP, dA, dX = [], [], []
+        own_p, own_a, own_x = self._own
+        for pid, b in own_p:
+            self.props[pid].add(b)
+            dP.append((pid, b))
+        for y, c in own_a:
+            self.acts.add((y, c))
+            dA.append((y, c))
+        for x, r, y in own_x:
+            self.succ[x].add((r, y))
+            dX.append((x, r, y))
         for g in gathered:
+            if g["rows"] == (self.lo, self.hi):
+                continue
             for pid, b in g["props"]:
                 if b not in self.props[pid]:
                     self.props[pid].add(b)
@@ -182,11 +254,14 @@ class Rank:
                 self.succ[x].add((r, y))
                 dX.append((x, r, y))
         self.dP, self.dA, self.dX = dP, dA, dX
-        return sum(g["ds"] + g["dl"] + len(g["props"]) + len(g["acts"]) + len(g["xlinks"]) for g in gathered)
+        return sum(g["ds"] + g["dl"] + g["dp"] + g["da"] + g["dx"] + len(g["props"]) + len(g["acts"]) +
+                   len(g["xlinks"]) for g in gathered)
 
 
-def run(rank: Rank, allgather: Callable[[dict], List[dict]], max_steps: int = 100000) -> int:
-    """Drive one rank to the global fixpoint; returns the superstep count."""
+def run(rank: Rank, allgather: Callable[[object], List[object]], max_steps: int = 100000) -> int:
+    """Drive one rank to the global fixpoint (after the one-time window exchange); returns the
+    superstep count."""
+    rank.set_windows(allgather((rank.lo, rank.hi, rank.win)))
     for t in range(1, max_steps + 1):
         if rank.absorb(allgather(rank.step())) == 0:
             return t
@@ -203,6 +278,9 @@ def saturate_inprocess(ax, parts: int, compat_range: bool = True):
         from distel_amd import ir
         ax = ir.elk_ranges(ax)[0]
     rs = [Rank(ax, lo, hi) for lo, hi in ranges(ax.n_concepts, parts)]
+    wins = [(r.lo, r.hi, r.win) for r in rs]
+    for r in rs:
+        r.set_windows(wins)
     t = 0
     while True:
         t += 1

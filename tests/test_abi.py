@@ -116,7 +116,7 @@ def test_stream_run_decode():
     assert fx.tolist() == [10] * 6 + [11] and fb.tolist() == [1, 2, 3, 4, 5, 7, 9]
     s.s_run = np.array([[10, 2], [11, 6]], np.uint32)
     s.n_s_runs = 2
-    with pytest.raises(AssertionError):
+    with pytest.raises(ValueError):
         s.fact_rows()
     empty = engine.Stream()
     empty.s_b, empty.s_run = np.zeros(0, np.uint32), np.zeros((0, 2), np.uint32)

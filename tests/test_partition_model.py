@@ -90,3 +90,42 @@ def test_partition_model_gloo_two_ranks():
             R |= set(links)
         assert len(steps) == 1          # every rank stops at the same superstep
         assert S == S0 and R == R0, seed
+
+
+def test_partition_model_aligned_copies_send_nothing():
+    """OntologyMultiplier copies on ranks aligned with them: no record is routed to another
+    rank (no other window holds a copy's concepts) — the exchange carries the counts only —
+    and the union is still the naive closure of the whole ×k ontology."""
+    from distel_amd import ir
+    aligned = 0
+    for seed in range(120):
+        if aligned >= 6:
+            break
+        base = generators.random_small(500 + seed, n=12 + seed % 20, n_roles=1 + seed % 3)
+        k = 3
+        ax = ir.replicate(base, k)
+        bounds = [ir.copy_slice(base, k, i) for i in range(k)]
+        bounds[0] = (0, bounds[0][1])
+        rs = [pm.Rank(ax, lo, hi) for lo, hi in bounds]
+        wins = [(r.lo, r.hi, r.win) for r in rs]
+        for r in rs:
+            r.set_windows(wins)
+        # (a base with axioms on ⊤ — ⊤ ⊑ C — puts every copy's C into every row: those copies are
+        # not disjoint, and their windows overlap)
+        disjoint = all(w[1] <= v[0] or v[1] <= w[0] for i, (_, _, w) in enumerate(wins) for _, _, v in wins[i + 1:])
+        aligned += disjoint
+        while True:
+            out = [r.step() for r in rs]
+            for o in out:
+                if disjoint:  # (⊥ / ⊤-keyed records are in every window: the copies share them)
+                    assert all(p[0][1] < 2 for p in o["props"]) and all(a[0] < 2 for a in o["acts"]), seed
+                    assert all(x[0] < 2 for x in o["xlinks"]), seed
+            if [r.absorb(out) for r in rs][0] == 0:
+                break
+        S, R = {}, set()
+        for r in rs:
+            S.update(r.S)
+            R |= r.links
+        S0, R0 = naive.saturate(ax, distel_range=True)
+        assert S == S0 and R == R0, seed
+    assert aligned >= 6, aligned
