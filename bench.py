@@ -50,6 +50,18 @@ sys.path.insert(0, ROOT)
 # Two engines in flight use 8 HIP streams; with HIP's default of 4 hardware queues, streams of
 # different engines would share a queue and one engine's DMAs would hold up the other's kernels.
 os.environ.setdefault("GPU_MAX_HW_QUEUES", "12")
+# One GPU: load the system ROCm HIP runtime — the one libel_gpu.so is built against — before
+# torch brings its bundled copy under the same soname (whichever loads first serves the whole
+# process).  With torch's runtime the streamed result's D2H copies into page-locked memory run as
+# blit kernels on the CUs (scripts/micro/d2h_py.py: __amd_rocclr_copyBuffer in the trace, ≈14 ms of
+# CU time per G3 classification beside the supersteps); with the system runtime they go to an SDMA
+# engine and a rocprofv3 kernel trace of the timed step stays within 6 % of its untraced time
+# (round-4 A/B: no change in the untraced time itself).  Multi-rank runs keep torch's runtime (its
+# RCCL and process groups are built against it).  EL_HIP_RUNTIME=torch selects torch's at N = 1.
+if (os.environ.get("EL_HIP_RUNTIME", "system") == "system" and int(os.environ.get("WORLD_SIZE", "1")) == 1
+        and "torch" not in sys.modules and os.path.exists("/opt/rocm/lib/libamdhip64.so.7")):
+    import ctypes
+    ctypes.CDLL("/opt/rocm/lib/libamdhip64.so.7", mode=ctypes.RTLD_GLOBAL)
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 

@@ -541,8 +541,10 @@ __device__ __forceinline__ uint32_t lds_reserve(uint32_t* qn, bool pred) {
 // global atomic (WQ records).  No block barrier is involved, so a wave may flush in the
 // middle of a divergent inner loop (a told closure, a fan-out row): only the wave's
 // active lanes take part, and LDS accesses of one wave execute in program order.
+// 128 records: 20.7 KB of LDS per block, so VGPRs (not LDS) bound k_expand's occupancy at 7 waves
+// per SIMD instead of 4 (G3 A/B, round 4: 26.09 / 25.93 vs 26.19 / 26.51 ms per classification).
 #ifndef EL_WQ
-#define EL_WQ 256
+#define EL_WQ 128
 #endif
 constexpr uint32_t WQ = EL_WQ;  // (x, a) / (x, pid) records per wave and queue
 constexpr uint32_t WQJ = 64;   // fan-out job records per wave

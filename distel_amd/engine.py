@@ -27,7 +27,7 @@ EL_RESULT_ASYNC = 0x2    # el_result.flags: return once enqueued; el_result_wait
 
 # work phases (el_kernel); "kernel:role" where several phases share one launch
 KERNEL_NAMES = ["k_expand:s", "k_expand:l", "k_jobs", "k_expand:a", "k_commit:s", "k_commit:l", "k_commit:a",
-                "k_gap_caps", "k_gap_caps:scan", "k_gap_move", "k_gap_ovf", "k_init", "k_rehash",
+                "k_reloc_claim", "k_reloc_commit", "k_reloc_move", "k_reloc_move:ovf", "k_init", "k_rehash",
                 "k_expand:p", "k_commit:p", "k_commit_told", "k_closure"]
 EVENT_NAMES = ["trig", "row", "ent", "test", "hash", "emit", "job", "rmw"]
 EVENT_BYTES = [8, 8, 4, 4, 8, 8, 16, 8]

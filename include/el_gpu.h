@@ -135,11 +135,13 @@ typedef struct el_axioms {
 
 /* Row partition of the concept space.  A partitioned context owns the
  * rows S(X), X in [row_lo, row_hi), and the links (X, r, Y) of those X; CR4 propagations,
- * range activations and the links of chain-second roles are replicated.  Every
- * superstep all-gathers each rank's new propagations / activations / chain links (the
- * delta exchange) and the per-rank delta counts, whose sum is the termination test
- * (replaces the "anything new?" broadcast, CommunicationHandler.java:49-84).  All ranks
- * of a group must call el_init / el_saturate together (they are collective). */
+ * range activations and the links of chain-second roles are replicated where they can matter.
+ * Every superstep all-gathers the per-rank delta counts, whose sum is the termination test
+ * (replaces the "anything new?" broadcast, CommunicationHandler.java:49-84), and each rank's
+ * new propagations / activations / chain links that some OTHER rank's rows can reach (the
+ * delta exchange; every rank's column window is all-gathered once, at the first el_saturate
+ * after el_load).  All ranks of a group must call el_saturate together (it is collective),
+ * except a re-stream at the fixpoint after EL_ERANGE, which runs no superstep. */
 #define EL_XCHG_NONE  0   /* whole ontology, no partition (the default) */
 #define EL_XCHG_LOCAL 1   /* in-process group: one context per thread (el_group_create) */
 #define EL_XCHG_RCCL  2   /* one context per process/GPU, RCCL all-gather over xGMI */
@@ -205,10 +207,10 @@ typedef enum el_kernel {
   EL_K_COMMIT_S = 4,     /* k_commit, S role:    bit-row atomicOr dedup + ΔS append */
   EL_K_COMMIT_L = 5,     /* k_commit, link role: link hash-set dedup + Δlink append */
   EL_K_COMMIT_A = 6,     /* k_commit, activation role: activation set dedup */
-  EL_K_SCAN = 7,         /* k_gap_caps: re-layout of a gapped CSR whose rows overflowed: row capacities */
-  EL_K_MERGE_PTR = 8,    /*   … and their scan into new row starts (library scan, carried by k_gap_caps) */
-  EL_K_SCATTER_OLD = 9,  /* k_gap_move: in-place entries to their new rows */
-  EL_K_SCATTER_NEW = 10, /* k_gap_ovf: overflow entries placed at their rank */
+  EL_K_SCAN = 7,         /* k_reloc_claim: gapped-CSR rows that overflowed claim fresh slots */
+  EL_K_MERGE_PTR = 8,    /* k_reloc_commit: the relocated rows' new bounds */
+  EL_K_SCATTER_OLD = 9,  /* k_reloc_move: a relocated row's in-place entries to its new slots */
+  EL_K_SCATTER_NEW = 10, /*   … and the overflow entries placed at their rank (same launch) */
   EL_K_INIT = 11,        /* k_init_facts: S(X) = {X, ⊤} ∪ told*(X); the base links / propagations */
   EL_K_REHASH = 12,      /* k_rehash:    link / activation / propagation set growth */
   EL_K_EXPAND_P = 13,    /* k_expand, propagation role: new CR4 propagations × predecessors */

@@ -776,10 +776,37 @@ static int prop_known(elo_ctx* c, int kern, uint32_t pid, uint32_t b, int pempty
 
 /* predecessor / succ / S-row "CSR" views: begin offset is irrelevant on the CPU, the
  * job carries the list identity (kind + owner) instead */
+/* diagnostic (ELO_CR1STAT): per superstep, the CR1 told-closure walk — facts walked, entries
+ * tested, entries already in S(X), distinct (X, B) among the tested entries */
+static int cr1_stat = -1;
+static uint64_t cr1_facts, cr1_tests, cr1_hit, cr1_n, cr1_cap;
+static uint64_t* cr1_keys;
+static int cmp_u64(const void* a, const void* b) {
+  const uint64_t x = *(const uint64_t*)a, y = *(const uint64_t*)b;
+  return x < y ? -1 : x > y;
+}
+static void cr1_report(uint32_t step) {
+  uint64_t i, u = 0;
+  if (cr1_stat <= 0) return;
+  qsort(cr1_keys, cr1_n, sizeof(uint64_t), cmp_u64);
+  for (i = 0; i < cr1_n; ++i) u += i == 0 || cr1_keys[i] != cr1_keys[i - 1];
+  fprintf(stderr, "cr1 step %u facts %llu tests %llu already %llu distinct %llu%s\n", step,
+          (unsigned long long)cr1_facts, (unsigned long long)cr1_tests, (unsigned long long)cr1_hit,
+          (unsigned long long)u, cr1_n < cr1_tests ? " (distinct over a prefix)" : "");
+  cr1_facts = cr1_tests = cr1_hit = cr1_n = 0;
+}
+
 static void expand_s(elo_ctx* c, cands* k, uint32_t mask, uint64_t b, uint64_t e, uint64_t a_end) {
   const int K = EL_K_EXPAND_S;
   uint64_t i;
   uint32_t j;
+  if (cr1_stat < 0) {
+    cr1_stat = getenv("ELO_CR1STAT") != NULL;
+    if (cr1_stat) {
+      cr1_cap = 1ull << 28;
+      cr1_keys = (uint64_t*)malloc(cr1_cap * sizeof(uint64_t));
+    }
+  }
   for (i = b; i < e; ++i) {
     uint32_t X = c->slog_x.v[i], A = c->slog_a.v[i];
     EV(K, EL_EV_TRIG);
@@ -788,10 +815,16 @@ static void expand_s(elo_ctx* c, cands* k, uint32_t mask, uint64_t b, uint64_t e
     if (mask & M_R1) {
       if (!c->slog_f.v[i]) {
         EV(K, EL_EV_ROW);
+        if (cr1_stat) cr1_facts++;
         for (j = c->toldc.ptr[A]; j < c->toldc.ptr[A + 1]; ++j) {
           uint32_t B = c->toldc.a[j];
           EV(K, EL_EV_ENT);
           EV(K, EL_EV_TEST);
+          if (cr1_stat) {
+            cr1_tests++;
+            cr1_hit += bit(c, X, B) ? 1 : 0;
+            if (cr1_n < cr1_cap) cr1_keys[cr1_n++] = ((uint64_t)X << 32) | B;
+          }
           if (!bit(c, X, B)) {
             EV(K, EL_EV_EMIT);
             vpush(&k->s1x, X);
@@ -1107,12 +1140,15 @@ static int superstep(elo_ctx* c, uint32_t mask, uint64_t sb, uint64_t se, uint64
   size_t i;
   uint64_t s0 = c->slog_x.n, l0 = c->llog_x.n, a0 = c->alog_y.n, p0 = c->plog_p.n;
   int do_a = (mask & M_RRNG) && ae > ab, do_p = (mask & M_R4P) && pe > pb;
+  uint64_t ev0[EL_NUM_KERNELS][EL_NUM_EVENTS];
   if (!(se > sb || le > lb || do_a || do_p)) return 0;
+  memcpy(ev0, c->ev, sizeof ev0);
   if (c->llog_x.n == c->l_base) mask |= M_LEMPTY; /* empty sets: their probes are skipped (as on the GPU) */
   if (c->plog_p.n == c->p_base) mask |= M_PEMPTY;
   memset(&k, 0, sizeof k);
   /* generation: reads only the state of the previous step */
   expand_s(c, &k, mask, sb, se, a0);
+  cr1_report(c->supersteps);
   expand_l(c, &k, mask, lb, le);
   if (do_a) expand_a(c, &k, se, ab, ae);
   if (do_p) expand_p(c, &k, pb, pe);
@@ -1194,6 +1230,17 @@ static int superstep(elo_ctx* c, uint32_t mask, uint64_t sb, uint64_t se, uint64
   gap_step_end(c, c->pred, c->P, c->cap_pr, &c->ov_pr, c->llog_x.n);
   gap_step_end(c, c->succ, c->N, c->cap_sc, &c->ov_sc, c->llog_x.n);
   gap_step_end(c, c->prow, c->P, c->cap_pp, &c->ov_pp, c->plog_p.n);
+  if (getenv("ELO_STEPEV")) { /* diagnostic: this superstep's events per kernel (nonzero rows) */
+    int kk, ee;
+    for (kk = 0; kk < EL_NUM_KERNELS; ++kk) {
+      uint64_t tot = 0;
+      for (ee = 0; ee < EL_NUM_EVENTS; ++ee) tot += c->ev[kk][ee] - ev0[kk][ee];
+      if (!tot) continue;
+      fprintf(stderr, "stepev %u k%d", c->supersteps, kk);
+      for (ee = 0; ee < EL_NUM_EVENTS; ++ee) fprintf(stderr, " %llu", (unsigned long long)(c->ev[kk][ee] - ev0[kk][ee]));
+      fprintf(stderr, "\n");
+    }
+  }
   return c->slog_x.n > s0 || c->llog_x.n > l0 || c->alog_y.n > a0 || c->plog_p.n > p0;
 }
 

@@ -8,6 +8,7 @@
 //   C  B behind an event (hipEventReleaseToSystem) recorded on s0 after a kernel
 //   D  A behind that event
 //   E  dst = host pointer, kind Default
+// (argv[1]: run only the case with that letter, so each case can get a trace of its own)
 // Build: hipcc --offload-arch=gfx950 -O2 scripts/micro/d2h_mode.hip -o scripts/micro/d2h_mode
 #include <hip/hip_runtime.h>
 
@@ -33,7 +34,8 @@ __global__ void k_read(const uint4* __restrict__ a, size_t n, unsigned* out) {
   if (s == 0x12345678u) out[0] = s;
 }
 
-int main() {
+int main(int argc, char** argv) {
+  const char only = argc > 1 ? argv[1][0] : 0;  // one case (its letter), or all
   const size_t cb = 64ull << 20, kb = 2ull << 30;
   void *d, *big, *h;
   unsigned* o;
@@ -62,6 +64,7 @@ int main() {
                {"D dev-dst D2D-NoCU after event", true, true, hipMemcpyDeviceToDeviceNoCU},
                {"E host-dst Default", false, false, hipMemcpyDefault}};
   for (auto& c : cases) {
+    if (only && c.name[0] != only) continue;
     CK(hipDeviceSynchronize());
     const auto t0 = std::chrono::steady_clock::now();
     for (int r = 0; r < 20; ++r) {

@@ -16,8 +16,8 @@ file ties the numbers to the build that produced them (bench.py uses them only f
 
 # read pattern per kernel: random gathers (FETCH_SIZE = bytes of the line requests) or
 # coalesced streaming (FETCH_SIZE = half the bytes); calibration: r03_pmc_calibration.json
-RANDOM_READ = {"k_expand", "k_jobs", "k_commit", "k_commit_told", "k_rehash", "k_level", "k_relax", "k_gap_move_e",
-               "k_gap_ovf", "k_ximport", "k_clear_logged", "k_init_facts", "k_stats", "k_succ_fill", "k_group_fill"}
+RANDOM_READ = {"k_expand", "k_jobs", "k_commit", "k_commit_told", "k_rehash", "k_level", "k_relax", "k_reloc_move",
+               "k_reloc_claim", "k_ximport", "k_clear_logged", "k_init_facts", "k_stats", "k_succ_fill", "k_group_fill"}
 import csv
 import glob
 import hashlib

@@ -28,7 +28,7 @@ for r in seg:
     tot[n] += d
     if step >= 0:
         table[step][n] = table[step].get(n, 0) + d
-cols = ["k_expand", "k_jobs", "k_commit", "k_gap_caps", "k_gap_move_e", "k_gap_ovf"]
+cols = ["k_expand", "k_jobs", "k_commit", "k_reloc_claim", "k_reloc_move", "k_reloc_commit"]
 print("step " + " ".join(f"{c[2:]:>12s}" for c in cols))
 for s in sorted(table):
     print(f"{s:4d} " + " ".join(f"{table[s].get(c, 0):12.1f}" for c in cols))
