@@ -357,9 +357,11 @@ __device__ void gather(const Axioms& ax, const Out& o, uint32_t A, uint32_t pb, 
 // finds its place in P's row by a binary search (and drops out if P's row holds it), each entry
 // of P's row moves up by the list entries below it, and the row is written straight into its
 // reservation (coalesced).  Returns false when the list has more than 64 entries (the caller
-// sorts).  Writes meta like task().
+// sorts).  Writes meta like task().  P's row is staged in the wave's LDS first (one coalesced read)
+// when it fits, so the binary searches cost LDS latency, not a chain of dependent global loads.
 template <uint32_t T>
-__device__ bool task_merge1(const Axioms& ax, const Out& o, uint32_t A, uint32_t pb, uint32_t pe, Rsv& rs) {
+__device__ bool task_merge1(const Axioms& ax, const Out& o, uint32_t A, uint32_t pb, uint32_t pe, uint32_t* lbuf,
+                            Rsv& rs) {
   using K = typename RowT<T>::K;
   uint32_t s = 0;
   K sv = 0;
@@ -383,11 +385,18 @@ __device__ bool task_merge1(const Axioms& ax, const Out& o, uint32_t A, uint32_t
     lb = meta_word(o.meta, P, 0, RowT<T>::comp);
     n = meta_word(o.meta, P, 1, RowT<T>::comp) - lb;
   }
-  auto at = [&](uint32_t j) -> K {
+  auto at_g = [&](uint32_t j) -> K {
     if (T == R_TOLD) return (K)o.t_val[lb + j];
     if (T == R_EXR) return (K)o.e_val[lb + j];
     return ((K)o.l_r[lb + j] << 32) | o.l_b[lb + j];
   };
+  K* rowl = reinterpret_cast<K*>(lbuf);
+  const bool staged = n <= RowT<T>::lds_cap;
+  if (staged) {
+    for (uint32_t j = lane(); j < n; j += 64) rowl[j] = at_g(j);
+    Lds::sync();
+  }
+  auto at = [&](uint32_t j) -> K { return staged ? rowl[j] : at_g(j); };
   // the list entries: rank in P's row, dropped when P's row holds them
   uint32_t rank = 0;
   bool kept = false;
@@ -408,7 +417,10 @@ __device__ bool task_merge1(const Axioms& ax, const Out& o, uint32_t A, uint32_t
   const uint32_t cap = T == R_TOLD ? o.t_cap : T == R_EXR ? o.e_cap : o.l_cap;
   uint32_t* tail = T == R_TOLD ? &o.ctr->t_tail : T == R_EXR ? &o.ctr->e_tail : &o.ctr->l_tail;
   const uint32_t r = reserve(o, rs, T, nout, cap, tail);
-  if (r == NONE) return true;  // (overflow flagged: the build is redone larger)
+  if (r == NONE) {  // (overflow flagged: the build is redone larger)
+    Lds::sync();
+    return true;
+  }
   auto put = [&](uint32_t i, K v) {
     if (T == R_TOLD) {
       o.t_val[r + i] = (uint32_t)v;
@@ -436,6 +448,7 @@ __device__ bool task_merge1(const Axioms& ax, const Out& o, uint32_t A, uint32_t
     reinterpret_cast<uint32_t*>(o.meta + 2 * A)[RowT<T>::comp] = r;
     reinterpret_cast<uint32_t*>(o.meta + 2 * A + 1)[RowT<T>::comp] = r + nout;
   }
+  Lds::sync();  // (lbuf is reused by the wave's next task)
   return true;
 }
 
@@ -445,7 +458,8 @@ __device__ bool task_merge1(const Axioms& ax, const Out& o, uint32_t A, uint32_t
 // P2's row not in P1's (a prefix count over P2's row, in the wave's LDS), and the list entries in
 // neither row below it.  An entry of P2's row or of the list that an earlier source holds drops
 // out.  Returns false (the caller sorts) when the list has more than 64 entries or P2's row does
-// not fit the LDS prefix.
+// not fit the LDS prefix.  Both rows are staged in the wave's LDS beside the prefix array when
+// they fit, so the binary searches cost LDS latency instead of chains of dependent global loads.
 template <uint32_t T>
 __device__ bool task_merge2(const Axioms& ax, const Out& o, uint32_t A, uint32_t pb, uint32_t* lbuf, Rsv& rs) {
   using K = typename RowT<T>::K;
@@ -469,11 +483,22 @@ __device__ bool task_merge2(const Axioms& ax, const Out& o, uint32_t A, uint32_t
     if (s > 64) return false;
     if (lane() < s) sv = ((K)ax.xl_r[b0 + lane()] << 32) | ax.xl_b[b0 + lane()];
   }
-  auto at = [&](uint32_t b, uint32_t j) -> K {
+  auto at_g = [&](uint32_t b, uint32_t j) -> K {
     if (T == R_TOLD) return (K)o.t_val[b + j];
     if (T == R_EXR) return (K)o.e_val[b + j];
     return ((K)o.l_r[b + j] << 32) | o.l_b[b + j];
   };
+  constexpr uint32_t KW = sizeof(K) / 4;  // 32-bit words per key
+  const bool staged = (uint64_t)(n1 + n2) * KW + n2 + 1 <= CAPW;
+  K* row1 = reinterpret_cast<K*>(lbuf);
+  K* row2 = row1 + n1;
+  if (staged) {
+    for (uint32_t j = lane(); j < n1; j += 64) row1[j] = at_g(b1, j);
+    for (uint32_t j = lane(); j < n2; j += 64) row2[j] = at_g(b2, j);
+    Lds::sync();
+  }
+  // (rows are named by their base in the global arrays: b1 or b2)
+  auto at = [&](uint32_t b, uint32_t j) -> K { return staged ? (b == b1 && n1 ? row1[j] : row2[j]) : at_g(b, j); };
   auto lower = [&](uint32_t b, uint32_t n, K v) {  // entries of row [b, b + n) below v
     uint32_t lo = 0, hi = n;
     while (lo < hi) {
@@ -486,7 +511,7 @@ __device__ bool task_merge2(const Axioms& ax, const Out& o, uint32_t A, uint32_t
     return lo;
   };
   // P2's row: which entries P1's row holds; pre[j] = entries of P2's row before j it does not
-  uint32_t* pre = lbuf;
+  uint32_t* pre = staged ? reinterpret_cast<uint32_t*>(row2 + n2) : lbuf;
   uint32_t run = 0;
   for (uint32_t j0 = 0; j0 < n2; j0 += 64) {  // (wave-uniform)
     const uint32_t j = j0 + lane();
@@ -577,7 +602,7 @@ template <uint32_t T, bool RELAX>
 __device__ bool task(const Axioms& ax, const Out& o, uint32_t A, uint32_t* lbuf, Rsv& rs) {
   using K = typename RowT<T>::K;
   const uint32_t pb = ax.par_ptr[A], pe = ax.par_ptr[A + 1];
-  if (!RELAX && pe - pb <= 1 && task_merge1<T>(ax, o, A, pb, pe, rs)) return true;
+  if (!RELAX && pe - pb <= 1 && task_merge1<T>(ax, o, A, pb, pe, lbuf, rs)) return true;
   if (!RELAX && pe - pb == 2 && task_merge2<T>(ax, o, A, pb, lbuf, rs)) return true;
   unsigned long long raw = 0;
   for (uint32_t q = pb + lane(); q < pe; q += 64) {
@@ -704,6 +729,76 @@ __global__ void __launch_bounds__(BLOCK) k_level(Axioms ax, Out o, uint32_t L) {
   if (any) sany = 1;
   __syncthreads();
   if (threadIdx.x == 0 && sany) o.lvl_flag[L + 1] = 1;
+}
+
+// Level 0 — the concepts without told supers: told* is empty and exr* / exl* are the concept's
+// own axiom lists (sorted, unique), so a lane per concept copies them (the wave reserves its
+// lanes' rows with one atomic per row type), and the subs whose last super it was are counted
+// down with the wave walking its lanes' child lists together.  As wave-per-concept tasks of
+// k_level each root cost a chain of dependent loads (G3: 90 k roots, 0.7 ms).
+__global__ void __launch_bounds__(BLOCK) k_level0(Axioms ax, Out o) {
+  if (o.lvl_flag[0] == 0) return;  // (block-uniform)
+  __shared__ uint32_t sany;
+  if (threadIdx.x == 0) sany = 0;
+  __syncthreads();
+  bool any = false;
+  const uint32_t stride = gridDim.x * blockDim.x;
+  for (uint32_t base = blockIdx.x * blockDim.x; base < ax.N; base += stride) {  // (uniform trip count)
+    const uint32_t A = base + threadIdx.x;
+    const bool on = A < ax.N && o.level[A] == 0u;
+    uint32_t xb = 0, ne = 0, lb = 0, nl = 0, cb = 0, nc = 0;
+    if (on) {
+      xb = ax.xr_ptr[A];
+      ne = ax.xr_ptr[A + 1] - xb;
+      lb = ax.xl_ptr[A];
+      nl = ax.xl_ptr[A + 1] - lb;
+      cb = ax.chi_ptr[A];
+      nc = ax.chi_ptr[A + 1] - cb;
+    }
+    uint32_t ie = ne, il = nl;  // inclusive wave scans of the row sizes
+#pragma unroll
+    for (uint32_t d = 1; d < 64; d <<= 1) {
+      const uint32_t ve = __shfl_up(ie, d), vl = __shfl_up(il, d);
+      if (lane() >= d) ie += ve, il += vl;
+    }
+    const uint32_t te = __shfl(ie, 63), tl = __shfl(il, 63);
+    uint32_t re = 0, rl = 0;
+    if (lane() == 0) {
+      if (te) re = atomicAdd(&o.ctr->e_tail, te);
+      if (tl) rl = atomicAdd(&o.ctr->l_tail, tl);
+    }
+    re = __shfl(re, 0);
+    rl = __shfl(rl, 0);
+    const bool eok = (uint64_t)re + te <= o.e_cap, lok = (uint64_t)rl + tl <= o.l_cap;
+    if (lane() == 0 && ((te && !eok) || (tl && !lok))) atomicOr(&o.ctr->ovf, 1u);  // (redone larger)
+    if (on && ne && eok) {
+      const uint32_t e0 = re + ie - ne;
+      for (uint32_t j = 0; j < ne; ++j) o.e_val[e0 + j] = ax.xr[xb + j];
+      reinterpret_cast<uint32_t*>(o.meta + 2 * A)[RowT<R_EXR>::comp] = e0;
+      reinterpret_cast<uint32_t*>(o.meta + 2 * A + 1)[RowT<R_EXR>::comp] = e0 + ne;
+    }
+    if (on && nl && lok) {
+      const uint32_t l0 = rl + il - nl;
+      for (uint32_t j = 0; j < nl; ++j) {
+        o.l_r[l0 + j] = ax.xl_r[lb + j];
+        o.l_b[l0 + j] = ax.xl_b[lb + j];
+      }
+      reinterpret_cast<uint32_t*>(o.meta + 2 * A)[RowT<R_EXL>::comp] = l0;
+      reinterpret_cast<uint32_t*>(o.meta + 2 * A + 1)[RowT<R_EXL>::comp] = l0 + nl;
+    }
+    wave_concat(nc, [&](bool v, uint32_t own, uint32_t j, uint32_t) {
+      const uint32_t cbo = __shfl(cb, (int)own);
+      if (!v) return;
+      const uint32_t c = ax.chi[cbo + j];
+      if (o.level[c] != SKIP && atomicSub(o.indeg + c, 1u) == 1u) {
+        o.level[c] = 1u;
+        any = true;
+      }
+    });
+  }
+  if (any) sany = 1;
+  __syncthreads();
+  if (threadIdx.x == 0 && sany) o.lvl_flag[1] = 1;
 }
 
 // after the levels: concepts never ready (told cycles and everything below them) are stuck;
@@ -1067,7 +1162,10 @@ void start(hipStream_t s, const Axioms& ax, const Out& o) {
 }
 
 void level(hipStream_t s, const Axioms& ax, const Out& o, uint32_t L) {
-  hipLaunchKernelGGL(k_level, dim3(GRID), dim3(BLOCK), 0, s, ax, o, L);
+  if (L == 0)
+    hipLaunchKernelGGL(k_level0, dim3(grid_for(ax.N)), dim3(BLOCK), 0, s, ax, o);
+  else
+    hipLaunchKernelGGL(k_level, dim3(GRID), dim3(BLOCK), 0, s, ax, o, L);
   CCHK(hipGetLastError());
 }
 

@@ -2017,6 +2017,7 @@ __global__ void k_gap_ends(const uint32_t* __restrict__ start, uint32_t* __restr
 // ---- relocation of the rows that overflowed in a step (el_ctx::gap_relocate).  rc[0] = the
 // slot array's next free slot (64-bit), rc[1] = rows claimed, rc[2] = their in-place entries.
 struct Reloc {
+  uint64_t base;  // the slot array's tail before this relocation (new slots start there)
   uint32_t* start;
   uint32_t* end;
   const uint32_t* len;
@@ -2059,7 +2060,7 @@ __global__ void k_reloc_claim(Reloc a) {
     b = __shfl(b, 0);
     const uint32_t k = wave_append(reinterpret_cast<uint32_t*>(a.rc + 1), won);
     if (won) {
-      a.nstart[row] = (uint32_t)(b + inc - sz);  // (the host checked the tail fits 32 bits first)
+      a.nstart[row] = (uint32_t)(a.base + b + inc - sz);  // (the host checks the tail fits 32 bits first)
       a.rlist[k] = row;
     }
   }
@@ -2080,6 +2081,24 @@ __global__ void k_reloc_move(Reloc a, uint32_t nb) {
   for (uint32_t i = (blockIdx.x - nb) * blockDim.x + threadIdx.x; i < a.n_ovf; i += stride) {
     const uint32_t row = a.ovq[3 * (size_t)i];
     a.val[a.nstart[row] + a.ovq[3 * (size_t)i + 2]] = a.ovq[3 * (size_t)i + 1];
+  }
+}
+
+// Before the claims: the relocation counters of the three CSRs and the step's overflow counts
+// (DCounters ov_pr, ov_sc, ov_pp: the host read them with the step's counters) start over.
+__global__ void k_reloc_reset(unsigned long long* rc, uint32_t* ov) {
+  if (threadIdx.x < 9) rc[threadIdx.x] = 0;
+  if (threadIdx.x < 3) ov[threadIdx.x * CTR_STRIDE] = 0;
+}
+
+// After the claims: the counters to coherent pinned host memory, then the sequence word (the
+// host spins on it instead of a stream synchronisation).
+__global__ void k_reloc_publish(const unsigned long long* rc, volatile unsigned long long* host, uint32_t seq) {
+  if (threadIdx.x == 0) {
+    for (int i = 0; i < 9; ++i) host[i] = rc[i];
+    __threadfence_system();
+    host[9] = seq;
+    __threadfence_system();
   }
 }
 
@@ -2835,7 +2854,11 @@ struct el_ctx {
   void stream_runs(const uint32_t* keys, uint64_t a, uint64_t b, uint2* out, uint64_t cap, int which);
   void stream_out();    // stream_mark + stream_flush
   void stream_mark();
-  void stream_flush();
+  // force: flush whatever is marked; else only a segment of stream_min entries or more (a late
+  // superstep's few entries wait for a later flush: the host's enqueue work for copies and run
+  // encodings — a dozen API calls — would otherwise sit between two short supersteps)
+  void stream_flush(bool force = true);
+  uint64_t stream_min = env_u32("EL_STREAM_MIN", 1u << 17);
   uint64_t mark_s = 0, mark_l = 0;  // the marked segment ends [strm_s, mark_s), [strm_l, mark_l)
   bool mark_pending = false;
   void stream_end(bool release);
@@ -2866,7 +2889,9 @@ struct el_ctx {
   uint64_t sc_ovq() const { return cl_cap + (part() ? (uint64_t)part_count * xcap : 0u); }
   void fill_stats(el_stats* st, double ms);
   void gap_relocate_all();
-  unsigned long long *reloc_rc = nullptr, *reloc_h = nullptr;  // relocation counters (device / pinned), 3 per CSR
+  // relocation counters (device; their published copy in coherent pinned memory + sequence word)
+  unsigned long long *reloc_rc = nullptr, *reloc_h = nullptr, *reloc_hd = nullptr;
+  unsigned long long reloc_seq = 0;
   void gap_build_from_log(GapCsr& g, const uint32_t* rows, const uint32_t* vals, uint64_t n,
                           const uint8_t* keep = nullptr);
   void launch_gap_scan(const uint32_t* len, uint32_t R, uint32_t* start_out);
@@ -3694,7 +3719,7 @@ bool el_ctx::superstep(uint32_t mask, uint64_t sb, uint64_t se, uint64_t lb, uin
     });
     if (strm) {  // the last step's segment goes now, beside this step's kernels; this step's
                  // entries are final behind the event recorded here (stream_mark picks it up)
-      stream_flush();
+      stream_flush(false);
       HIPCHK(hipEventRecord(ev_strm, stream));
       strm_marked = true;
     }
@@ -4449,8 +4474,9 @@ void el_ctx::stream_mark() {
   mark_pending = true;
 }
 
-void el_ctx::stream_flush() {
+void el_ctx::stream_flush(bool force) {
   if (!strm || !mark_pending) return;
+  if (!force && (mark_s - strm_s) + (mark_l - strm_l) < stream_min) return;
   mark_pending = false;
   const uint64_t s1 = mark_s, l1 = mark_l;
   HIPCHK(hipStreamWaitEvent(dstream, ev_strm, 0));
@@ -4705,31 +4731,44 @@ void el_ctx::gap_relocate_all() {
   GapCsr* gs[3] = {&PR, &SC, &PP};
   if (!reloc_rc) {
     reloc_rc = dalloc<unsigned long long>(9);
-    HIPCHK(hipHostMalloc((void**)&reloc_h, 18 * sizeof(unsigned long long), hipHostMallocDefault));
+    HIPCHK(hipHostMalloc((void**)&reloc_h, 10 * sizeof(unsigned long long), hipHostMallocCoherent | hipHostMallocMapped));
+    memset(reloc_h, 0, 10 * sizeof(unsigned long long));
+    HIPCHK(hipHostGetDevicePointer((void**)&reloc_hd, reloc_h, 0));
   }
-  unsigned long long* init_h = reloc_h + 9;  // (a separate pinned block: the readback lands in reloc_h)
   auto args = [&](int i) {
     GapCsr& g = *gs[i];
-    return Reloc{g.start, g.end, g.len, g.val, g.ovq, ov[i], g.flag, g.nstart, g.rlist, reloc_rc + 3 * i};
+    return Reloc{g.used, g.start, g.end, g.len, g.val, g.ovq, ov[i], g.flag, g.nstart, g.rlist, reloc_rc + 3 * i};
   };
-  for (int i = 0; i < 3; ++i) {
-    init_h[3 * i] = gs[i]->used;
-    init_h[3 * i + 1] = init_h[3 * i + 2] = 0;
-  }
-  HIPCHK(hipMemcpyAsync(reloc_rc, init_h, 9 * sizeof(unsigned long long), hipMemcpyHostToDevice, stream));
+  hipLaunchKernelGGL(k_reloc_reset, dim3(1), dim3(64), 0, stream, reloc_rc, &ctr->ov_pr);
+  HIPCHK(hipGetLastError());
   for (int i = 0; i < 3; ++i) {
     if (!ov[i]) continue;
     if (ov[i] > gs[i]->ovq_cap) throw std::runtime_error("gapped-CSR overflow queue overrun");
     launch(EL_K_SCAN, [&] { hipLaunchKernelGGL(k_reloc_claim, dim3(grid_for(ov[i])), dim3(BLOCK), 0, stream, args(i)); });
   }
-  HIPCHK(hipMemcpyAsync(reloc_h, reloc_rc, 9 * sizeof(unsigned long long), hipMemcpyDeviceToHost, stream));
-  sync();
+  const unsigned long long seq = ++reloc_seq;
+  hipLaunchKernelGGL(k_reloc_publish, dim3(1), dim3(64), 0, stream, reloc_rc, reloc_hd, (uint32_t)seq);
+  HIPCHK(hipGetLastError());
+  {  // the claims' totals (a spin on the published sequence word, as wait_commit does)
+    volatile unsigned long long* p = reloc_h;
+    for (uint64_t it = 1; p[9] != seq; ++it) {
+      if ((it & 1023) == 0) {
+        const hipError_t e = hipStreamQuery(stream);
+        if (e == hipSuccess && p[9] != seq) throw std::runtime_error("relocation counters were not published");
+        if (e != hipSuccess && e != hipErrorNotReady) HIPCHK(e);
+      }
+      __builtin_ia32_pause();
+    }
+    std::atomic_thread_fence(std::memory_order_acquire);
+  }
   for (int i = 0; i < 3; ++i) {
     if (!ov[i]) continue;
     GapCsr& g = *gs[i];
-    const uint64_t tail = reloc_h[3 * i], nrows = reloc_h[3 * i + 1] & 0xffffffffull, moved = reloc_h[3 * i + 2];
+    const uint64_t tail = g.used + reloc_h[3 * i], nrows = reloc_h[3 * i + 1] & 0xffffffffull,
+                   moved = reloc_h[3 * i + 2];
     if (tail > 0xffffffffull) throw ElError{EL_ENOMEM, "gapped CSR beyond 2^32 slots"};
-    if (tail > g.val_cap) {  // (the stream is idle: the readback synchronised it)
+    if (tail > g.val_cap) {  // (rare: the copy needs the stream idle)
+      sync();
       const uint64_t c = std::min<uint64_t>(tail + tail / 2, 0xffffffffull);
       dgrow(g.val, g.used, c);
       g.val_cap = c;
@@ -4753,9 +4792,7 @@ void el_ctx::gap_relocate_all() {
     host_ev[EL_K_SCATTER_NEW][EL_EV_ENT] += 3ull * ov[i];
     host_ev[EL_K_SCATTER_NEW][EL_EV_EMIT] += ov[i];
   }
-  // the overflow counters start over (stream-ordered after the relocation kernels)
-  HIPCHK(hipMemsetAsync(&ctr->ov_pr, 0, 3 * CTR_STRIDE * sizeof(uint32_t), stream));
-  hc.ov_pr = hc.ov_sc = hc.ov_pp = 0;
+  hc.ov_pr = hc.ov_sc = hc.ov_pp = 0;  // (zeroed on the device by k_reloc_reset)
 }
 
 void el_ctx::fill_stats(el_stats* out, double ms) {
@@ -5093,7 +5130,8 @@ int el_saturate(el_ctx* c, el_stats* stats) {
         c->tr_l.push_back(le - lb);
         c->tr_a.push_back(ae - ab);
         const uint64_t g = c->superstep_part(mask, sb, se, lb, le, ab, ae, pb, pe2, xb, xe);
-        c->stream_out();
+        c->stream_mark();
+        c->stream_flush(false);
         sb = se, lb = le, ab = ae, pb = pe2, xb = xe;
         if (g == 0) break;
       }

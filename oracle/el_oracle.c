@@ -1171,6 +1171,26 @@ static int superstep(elo_ctx* c, uint32_t mask, uint64_t sb, uint64_t se, uint64
       vpush(&c->srow[x], a);
     }
   }
+  if (getenv("ELO_WINSTAT") && k.sx.n) { /* diagnostic: distinct (x, word) / (x, a) per window of W candidates */
+    size_t w, W, q, r;
+    for (W = 64; W <= 4096; W *= 8) {
+      uint64_t dw = 0, da = 0;
+      uint64_t* key = (uint64_t*)malloc(W * sizeof(uint64_t));
+      for (w = 0; w < k.sx.n; w += W) {
+        size_t m = k.sx.n - w < W ? k.sx.n - w : W;
+        for (q = 0; q < m; ++q) key[q] = ((uint64_t)k.sx.v[w + q] << 32) | k.sa.v[w + q];
+        qsort(key, m, sizeof(uint64_t), cmp_u64);
+        for (q = 0; q < m; ++q) {
+          da += q == 0 || key[q] != key[q - 1];
+          r = q == 0 || (key[q] >> 5) != (key[q - 1] >> 5);
+          dw += r;
+        }
+      }
+      free(key);
+      fprintf(stderr, "winstat step %u cands %zu window %zu distinct_fact %llu distinct_word %llu\n", c->supersteps,
+              k.sx.n, W, (unsigned long long)da, (unsigned long long)dw);
+    }
+  }
   for (i = 0; i < k.sx.n; ++i) {
     uint32_t x = k.sx.v[i], a = k.sa.v[i];
     EV(EL_K_COMMIT_S, EL_EV_TRIG);

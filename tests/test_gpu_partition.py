@@ -144,10 +144,13 @@ def test_g4_shape_eight_partitions(name, oracle_lib):
     _close(engs)
 
 
-def test_partitioned_stream_result(oracle_lib):
+@pytest.mark.parametrize("short_rank", [None, 1], ids=["fitted", "short_buffer_rank1"])
+def test_partitioned_stream_result(short_rank, oracle_lib):
     """Every rank of a row partition streams its own rows while the collective supersteps run
     (el_stream_result with release, as bench.py's exchange leg does); the union of the streamed
-    rows is the oracle's closure."""
+    rows is the oracle's closure.  short_buffer_rank1: rank 1's buffers are far too small, so its
+    result_wait gets EL_ERANGE and streams again at the fixpoint on its own (Engine.result_wait) —
+    that saturation runs no collective superstep, so it cannot wait for peers that have left."""
     import threading
     ax = generators.workload("g3", scale=0.02)
     parts = 3
@@ -158,6 +161,9 @@ def test_partitioned_stream_result(oracle_lib):
         e.load(ax)
     strms = [engine.Stream() for _ in range(parts)]
     errs = []
+
+    if short_rank is not None:  # (buffers sized from "the last saturation": 16 facts, 16 links)
+        engs[short_rank]._last = {"s_facts": 16, "links": 16}
 
     def run(q):
         try:
@@ -175,7 +181,10 @@ def test_partitioned_stream_result(oracle_lib):
         t.start()
     for t in ts:
         t.join(timeout=300)
+    assert not any(t.is_alive() for t in ts), "a rank is stuck"
     assert not errs, errs
+    if short_rank is not None:
+        assert strms[short_rank].s_b.size > 64  # (refitted by the recovery)
     fx = np.concatenate([s.facts(ax.n_concepts)[0] for s in strms])
     fa = np.concatenate([s.facts(ax.n_concepts)[1] for s in strms])
     o = np.lexsort((fa, fx))
