@@ -42,6 +42,9 @@ struct Axioms {
   const uint32_t* psup_ptr = nullptr;                   // pid -> super-role pairs (CR5 lifts)
   const uint8_t* sc_self = nullptr;                     // pid -> its role is second in a chain
   const uint32_t* sc_w = nullptr;                       // pid -> sc_self + Σ sc_self of its lifts
+  // k_stats' per-entry lookups packed (one load per row entry instead of two or three lines):
+  const uint2* pstat = nullptr;    // pid -> {sc_w, |psup(pid)| << 1 | sc_self}
+  const uint32_t* cz = nullptr;    // A -> |cidx(A)|
   const uint32_t *fp_ptr = nullptr, *pair_role = nullptr;  // Y -> pairs (r, Y), sorted by r
   const uint8_t* kind = nullptr;
   // the concepts whose rows are built: ⊥, ⊤ and [w_lo, w_hi) (a partitioned context: its column

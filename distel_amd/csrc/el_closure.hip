@@ -351,6 +351,48 @@ __device__ void gather(const Axioms& ax, const Out& o, uint32_t A, uint32_t pb, 
   }
 }
 
+// A level task's head values, loaded for 64 tasks at once (one lane each) before the wave runs
+// them one by one: the told supers (≤ 2 of them), their rows of the task's type, and the
+// concept's own list (xr / xl range; for told*, its subs).  Each was a dependent global load at the
+// head of every task (par_ptr -> par -> meta, xr_ptr), ~1-2 µs apiece under load.
+struct Pre {
+  uint32_t pb, pe;     // told supers [pb, pe) in par
+  uint32_t P1, P2;     // the first two supers
+  uint32_t b1, n1, b2, n2;  // their rows of the task's type
+  uint32_t ob, on;     // own list: xr / xl range (exr* / exl*), subs in chi (told*)
+};
+
+__device__ __forceinline__ Pre pre_load(const Axioms& ax, const Out& o, uint32_t A, uint32_t T) {
+  Pre p{};
+  p.pb = ax.par_ptr[A];
+  p.pe = ax.par_ptr[A + 1];
+  const uint32_t comp = T == R_TOLD ? 0u : T == R_EXR ? 2u : 3u;
+  if (p.pe > p.pb) {
+    p.P1 = ax.par[p.pb];
+    p.b1 = meta_word(o.meta, p.P1, 0, comp);
+    p.n1 = meta_word(o.meta, p.P1, 1, comp) - p.b1;
+  }
+  if (p.pe - p.pb == 2) {
+    p.P2 = ax.par[p.pb + 1];
+    p.b2 = meta_word(o.meta, p.P2, 0, comp);
+    p.n2 = meta_word(o.meta, p.P2, 1, comp) - p.b2;
+  }
+  const uint32_t* op = T == R_TOLD ? ax.chi_ptr : T == R_EXR ? ax.xr_ptr : ax.xl_ptr;
+  p.ob = op[A];
+  p.on = op[A + 1] - p.ob;
+  return p;
+}
+
+// lane i's Pre, wave-uniform
+__device__ __forceinline__ Pre pre_of(const Pre& p, int i) {
+  Pre q;
+  q.pb = __shfl(p.pb, i), q.pe = __shfl(p.pe, i);
+  q.P1 = __shfl(p.P1, i), q.P2 = __shfl(p.P2, i);
+  q.b1 = __shfl(p.b1, i), q.n1 = __shfl(p.n1, i), q.b2 = __shfl(p.b2, i), q.n2 = __shfl(p.n2, i);
+  q.ob = __shfl(p.ob, i), q.on = __shfl(p.on, i);
+  return q;
+}
+
 // A concept with at most one told super P (in the Kahn levels: no cycle through A, so A is not in
 // P's rows): its row of type T is P's row merged with a short sorted list — {P} for told*, A's own
 // axioms xr(A) / xl(A) (sorted, unique) for exr* / exl*.  A merge, not a sort: each list entry
@@ -360,30 +402,29 @@ __device__ void gather(const Axioms& ax, const Out& o, uint32_t A, uint32_t pb, 
 // sorts).  Writes meta like task().  P's row is staged in the wave's LDS first (one coalesced read)
 // when it fits, so the binary searches cost LDS latency, not a chain of dependent global loads.
 template <uint32_t T>
-__device__ bool task_merge1(const Axioms& ax, const Out& o, uint32_t A, uint32_t pb, uint32_t pe, uint32_t* lbuf,
-                            Rsv& rs) {
+__device__ bool task_merge1(const Axioms& ax, const Out& o, uint32_t A, const Pre& pr, uint32_t* lbuf, Rsv& rs) {
   using K = typename RowT<T>::K;
+  const uint32_t pb = pr.pb, pe = pr.pe;
   uint32_t s = 0;
   K sv = 0;
   if (T == R_TOLD) {
     s = pe > pb ? 1u : 0u;
-    if (s && lane() == 0) sv = (K)ax.par[pb];
+    if (s && lane() == 0) sv = (K)pr.P1;
   } else if (T == R_EXR) {
-    const uint32_t b0 = ax.xr_ptr[A];
-    s = ax.xr_ptr[A + 1] - b0;
+    const uint32_t b0 = pr.ob;
+    s = pr.on;
     if (s > 64) return false;
     if (lane() < s) sv = (K)ax.xr[b0 + lane()];
   } else {
-    const uint32_t b0 = ax.xl_ptr[A];
-    s = ax.xl_ptr[A + 1] - b0;
+    const uint32_t b0 = pr.ob;
+    s = pr.on;
     if (s > 64) return false;
     if (lane() < s) sv = ((K)ax.xl_r[b0 + lane()] << 32) | ax.xl_b[b0 + lane()];
   }
   uint32_t lb = 0, n = 0;
   if (pe > pb) {
-    const uint32_t P = ax.par[pb];
-    lb = meta_word(o.meta, P, 0, RowT<T>::comp);
-    n = meta_word(o.meta, P, 1, RowT<T>::comp) - lb;
+    lb = pr.b1;
+    n = pr.n1;
   }
   auto at_g = [&](uint32_t j) -> K {
     if (T == R_TOLD) return (K)o.t_val[lb + j];
@@ -461,11 +502,11 @@ __device__ bool task_merge1(const Axioms& ax, const Out& o, uint32_t A, uint32_t
 // not fit the LDS prefix.  Both rows are staged in the wave's LDS beside the prefix array when
 // they fit, so the binary searches cost LDS latency instead of chains of dependent global loads.
 template <uint32_t T>
-__device__ bool task_merge2(const Axioms& ax, const Out& o, uint32_t A, uint32_t pb, uint32_t* lbuf, Rsv& rs) {
+__device__ bool task_merge2(const Axioms& ax, const Out& o, uint32_t A, const Pre& pr, uint32_t* lbuf, Rsv& rs) {
   using K = typename RowT<T>::K;
-  const uint32_t P1 = ax.par[pb], P2 = ax.par[pb + 1];
-  const uint32_t b1 = meta_word(o.meta, P1, 0, RowT<T>::comp), n1 = meta_word(o.meta, P1, 1, RowT<T>::comp) - b1;
-  const uint32_t b2 = meta_word(o.meta, P2, 0, RowT<T>::comp), n2 = meta_word(o.meta, P2, 1, RowT<T>::comp) - b2;
+  const uint32_t P1 = pr.P1, P2 = pr.P2;
+  const uint32_t b1 = pr.b1, n1 = pr.n1;
+  const uint32_t b2 = pr.b2, n2 = pr.n2;
   if (n2 + 1 > CAPW) return false;
   uint32_t s = 0;
   K sv = 0;
@@ -473,13 +514,13 @@ __device__ bool task_merge2(const Axioms& ax, const Out& o, uint32_t A, uint32_t
     s = 2;
     if (lane() < 2) sv = (K)(lane() ? P2 : P1);  // (par is sorted: P1 < P2)
   } else if (T == R_EXR) {
-    const uint32_t b0 = ax.xr_ptr[A];
-    s = ax.xr_ptr[A + 1] - b0;
+    const uint32_t b0 = pr.ob;
+    s = pr.on;
     if (s > 64) return false;
     if (lane() < s) sv = (K)ax.xr[b0 + lane()];
   } else {
-    const uint32_t b0 = ax.xl_ptr[A];
-    s = ax.xl_ptr[A + 1] - b0;
+    const uint32_t b0 = pr.ob;
+    s = pr.on;
     if (s > 64) return false;
     if (lane() < s) sv = ((K)ax.xl_r[b0 + lane()] << 32) | ax.xl_b[b0 + lane()];
   }
@@ -599,11 +640,11 @@ __device__ bool task_merge2(const Axioms& ax, const Out& o, uint32_t A, uint32_t
 // appended when it grew; its range goes to meta2 (committed after the round).  Returns whether
 // the row was written.
 template <uint32_t T, bool RELAX>
-__device__ bool task(const Axioms& ax, const Out& o, uint32_t A, uint32_t* lbuf, Rsv& rs) {
+__device__ bool task(const Axioms& ax, const Out& o, uint32_t A, uint32_t* lbuf, Rsv& rs, const Pre* pr = nullptr) {
   using K = typename RowT<T>::K;
-  const uint32_t pb = ax.par_ptr[A], pe = ax.par_ptr[A + 1];
-  if (!RELAX && pe - pb <= 1 && task_merge1<T>(ax, o, A, pb, pe, lbuf, rs)) return true;
-  if (!RELAX && pe - pb == 2 && task_merge2<T>(ax, o, A, pb, lbuf, rs)) return true;
+  const uint32_t pb = pr ? pr->pb : ax.par_ptr[A], pe = pr ? pr->pe : ax.par_ptr[A + 1];
+  if (!RELAX && pe - pb <= 1 && task_merge1<T>(ax, o, A, *pr, lbuf, rs)) return true;
+  if (!RELAX && pe - pb == 2 && task_merge2<T>(ax, o, A, *pr, lbuf, rs)) return true;
   unsigned long long raw = 0;
   for (uint32_t q = pb + lane(); q < pe; q += 64) {
     const uint32_t p = ax.par[q];
@@ -667,7 +708,7 @@ __device__ __forceinline__ void for_tasks(uint32_t N, Sel&& sel, Run&& run) {
   const uint64_t ntask = 3ull * N;
   for (uint64_t base = 0; base * nw + w < ntask; base += 64) {  // (wave-uniform)
     const uint64_t t0 = (base + lane()) * nw + w;
-    const bool in = t0 < ntask && sel((uint32_t)(t0 / 3));
+    const bool in = t0 < ntask && sel((uint32_t)(t0 / 3), (uint32_t)(t0 % 3));
     unsigned long long m = __ballot(in);
     while (m) {
       const uint32_t i = (uint32_t)__ffsll((long long)m) - 1;
@@ -707,24 +748,38 @@ __global__ void __launch_bounds__(BLOCK) k_level(Axioms ax, Out o, uint32_t L) {
   uint32_t* lbuf = reinterpret_cast<uint32_t*>(lds + (threadIdx.x >> 6) * (CAPW / 2));
   Rsv rs = rsv_load(o);
   bool any = false;
-  for_tasks(ax.N, [&](uint32_t A) { return o.level[A] == L; }, [&](uint32_t A, uint32_t T) {
-    if (T == R_EXR) {
-      task<R_EXR, false>(ax, o, A, lbuf, rs);
-    } else if (T == R_EXL) {
-      task<R_EXL, false>(ax, o, A, lbuf, rs);
-    } else {
-      task<R_TOLD, false>(ax, o, A, lbuf, rs);
-      // a sub whose last super this was is ready for the next level
-      const uint32_t cb = ax.chi_ptr[A], ce = ax.chi_ptr[A + 1];
-      for (uint32_t q = cb + lane(); q < ce; q += 64) {
-        const uint32_t c = ax.chi[q];
-        if (o.level[c] != SKIP && atomicSub(o.indeg + c, 1u) == 1u) {
-          o.level[c] = L + 1;
-          any = true;
+  // for_tasks with each selected task's head values loaded by its lane first (pre_load)
+  const uint32_t nw = gridDim.x * WAVES, w = slot_id();
+  const uint64_t ntask = 3ull * ax.N;
+  for (uint64_t base = 0; base * nw + w < ntask; base += 64) {  // (wave-uniform)
+    const uint64_t t0 = (base + lane()) * nw + w;
+    const uint32_t A0 = (uint32_t)(t0 / 3), T0 = (uint32_t)(t0 % 3);
+    const bool in = t0 < ntask && o.level[A0] == L;
+    const Pre mine = in ? pre_load(ax, o, A0, T0) : Pre{};
+    unsigned long long m = __ballot(in);
+    while (m) {
+      const int i = __ffsll((long long)m) - 1;
+      m &= m - 1;
+      const uint32_t A = __shfl(A0, i), T = __shfl(T0, i);
+      const Pre pr = pre_of(mine, i);
+      if (T == R_EXR) {
+        task<R_EXR, false>(ax, o, A, lbuf, rs, &pr);
+      } else if (T == R_EXL) {
+        task<R_EXL, false>(ax, o, A, lbuf, rs, &pr);
+      } else {
+        task<R_TOLD, false>(ax, o, A, lbuf, rs, &pr);
+        // a sub whose last super this was is ready for the next level
+        const uint32_t cb = pr.ob, ce = pr.ob + pr.on;
+        for (uint32_t q = cb + lane(); q < ce; q += 64) {
+          const uint32_t c = ax.chi[q];
+          if (o.level[c] != SKIP && atomicSub(o.indeg + c, 1u) == 1u) {
+            o.level[c] = L + 1;
+            any = true;
+          }
         }
       }
     }
-  });
+  }
   rsv_store(o, rs);
   if (any) sany = 1;
   __syncthreads();
@@ -830,7 +885,7 @@ __global__ void __launch_bounds__(BLOCK) k_relax(Axioms ax, Out o) {
   __shared__ unsigned long long lds[WAVES * (CAPW / 2)];
   uint32_t* lbuf = reinterpret_cast<uint32_t*>(lds + (threadIdx.x >> 6) * (CAPW / 2));
   Rsv rs = rsv_load(o);
-  for_tasks(ax.N, [&](uint32_t A) { return o.dirty[A] != 0; }, [&](uint32_t A, uint32_t T) {
+  for_tasks(ax.N, [&](uint32_t A, uint32_t) { return o.dirty[A] != 0; }, [&](uint32_t A, uint32_t T) {
     const bool grew = T == R_TOLD  ? task<R_TOLD, true>(ax, o, A, lbuf, rs)
                       : T == R_EXR ? task<R_EXR, true>(ax, o, A, lbuf, rs)
                                    : task<R_EXL, true>(ax, o, A, lbuf, rs);
@@ -873,6 +928,21 @@ __global__ void __launch_bounds__(BLOCK) k_relax_commit(Axioms ax, Out o) {
 // init facts, CR2 candidates over told*, successor-row weights and CR5 lifts over exr*, base
 // propagations over exl*.  Lanes own concepts; the wave walks the concatenation of its 64
 // concepts' rows (coalesced) and adds each entry's contribution to its owner in LDS.
+// acc[own] += v over a wave_concat round: the lanes of one owner are consecutive, so a segmented
+// scan leaves each owner's sum in its last lane, which adds it alone (an LDS atomic per lane on a
+// handful of owner words serialised, k_stats 0.68 ms on G3).  Invalid lanes: own = 64 (no owner).
+__device__ __forceinline__ void seg_add(uint32_t* acc, uint32_t own, uint32_t v) {
+  const uint32_t ln = lane();
+  uint32_t sum = v;
+#pragma unroll
+  for (uint32_t d = 1; d < 64; d <<= 1) {
+    const uint32_t t = __shfl_up(sum, d), ow = __shfl_up(own, d);
+    if (ln >= d && ow == own) sum += t;
+  }
+  const uint32_t next = __shfl_down(own, 1);
+  if (own < 64 && (ln == 63 || next != own) && sum) acc[own] += sum;
+}
+
 __global__ void __launch_bounds__(BLOCK) k_stats(Axioms ax, Out o, uint32_t lo, uint32_t hi, uint32_t props) {
   __shared__ uint32_t acc[WAVES][6][64];
   uint32_t(&a)[6][64] = acc[threadIdx.x >> 6];
@@ -894,25 +964,28 @@ __global__ void __launch_bounds__(BLOCK) k_stats(Axioms ax, Out o, uint32_t lo, 
     // told*: CR2 candidates (|cidx| of every entry), ⊤ among the first two entries
     wave_concat(e.x - b.x, [&](bool v, uint32_t own, uint32_t j, uint32_t) {
       const uint32_t ro = __shfl(b.x, (int)own);
-      if (!v) return;
-      const uint32_t t = o.t_val[ro + j];
-      atomicAdd(&a[0][own], ax.cidx_ptr[t + 1] - ax.cidx_ptr[t]);
-      if (j < 2 && t == TOP) a[1][own] = 1;
+      uint32_t cz = 0;
+      if (v) {
+        const uint32_t t = o.t_val[ro + j];
+        cz = ax.cz[t];
+        if (j < 2 && t == TOP) a[1][own] = 1;
+      }
+      seg_add(a[0], v ? own : 64u, cz);
     });
     // exr*: successor-row weight, chain-second base links, CR5 lifts
     wave_concat(e.z - b.z, [&](bool v, uint32_t own, uint32_t j, uint32_t) {
       const uint32_t ro = __shfl(b.z, (int)own);
-      if (!v) return;
-      const uint32_t p = o.e_val[ro + j];
-      atomicAdd(&a[2][own], ax.sc_w[p]);
-      atomicAdd(&a[3][own], (uint32_t)ax.sc_self[p]);
-      atomicAdd(&a[4][own], ax.psup_ptr[p + 1] - ax.psup_ptr[p]);
+      const uint2 ps = v ? ax.pstat[o.e_val[ro + j]] : make_uint2(0u, 0u);
+      const uint32_t ow = v ? own : 64u;
+      seg_add(a[2], ow, ps.x);
+      seg_add(a[3], ow, ps.y & 1u);
+      seg_add(a[4], ow, ps.y >> 1);
     });
     // exl*: base propagations ((r, x), B) with (r, x) a pair
     wave_concat(props && fe > fb ? e.w - b.w : 0u, [&](bool v, uint32_t own, uint32_t j, uint32_t) {
       const uint32_t ro = __shfl(b.w, (int)own), f0 = __shfl(fb, (int)own), f1 = __shfl(fe, (int)own);
-      if (!v) return;
-      if (pid_of(ax, o.l_r[ro + j], f0, f1) != NONE) atomicAdd(&a[5][own], 1u);
+      const bool hit = v && pid_of(ax, o.l_r[ro + j], f0, f1) != NONE;
+      seg_add(a[5], v ? own : 64u, hit ? 1u : 0u);
     });
     Lds::sync();
     if (ok) {

@@ -124,6 +124,9 @@ struct DIndex {
   const uint32_t *exl_r, *exl_b;
   const uint32_t *fp_ptr, *pair_role, *pair_y;
   const uint32_t *psup_ptr, *psup_pid;
+  // pid -> {role, filler, psup begin, psup end}: what a link trigger reads of its pair, one 16-B
+  // load instead of three random lines (k_expand's link role)
+  const uint4* pinfo;
   const uint32_t *chf_ptr, *chf_s, *chf_t;
   const uint32_t *chs_ptr, *chs_p, *chs_t;
   const uint32_t *dom_ptr, *dom_c;
@@ -246,6 +249,9 @@ struct DState {
   DGap sc;                          // successors per X (chain-second links in partitioned mode)
   uint32_t need_pred, need_succ;  // CSRs with readers: only those get delta counts
   uint32_t dedup;                 // in-wave S-candidate filter on (EL_DEDUP_OFF: off)
+  uint32_t csort;                 // S commit in sorted chunks (commit_s_sorted; EL_COMMIT_SORT=0: off)
+  unsigned long long* lines;      // diagnostic (EL_TRACE_CANDS): S-commit atomics, distinct 64-B lines per
+                                  // wave-instruction summed, instructions (nullptr: off)
   uint32_t succ_at_commit;        // successor counts taken by k_commit (whole-ontology mode)
   // partitioned exchange: replicated chain-second link log; this step's records for other ranks:
   // chain-second links (xs), propagations (xp), activations (xa)
@@ -1071,13 +1077,16 @@ __device__ void expand_l(const DIndex& ix, const DState& st, BlockQ& q, uint32_t
   for (uint32_t base = begin + w0 * tpw; base < end; base += nw * tpw) {  // (wave-uniform)
     const uint32_t i = base + lane_id();
     const bool act = lane_id() < tpw && i < end;
-    uint32_t X = 0, pid = 0, r = 0, Y = 0;
+    uint32_t X = 0, pid = 0, r = 0, Y = 0, q0 = 0, q1 = 0;
     if (act) {
       X = st.llog_x[i];
       pid = st.llog_p[i];
       ev.v[EL_EV_TRIG]++;
-      r = ix.pair_role[pid];
-      Y = ix.pair_y[pid];
+      const uint4 pi = ix.pinfo[pid];  // (role, filler; the CR5 lift range below)
+      r = pi.x;
+      Y = pi.y;
+      q0 = pi.z;
+      q1 = pi.w;
       ev.v[EL_EV_ENT] += 2;
     }
     {  // (X, Y) ∈ R(r) new, propagation ((r, Y), B)  =>  B ∈ S(X)
@@ -1113,8 +1122,7 @@ __device__ void expand_l(const DIndex& ix, const DState& st, BlockQ& q, uint32_t
       }
       if (mask & M_R5) {  // r ⊑ s  =>  (X, Y) ∈ R(s)
         ev.v[EL_EV_ROW]++;
-        const uint32_t q1 = ix.psup_ptr[pid + 1];
-        for (uint32_t j = ix.psup_ptr[pid]; j < q1; ++j) {
+        for (uint32_t j = q0; j < q1; ++j) {
           const uint32_t sp = ix.psup_pid[j];
           ev.v[EL_EV_ENT]++;
           emit_l(st, q, !link_known(ix, st, X, sp, mask & M_LEMPTY, ev), X, sp, ev);
@@ -1296,11 +1304,43 @@ __device__ void expand_a(const DIndex& ix, const DState& st, BlockQ& q, uint32_t
   ev_flush(st.ev, EL_K_EXPAND_A, ev);
 }
 
-// LDS staging of the commit roles (one role per block)
+// S candidates per chunk of the sorted S commit (commit_s_sorted)
+constexpr uint32_t CC_BITS = 11, CC = 1u << CC_BITS;
+static_assert(CC % BLOCK == 0, "chunk per thread");
+constexpr uint32_t CSORT_MIN = 1u << 18;  // smaller commits: plain order (the sort's barriers cost more)
+
+// LDS of the commit roles (one role per block): staging of new facts / links, or the S role's
+// counting sort of a candidate chunk (bin counts, then the chunk in bin order)
 struct CommitLds {
-  uint32_t x[QS_CAP > QL_CAP ? QS_CAP : QL_CAP], v[QS_CAP > QL_CAP ? QS_CAP : QL_CAP];
-  uint32_t n, base;
+  union {
+    struct {
+      uint32_t x[QS_CAP > QL_CAP ? QS_CAP : QL_CAP], v[QS_CAP > QL_CAP ? QS_CAP : QL_CAP];
+    } q;
+    struct {
+      uint32_t bin[CC];
+      unsigned long long srt[CC];  // x << 32 | a
+      uint32_t part[BLOCK / 64];
+    } c;
+  };
+  uint32_t n, base, total;
 };
+
+// Diagnostic (EL_TRACE_CANDS): count this wave-instruction's atomics and the distinct 64-B lines
+// they address (the memory-side requests of the atomic, commit_s_sorted)
+__device__ void count_lines(unsigned long long* out, bool valid, uint32_t x, uint32_t c) {
+  const unsigned long long k = valid ? ((unsigned long long)x << 24) | (c >> 9) : ~0ull;
+  bool first = valid;
+  for (int j = 0; j < 64; ++j) {
+    const unsigned long long o = __shfl(k, j);
+    if (j < (int)lane_id() && o == k) first = false;
+  }
+  const unsigned long long v = __ballot(valid), f = __ballot(first);
+  if (lane_id() == 0 && v) {
+    atomicAdd(out, (unsigned long long)__popcll(v));
+    atomicAdd(out + 1, (unsigned long long)__popcll(f));
+    atomicAdd(out + 2, 1ull);
+  }
+}
 
 // Dedup S candidates against the bit rows; new facts go to the log (the versioned
 // ZADD of every Lua kernel, e.g. Type1_1AxiomProcessorBase.java:36-41).
@@ -1308,8 +1348,8 @@ struct CommitLds {
 __device__ void commit_s(const DIndex& ix, const DState& st, CommitLds& sm, uint32_t bid, uint32_t nb,
                          uint32_t n, const uint32_t* __restrict__ qx, const uint32_t* __restrict__ qa,
                          uint8_t flag, int kev) {
-  uint32_t* lx = sm.x;
-  uint32_t* la = sm.v;
+  uint32_t* lx = sm.q.x;
+  uint32_t* la = sm.q.v;
   uint32_t& ln = sm.n;
   uint32_t& lbase = sm.base;
   if (threadIdx.x == 0) ln = 0;
@@ -1331,6 +1371,7 @@ __device__ void commit_s(const DIndex& ix, const DState& st, CommitLds& sm, uint
       if (nw && st.summ) st.summ[(uint64_t)x * st.SB + (c >> 12)] = 1;  // (idempotent: plain store)
       if (nw) ev.v[EL_EV_EMIT]++;
     }
+    if (st.lines) count_lines(st.lines, i < n && qx[i] != NONE, x, col_of(ix, a));
     // one LDS slot per new fact; blockDim <= QS_CAP/2 so a round never overflows
     const uint32_t off = lds_reserve(&ln, nw);
     if (nw) {
@@ -1355,12 +1396,159 @@ __device__ void commit_s(const DIndex& ix, const DState& st, CommitLds& sm, uint
   ev_flush(st.ev, kev, ev);
 }
 
+// Block-wide exclusive scan of one value per thread (thread order); *total = the sum.
+// Uses sm.c.part; every thread must call it.
+__device__ __forceinline__ uint32_t block_excl(CommitLds& sm, uint32_t v, uint32_t* total) {
+  const uint32_t lane = lane_id(), wv = threadIdx.x >> 6;
+  uint32_t inc = v;
+#pragma unroll
+  for (uint32_t o = 1; o < 64; o <<= 1) {
+    const uint32_t u = __shfl_up(inc, o);
+    if (lane >= o) inc += u;
+  }
+  if (lane == 63) sm.c.part[wv] = inc;
+  __syncthreads();
+  uint32_t base = 0, tot = 0;
+#pragma unroll
+  for (uint32_t w = 0; w < BLOCK / 64; ++w) {
+    const uint32_t u = sm.c.part[w];
+    base += w < wv ? u : 0u;
+    tot += u;
+  }
+  __syncthreads();  // (part is reused by the next call)
+  *total = tot;
+  return base + inc - v;
+}
+
+// The S commit in sorted chunks.  A commit is bound by the bit-word atomics, which run at the
+// memory side, one 64-B request per distinct line of a wave-instruction: 64 lanes in 64 random
+// lines made 20 G atomics/s, the same 64 lanes in 16 / 4 lines 54 / 80 G/s (MI355X,
+// scripts/micro/commit_rate.hip, profiles/r04_commit_rate_micro.txt).  The candidates of one
+// row arrive together in the queue (a wave's triggers are consecutive log entries, mostly of one
+// X) and a row's subsumers cluster in its columns (G3 at scale 0.25: 8.6 facts per 128-B line at
+// the fixpoint), so a block counting-sorts each chunk of CC candidates in LDS before its atomics:
+// bin = (x-run of the chunk, hash of the column's 64-B line) — the chunk's runs of one x keep their
+// order (the log stays in x-runs: the streamed result's run encoding depends on it) and inside a
+// run the candidates of one line become adjacent, so the lanes of a wave-instruction meet few
+// lines.  New facts reach the log in sorted order (a block scan, no LDS atomics).  Same facts and
+// events as commit_s: a step's delta is a set.
+__device__ void commit_s_sorted(const DIndex& ix, const DState& st, CommitLds& sm, uint32_t bid, uint32_t nb,
+                                uint32_t n, const uint32_t* __restrict__ qx, const uint32_t* __restrict__ qa,
+                                uint8_t flag, int kev) {
+  constexpr uint32_t PER = CC / BLOCK;
+  Ev ev;
+  const uint32_t tid = threadIdx.x, lane = lane_id(), wv = tid >> 6;
+  for (uint32_t c0 = bid * CC; c0 < n; c0 += nb * CC) {  // (block-uniform)
+    for (uint32_t k = tid; k < CC; k += BLOCK) sm.c.bin[k] = 0;
+    // 1. this thread's PER consecutive candidates, the x-runs that start among them
+    uint32_t hx[PER], ha[PER], hb[PER], hr[PER];
+    const uint32_t e0 = c0 + tid * PER;
+    uint32_t prev = (e0 > c0 && e0 - 1 < n) ? qx[e0 - 1] : NONE;
+    uint32_t heads = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < PER; ++k) {
+      const uint32_t i = e0 + k;
+      hx[k] = i < n ? qx[i] : NONE;  // (NONE: a hole of a wave's reservation, wq_publish_s)
+      ha[k] = hx[k] != NONE ? qa[i] : 0u;
+      hr[k] = hx[k] != NONE && (i == c0 || hx[k] != prev);  // (a run head)
+      heads += hr[k];
+      if (hx[k] != NONE) prev = hx[k];
+    }
+    uint32_t nruns;
+    uint32_t run = block_excl(sm, heads, &nruns);  // heads before this thread's first candidate
+    // 2. bins: run-major, then the line hash; sbits = the line-hash bits a run gets
+    uint32_t lg = 0;
+    while ((1u << lg) < nruns) ++lg;
+    const uint32_t sbits = lg < CC_BITS ? CC_BITS - lg : 0u;
+#pragma unroll
+    for (uint32_t k = 0; k < PER; ++k) {
+      run += hr[k];
+      hb[k] = NONE;
+      if (hx[k] != NONE) {
+        const uint32_t c = col_of(ix, ha[k]);
+        const uint32_t h = sbits ? ((hx[k] * 769u + (c >> 9)) * 2654435761u) >> (32 - sbits) : 0u;
+        hb[k] = ((run - 1) << sbits) | h;
+        hr[k] = atomicAdd(&sm.c.bin[hb[k]], 1u);
+      }
+    }
+    __syncthreads();
+    // 3. exclusive scan of the bin counts (PER consecutive bins per thread), then the chunk in bin order
+    uint32_t loc[PER], sum = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < PER; ++k) {
+      loc[k] = sum;
+      sum += sm.c.bin[tid * PER + k];
+    }
+    uint32_t total;
+    const uint32_t excl = block_excl(sm, sum, &total);
+#pragma unroll
+    for (uint32_t k = 0; k < PER; ++k) sm.c.bin[tid * PER + k] = excl + loc[k];
+    __syncthreads();
+#pragma unroll
+    for (uint32_t k = 0; k < PER; ++k)
+      if (hb[k] != NONE) sm.c.srt[sm.c.bin[hb[k]] + hr[k]] = ((unsigned long long)hx[k] << 32) | ha[k];
+    __syncthreads();
+    // 4. the atomics, 64 consecutive sorted candidates per wave-instruction
+    bool nw[PER];
+    unsigned long long key[PER];
+#pragma unroll
+    for (uint32_t k = 0; k < PER; ++k) {
+      const uint32_t i = k * BLOCK + tid;
+      nw[k] = false;
+      key[k] = 0;
+      if (i < total) {
+        key[k] = sm.c.srt[i];
+        const uint32_t x = (uint32_t)(key[k] >> 32), a = (uint32_t)key[k];
+        ev.v[EL_EV_TRIG]++;
+        ev.v[EL_EV_RMW]++;
+        const uint32_t c = col_of(ix, a);  // (every candidate of an owned row lies inside the window)
+        const uint32_t m = 1u << (c & 31u);
+        const uint32_t old = c != NONE ? atomicOr(st.bits + (uint64_t)x * ix.W + (c >> 5), m) : m;
+        nw[k] = (old & m) == 0;
+        if (nw[k] && st.summ) st.summ[(uint64_t)x * st.SB + (c >> 12)] = 1;  // (idempotent: plain store)
+        if (nw[k]) ev.v[EL_EV_EMIT]++;
+      }
+      if (st.lines) count_lines(st.lines, i < total, (uint32_t)(key[k] >> 32), col_of(ix, (uint32_t)key[k]));
+    }
+    // 5. the new facts, in sorted order: per round k, the waves' counts in LDS (one barrier)
+#pragma unroll
+    for (uint32_t k = 0; k < PER; ++k) {
+      const unsigned long long m = __ballot(nw[k]);
+      if (lane == 0) sm.c.bin[k * (BLOCK / 64) + wv] = (uint32_t)__popcll(m);  // (bins are free again)
+      hr[k] = (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+    }
+    __syncthreads();  // (also: every sorted entry has been read)
+    uint32_t cnt = 0;
+    for (uint32_t j = 0; j < PER * (BLOCK / 64); ++j) {
+      const uint32_t v = sm.c.bin[j];
+#pragma unroll
+      for (uint32_t k = 0; k < PER; ++k)
+        if (j < k * (BLOCK / 64) + wv) hr[k] += v;
+      cnt += v;
+    }
+#pragma unroll
+    for (uint32_t k = 0; k < PER; ++k)
+      if (nw[k]) sm.c.srt[hr[k]] = key[k];
+    if (tid == 0) sm.base = cnt ? atomicAdd(&st.ctr->s_log, cnt) : 0u;
+    __syncthreads();
+    const uint32_t lbase = sm.base;
+    for (uint32_t k = tid; k < cnt; k += BLOCK) {
+      const unsigned long long v = sm.c.srt[k];
+      st.slog_x[lbase + k] = (uint32_t)(v >> 32);
+      st.slog_a[lbase + k] = (uint32_t)v;
+      st.slog_f[lbase + k] = flag;
+    }
+    __syncthreads();  // (the next chunk reuses the bins and the sorted entries)
+  }
+  ev_flush(st.ev, kev, ev);
+}
+
 // Dedup link candidates against the link set (checkAndInsertScript,
 // RolePairHandler.java:133-168); new links feed the predecessor/successor CSRs.
 __device__ void commit_l(const DIndex& ix, const DState& st, CommitLds& sm, uint32_t bid, uint32_t nb,
                          uint32_t n) {
-  uint32_t* lx = sm.x;
-  uint32_t* lp = sm.v;
+  uint32_t* lx = sm.q.x;
+  uint32_t* lp = sm.q.v;
   uint32_t& ln = sm.n;
   uint32_t& lbase = sm.base;
   if (threadIdx.x == 0) ln = 0;
@@ -1612,7 +1800,11 @@ __device__ __forceinline__ bool gen_overflowed(const DState& st) {
 __global__ void k_commit_told(DIndex ix, DState st, uint32_t cap) {
   __shared__ CommitLds sm;
   if (gen_overflowed(st)) return;
-  commit_s(ix, st, sm, blockIdx.x, gridDim.x, min(st.ctr->cand_t, cap), st.ct_x, st.ct_a, 1, EL_K_COMMIT_T);
+  const uint32_t n = min(st.ctr->cand_t, cap);
+  if (st.csort && n >= CSORT_MIN)
+    commit_s_sorted(ix, st, sm, blockIdx.x, gridDim.x, n, st.ct_x, st.ct_a, 1, EL_K_COMMIT_T);
+  else
+    commit_s(ix, st, sm, blockIdx.x, gridDim.x, n, st.ct_x, st.ct_a, 1, EL_K_COMMIT_T);
 }
 
 // Block-wide: copy every counter but seq to the host mirror, then zero those in zero_mask
@@ -1646,7 +1838,11 @@ __global__ void k_commit(DIndex ix, DState st, CommitArgs a) {
   if (gen_overflowed(st)) {
     // nothing committed (see gen_overflowed); the counters still reach the host
   } else if (b < a.gs) {
-    commit_s(ix, st, sm, b, a.gs, min(st.ctr->cand_s, a.cs_cap), st.cs_x, st.cs_a, 0, EL_K_COMMIT_S);
+    const uint32_t n = min(st.ctr->cand_s, a.cs_cap);
+    if (st.csort && n >= CSORT_MIN)
+      commit_s_sorted(ix, st, sm, b, a.gs, n, st.cs_x, st.cs_a, 0, EL_K_COMMIT_S);
+    else
+      commit_s(ix, st, sm, b, a.gs, n, st.cs_x, st.cs_a, 0, EL_K_COMMIT_S);
   } else if ((b -= a.gs) < a.gl) {
     commit_l(ix, st, sm, b, a.gl, min(st.ctr->cand_l, a.cl_cap));
   } else if ((b -= a.gl) < a.ga) {
@@ -2561,6 +2757,7 @@ struct el_ctx {
   bool split_commit = getenv("EL_SPLIT_COMMIT") != nullptr;  // diagnostic only
   bool split_expand = getenv("EL_SPLIT_EXPAND") != nullptr;  // diagnostic: one k_expand launch per role
   unsigned long long* ev_sum = nullptr;   // k_ev_reduce output
+  unsigned long long* lines_dbg = nullptr;  // EL_TRACE_CANDS: DState::lines
   unsigned long long* ev_host = nullptr;  // pinned copy of ev_sum
   bool events_queued = false;
   uint64_t s_count = 0, l_count = 0, a_count = 0, p_count = 0, s_init = 0;
@@ -2657,6 +2854,12 @@ struct el_ctx {
   uint32_t tune_jobs = env_u32("EL_JOBS_BLOCKS", 1024);
   uint32_t tune_scatter = env_u32("EL_SCATTER_BLOCKS", 512);
   bool small_queues = getenv("EL_QUEUE_CAP") != nullptr;
+  bool commit_sort = !getenv("EL_COMMIT_SORT") || getenv("EL_COMMIT_SORT")[0] != '0';
+  // workgroups of the summary clear.  It runs beside the told closure (rstream): with 2048
+  // workgroups it held every CU and the closure's small launches queued behind it (a 5-µs fill
+  // took 615 µs in the trace); 256 leave room (G3 A/B: 25.55 / 25.68 vs 25.86 ms, init 6.38 vs
+  // 6.67 ms; 512: 25.83 / 25.93)
+  uint32_t clear_grid = getenv("EL_CLEAR_GRID") ? (uint32_t)std::max(1, atoi(getenv("EL_CLEAR_GRID"))) : 256u;
   bool dedup_off = getenv("EL_DEDUP_OFF") != nullptr;  // diagnostic A/B of the in-wave filter  // tests: queues start small, grow only on demand
 
   DState dstate() const {
@@ -2695,6 +2898,8 @@ struct el_ctx {
     s.need_pred = need_pred ? 1u : 0u;
     s.need_succ = need_succ ? 1u : 0u;
     s.dedup = dedup_off ? 0u : 1u;
+    s.csort = commit_sort ? 1u : 0u;
+    s.lines = lines_dbg;
     s.succ_at_commit = (need_succ && !part()) ? 1u : 0u;
     s.xlog_x = xlog_x;
     s.xlog_p = xlog_p;
@@ -2863,6 +3068,7 @@ struct el_ctx {
   bool mark_pending = false;
   void stream_end(bool release);
   hipEvent_t ev_base[2] = {nullptr, nullptr};  // base links logged (stream) / in the link set (rstream)
+  hipEvent_t ev_init[2] = {nullptr, nullptr};  // closure rows ready (stream) / init facts written (rstream)
   bool base_filling = false;                   // the set fill runs beside the first superstep
   void join_base();
   bool pre_reset = false;         // the device part of the next reset_state is already enqueued
@@ -2950,6 +3156,13 @@ std::string el_ctx::install_index(el::HostIndex&& hnew) {
   d.fp_ptr = up32(h.fp_ptr);
   d.pair_role = up32(h.pair_role);
   d.pair_y = up32(h.pair_y);
+  {
+    std::vector<uint4> pi(h.P);
+    for (uint32_t q = 0; q < h.P; ++q) pi[q] = make_uint4(h.pair_role[q], h.pair_y[q], h.psup.ptr[q], h.psup.ptr[q + 1]);
+    uint4* pp = dupload(pi);
+    index_bufs.push_back(pp);
+    d.pinfo = pp;
+  }
   d.psup_ptr = up32(h.psup.ptr);
   d.psup_pid = up32(h.psup.a);
   d.chf_ptr = up32(h.chf.ptr);
@@ -2980,6 +3193,17 @@ std::string el_ctx::install_index(el::HostIndex&& hnew) {
     a.psup_ptr = d.psup_ptr;
     a.sc_self = up8(h.sc_self);
     a.sc_w = up32(h.sc_w);
+    {
+      std::vector<uint2> ps(h.P);
+      for (uint32_t q = 0; q < h.P; ++q)
+        ps[q] = make_uint2(h.sc_w[q], ((h.psup.ptr[q + 1] - h.psup.ptr[q]) << 1) | (h.sc_self[q] ? 1u : 0u));
+      std::vector<uint32_t> cz(h.N);
+      for (uint32_t q = 0; q < h.N; ++q) cz[q] = h.cidx.ptr[q + 1] - h.cidx.ptr[q];
+      uint2* pp = dupload(ps);
+      index_bufs.push_back(pp);
+      a.pstat = pp;
+      a.cz = up32(cz);
+    }
     a.fp_ptr = d.fp_ptr;
     a.pair_role = d.pair_role;
     a.kind = d.kind;
@@ -3207,6 +3431,7 @@ void el_ctx::free_state() {
   if (hc_pinned) (void)hipHostFree(hc_pinned);
   hc_pinned = nullptr;
   dfree(ev_sum);
+  dfree(lines_dbg);
   if (ev_host) (void)hipHostFree(ev_host);
   ev_host = nullptr;
   events_queued = false;
@@ -3309,6 +3534,10 @@ void el_ctx::alloc_state() {
   commit_seq = 0;
   ev = dalloc<unsigned long long>(EV_WORDS);
   ev_sum = dalloc<unsigned long long>(EV_TOTAL);
+  if (trace_cands) {
+    lines_dbg = dalloc<unsigned long long>(3);
+    HIPCHK(hipMemset(lines_dbg, 0, 3 * sizeof(unsigned long long)));
+  }
   HIPCHK(hipHostMalloc((void**)&ev_host, EV_TOTAL * sizeof(unsigned long long), hipHostMallocDefault));
   HIPCHK(hipHostGetDevicePointer((void**)&hc_dev, hc_pinned, 0));
   scan_tiles = 0;
@@ -3343,7 +3572,7 @@ void el_ctx::reset_device(hipStream_t stream, uint32_t clear_from, uint32_t summ
     // by the block summary (it marks every block holding a bit, whoever set it, once the matrix
     // was cleared whole: bits_logged); clears the summary of those rows too
     const uint64_t r0 = clear_from - lo;
-    hipLaunchKernelGGL(k_clear_summ, dim3(2048), dim3(BLOCK), 0, stream, bits + r0 * W, (uint64_t)W, summ + r0 * SB,
+    hipLaunchKernelGGL(k_clear_summ, dim3(clear_grid), dim3(BLOCK), 0, stream, bits + r0 * W, (uint64_t)W, summ + r0 * SB,
                        SB, (uint64_t)(hi - clear_from));
     HIPCHK(hipGetLastError());
     summ_from = hi;
@@ -3727,9 +3956,18 @@ bool el_ctx::superstep(uint32_t mask, uint64_t sb, uint64_t se, uint64_t lb, uin
     // built lazily, for export only
     wait_commit(ca.pub.seq);
     if (trace_cands)  // diagnostic (EL_TRACE_CANDS): candidates vs. new facts per step
-      fprintf(stderr, "step cand_t %u cand_s %u new_s %llu cand_l %u new_l %llu cand_p %u jobs %u\n", hc.cand_t, hc.cand_s,
-              (unsigned long long)(hc.s_log - s_count), hc.cand_l, (unsigned long long)(hc.l_log - l_count), hc.cand_p,
-              hc.jobs);
+    {
+      unsigned long long ln[3] = {0, 0, 0};
+      if (lines_dbg) {
+        HIPCHK(hipMemcpy(ln, lines_dbg, sizeof(ln), hipMemcpyDeviceToHost));
+        HIPCHK(hipMemset(lines_dbg, 0, sizeof(ln)));
+      }
+      fprintf(stderr,
+              "step cand_t %u cand_s %u new_s %llu cand_l %u new_l %llu cand_p %u jobs %u | S atomics %llu lines %llu "
+              "instr %llu\n",
+              hc.cand_t, hc.cand_s, (unsigned long long)(hc.s_log - s_count), hc.cand_l,
+              (unsigned long long)(hc.l_log - l_count), hc.cand_p, hc.jobs, ln[0], ln[1], ln[2]);
+    }
     const uint64_t next_trig = (hc.s_log - s_count) + (hc.l_log - l_count);  // the next step's triggers
     s_count = hc.s_log;
     l_count = hc.l_log;
@@ -4308,12 +4546,24 @@ void el_ctx::closure_state() {
     }
   }
   set_closure_ix();
-  // ---- the init facts
+  // ---- the init facts: a random-access kernel (a bit per fact) beside the base links and the
+  // layouts below (streaming work), on rstream unless profiled; they touch disjoint buffers and the
+  // engine stream joins at the end of closure_state
   DState st = dstate();
-  launch(EL_K_INIT, [&] {
-    elcl::init_facts(stream, cax, cl, lo, hi, cpos[0], 0, slog_x, slog_a, slog_f, st.bits, W, ix.c_lo, ix.c_hi, st.summ,
-                     SB);
-  });
+  const bool init_side = !profile && !getenv("EL_INIT_INLINE");
+  if (init_side) {
+    HIPCHK(hipEventRecord(ev_init[0], stream));  // (the engine stream waited for the reset above)
+    HIPCHK(hipStreamWaitEvent(rstream, ev_init[0], 0));
+    launches[EL_K_INIT]++;
+    elcl::init_facts(rstream, cax, cl, lo, hi, cpos[0], 0, slog_x, slog_a, slog_f, st.bits, W, ix.c_lo, ix.c_hi,
+                     st.summ, SB);
+    HIPCHK(hipEventRecord(ev_init[1], rstream));
+  } else {
+    launch(EL_K_INIT, [&] {
+      elcl::init_facts(stream, cax, cl, lo, hi, cpos[0], 0, slog_x, slog_a, slog_f, st.bits, W, ix.c_lo, ix.c_hi,
+                       st.summ, SB);
+    });
+  }
   hipLaunchKernelGGL(k_set_u32, dim3(1), dim3(1), 0, stream, &ctr->s_log, (uint32_t)n_init);
   HIPCHK(hipGetLastError());
   s_count = n_init;
@@ -4371,6 +4621,7 @@ void el_ctx::closure_state() {
                        g->laid ? g->start0 : nullptr);
     HIPCHK(hipGetLastError());
   }
+  if (init_side) HIPCHK(hipStreamWaitEvent(stream, ev_init[1], 0));  // (everything after sees the init facts)
 }
 
 // The base links {(X, p) : p ∈ exr*(X)} — what CR3 derives from the init facts X ∈ S(X) in the
@@ -4921,6 +5172,7 @@ int el_create(el_ctx** out, const el_config* cfg) {
     HIPCHK(hipEventCreateWithFlags(&c->ev_reset, hipEventDisableTiming));
     for (hipEvent_t& e : c->ev_copied) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     for (hipEvent_t& e : c->ev_base) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    for (hipEvent_t& e : c->ev_init) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     HIPCHK(hipEventCreateWithFlags(&c->ev_strm, hipEventDisableTiming | hipEventReleaseToSystem));
     if (c->xmode == EL_XCHG_LOCAL) c->xchg.reset(new LocalExchange(cfg->group, (int)c->part_rank));
     if (c->xmode == EL_XCHG_RCCL)  // collective: every rank of the group calls el_create
@@ -4943,6 +5195,8 @@ int el_create(el_ctx** out, const el_config* cfg) {
     for (hipEvent_t e : c->ev_copied)
       if (e) (void)hipEventDestroy(e);
     for (hipEvent_t e : c->ev_base)
+      if (e) (void)hipEventDestroy(e);
+    for (hipEvent_t e : c->ev_init)
       if (e) (void)hipEventDestroy(e);
     for (hipEvent_t e : c->ev_stage)
       if (e) (void)hipEventDestroy(e);
@@ -5634,6 +5888,8 @@ void el_destroy(el_ctx* c) {
   for (hipEvent_t e : c->ev_copied)
     if (e) (void)hipEventDestroy(e);
   for (hipEvent_t e : c->ev_base)
+    if (e) (void)hipEventDestroy(e);
+  for (hipEvent_t e : c->ev_init)
     if (e) (void)hipEventDestroy(e);
   for (hipEvent_t e : c->ev_stage)
     if (e) (void)hipEventDestroy(e);

@@ -203,6 +203,32 @@ def test_empty_and_edge():
     eng.close()
 
 
+def test_told_cycle_large_subtree(oracle_mod):
+    """A told 2-cycle (A ≡ B) at the top of a 3000-concept subtree (a random tree of depth up to
+    ~40 with existentials into it): every concept below the cycle is closed by the Jacobi
+    relaxation instead of the Kahn levels (advisor, round 3: the relaxation's capacity cliff).
+    Bit-exact against the oracle."""
+    rng = np.random.default_rng(7)
+    n = 3002
+    a, b = 2, 3
+    sub = [(a, b), (b, a)]
+    for c in range(4, n):  # each concept below one or two earlier ones (a DAG under the cycle)
+        sub.append((c, int(rng.integers(2, c))))
+        if rng.random() < 0.3:
+            sub.append((c, int(rng.integers(2, c))))
+    ex_rhs = [(int(rng.integers(2, n)), int(rng.integers(0, 3)), int(rng.integers(2, n))) for _ in range(600)]
+    ex_lhs = [(int(rng.integers(0, 3)), int(rng.integers(2, n)), int(rng.integers(2, n))) for _ in range(200)]
+    ax = ir.Axioms.build(n, 3, sub=sub, ex_rhs=ex_rhs, ex_lhs=ex_lhs)
+    o = oracle_mod.saturate(ax)
+    eng, st = _gpu(ax)
+    _assert_same(eng, o)
+    gx, ga = eng.facts()
+    assert np.count_nonzero((gx == 1000) & (ga == a)) == 1  # (deep in the subtree: A and B above it)
+    assert np.count_nonzero((gx == 1000) & (ga == b)) == 1
+    eng.close()
+    o.close()
+
+
 def test_bad_input_rejected():
     eng = engine.Engine(device=0)
     ax = ir.Axioms.build(4, 1, sub=[(2, 3)])
