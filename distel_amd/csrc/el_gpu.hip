@@ -2220,7 +2220,6 @@ struct Reloc {
   uint32_t* val;
   const uint32_t* ovq;  // (row, value, rank) per overflowing entry
   uint32_t n_ovf;
-  uint32_t* flag;    // rows: 1 while claimed (zero otherwise)
   uint32_t* nstart;  // rows: new start of a claimed row
   uint32_t* rlist;   // claimed rows (≤ n_ovf)
   unsigned long long* rc;
@@ -2235,11 +2234,15 @@ __global__ void k_reloc_claim(Reloc a) {
     uint32_t row = 0, sz = 0, old = 0;
     bool won = false;
     if (i < a.n_ovf) {
+      // the record whose rank is the row's capacity claims it: ranks come from the row's len
+      // atomic, so exactly one overflow record per row has it (an atomicExch on a per-row flag
+      // put every record of a hub row on one word: 173 µs in G3's first superstep)
       row = a.ovq[3 * (size_t)i];
-      won = atomicExch(a.flag + row, 1u) == 0u;
+      const uint32_t cap = a.end[row] - a.start[row];
+      won = a.ovq[3 * (size_t)i + 2] == cap;
       if (won) {
         sz = gap_cap(a.len[row]);
-        old = a.end[row] - a.start[row];  // (an overflowing row is full: every slot holds an entry)
+        old = cap;  // (an overflowing row is full: every slot holds an entry)
       }
     }
     uint32_t inc = sz;
@@ -2304,7 +2307,6 @@ __global__ void k_reloc_commit(Reloc a) {
     const uint32_t row = a.rlist[k];
     a.start[row] = a.nstart[row];
     a.end[row] = a.nstart[row] + gap_cap(a.len[row]);
-    a.flag[row] = 0u;
   }
 }
 
@@ -2425,7 +2427,7 @@ struct GapCsr {
   uint64_t used = 0;  // slots in use: the layout's, then every relocated row's (val[used, val_cap) is free)
   uint32_t* ovq = nullptr;
   uint64_t ovq_cap = 0;
-  uint32_t *flag = nullptr, *nstart = nullptr;  // relocation: per row (flag zero between relocations)
+  uint32_t* nstart = nullptr;  // relocation: a claimed row's new start
   uint32_t* rlist = nullptr;                    // relocation: claimed rows (ovq_cap)
   bool live = false;  // maintained for this ontology (it has readers)
   // The classification's initial layout (el_init: a device scan of the row capacities the
@@ -2440,8 +2442,6 @@ struct GapCsr {
     end = dalloc<uint32_t>(n);
     len = dalloc<uint32_t>(n);
     start0 = dalloc<uint32_t>(n + 1);
-    flag = dalloc<uint32_t>(n);
-    HIPCHK(hipMemset(flag, 0, (uint64_t)n * sizeof(uint32_t)));
     nstart = dalloc<uint32_t>(n);
     laid = false;
     total0 = (uint64_t)gap_cap(0) * n;
@@ -2466,7 +2466,6 @@ struct GapCsr {
     dfree(val);
     dfree(ovq);
     dfree(rlist);
-    dfree(flag);
     dfree(nstart);
     dfree(start0);
     val_cap = ovq_cap = total0 = used = 0;
@@ -4988,7 +4987,7 @@ void el_ctx::gap_relocate_all() {
   }
   auto args = [&](int i) {
     GapCsr& g = *gs[i];
-    return Reloc{g.used, g.start, g.end, g.len, g.val, g.ovq, ov[i], g.flag, g.nstart, g.rlist, reloc_rc + 3 * i};
+    return Reloc{g.used, g.start, g.end, g.len, g.val, g.ovq, ov[i], g.nstart, g.rlist, reloc_rc + 3 * i};
   };
   hipLaunchKernelGGL(k_reloc_reset, dim3(1), dim3(64), 0, stream, reloc_rc, &ctr->ov_pr);
   HIPCHK(hipGetLastError());
