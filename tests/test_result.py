@@ -110,6 +110,34 @@ def test_set_digest_order_independent_and_pinned(oracle_lib):
     assert result.set_digest(*o.facts(), *o.links()) == pins[("g1", 0.1)][1]
 
 
+def test_oracle_run_fixtures_consistent():
+    """The pinned full-size oracle runs (tests/golden/runs, what the -m gpu full-size tests compare
+    the engine with) match their generators' inputs, and the G3 one matches G3's set-digest pin."""
+    import json
+    from distel_amd import generators
+    here = os.path.join(os.path.dirname(__file__), "golden")
+    pins = {}
+    for line in open(os.path.join(here, "set_digests.txt")):
+        f = line.split()
+        if len(f) == 4 and not line.startswith("#"):
+            pins[(f[0], float(f[1]))] = (f[2], f[3])
+    inputs = {}
+    for case in ("g3", "g3x_compat", "g3x_elk"):
+        with open(os.path.join(here, "runs", f"{case}.json")) as fh:
+            run = json.load(fh)
+        name = run["workload"]
+        if name not in inputs:
+            inputs[name] = generators.workload(name).digest()
+        assert run["input_sha256"] == inputs[name]
+        ev = np.asarray(run["events"])
+        assert ev.ndim == 2 and ev.sum() > 0 and len(run["trace"]) == 3
+        assert len(run["trace"][0]) == run["stats"]["supersteps"]
+        if case == "g3":  # (no range fillers: every fact is the caller's)
+            assert run["set_digest"].startswith(f"{run['stats']['s_facts']}:{run['stats']['links']}:")
+    with open(os.path.join(here, "runs", "g3.json")) as fh:
+        assert json.load(fh)["set_digest"] == pins[("g3", 1.0)][1]
+
+
 def test_stream_runs_malformed_raise():
     """A streamed result's run table that does not cover its entries is an error, not an assert
     (python -O keeps the check)."""
