@@ -135,6 +135,8 @@ def parse():
     ap.add_argument("--no-cpu", action="store_true", help="skip the cpu_baseline leg")
     ap.add_argument("--no-profile", action="store_true", help="skip the profiled roofline pass")
     ap.add_argument("--cpu-procs", type=int, default=16, help="host cores for the cpu_baseline leg (at most 16)")
+    ap.add_argument("--no-cpu-full", action="store_true",
+                    help="skip the whole-workload one-core oracle run beside the cpu_baseline sample")
     ap.add_argument("--cpu-scale", type=float, default=0.0,
                     help="workload scale of the cpu_baseline sample (default: --scale, capped at ~100 k concepts)")
     ap.add_argument("--partition", default="auto", choices=["auto", "copies", "exchange"],
@@ -453,6 +455,17 @@ def main():
                "init_saturate_s": round(cb["single_s"] - cb["single_create_s"], 4)}
         if cpu_scale == args.scale and world == 1:
             cpu["parity_derived_equal"] = cb["single_derived"] == st["derived"]
+        if world == 1 and cpu_scale < args.scale and not args.no_cpu_full:
+            # beside the sample: the whole workload classified by the oracle on one host core
+            # (G3: ≈15 s, 19 GB of host memory for its bit matrix)
+            out = subprocess.run([sys.executable, os.path.join(ROOT, "oracle", "cpu_baseline.py"), args.workload,
+                                  str(args.scale), "1"], check=True, capture_output=True, text=True).stdout
+            fb = json.loads(out.strip().splitlines()[-1])
+            cpu["full_1core"] = {"value": round(fb["single_derived"] / fb["single_s"], 1), "unit": "axioms/s",
+                                 "classification_s": round(fb["single_s"], 4),
+                                 "closure_index_s": round(fb["single_create_s"], 4),
+                                 "derived": fb["single_derived"], "parity_derived_equal": fb["single_derived"] == st["derived"],
+                                 "sample": f"the whole {args.workload} workload, one classification by the CPU oracle on one core"}
 
     if rank == 0:
         extra = {}
