@@ -162,6 +162,39 @@ def parse():
     return ap.parse_args()
 
 
+def bind_gpu_numa(dev: int):
+    """Pin this process (and the children it starts) to the CPUs of its GPU's NUMA node, before
+    any page-locked buffer is allocated, so those buffers and the host threads that wait on the
+    device sit next to the GPU's PCIe link.  Page-locked memory on the far node halves the D2H
+    rate of the streamed result; which node a run lands on otherwise varies from run to run.
+    EL_NUMA_BIND=0 leaves the affinity alone.  Returns what was done (for the bench line)."""
+    if os.environ.get("EL_NUMA_BIND", "1") == "0":
+        return {"bound": False, "reason": "EL_NUMA_BIND=0"}
+    try:
+        import ctypes
+        hip = ctypes.CDLL("libamdhip64.so.7")
+        buf = ctypes.create_string_buffer(64)
+        if hip.hipDeviceGetPCIBusId(buf, 64, int(dev)) != 0:
+            return {"bound": False, "reason": "hipDeviceGetPCIBusId failed"}
+        bus = buf.value.decode().lower()
+        with open(f"/sys/bus/pci/devices/{bus}/numa_node") as f:
+            node = int(f.read())
+        if node < 0:
+            return {"bound": False, "pci": bus, "node": node}
+        cpus = set()
+        with open(f"/sys/devices/system/node/node{node}/cpulist") as f:
+            for part in f.read().strip().split(","):
+                a, _, b = part.partition("-")
+                cpus.update(range(int(a), int(b or a) + 1))
+        use = cpus & os.sched_getaffinity(0)
+        if not use:
+            return {"bound": False, "pci": bus, "node": node, "reason": "no allowed CPU on the node"}
+        os.sched_setaffinity(0, use)
+        return {"bound": True, "pci": bus, "node": node, "cpus": len(use)}
+    except (OSError, ValueError, AttributeError) as e:
+        return {"bound": False, "reason": str(e)[:80]}
+
+
 def main():
     args = parse()
     import threading
@@ -175,6 +208,7 @@ def main():
     world, rank, local = rk.world, rk.rank, rk.local
     has_cuda = torch.cuda.is_available()
     dev = local if has_cuda else 0
+    numa = bind_gpu_numa(dev) if has_cuda else None
 
     t0 = time.time()
     ax = generators.workload(args.workload, args.scale)   # this rank's copy (×world disjoint copies)
@@ -474,6 +508,7 @@ def main():
             extra["copies"] = leg_summary(legs["copies"]) if "copies" in legs else None
         extra["roofline"] = roofline
         extra["cpu_baseline"] = cpu
+        extra["numa"] = numa
         line = build_line(head, head_name, extra)
         if kernels:  # the record roofline is computed from (HIP events, the profiled classification)
             line["kernels"] = kernels
