@@ -20,7 +20,12 @@ namespace elcl {
 namespace {
 
 constexpr uint32_t NONE = 0xffffffffu;
-constexpr uint32_t CAPW = 2048;   // LDS per wave: 2048 32-bit keys = 1024 64-bit keys (8 KB)
+#ifndef EL_CLOSURE_CAPW
+#define EL_CLOSURE_CAPW 2048
+#endif
+constexpr uint32_t CAPW = EL_CLOSURE_CAPW;  // LDS per wave: 2048 32-bit keys = 1024 64-bit keys (8 KB)
+// (a power of two: the LDS bitonic sort pads a row of up to CAPW keys to the next power of two in place)
+static_assert((CAPW & (CAPW - 1)) == 0, "CAPW must be a power of two");
 constexpr uint32_t TOP = 1, BOT = 0;
 constexpr uint8_t KIND_DATATYPE = 3;
 constexpr uint32_t WAVES = BLOCK / 64;
@@ -739,7 +744,12 @@ __global__ void __launch_bounds__(BLOCK) k_start(Axioms ax, Out o) {
   if (root) o.lvl_flag[0] = 1;  // (zeroed by the host before this launch)
 }
 
+#ifdef EL_LEVEL_WAVES  // (A/B builds: a VGPR budget for more waves per SIMD; CAPW sets the LDS one)
+__global__ void __attribute__((amdgpu_flat_work_group_size(BLOCK, BLOCK), amdgpu_waves_per_eu(EL_LEVEL_WAVES, 8)))
+k_level(Axioms ax, Out o, uint32_t L) {
+#else
 __global__ void __launch_bounds__(BLOCK) k_level(Axioms ax, Out o, uint32_t L) {
+#endif
   if (o.lvl_flag[L] == 0) return;  // (block-uniform: nothing at this level)
   __shared__ unsigned long long lds[WAVES * (CAPW / 2)];
   __shared__ uint32_t sany;

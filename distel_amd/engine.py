@@ -17,6 +17,8 @@ from .ir import Axioms
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "lib", "libel_gpu.so")
+if os.environ.get("EL_LIB_VARIANT"):  # A/B of a differently compiled build (scripts/build_variant.sh)
+    LIB_PATH = os.path.join(_HERE, "lib", "variants", f"libel_gpu_{os.environ['EL_LIB_VARIANT']}.so")
 
 EL_OK, EL_EINVAL, EL_ENOMEM, EL_EHIP, EL_ESTATE, EL_ERANGE = 0, -1, -2, -3, -4, -5
 LAYOUT_X_TO_B, LAYOUT_B_TO_X = 0, 1
