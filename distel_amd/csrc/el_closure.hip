@@ -777,16 +777,20 @@ __global__ void __launch_bounds__(BLOCK) k_level(Axioms ax, Out o, uint32_t L) {
       } else if (T == R_EXL) {
         task<R_EXL, false>(ax, o, A, lbuf, rs, &pr);
       } else {
-        task<R_TOLD, false>(ax, o, A, lbuf, rs, &pr);
-        // a sub whose last super this was is ready for the next level
+        // the first 64 subs are loaded before the merge, so their loads overlap it
         const uint32_t cb = pr.ob, ce = pr.ob + pr.on;
-        for (uint32_t q = cb + lane(); q < ce; q += 64) {
-          const uint32_t c = ax.chi[q];
-          if (o.level[c] != SKIP && atomicSub(o.indeg + c, 1u) == 1u) {
+        const uint32_t c0 = cb + lane() < ce ? ax.chi[cb + lane()] : NONE;
+        task<R_TOLD, false>(ax, o, A, lbuf, rs, &pr);
+        // a sub whose last super this was is ready for the next level.  The count first: the level
+        // word is read only for the sub that reaches zero (a skipped concept's count is never read)
+        auto ready = [&](uint32_t c) {
+          if (atomicSub(o.indeg + c, 1u) == 1u && o.level[c] != SKIP) {
             o.level[c] = L + 1;
             any = true;
           }
-        }
+        };
+        if (c0 != NONE) ready(c0);
+        for (uint32_t q = cb + 64 + lane(); q < ce; q += 64) ready(ax.chi[q]);
       }
     }
   }
@@ -855,7 +859,7 @@ __global__ void __launch_bounds__(BLOCK) k_level0(Axioms ax, Out o) {
       const uint32_t cbo = __shfl(cb, (int)own);
       if (!v) return;
       const uint32_t c = ax.chi[cbo + j];
-      if (o.level[c] != SKIP && atomicSub(o.indeg + c, 1u) == 1u) {
+      if (atomicSub(o.indeg + c, 1u) == 1u && o.level[c] != SKIP) {  // (as in k_level)
         o.level[c] = 1u;
         any = true;
       }
