@@ -957,6 +957,41 @@ __device__ __forceinline__ void seg_add(uint32_t* acc, uint32_t own, uint32_t v)
   if (own < 64 && (ln == 63 || next != own) && sum) acc[own] += sum;
 }
 
+// wave_concat four rounds at a time, the rounds' loads in flight together: first(v, own, j)
+// returns a round's first load, second(v, own, x) its dependent load, use(v, own, y) consumes it.
+// (k_stats' per-entry lookups were one dependent chain per round: ~220 rounds per wave on G3.)
+template <class First, class Second, class Use>
+__device__ __forceinline__ void wave_concat4(uint32_t len, First&& first, Second&& second, Use&& use) {
+  const uint32_t ln = lane();
+  uint32_t inc = len;
+#pragma unroll
+  for (uint32_t o = 1; o < 64; o <<= 1) {
+    const uint32_t v = __shfl_up(inc, o);
+    if (ln >= o) inc += v;
+  }
+  const uint32_t total = __shfl(inc, 63), excl = inc - len;
+  for (uint32_t base = 0; base < total; base += 256) {  // (wave-uniform)
+    uint32_t own[4], x[4];
+    bool v[4];
+#pragma unroll
+    for (uint32_t r = 0; r < 4; ++r) {
+      const uint32_t k = base + r * 64 + ln;
+      uint32_t ow = 0;
+#pragma unroll
+      for (uint32_t step = 32; step > 0; step >>= 1)
+        if (__shfl(inc, (int)(ow + step - 1)) <= k) ow += step;
+      v[r] = k < total;
+      own[r] = v[r] ? ow : 0u;
+      x[r] = first(v[r], own[r], k - __shfl(excl, (int)own[r]));
+    }
+    decltype(second(false, 0u, 0u)) y[4];
+#pragma unroll
+    for (uint32_t r = 0; r < 4; ++r) y[r] = second(v[r], own[r], x[r]);
+#pragma unroll
+    for (uint32_t r = 0; r < 4; ++r) use(v[r], own[r], x[r], y[r]);
+  }
+}
+
 __global__ void __launch_bounds__(BLOCK) k_stats(Axioms ax, Out o, uint32_t lo, uint32_t hi, uint32_t props) {
   __shared__ uint32_t acc[WAVES][6][64];
   uint32_t(&a)[6][64] = acc[threadIdx.x >> 6];
@@ -976,31 +1011,44 @@ __global__ void __launch_bounds__(BLOCK) k_stats(Axioms ax, Out o, uint32_t lo, 
     for (int k = 0; k < 6; ++k) a[k][lane()] = 0;
     Lds::sync();
     // told*: CR2 candidates (|cidx| of every entry), ⊤ among the first two entries
-    wave_concat(e.x - b.x, [&](bool v, uint32_t own, uint32_t j, uint32_t) {
-      const uint32_t ro = __shfl(b.x, (int)own);
-      uint32_t cz = 0;
-      if (v) {
-        const uint32_t t = o.t_val[ro + j];
-        cz = ax.cz[t];
-        if (j < 2 && t == TOP) a[1][own] = 1;
-      }
-      seg_add(a[0], v ? own : 64u, cz);
-    });
+    // (the entry's position among the first two of its row: j < 2 ⇔ the row's begin + j < begin + 2)
+    wave_concat4(
+        e.x - b.x,
+        [&](bool v, uint32_t own, uint32_t j) {
+          const uint32_t ro = __shfl(b.x, (int)own);
+          return v ? (o.t_val[ro + j] | (j < 2 ? 0x80000000u : 0u)) : 0u;  // (concept ids < 2^31)
+        },
+        [&](bool v, uint32_t, uint32_t t) { return v ? ax.cz[t & 0x7fffffffu] : 0u; },
+        [&](bool v, uint32_t own, uint32_t t, uint32_t cz) {
+          if (v && (t >> 31) && (t & 0x7fffffffu) == TOP) a[1][own] = 1;
+          seg_add(a[0], v ? own : 64u, cz);
+        });
     // exr*: successor-row weight, chain-second base links, CR5 lifts
-    wave_concat(e.z - b.z, [&](bool v, uint32_t own, uint32_t j, uint32_t) {
-      const uint32_t ro = __shfl(b.z, (int)own);
-      const uint2 ps = v ? ax.pstat[o.e_val[ro + j]] : make_uint2(0u, 0u);
-      const uint32_t ow = v ? own : 64u;
-      seg_add(a[2], ow, ps.x);
-      seg_add(a[3], ow, ps.y & 1u);
-      seg_add(a[4], ow, ps.y >> 1);
-    });
+    wave_concat4(
+        e.z - b.z,
+        [&](bool v, uint32_t own, uint32_t j) {
+          const uint32_t ro = __shfl(b.z, (int)own);
+          return v ? o.e_val[ro + j] : 0u;
+        },
+        [&](bool v, uint32_t, uint32_t p) { return v ? ax.pstat[p] : make_uint2(0u, 0u); },
+        [&](bool v, uint32_t own, uint32_t, uint2 ps) {
+          const uint32_t ow = v ? own : 64u;
+          seg_add(a[2], ow, ps.x);
+          seg_add(a[3], ow, ps.y & 1u);
+          seg_add(a[4], ow, ps.y >> 1);
+        });
     // exl*: base propagations ((r, x), B) with (r, x) a pair
-    wave_concat(props && fe > fb ? e.w - b.w : 0u, [&](bool v, uint32_t own, uint32_t j, uint32_t) {
-      const uint32_t ro = __shfl(b.w, (int)own), f0 = __shfl(fb, (int)own), f1 = __shfl(fe, (int)own);
-      const bool hit = v && pid_of(ax, o.l_r[ro + j], f0, f1) != NONE;
-      seg_add(a[5], v ? own : 64u, hit ? 1u : 0u);
-    });
+    wave_concat4(
+        props && fe > fb ? e.w - b.w : 0u,
+        [&](bool v, uint32_t own, uint32_t j) {
+          const uint32_t ro = __shfl(b.w, (int)own);
+          return v ? o.l_r[ro + j] : 0u;
+        },
+        [&](bool v, uint32_t own, uint32_t r) {
+          const uint32_t f0 = __shfl(fb, (int)own), f1 = __shfl(fe, (int)own);
+          return (v && pid_of(ax, r, f0, f1) != NONE) ? 1u : 0u;
+        },
+        [&](bool v, uint32_t own, uint32_t, uint32_t hit) { seg_add(a[5], v ? own : 64u, hit); });
     Lds::sync();
     if (ok) {
       const bool two = two_of(ax, x);

@@ -856,6 +856,53 @@ __device__ __forceinline__ void wave_rows(uint32_t b, uint32_t e, F&& f) {
   }
 }
 
+// wave_rows four rounds at a time, each round's loads issued before any is used: first(valid,
+// owner, j) makes a round's first load, second(valid, owner, x) its dependent load, use(valid,
+// owner, x, y) the rest.  A round of a row walk is otherwise a chain (entry -> bit word) the wave
+// waits out alone; four in flight quadruple its memory-level parallelism.
+template <class First, class Second, class Use>
+__device__ __forceinline__ void wave_rows4(uint32_t b, uint32_t e, First&& first, Second&& second, Use&& use) {
+  const uint32_t lane = lane_id(), len = e - b;
+  uint32_t inc = len;
+#pragma unroll
+  for (uint32_t o = 1; o < 64; o <<= 1) {
+    const uint32_t v = __shfl_up(inc, o);
+    if (lane >= o) inc += v;
+  }
+  const uint32_t total = __shfl(inc, 63), excl = inc - len;
+  for (uint32_t base = 0; base < total; base += 256) {  // (wave-uniform)
+    uint32_t own[4];
+    bool valid[4];
+    decltype(first(false, 0u, 0u)) x[4];
+#pragma unroll
+    for (uint32_t r = 0; r < 4; ++r) {
+      const uint32_t k = base + r * 64 + lane;
+      uint32_t ow = 0;
+#pragma unroll
+      for (uint32_t step = 32; step > 0; step >>= 1)
+        if (__shfl(inc, (int)(ow + step - 1)) <= k) ow += step;
+      valid[r] = k < total;
+      own[r] = valid[r] ? ow : 0u;
+      x[r] = first(valid[r], own[r], __shfl(b, (int)own[r]) + (k - __shfl(excl, (int)own[r])));
+    }
+    decltype(second(false, 0u, x[0])) y[4];
+#pragma unroll
+    for (uint32_t r = 0; r < 4; ++r) y[r] = second(valid[r], own[r], x[r]);
+#pragma unroll
+    for (uint32_t r = 0; r < 4; ++r) use(valid[r], own[r], x[r], y[r]);
+  }
+}
+
+// the bit word holding (x, b)'s bit, and the bit (NONE-column: no word, bit 32 = never set)
+__device__ __forceinline__ uint32_t bit_word(const DIndex& ix, const uint32_t* bits, uint32_t x, uint32_t b) {
+  const uint32_t c = col_of(ix, b);
+  return c != NONE ? bits[(uint64_t)x * ix.W + (c >> 5)] : 0u;
+}
+__device__ __forceinline__ bool bit_in(const DIndex& ix, uint32_t word, uint32_t b) {
+  const uint32_t c = col_of(ix, b);
+  return c != NONE && ((word >> (c & 31u)) & 1u);
+}
+
 // Rules triggered by new S-facts (X, A) = log[begin, end).
 //  CR1  Type1_1AxiomProcessorBase.java:22-43      CR2  Type1_2AxiomProcessorBase.java:45-66
 //  CR3  Type2AxiomProcessorBase.java:45-75        CR4½ Type3_1AxiomProcessorBase.java:194-239
@@ -863,7 +910,7 @@ __device__ __forceinline__ void wave_rows(uint32_t b, uint32_t e, F&& f) {
 // The index rows of CR1, CR3 and CR4 half-1 (told closure, its links, its propagations) are
 // walked wave-cooperatively (wave_rows); the short CR2 rows per lane.
 // tpw: triggers per wave (lanes [0, tpw) take one each) — see wave_triggers.
-__device__ void expand_s(const DIndex& ix, const DState& st, BlockQ& q, uint32_t bid, uint32_t nb,
+__device__ __forceinline__ void expand_s(const DIndex& ix, const DState& st, BlockQ& q, uint32_t bid, uint32_t nb,
                          uint32_t begin, uint32_t end, uint32_t mask, uint32_t a_end, uint32_t tpw) {
   Ev ev;
   const uint32_t w0 = bid * (blockDim.x >> 6) + (threadIdx.x >> 6), nw = nb * (blockDim.x >> 6);
@@ -885,18 +932,22 @@ __device__ void expand_s(const DIndex& ix, const DState& st, BlockQ& q, uint32_t
     {
       const bool on = act && (mask & M_R1) && f == 0;
       if (on) ev.v[EL_EV_ROW]++;
-      wave_rows(on ? m0.x : 0u, on ? m1.x : 0u, [&](bool v, uint32_t own, uint32_t j) {
-        const uint32_t Xo = __shfl(X, (int)own);
-        uint32_t B = 0;
-        bool nw = false;
-        if (v) {
-          B = ix.told_b[j];
-          ev.v[EL_EV_ENT]++;
-          ev.v[EL_EV_TEST]++;
-          nw = !test_bit(ix, st.bits, Xo, B);
-        }
-        emit_t(st, q, nw, Xo, B, ev);
-      });
+      wave_rows4(
+          on ? m0.x : 0u, on ? m1.x : 0u,
+          [&](bool v, uint32_t own, uint32_t j) {
+            const uint32_t Xo = __shfl(X, (int)own);
+            return make_uint2(Xo, v ? ix.told_b[j] : 0u);
+          },
+          [&](bool v, uint32_t, uint2 xb) { return v ? bit_word(ix, st.bits, xb.x, xb.y) : 0u; },
+          [&](bool v, uint32_t, uint2 xb, uint32_t word) {
+            bool nw = false;
+            if (v) {
+              ev.v[EL_EV_ENT]++;
+              ev.v[EL_EV_TEST]++;
+              nw = !bit_in(ix, word, xb.y);
+            }
+            emit_t(st, q, nw, xb.x, xb.y, ev);
+          });
     }
     if (act && (mask & M_R2)) {  // A1..An ∈ S(X), ⊓Ai ⊑ B  =>  B ∈ S(X)
       ev.v[EL_EV_ROW]++;
@@ -1070,7 +1121,7 @@ __device__ __forceinline__ void r6_second(const DIndex& ix, const DState& st, Bl
 //  CR4½ Type3_2AxiomProcessorBase.java:67-96,182-224   CR5 Type4AxiomProcessorBase.java:38-76
 //  CR6  Type5AxiomProcessorBase.java:115-154           ⊥   RolePairHandler.java:358-372
 //  domain/range RolePairHandler.java:456-491
-__device__ void expand_l(const DIndex& ix, const DState& st, BlockQ& q, uint32_t bid, uint32_t nb,
+__device__ __forceinline__ void expand_l(const DIndex& ix, const DState& st, BlockQ& q, uint32_t bid, uint32_t nb,
                          uint32_t begin, uint32_t end, uint32_t mask, uint32_t tpw) {
   Ev ev;
   const uint32_t w0 = bid * (blockDim.x >> 6) + (threadIdx.x >> 6), nw = nb * (blockDim.x >> 6);
@@ -1214,18 +1265,30 @@ __global__ void k_jobs(DIndex ix, DState st, uint32_t mask) {
       ev.v[EL_EV_JOB]++;
     }
     const uint32_t type = jb.y >> 28;
-    wave_rows(jb.x, jb.x + len, [&](bool v, uint32_t own, uint32_t k) {
+    // (four rounds of entries at a time: the list entry, then the bit word a JOB_PRED_S tests)
+    wave_rows4(
+        jb.x, jb.x + len,
+        [&](bool v, uint32_t own, uint32_t k) {
+          const uint32_t t = __shfl(type, (int)own);
+          return v ? ((t == JOB_R6A) ? st.sc.val[k] : st.pr.val[k]) : 0u;
+        },
+        [&](bool v, uint32_t own, uint32_t val) {
+          const uint32_t t = __shfl(type, (int)own), b = __shfl(jb.w, (int)own);
+          return (v && t == JOB_PRED_S) ? bit_word(ix, st.bits, val, b) : 0u;
+        },
+        [&](bool v, uint32_t own, uint32_t val, uint32_t word) {
       const uint32_t t = __shfl(type, (int)own), a = __shfl(jb.z, (int)own), b = __shfl(jb.w, (int)own);
+      const uint4 e = make_uint4(val, t, a, b);
       if (t == JOB_PRED_S || t == JOB_PRED_U) {  // preds(pid) × {B}
         uint32_t xp = 0;
         bool nw = false;
         if (v) {
-          xp = st.pr.val[k];
+          xp = e.x;
           ev.v[EL_EV_ENT]++;
           nw = true;
           if (t == JOB_PRED_S) {
             ev.v[EL_EV_TEST]++;
-            nw = !test_bit(ix, st.bits, xp, b);
+            nw = !bit_in(ix, word, b);
           }
         }
         emit_s(st, q, nw, xp, b, ev);
@@ -1233,7 +1296,7 @@ __global__ void k_jobs(DIndex ix, DState st, uint32_t mask) {
         uint32_t xp = 0;
         bool nw = false;
         if (v) {
-          xp = st.pr.val[k];
+          xp = e.x;
           ev.v[EL_EV_ENT]++;
           nw = !link_known(ix, st, xp, a, lempty, ev);
         }
@@ -1242,7 +1305,7 @@ __global__ void k_jobs(DIndex ix, DState st, uint32_t mask) {
         const uint32_t X = a, r = b;
         uint32_t s2 = NONE, Z = 0, f0 = 0, f1 = 0;
         if (v) {
-          const uint32_t sq = st.sc.val[k];
+          const uint32_t sq = e.x;
           ev.v[EL_EV_ENT]++;
           s2 = ix.pair_role[sq];
           Z = ix.pair_y[sq];
@@ -1275,7 +1338,7 @@ __global__ void k_jobs(DIndex ix, DState st, uint32_t mask) {
 // X's holding Y are found in the fact log (one coalesced pass over the facts known at t-1,
 // each fact (X, Y) meeting the new activations of Y through the activation index), not by
 // sweeping column Y of the bit matrix (one random line per row and activation).
-__device__ void expand_a(const DIndex& ix, const DState& st, BlockQ& q, uint32_t bid, uint32_t nb,
+__device__ __forceinline__ void expand_a(const DIndex& ix, const DState& st, BlockQ& q, uint32_t bid, uint32_t nb,
                          uint32_t s_end, uint32_t a_begin, uint32_t a_end) {
   Ev ev;
   for (uint32_t base = bid * blockDim.x; base < s_end; base += nb * blockDim.x) {
@@ -1640,7 +1703,7 @@ __device__ void commit_a(const DIndex& ix, const DState& st, uint32_t bid, uint3
 // New CR4 propagations ((r, Y), B) = prop log[begin, end) × existing predecessors of (r, Y)
 // (per-rule stepping: Type3_2AxiomProcessor part 1, ΔB × all X).  In fused saturation the
 // fan-out happens when the propagation is generated (M_R4D), so this kernel is idle there.
-__device__ void expand_p(const DIndex& ix, const DState& st, BlockQ& q, uint32_t bid, uint32_t nb,
+__device__ __forceinline__ void expand_p(const DIndex& ix, const DState& st, BlockQ& q, uint32_t bid, uint32_t nb,
                          uint32_t begin, uint32_t end) {
   Ev ev;
   for (uint32_t base = begin + bid * blockDim.x; base < end; base += nb * blockDim.x) {
@@ -1699,7 +1762,7 @@ struct ExpandArgs {
 
 // Partitioned mode: new chain-second links of every rank = xlog[begin, end) meet this
 // rank's predecessors (CR6, r second; oracle/partition_model.py Rank.step).
-__device__ void expand_x(const DIndex& ix, const DState& st, BlockQ& q, uint32_t bid, uint32_t nb,
+__device__ __forceinline__ void expand_x(const DIndex& ix, const DState& st, BlockQ& q, uint32_t bid, uint32_t nb,
                          uint32_t begin, uint32_t end) {
   Ev ev;
   for (uint32_t base = begin + bid * blockDim.x; base < end; base += nb * blockDim.x) {
