@@ -1151,15 +1151,15 @@ __device__ __forceinline__ void expand_l(const DIndex& ix, const DState& st, Blo
       // No probe of B ∈ S(X) here: a new link's conclusions are nearly all new (G3: 103 M of
       // 107 M), so the probe was one random line read per conclusion that the commit's
       // atomicOr repeats anyway; the commit drops the few already present.
-      wave_rows(row.x, row.x + row.y, [&](bool v, uint32_t own, uint32_t j) {
-        const uint32_t Xo = __shfl(X, (int)own);
-        uint32_t B = 0;
-        if (v) {
-          B = st.pp.val[j];
-          ev.v[EL_EV_ENT]++;
-        }
-        emit_s(st, q, v, Xo, B, ev);
-      });
+      // (four rounds' entries loaded before the first is emitted: wave_rows4)
+      wave_rows4(
+          row.x, row.x + row.y,
+          [&](bool v, uint32_t own, uint32_t j) { return make_uint2(__shfl(X, (int)own), v ? st.pp.val[j] : 0u); },
+          [&](bool, uint32_t, uint2) { return 0u; },
+          [&](bool v, uint32_t, uint2 xb, uint32_t) {
+            if (v) ev.v[EL_EV_ENT]++;
+            emit_s(st, q, v, xb.x, xb.y, ev);
+          });
     }
     if (act) {
       if ((mask & M_RBOT) && ix.has_bot && !ix.part) {  // ⊥ ∈ S(Y) => ⊥ ∈ S(X)  (partitioned: via propagations)
