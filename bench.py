@@ -146,7 +146,7 @@ def parse():
     ap.add_argument("--transport", default="rccl", choices=["rccl", "host"],
                     help="exchange leg's all-gather: rccl = ncclAllGather over xGMI on the engine stream; host = "
                          "EL_XCHG_HOST through a gloo group (a rehearsal of N ranks on one GPU)")
-    ap.add_argument("--exchange-timeout", type=float, default=420.0,
+    ap.add_argument("--exchange-timeout", type=float, default=180.0,
                     help="seconds the exchange leg may take before rank 0 reports the copies leg alone")
     ap.add_argument("--inflight", type=int, default=1, choices=[1, 2],
                     help="classifications in flight in the timed loop: 1 = one at a time (the default: "
