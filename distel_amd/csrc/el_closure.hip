@@ -9,6 +9,7 @@
 // one per concept: a counter hit by 390 k concepts would serialise at ~12 ns a hit,
 // MI355X_MICROARCH.md "fanin").
 #include "el_closure.h"
+#include "el_rows.h"
 
 #include <hipcub/hipcub.hpp>
 
@@ -1182,7 +1183,7 @@ __global__ void __launch_bounds__(BLOCK) k_init_facts(Axioms ax, Out o, uint32_t
     if (col != NONE) {
       __hip_atomic_fetch_or(bits + (uint64_t)x * W + (col >> 5), 1u << (col & 31u), __ATOMIC_RELAXED,
                             __HIP_MEMORY_SCOPE_AGENT);
-      if (summ) summ[(uint64_t)x * SB + (col >> 12)] = 1;
+      if (summ) summ[(uint64_t)x * SB + (col >> elrows::SUMM_SHIFT)] = 1;
     }
   });
 }

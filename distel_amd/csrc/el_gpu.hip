@@ -824,7 +824,7 @@ __global__ void k_summ_build(const uint32_t* __restrict__ bits, uint64_t W, uint
                              uint32_t SB) {
   const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
   for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < words; i += stride)
-    if (bits[i]) summ[(i / W) * SB + (i % W >> 7)] = 1;
+    if (bits[i]) summ[(i / W) * SB + (i % W) / elrows::SUMM_WORDS] = 1;
 }
 
 // Wave-cooperative loop over one CSR row per lane, [b, e) (an idle lane passes b = e): the
@@ -1431,7 +1431,7 @@ __device__ void commit_s(const DIndex& ix, const DState& st, CommitLds& sm, uint
       const uint32_t m = 1u << (c & 31u);
       const uint32_t old = c != NONE ? atomicOr(st.bits + (uint64_t)x * ix.W + (c >> 5), m) : m;
       nw = (old & m) == 0;
-      if (nw && st.summ) st.summ[(uint64_t)x * st.SB + (c >> 12)] = 1;  // (idempotent: plain store)
+      if (nw && st.summ) st.summ[(uint64_t)x * st.SB + (c >> elrows::SUMM_SHIFT)] = 1;  // (idempotent: plain store)
       if (nw) ev.v[EL_EV_EMIT]++;
     }
     if (st.lines) count_lines(st.lines, i < n && qx[i] != NONE, x, col_of(ix, a));
@@ -1568,7 +1568,7 @@ __device__ void commit_s_sorted(const DIndex& ix, const DState& st, CommitLds& s
         const uint32_t m = 1u << (c & 31u);
         const uint32_t old = c != NONE ? atomicOr(st.bits + (uint64_t)x * ix.W + (c >> 5), m) : m;
         nw[k] = (old & m) == 0;
-        if (nw[k] && st.summ) st.summ[(uint64_t)x * st.SB + (c >> 12)] = 1;  // (idempotent: plain store)
+        if (nw[k] && st.summ) st.summ[(uint64_t)x * st.SB + (c >> elrows::SUMM_SHIFT)] = 1;  // (idempotent: plain store)
         if (nw[k]) ev.v[EL_EV_EMIT]++;
       }
       if (st.lines) count_lines(st.lines, i < total, (uint32_t)(key[k] >> 32), col_of(ix, (uint32_t)key[k]));
@@ -2211,11 +2211,27 @@ __global__ void k_rehash(unsigned long long* t, unsigned long long mask, const u
 
 // el_init after a classification: only the words the fact log names can be non-zero, and
 // when the log is small next to the matrix, clearing those words beats streaming it all
-// Clear the bit matrix by its block summary: every marked 512-B block is zeroed by one wave
-// (8 B per lane, one coalesced store), its summary byte with it.  Reads the summary (1/512 of
-// the matrix) and writes only the blocks that hold a bit: G3's 104 M facts lie in ~10 M of 37 M
-// blocks, so ~5 GB of streaming stores instead of 104 M scattered ones (k_clear_logged) or a
-// 19 GB memset.  rows: the summary's rows (relative to the matrix base), SB bytes each.
+// Clear the bit matrix by its block summary: every marked block is zeroed (512-B blocks: by one
+// wave, 8 B per lane, one coalesced store; smaller blocks: SUMM_WORDS / 4 lanes of 16 B each, so
+// one store instruction zeroes 64 / (SUMM_WORDS / 4) whole blocks), its summary byte with it.
+// Reads the summary and writes only the blocks that hold a bit: G3's 104 M facts lie in 10.0 M
+// of 37 M 512-B blocks (5.1 GB of stores), 27.9 M 128-B blocks (3.6 GB) or 43.0 M 64-B lines
+// (2.8 GB), instead of 104 M scattered stores (k_clear_logged) or a 19 GB memset.
+// rows: the summary's rows (relative to the matrix base), SB bytes each.
+__device__ __forceinline__ uint32_t nth_set(unsigned long long m, uint32_t k) {  // k-th set bit of m
+  uint32_t pos = 0;
+#pragma unroll
+  for (uint32_t w = 32; w >= 1; w >>= 1) {
+    const uint32_t c = (uint32_t)__popcll(m & ((1ull << w) - 1ull));
+    if (k >= c) {
+      k -= c;
+      m >>= w;
+      pos += w;
+    }
+  }
+  return pos;
+}
+
 __global__ void k_clear_summ(uint32_t* __restrict__ bits, uint64_t W, uint8_t* __restrict__ summ, uint32_t SB,
                              uint64_t rows) {
   const uint32_t lane = threadIdx.x & 63u;
@@ -2223,21 +2239,34 @@ __global__ void k_clear_summ(uint32_t* __restrict__ bits, uint64_t W, uint8_t* _
   const uint64_t wave = (blockIdx.x * (uint64_t)blockDim.x + threadIdx.x) >> 6;
   const uint64_t waves = ((uint64_t)gridDim.x * blockDim.x) >> 6;
   uint32_t* sw = reinterpret_cast<uint32_t*>(summ);
+  constexpr uint32_t G = elrows::SUMM_WORDS / 4, PER = 64 / G;  // lanes per block, blocks per store
   for (uint64_t base = wave * 64; base < dwords; base += waves * 64) {  // (wave-uniform)
     const uint64_t d = base + lane;
     const uint32_t v = d < dwords ? sw[d] : 0u;
     for (uint32_t j = 0; j < 4; ++j) {
       unsigned long long m = __ballot(((v >> (8 * j)) & 0xffu) != 0u);
-      while (m) {
-        const uint32_t L = (uint32_t)__ffsll((long long)m) - 1u;
-        m &= m - 1ull;
-        const uint64_t sb = (base + L) * 4 + j;  // summary byte: row sb / SB, block sb % SB
-        const uint64_t row = sb / SB, w0 = (sb - row * SB) * 128 + 2 * lane;
-        uint32_t* p = bits + row * W + w0;
-        if (w0 + 1 < W) {
-          *reinterpret_cast<uint2*>(p) = make_uint2(0u, 0u);
-        } else if (w0 < W) {
-          *p = 0u;
+      if constexpr (G == 32) {  // 512-B blocks
+        while (m) {
+          const uint32_t L = (uint32_t)__ffsll((long long)m) - 1u;
+          m &= m - 1ull;
+          const uint64_t sb = (base + L) * 4 + j;  // summary byte: row sb / SB, block sb % SB
+          const uint64_t row = sb / SB, w0 = (sb - row * SB) * 128 + 2 * lane;
+          uint32_t* p = bits + row * W + w0;
+          if (w0 + 1 < W) {
+            *reinterpret_cast<uint2*>(p) = make_uint2(0u, 0u);
+          } else if (w0 < W) {
+            *p = 0u;
+          }
+        }
+      } else {
+        const uint32_t n = (uint32_t)__popcll(m);
+        for (uint32_t r = 0; r < n; r += PER) {  // (wave-uniform)
+          const uint32_t k = r + lane / G;
+          if (k < n) {
+            const uint64_t sb = (base + nth_set(m, k)) * 4 + j;
+            const uint64_t row = sb / SB, w0 = (sb - row * SB) * elrows::SUMM_WORDS + (lane % G) * 4;
+            if (w0 < W) *reinterpret_cast<uint4*>(bits + row * W + w0) = make_uint4(0u, 0u, 0u, 0u);  // (W % 4 == 0)
+          }
         }
       }
     }
@@ -2719,14 +2748,18 @@ struct el_ctx {
   // state
   uint32_t* bits = nullptr;
   uint64_t W = 0;
-  // Block summary of the bit rows: one byte per 512-B block (128 words) of each owned row, set
+  // Block summary of the bit rows: one byte per block of SUMM_WORDS words (512 B by default,
+  // EL_SUMM_SHIFT) of each owned row, set
   // with a plain store by every writer of a bit (k_commit, k_init, k_init_bits), cleared with
   // the matrix; the copy-back read-out loads only the blocks it marks.
   uint8_t* summ = nullptr;
   uint32_t SB = 0;
   bool no_summary = getenv("EL_NO_SUMMARY") != nullptr;  // A/B: dense read-out
-  // one byte per 128 words, rows padded to 16 B (k_fill clears from any row with 16-B stores)
-  static uint32_t summ_stride(uint64_t w) { return (uint32_t)((((w + 127) / 128) + 15) & ~15ull); }
+  // one byte per SUMM_WORDS words, rows padded to 16 B (k_fill clears from any row with 16-B
+  // stores; whole 512-B blocks of the read-out)
+  static uint32_t summ_stride(uint64_t w) {
+    return (uint32_t)((((w + elrows::SUMM_WORDS - 1) / elrows::SUMM_WORDS) + 15) & ~15ull);
+  }
   uint32_t *slog_x = nullptr, *slog_a = nullptr;
   uint8_t* slog_f = nullptr;  // told-closure flags of the facts (slog_cap)
   uint64_t slog_cap = 0;

@@ -27,7 +27,18 @@
 
 #include <cstdint>
 
+// Block summary granularity: one summary byte per 2^EL_SUMM_SHIFT bits of a matrix row (12: a
+// 512-B block, 9: a 64-B line).  The read-out works in 512-B blocks (the OR of SUMM_SUB bytes).
+#ifndef EL_SUMM_SHIFT
+#define EL_SUMM_SHIFT 9
+#endif
+static_assert(EL_SUMM_SHIFT >= 9 && EL_SUMM_SHIFT <= 12, "summary block: 64 B .. 512 B");
+
 namespace elrows {
+
+constexpr uint32_t SUMM_SHIFT = EL_SUMM_SHIFT;
+constexpr uint32_t SUMM_WORDS = 1u << (SUMM_SHIFT - 5);   // matrix words per summary byte
+constexpr uint32_t SUMM_SUB = 1u << (12 - SUMM_SHIFT);     // summary bytes per 512-B block
 
 // The S bit matrix: row x at bits + x·W, rows r of the build at x = r + lo; columns ⊥, ⊤,
 // then the concepts [c_lo, c_hi) (column c >= 2 is concept c + c_lo - 2).  Read by the
@@ -38,8 +49,9 @@ struct Clear {
   uint64_t W = 0;
   uint32_t lo = 0;
   uint32_t c_lo = 2, c_hi = 0xffffffffu;
-  // optional block summary: byte x·SB + k is non-zero if row x may hold a set bit in its 512-B
-  // block k (words [128 k, 128 k + 128)); the read-out then reads only those blocks
+  // optional block summary: byte x·SB + k is non-zero if row x may hold a set bit in its block k
+  // (words [SUMM_WORDS k, SUMM_WORDS (k + 1))); the read-out then reads only the 512-B blocks
+  // whose SUMM_SUB bytes are not all zero
   uint8_t* summ = nullptr;  // (the read-out zeroes a row's bytes with its words when clearing)
   uint32_t SB = 0;
   __device__ void bit(uint32_t r, uint32_t v) const;

@@ -536,6 +536,20 @@ __global__ void __launch_bounds__(BLOCK) k_rows_global(const uint64_t* __restric
 
 }  // namespace
 
+// The read-out's 512-B block k of a summary row: marked if any of its SUMM_SUB bytes is set.
+__device__ __forceinline__ bool summ_any(const uint8_t* sr, uint32_t k) {
+  if constexpr (SUMM_SUB == 8) return reinterpret_cast<const uint64_t*>(sr)[k] != 0ull;
+  if constexpr (SUMM_SUB == 4) return reinterpret_cast<const uint32_t*>(sr)[k] != 0u;
+  if constexpr (SUMM_SUB == 2) return reinterpret_cast<const uint16_t*>(sr)[k] != 0u;
+  return sr[k] != 0;
+}
+__device__ __forceinline__ void summ_zero(uint8_t* sr, uint32_t k) {
+  if constexpr (SUMM_SUB == 8) reinterpret_cast<uint64_t*>(sr)[k] = 0ull;
+  else if constexpr (SUMM_SUB == 4) reinterpret_cast<uint32_t*>(sr)[k] = 0u;
+  else if constexpr (SUMM_SUB == 2) reinterpret_cast<uint16_t*>(sr)[k] = 0u;
+  else sr[k] = 0;
+}
+
 // k_rows_readout over the block summary: a row's non-zero 512-B blocks (summary bytes set by
 // every writer of the matrix) are listed in LDS in column order, and the read-out loads only
 // those — G3's rows hold their 104 M facts in 9.9 M of 37 M blocks, so the copy-back reads
@@ -559,10 +573,11 @@ __global__ void __launch_bounds__(BLOCK) k_rows_readout_sparse(const uint64_t* _
     uint4* __restrict__ row = reinterpret_cast<uint4*>(m.bits + (uint64_t)(r + m.lo) * m.W);
     uint8_t* __restrict__ sr = m.summ + (uint64_t)(r + m.lo) * m.SB;
     uint64_t done = 0;
-    for (uint32_t k0 = 0; k0 < m.SB && done < len; k0 += BLOCK) {
+    const uint32_t NB = m.SB / SUMM_SUB;  // 512-B blocks of the summary row
+    for (uint32_t k0 = 0; k0 < NB && done < len; k0 += BLOCK) {
       // list this chunk's non-zero blocks, ascending (wave ballots, then the waves in order)
-      const bool nz = k0 + tid < m.SB && sr[k0 + tid] != 0;
-      if (clear && nz) sr[k0 + tid] = 0;  // (the reset leaves the read-out's rows to it)
+      const bool nz = k0 + tid < NB && summ_any(sr, k0 + tid);
+      if (clear && nz) summ_zero(sr, k0 + tid);  // (the reset leaves the read-out's rows to it)
       const unsigned long long bal = __ballot(nz);
       if (lane == 0) wsum[0][wv] = (uint32_t)__popcll(bal);
       __syncthreads();
@@ -653,9 +668,10 @@ __global__ void __launch_bounds__(BLOCK) k_rows_readout_wave(const uint64_t* __r
     uint8_t* __restrict__ sr = m.summ + (uint64_t)(r + m.lo) * m.SB;
     uint32_t* __restrict__ out = dst + (b - out0);
     uint64_t done = 0;
-    for (uint32_t k0 = 0; k0 < m.SB && done < len; k0 += 64) {
-      const bool nz = k0 + lane < m.SB && sr[k0 + lane] != 0;
-      if (clear && nz) sr[k0 + lane] = 0;  // (the reset leaves the read-out's rows to it)
+    const uint32_t NB = m.SB / SUMM_SUB;  // 512-B blocks of the summary row
+    for (uint32_t k0 = 0; k0 < NB && done < len; k0 += 64) {
+      const bool nz = k0 + lane < NB && summ_any(sr, k0 + lane);
+      if (clear && nz) summ_zero(sr, k0 + lane);  // (the reset leaves the read-out's rows to it)
       unsigned long long bal = __ballot(nz);
       while (bal && done < len) {
         uint4 v[4];
