@@ -3670,17 +3670,16 @@ void el_ctx::reset_device(hipStream_t stream, uint32_t clear_from, uint32_t summ
   // the sets first 23.91 / 23.79 vs 23.81 / 23.68 ms, `EL_RESET_SETS_FIRST=1`)
   static const bool clear_first = getenv("EL_RESET_SETS_FIRST") == nullptr;
   auto sets = [&]() {
-    // the large sets (G3's link set 1 GB and more) by the runtime's fill: it reaches a higher
-    // write rate than k_fill's grid-stride loop (k_fill: 2.0 ms for G3's link set)
-    auto set = [&](unsigned long long* p, uint64_t cap) {
-      if (cap * sizeof(unsigned long long) >= (64ull << 20))
-        HIPCHK(hipMemsetAsync(p, 0xff, cap * sizeof(unsigned long long), stream));
-      else
-        add(p, cap * sizeof(unsigned long long), ~0u);
-    };
-    set(lhash, lhash_cap);
-    set(ahash, ahash_cap);
-    set(phash, phash_cap);
+    // the link set is by far the largest (G3: 2 GB): the runtime's fill reaches a higher write
+    // rate than k_fill's grid-stride loop for it (k_fill: 2.0 ms per G3 classification); the
+    // activation and propagation sets go with the counters in one k_fill (A/B with the runtime
+    // fill for them too: 23.73–23.97 vs 23.95–24.10 ms, `profiles/r04_clear_kernel_ab.txt`)
+    if (lhash_cap * sizeof(unsigned long long) >= (64ull << 20))
+      HIPCHK(hipMemsetAsync(lhash, 0xff, lhash_cap * sizeof(unsigned long long), stream));
+    else
+      add(lhash, lhash_cap * sizeof(unsigned long long), ~0u);
+    add(ahash, ahash_cap * sizeof(unsigned long long), ~0u);
+    add(phash, phash_cap * sizeof(unsigned long long), ~0u);
     add(has_act, hx.N, 0u);
     add(ctr, sizeof(DCounters), 0u);
     add(commit_done, (DONE_SHARDS + 1) * CTR_STRIDE * sizeof(uint32_t), 0u);
