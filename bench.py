@@ -50,18 +50,47 @@ sys.path.insert(0, ROOT)
 # Two engines in flight use 8 HIP streams; with HIP's default of 4 hardware queues, streams of
 # different engines would share a queue and one engine's DMAs would hold up the other's kernels.
 os.environ.setdefault("GPU_MAX_HW_QUEUES", "12")
-# One GPU: load the system ROCm HIP runtime — the one libel_gpu.so is built against — before
-# torch brings its bundled copy under the same soname (whichever loads first serves the whole
-# process).  With torch's runtime the streamed result's D2H copies into page-locked memory run as
-# blit kernels on the CUs (scripts/micro/d2h_py.py: __amd_rocclr_copyBuffer in the trace, ≈14 ms of
-# CU time per G3 classification beside the supersteps); with the system runtime they go to an SDMA
-# engine and a rocprofv3 kernel trace of the timed step stays within 6 % of its untraced time
-# (round-4 A/B: no change in the untraced time itself).  Multi-rank runs keep torch's runtime (its
-# RCCL and process groups are built against it).  EL_HIP_RUNTIME=torch selects torch's at N = 1.
-if (os.environ.get("EL_HIP_RUNTIME", "system") == "system" and int(os.environ.get("WORLD_SIZE", "1")) == 1
-        and "torch" not in sys.modules and os.path.exists("/opt/rocm/lib/libamdhip64.so.7")):
+# Load the system ROCm HIP runtime — the one libel_gpu.so is built against — before torch brings
+# its bundled copy under the same soname (whichever loads first serves the whole process).  With
+# torch's runtime the streamed result's D2H copies into page-locked memory run as blit kernels on
+# the CUs (scripts/micro/d2h_py.py: __amd_rocclr_copyBuffer in the trace, ≈14 ms of CU time per G3
+# classification beside the supersteps); with the system runtime they go to an SDMA engine.  Every
+# world size does this (round 5): the ranks' barrier and reductions run over gloo (dist.py), and the
+# data path's RCCL is opened by the engine itself, so torch's RCCL and CUDA process groups are not
+# used.  A runtime whose major version differs from the one torch was built for is not preloaded.
+# EL_HIP_RUNTIME=torch keeps torch's runtime.
+HIP_RUNTIME = {"loaded": "torch", "path": None, "version": None}
+
+
+def _preload_system_hip():
+    path = "/opt/rocm/lib/libamdhip64.so.7"
+    if os.environ.get("EL_HIP_RUNTIME", "system") != "system" or "torch" in sys.modules or not os.path.exists(path):
+        return
     import ctypes
-    ctypes.CDLL("/opt/rocm/lib/libamdhip64.so.7", mode=ctypes.RTLD_GLOBAL)
+    import importlib.util
+    import re
+    real = os.path.realpath(path)  # libamdhip64.so.7.2.70200: the version is in the file name
+    m = re.search(r"\.so\.(\d+)\.(\d+)\.(\d+)$", real)
+    have = int(m.group(1)) if m else None
+    want = None
+    try:  # torch.version.hip without importing torch (torch/version.py: hip = '7.0.51831')
+        spec = importlib.util.find_spec("torch")
+        with open(os.path.join(os.path.dirname(spec.origin), "version.py")) as f:
+            m = re.search(r"^hip\b[^=]*=\s*'(\d+)\.", f.read(), re.M)
+        want = int(m.group(1)) if m else None
+    except (OSError, AttributeError, TypeError):
+        pass
+    HIP_RUNTIME.update(path=real, version=real.rsplit(".so.", 1)[-1], torch_hip_major=want)
+    if have is None or (want is not None and have != want):
+        HIP_RUNTIME["loaded"] = f"torch (system runtime major {have} vs torch's {want})"
+        return
+    ctypes.CDLL(path, mode=ctypes.RTLD_GLOBAL)
+    HIP_RUNTIME["loaded"] = "system"
+
+
+_preload_system_hip()
+if int(os.environ.get("WORLD_SIZE", "1")) > 1:
+    os.environ.setdefault("EL_DIST_BACKEND", "gloo")  # barrier + reductions; the engine opens RCCL itself
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 
@@ -91,11 +120,14 @@ class _stdout_to_stderr:
 
 
 def source_sha256() -> str:
-    """SHA-256 over the engine's sources (the kernel table and the PMC summaries name it)."""
+    """SHA-256 over every file the engine library is compiled from — the HIP / C++ sources and
+    their headers, the list __graft_entry__ uses for rebuild detection — so two lines from
+    different kernels never share a hash (the kernel table and the PMC summaries name it)."""
     import hashlib
+    import __graft_entry__ as ge
     h = hashlib.sha256()
-    for f in ("el_gpu.hip", "el_closure.hip", "el_rows.hip", "el_stream.hip", "el_index.cpp"):
-        with open(os.path.join(ROOT, "distel_amd", "csrc", f), "rb") as fh:
+    for f in ge.lib_inputs():
+        with open(f, "rb") as fh:
             h.update(fh.read())
     return h.hexdigest()
 
@@ -146,6 +178,11 @@ def parse():
     ap.add_argument("--transport", default="rccl", choices=["rccl", "host"],
                     help="exchange leg's all-gather: rccl = ncclAllGather over xGMI on the engine stream; host = "
                          "EL_XCHG_HOST through a gloo group (a rehearsal of N ranks on one GPU)")
+    ap.add_argument("--scaling", default="weak", choices=["weak", "strong"],
+                    help="N > 1 headline: weak = the OntologyMultiplier ×N ontology row-partitioned (configs[3]); "
+                         "strong = ONE ontology (the workload itself) row-partitioned over the N ranks, balanced by "
+                         "told edges (configs[2] on 1..8 GPUs, the shape DistEL runs).  --partition auto runs both "
+                         "at N > 1 and reports the other one beside the headline")
     ap.add_argument("--exchange-timeout", type=float, default=180.0,
                     help="seconds the exchange leg may take before rank 0 reports the copies leg alone")
     ap.add_argument("--inflight", type=int, default=1, choices=[1, 2],
@@ -163,11 +200,13 @@ def parse():
 
 
 def bind_gpu_numa(dev: int):
-    """Pin this process (and the children it starts) to the CPUs of its GPU's NUMA node, before
-    any page-locked buffer is allocated, so those buffers and the host threads that wait on the
-    device sit next to the GPU's PCIe link.  Page-locked memory on the far node halves the D2H
-    rate of the streamed result; which node a run lands on otherwise varies from run to run.
-    EL_NUMA_BIND=0 leaves the affinity alone.  Returns what was done (for the bench line)."""
+    """Pin every thread of this process (the HIP runtime's and torch's worker threads included:
+    each thread has its own affinity mask, so all of /proc/self/task are set), and the threads and
+    children started later, to the CPUs of its GPU's NUMA node, before any page-locked buffer is
+    allocated, so those buffers and the host threads that wait on the device sit next to the GPU's
+    PCIe link.  Page-locked memory on the far node halves the D2H rate of the streamed result;
+    which node a run lands on otherwise varies from run to run.  EL_NUMA_BIND=0 leaves the affinity
+    alone.  Returns what was done (for the bench line)."""
     if os.environ.get("EL_NUMA_BIND", "1") == "0":
         return {"bound": False, "reason": "EL_NUMA_BIND=0"}
     try:
@@ -189,8 +228,15 @@ def bind_gpu_numa(dev: int):
         use = cpus & os.sched_getaffinity(0)
         if not use:
             return {"bound": False, "pci": bus, "node": node, "reason": "no allowed CPU on the node"}
+        threads = 0
+        for tid in os.listdir("/proc/self/task"):
+            try:
+                os.sched_setaffinity(int(tid), use)
+                threads += 1
+            except OSError:  # (a thread that ended meanwhile)
+                pass
         os.sched_setaffinity(0, use)
-        return {"bound": True, "pci": bus, "node": node, "cpus": len(use)}
+        return {"bound": True, "pci": bus, "node": node, "cpus": len(use), "threads": threads}
     except (OSError, ValueError, AttributeError) as e:
         return {"bound": False, "reason": str(e)[:80]}
 
@@ -215,6 +261,7 @@ def main():
     gen_s = time.time() - t0
     run_copies = args.partition != "exchange"
     run_exchange = args.partition == "exchange" or (world > 1 and args.partition == "auto")
+    run_strong = args.scaling == "strong" or (world > 1 and args.partition == "auto")
 
     def timed(engines, steps, warmup):
         """K classifications between barriers.  One engine: each step runs init + saturate +
@@ -303,11 +350,18 @@ def main():
         for e in engines:
             e.close()
 
-    def exchange_leg():
-        full = ir.replicate(ax, world) if world > 1 else ax
-        rows = ir.copy_slice(ax, world, rank) if world > 1 else (0, ax.n_concepts)
-        if rank == 0:
-            rows = (0, rows[1])  # ⊥ and ⊤ live on rank 0
+    def exchange_leg(strong=False):
+        """weak: the ×N ontology, rank i owning copy i's rows; strong: the workload itself, the
+        rows balanced by told edges (ir.balanced_rows) — one ontology's concept space sharded
+        over the ranks, every R(r) link into another rank's rows crossing the exchange."""
+        if strong:
+            full = ax
+            rows = ir.balanced_rows(ax, world)[rank] if world > 1 else (0, ax.n_concepts)
+        else:
+            full = ir.replicate(ax, world) if world > 1 else ax
+            rows = ir.copy_slice(ax, world, rank) if world > 1 else (0, ax.n_concepts)
+            if rank == 0:
+                rows = (0, rows[1])  # ⊥ and ⊤ live on rank 0
         if args.transport == "host":
             group = rk.dist.new_group(backend="gloo") if world > 1 else None
             part = engine.Partition(rank, world, engine.XCHG_HOST, rows=rows,
@@ -327,6 +381,7 @@ def main():
         load_s = time.time() - t0
         leg = timed([xeng], args.steps, args.warmup)
         leg["load_s"] = load_s
+        leg["rows"] = rows
         xeng.close()
         return leg
 
@@ -342,17 +397,21 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(head["ms_per_step"], 4),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if head_name == "strong" else "weak",
             "vs_baseline": None,
             "dtype": "u32",
             "data": "synthetic",
             "config": {"workload": WORKLOAD_DESC[args.workload] + (f" ×scale {args.scale}" if args.scale != 1 else "")
-                       + (f", OntologyMultiplier ×{world}" if world > 1 else ""),
+                       + (f", OntologyMultiplier ×{world}" if world > 1 and head_name != "strong" else ""),
                        "concepts_per_rank": ax.n_concepts, "roles": ax.n_roles, "axioms": ax.counts(),
                        "parallelism": (f"row partition of the ×{world} ontology over {world} GPUs (rank i owns copy "
                                        f"i's rows), {'RCCL' if args.transport == 'rccl' else 'host-staged gloo'} "
                                        f"delta all-gather + delta-count sum per superstep"
                                        if head_name == "exchange" else
+                                       f"row partition of ONE ontology over {world} GPUs (rows balanced by told "
+                                       f"edges), {'RCCL' if args.transport == 'rccl' else 'host-staged gloo'} "
+                                       f"delta all-gather + delta-count sum per superstep"
+                                       if head_name == "strong" else
                                        f"{world} disjoint copies, one per GPU, no data-path collective"
                                        if world > 1 else "one GPU, whole ontology"),
                        "schedule": ("two classifications in flight per GPU: one's result copy-back "
@@ -383,38 +442,48 @@ def main():
         }
 
     def leg_summary(leg):
+        xb = leg["st"].get("exchange_bytes", 0)
         return {"value": round(leg["value"], 1), "ms_per_step": round(leg["ms_per_step"], 4),
                 "derived_axioms": leg["derived"], "supersteps": leg["st"]["supersteps"],
-                "saturate_ms": round(leg["saturate_ms"], 4), "load_s": round(leg["load_s"], 3),
-                "exchange_bytes_per_rank": leg["st"].get("exchange_bytes", 0)}
+                "init_ms": round(leg["init_ms"], 4), "saturate_ms": round(leg["saturate_ms"], 4),
+                "copyback_ms": round(leg["copyback_ms"], 4), "load_s": round(leg["load_s"], 3), "rows_rank0": leg.get("rows"),
+                "exchange_bytes_per_rank": xb,
+                "exchange_bytes_per_superstep": round(xb / max(leg["st"]["supersteps"], 1), 1)}
 
-    if run_exchange:
+    def pick_head():
+        order = (["strong", "exchange"] if args.scaling == "strong" else ["exchange", "strong"]) + ["copies"]
+        for name in order:
+            if name in legs:
+                return name
+        return None
+
+    xlegs = ([("exchange", False)] if run_exchange else []) + ([("strong", True)] if run_strong else [])
+    if xlegs:
         done = threading.Event()
 
+        def fallback(err):
+            """A partitioned leg failed or hangs: rank 0 prints the line from the legs that finished."""
+            name = pick_head()
+            if rank == 0 and name is not None:
+                extra = {"roofline": None, "cpu_baseline": None, "errors": err}
+                for n in ("copies", "exchange", "strong"):
+                    extra[n] = leg_summary(legs[n]) if n in legs else None
+                print(json.dumps(build_line(legs[name], name, extra)), flush=True)
+            os._exit(0 if name is not None else 1)
+
         def watchdog():
-            if done.wait(args.exchange_timeout):
-                return
-            if rank == 0 and "copies" in legs:
-                line = build_line(legs["copies"], "copies", {
-                    "exchange": {"error": f"exchange leg unfinished after {args.exchange_timeout:.0f} s"},
-                    "roofline": None, "cpu_baseline": None})
-                print(json.dumps(line), flush=True)
-            os._exit(0 if "copies" in legs else 1)
+            if not done.wait(args.exchange_timeout * len(xlegs)):
+                fallback({"timeout": f"partitioned legs unfinished after {args.exchange_timeout * len(xlegs):.0f} s"})
         threading.Thread(target=watchdog, daemon=True).start()
-        try:
-            legs["exchange"] = exchange_leg()
-        except Exception as exc:  # noqa: BLE001 — reported on the line; the other ranks' watchdogs end them
-            legs["exchange_error"] = f"{type(exc).__name__}: {exc}"
-            print(f"rank {rank}: exchange leg failed: {legs['exchange_error']}", file=sys.stderr, flush=True)
-            if "copies" not in legs:
-                raise
-            if rank == 0:
-                line = build_line(legs["copies"], "copies", {"exchange": {"error": legs["exchange_error"]},
-                                                             "roofline": None, "cpu_baseline": None})
-                print(json.dumps(line), flush=True)
-            os._exit(0)
+        for name, strong in xlegs:
+            try:
+                legs[name] = exchange_leg(strong)
+            except Exception as exc:  # noqa: BLE001 — reported on the line; the other ranks' watchdogs end them
+                err = f"{type(exc).__name__}: {exc}"
+                print(f"rank {rank}: {name} leg failed: {err}", file=sys.stderr, flush=True)
+                fallback({name: err})
         done.set()
-    head_name = "exchange" if "exchange" in legs else "copies"
+    head_name = pick_head()
     head = legs[head_name]
     st = head["st"]
 
@@ -473,9 +542,15 @@ def main():
         n_cpu = int(ax.n_concepts * cpu_scale / args.scale)
         per_run = 1.5 * n_cpu * n_cpu / 8
         procs = max(1, min(16, os.cpu_count() or 1, args.cpu_procs, int(160e9 // per_run)))
-        out = subprocess.run([sys.executable, os.path.join(ROOT, "oracle", "cpu_baseline.py"), args.workload,
-                              str(cpu_scale), str(procs)], check=True, capture_output=True, text=True).stdout
-        cb = json.loads(out.strip().splitlines()[-1])
+        try:
+            out = subprocess.run([sys.executable, os.path.join(ROOT, "oracle", "cpu_baseline.py"), args.workload,
+                                  str(cpu_scale), str(procs)], check=True, capture_output=True, text=True).stdout
+            cb = json.loads(out.strip().splitlines()[-1])
+        except (subprocess.SubprocessError, OSError, ValueError, IndexError) as exc:
+            cb = {"error": f"{type(exc).__name__}: {str(exc)[:200]}"}
+    if rank == 0 and cpu is None and not args.no_cpu and "error" in cb:
+        cpu = {"value": None, "unit": "axioms/s", "cores": procs, "kind": "port", "sample": None, "error": cb["error"]}
+    elif rank == 0 and not args.no_cpu:
         cpu = {"value": round(cb["derived"] / cb["wall_s"], 1), "unit": "axioms/s", "cores": procs, "kind": "port",
                "sample": f"{procs} concurrent classifications of {args.workload} at scale {cpu_scale:.4g} "
                          f"(≈{n_cpu} concepts, {cb['single_derived']} derived axioms each) by the CPU oracle "
@@ -491,24 +566,32 @@ def main():
             cpu["parity_derived_equal"] = cb["single_derived"] == st["derived"]
         if world == 1 and cpu_scale < args.scale and not args.no_cpu_full:
             # beside the sample: the whole workload classified by the oracle on one host core
-            # (G3: ≈15 s, 19 GB of host memory for its bit matrix)
-            out = subprocess.run([sys.executable, os.path.join(ROOT, "oracle", "cpu_baseline.py"), args.workload,
-                                  str(args.scale), "1"], check=True, capture_output=True, text=True).stdout
-            fb = json.loads(out.strip().splitlines()[-1])
-            cpu["full_1core"] = {"value": round(fb["single_derived"] / fb["single_s"], 1), "unit": "axioms/s",
-                                 "classification_s": round(fb["single_s"], 4),
-                                 "closure_index_s": round(fb["single_create_s"], 4),
-                                 "derived": fb["single_derived"], "parity_derived_equal": fb["single_derived"] == st["derived"],
-                                 "sample": f"the whole {args.workload} workload, one classification by the CPU oracle on one core"}
+            # (G3: ≈15 s, 19 GB of host memory for its bit matrix); a failure (e.g. the child
+            # killed for memory) is reported in the line instead of losing the measured GPU result
+            try:
+                out = subprocess.run([sys.executable, os.path.join(ROOT, "oracle", "cpu_baseline.py"), args.workload,
+                                      str(args.scale), "1"], check=True, capture_output=True, text=True).stdout
+                fb = json.loads(out.strip().splitlines()[-1])
+                cpu["full_1core"] = {"value": round(fb["single_derived"] / fb["single_s"], 1), "unit": "axioms/s",
+                                     "classification_s": round(fb["single_s"], 4),
+                                     "closure_index_s": round(fb["single_create_s"], 4),
+                                     "derived": fb["single_derived"],
+                                     "parity_derived_equal": fb["single_derived"] == st["derived"],
+                                     "sample": f"the whole {args.workload} workload, one classification by the CPU "
+                                               f"oracle on one core"}
+            except (subprocess.SubprocessError, OSError, ValueError, KeyError, IndexError) as exc:
+                cpu["full_1core"] = {"error": f"{type(exc).__name__}: {str(exc)[:200]}"}
 
     if rank == 0:
         extra = {}
-        if world > 1 or "exchange" in legs:
-            extra["exchange"] = leg_summary(legs["exchange"]) if "exchange" in legs else None
-            extra["copies"] = leg_summary(legs["copies"]) if "copies" in legs else None
+        if world > 1 or "exchange" in legs or "strong" in legs:
+            for n in ("copies", "exchange", "strong"):
+                extra[n] = leg_summary(legs[n]) if n in legs else None
         extra["roofline"] = roofline
         extra["cpu_baseline"] = cpu
         extra["numa"] = numa
+        extra["hip_runtime"] = HIP_RUNTIME
+        extra["lib"] = os.path.relpath(engine.load_library()._name, ROOT)
         line = build_line(head, head_name, extra)
         if kernels:  # the record roofline is computed from (HIP events, the profiled classification)
             line["kernels"] = kernels

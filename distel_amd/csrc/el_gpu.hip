@@ -181,7 +181,7 @@ constexpr uint32_t CTR_STRIDE = 64;  // words
 // ov_* count the entries of this step that did not fit their slack row (gapped CSRs below).
 // cand_t counts the CR1 told-closure candidates (committed first, by k_commit_told).
 #define EL_COUNTERS(X) X(s_log) X(l_log) X(a_log) X(p_log) X(x_log) X(x_send) X(x_sp) X(x_sa) X(ov_pr) X(ov_sc) X(ov_pp) \
-  X(cand_s) X(cand_l) X(cand_a) X(jobs) X(cand_p) X(cand_t) X(g_delta) X(g_max) X(g_ovf) X(ticket) X(seq)
+  X(cand_s) X(cand_l) X(cand_a) X(jobs) X(cand_p) X(cand_t) X(g_delta) X(g_max) X(g_ovf) X(g_pown) X(ticket) X(seq)
 constexpr uint32_t CTR_KEEP = 11;
 #define EL_CTR_DEV(n) uint32_t n; uint32_t n##_pad[CTR_STRIDE - 1];
 #define EL_CTR_HOST(n) uint32_t n;
@@ -1065,8 +1065,10 @@ __device__ __forceinline__ void expand_s(const DIndex& ix, const DState& st, Blo
       for (uint32_t p = ix.fp_ptr[X]; p < p1; ++p) {
         if (ix.part) {  // partitioned: ⊥ rides the propagation set ((r, Y), ⊥) to every rank
           ev.v[EL_EV_HASH]++;
-          emit_p(st, !hash_contains(st.phash, st.pmask, link_key(p, EL_BOTTOM)), p, EL_BOTTOM, ev);
-          continue;
+          const bool fresh = !hash_contains(st.phash, st.pmask, link_key(p, EL_BOTTOM));
+          emit_p(st, fresh, p, EL_BOTTOM, ev);
+          if (!fresh || !(mask & M_R4D)) continue;
+          // fused: this rank's own predecessors now (the other ranks' after the import)
         }
         ev.v[EL_EV_ROW]++;
         const uint2 row = gap_row(st.pr, p);
@@ -2034,12 +2036,13 @@ __global__ void k_ximport(DIndex ix, DState st, XchgArgs x, PubArgs pub) {
       for (uint32_t q = 0; q < x.nranks; ++q) {
         const uint32_t* h = x.recv + (size_t)q * stride;
         gd += h[XH_NP] + h[XH_NA] + h[XH_NX] + h[XH_DS] + h[XH_DL] + h[XH_DP] + h[XH_DA] + h[XH_DX];
-        go += h[XH_OVF];
+        go += h[XH_OVF] + (h[XH_QOVF] << 16);  // (a lost send-queue record: the host throws)
       }
       auto put = [](uint32_t* w, uint32_t v) { __hip_atomic_store(w, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); };
       put(&st.ctr->g_delta, gd);
       put(&st.ctr->g_max, gmax);
       put(&st.ctr->g_ovf, go);
+      put(&st.ctr->g_pown, x.recv[(size_t)x.me * stride + XH_DP]);  // this rank's own new propagations
     }
     __syncthreads();
     // sent: the send queue and the candidate counters start over (on an exchange overflow
@@ -2929,13 +2932,14 @@ struct el_ctx {
   uint32_t* sc_own = nullptr;  // partitioned: successor-row capacities of the own rows only (layout)
   uint32_t* xsend = nullptr;                      // exchange slot: XH + 2 * xcap words
   uint32_t* xrecv = nullptr;                      // part_count slots
-  uint32_t* xhdr = nullptr;                       // part_count headers (the header round)
-  uint32_t* xhdr_h = nullptr;                     // their page-locked host copy
   uint64_t xcap = 0;                              // records per rank per exchange (grows on overflow)
+  uint64_t xspec = 0;                             // records per rank of the next round (exchange_round)
+  uint64_t p_import = 0;                          // propagation log: where the last import's records begin
   uint64_t xrounds_bytes = 0;                     // bytes all-gathered (received) since el_init
   bool part() const { return xmode != EL_XCHG_NONE; }
   bool part_fixpoint = false;  // partitioned: the last el_saturate reached the global fixpoint (el_init clears)
   bool bits_logged = false;
+  bool trace_xchg = getenv("EL_TRACE_XCHG") != nullptr;    // diagnostic: per-superstep exchange rounds
   bool trace_cands = getenv("EL_TRACE_CANDS") != nullptr;  // every set bit of the matrix is in the fact log (not after el_load)
 
   // launch shapes (workgroups per role): a workgroup costs dispatch time even when its
@@ -3545,9 +3549,6 @@ void el_ctx::free_state() {
   dfree(sc_own);
   dfree(xsend);
   dfree(xrecv);
-  dfree(xhdr);
-  if (xhdr_h) (void)hipHostFree(xhdr_h);
-  xhdr_h = nullptr;
   if (pin_word) (void)hipHostFree(pin_word);
   pin_word = nullptr;
 }
@@ -3648,8 +3649,6 @@ void el_ctx::alloc_state() {
     fit_xqueues(cl_cap, cp_cap, ca_cap);
     xsend = dalloc<uint32_t>(XH + 2 * xcap);
     xrecv = dalloc<uint32_t>((uint64_t)part_count * (XH + 2 * xcap));
-    xhdr = dalloc<uint32_t>((uint64_t)part_count * XH);
-    HIPCHK(hipHostMalloc((void**)&xhdr_h, (uint64_t)part_count * XH * sizeof(uint32_t), hipHostMallocDefault));
   }
   alloc_closure();
 }
@@ -3735,6 +3734,8 @@ void el_ctx::reset_state() {
   for (int r = 0; r < EL_NUM_RULE_TYPES; ++r) wm_s[r] = wm_l[r] = wm_a[r] = wm_p[r] = 0;
   wm_x = 0;
   xrounds_bytes = 0;
+  xspec = 0;
+  p_import = 0;
   memset(launches, 0, sizeof launches);
   memset(host_ev, 0, sizeof host_ev);
   memset(kms, 0, sizeof kms);
@@ -4182,34 +4183,41 @@ uint32_t el_ctx::exchange_round(uint32_t s0, uint32_t l0, uint32_t a0, uint32_t 
   xa.cp_cap = (uint32_t)cp_cap, xa.job_cap = (uint32_t)job_cap, xa.ct_cap = (uint32_t)ct_cap;
   hipLaunchKernelGGL(k_xpack, dim3(grid_for(xcap, 64)), dim3(BLOCK), 0, stream, st, xa);
   HIPCHK(hipGetLastError());
-  xchg->allgather(xsend, xhdr, XH * sizeof(uint32_t), stream);
-  HIPCHK(hipMemcpyAsync(xhdr_h, xhdr, (uint64_t)part_count * XH * sizeof(uint32_t), hipMemcpyDeviceToHost, stream));
-  HIPCHK(hipStreamSynchronize(stream));
-  uint32_t m = 0;
-  for (uint32_t q = 0; q < part_count; ++q) {
-    const uint32_t* h = xhdr_h + (uint64_t)q * XH;
-    m = std::max(m, h[XH_NP] + h[XH_NA] + h[XH_NX]);
-    if (h[XH_QOVF]) throw ElError{EL_EHIP, "exchange: a send queue overflowed on rank " + std::to_string(q)};
-  }
-  // this round's records per rank; a rank past xcap: headers only, the import takes nothing and
-  // publishes g_max (the caller grows and redoes; the commit's gapped-row overflows are placed first)
-  xa.cap = m > xcap ? 0u : std::min<uint32_t>((uint32_t)xcap, (m + 63) & ~63u);
-  if (xa.cap) {
-    xchg->allgather(xsend, xrecv, (XH + 2 * (uint64_t)xa.cap) * sizeof(uint32_t), stream);
-  } else {
-    xa.recv = xhdr;  // headers only
-  }
-  xrounds_bytes += (uint64_t)part_count * (2 * XH + 2 * (uint64_t)xa.cap) * sizeof(uint32_t);
-  const uint32_t seq = ++commit_seq;
-  hipLaunchKernelGGL(k_ximport, dim3(grid_for((uint64_t)part_count * xa.cap, 256)), dim3(BLOCK), 0, stream, ix, st,
-                     xa, PubArgs{hc_dev, commit_done, seq});
-  HIPCHK(hipGetLastError());
-  wait_commit(seq);
+  // One round in the common case: the headers and up to xspec records per rank (the size the
+  // previous superstep's largest rank suggests, agreed by every rank from gathered words) go in
+  // one all-gather, and the import — which reads every rank's header — publishes the step's
+  // global words with the one host wait of the superstep.  A rank with more records than the
+  // round carried makes every rank import nothing (g_max > round); the record round is then redone
+  // at the size g_max asks for (round 4 always ran a header round, a stream sync and the record
+  // round: two host round trips per superstep).
+  auto round = [&](uint32_t cap) {
+    xa.cap = cap;
+    xa.recv = xrecv;
+    xchg->allgather(xsend, xrecv, (XH + 2 * (uint64_t)cap) * sizeof(uint32_t), stream);
+    xrounds_bytes += (uint64_t)part_count * (XH + 2 * (uint64_t)cap) * sizeof(uint32_t);
+    const uint32_t seq = ++commit_seq;
+    hipLaunchKernelGGL(k_ximport, dim3(grid_for(std::max<uint64_t>((uint64_t)part_count * cap, 1), 256)), dim3(BLOCK),
+                       0, stream, ix, st, xa, PubArgs{hc_dev, commit_done, seq});
+    HIPCHK(hipGetLastError());
+    wait_commit(seq);
+    if (hc.g_ovf >> 16) throw ElError{EL_EHIP, "exchange: a send queue overflowed"};
+  };
+  const uint32_t spec = (uint32_t)std::min<uint64_t>(xspec, xcap);
+  round(spec);
+  const bool redo = hc.g_max > spec && hc.g_max <= xcap;
+  if (redo) round(std::min<uint32_t>((uint32_t)xcap, (hc.g_max + 63) & ~63u));
+  // (g_max > xcap: nothing imported; the caller grows the slots and redoes the whole exchange)
+  if (trace_xchg)
+    fprintf(stderr, "xchg rank %u: round %u records, largest rank %u%s\n", part_rank, spec, hc.g_max,
+            redo ? " (redone)" : "");
+  // the next round: this one's largest rank + 1/8 (the late supersteps shrink; a growing one redoes)
+  xspec = std::min<uint64_t>(xcap, ((uint64_t)hc.g_max + hc.g_max / 8 + 63) & ~63ull);
   s_count = hc.s_log;
   l_count = hc.l_log;
   a_count = hc.a_log;
   p_count = hc.p_log;
   x_count = hc.x_log;
+  p_import = p0 + hc.g_pown;  // [p0, p_import): this rank's own new propagations; then the imported
   gap_relocate_all();
   return hc.g_max;
 }
@@ -5483,19 +5491,24 @@ int el_saturate(el_ctx* c, el_stats* stats) {
     // el_init: a re-stream into fitted buffers after EL_ERANGE, which one rank may do alone) runs
     // no collective superstep: its peers have left the exchange.
     if (c->part() && !c->part_fixpoint) {  // collective: every rank runs the same supersteps (global delta)
-      constexpr uint32_t mask = (M_ALL & ~M_R4D) | M_R4P;
+      // The whole-ontology schedule: a propagation this rank generates fans out over its own
+      // predecessors at generation (M_R4D); the ones the import brought from other ranks fan out
+      // over this rank's predecessors in the next superstep (M_R4P over [p_import, p_count)).
       uint64_t xb = 0;
       for (int r = 0; r < EL_NUM_RULE_TYPES; ++r) pb = std::min(pb, c->wm_p[r]);
       xb = std::min<uint64_t>(c->x_count, c->wm_x);
+      uint64_t pe2 = c->p_count;
       for (;;) {
-        const uint64_t se = c->s_count, le = c->l_count, ae = c->a_count, pe2 = c->p_count, xe = c->x_count;
+        const uint64_t se = c->s_count, le = c->l_count, ae = c->a_count, xe = c->x_count;
         c->tr_s.push_back(se - sb);
         c->tr_l.push_back(le - lb);
         c->tr_a.push_back(ae - ab);
+        const uint32_t mask = pb < pe2 ? (M_ALL | M_R4P) : M_ALL;
         const uint64_t g = c->superstep_part(mask, sb, se, lb, le, ab, ae, pb, pe2, xb, xe);
         c->stream_mark();
         c->stream_flush(false);
-        sb = se, lb = le, ab = ae, pb = pe2, xb = xe;
+        sb = se, lb = le, ab = ae, xb = xe;
+        pb = c->p_import, pe2 = c->p_count;
         if (g == 0) break;
       }
       c->wm_x = c->x_count;

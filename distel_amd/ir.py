@@ -415,6 +415,25 @@ def elk_ranges(ax: Axioms) -> Tuple[Axioms, List[int], List[int]]:
     return out, fb, fr
 
 
+def balanced_rows(ax: Axioms, parts: int) -> List[Tuple[int, int]]:
+    """Contiguous row ranges [lo, hi) of ONE ontology for ``parts`` ranks (strong scaling:
+    the concept space sharded, as DistEL shards its keys over Redis nodes,
+    ``AxiomLoader.java:665-667``), balanced by told edges: concept X weighs 1 + its told supers
+    + its CR3 axioms + the CR4 axioms it fills.  ⊥ and ⊤ stay on rank 0; the last rank's range
+    ends at n_concepts (the engine gives it the ELK range fillers too)."""
+    n = ax.n_concepts
+    w = np.ones(n, dtype=np.int64)
+    for col, arr in ((0, ax.sub), (0, ax.ex_rhs), (1, ax.ex_lhs)):
+        if len(arr):
+            w += np.bincount(arr[:, col].astype(np.int64), minlength=n)[:n]
+    cum = np.cumsum(w)
+    cuts = [0] + [int(np.searchsorted(cum, cum[-1] * q / parts, side="right")) for q in range(1, parts)] + [n]
+    cuts = [max(c, 2) if 0 < q < parts else c for q, c in enumerate(cuts)]
+    for q in range(1, len(cuts)):  # monotone (a huge concept may swallow a whole share)
+        cuts[q] = max(cuts[q], cuts[q - 1])
+    return [(cuts[q], cuts[q + 1]) for q in range(parts)]
+
+
 def copy_slice(ax: Axioms, copies: int, index: int) -> Tuple[int, int]:
     """Concept-id range [lo, hi) owned by copy ``index`` of ``replicate(ax, copies)``."""
     m = ax.n_concepts - 2

@@ -205,6 +205,50 @@ def test_partitioned_stream_result(short_rank, oracle_lib):
     group.close()
 
 
+def _pinned_closure(name, scale, ax):
+    """The closure SHA-256 the oracle and the worklist saturator pinned (closure_digests.txt)."""
+    path = os.path.join(os.path.dirname(__file__), "golden", "closure_digests.txt")
+    for line in open(path):
+        if line.strip() and not line.startswith("#"):
+            n, sc, d_in, d_out = line.split()
+            if n == name and float(sc) == scale:
+                assert d_in == ax.digest(), "generator output changed"
+                return d_out
+    raise KeyError((name, scale))
+
+
+def _union_digest(engs):
+    """SHA-256 of the union's facts then links, sorted as one engine's facts() / links(): the
+    partitions own ascending disjoint row ranges, so their sorted rows concatenate in order."""
+    import hashlib
+    facts = [e.facts() for e in engs]
+    links = [e.links() for e in engs]
+    h = hashlib.sha256()
+    for k in range(2):
+        h.update(np.concatenate([f[k] for f in facts]).astype(np.uint32).tobytes())
+    for k in range(3):
+        h.update(np.concatenate([l[k] for l in links]).astype(np.uint32).tobytes())
+    return h.hexdigest()
+
+
+@pytest.mark.parametrize("name,parts", [("g3", 2), ("g3", 4), ("g5", 3)])
+def test_strong_full_size(name, parts):
+    """Strong scaling, the shape DistEL runs (one ontology's keys sharded over the nodes,
+    AxiomLoader.java:665-667, every R(r) pair crossing shards, RolePairHandler.java:353-446):
+    the WHOLE full-size workload on unaligned row partitions balanced by told edges
+    (ir.balanced_rows), exchanging propagations, activations and chain links every superstep.
+    The union of the partitions hashes to the closure the oracle and the independent worklist
+    saturator pinned (closure_digests.txt), in lock-step supersteps."""
+    ax = generators.workload(name)
+    want = _pinned_closure(name, 1.0, ax)
+    rows = ir.balanced_rows(ax, parts)
+    engs, st = engine.classify_partitioned(ax, parts, rows=rows)
+    assert len({s["supersteps"] for s in st}) == 1
+    assert all(s["exchange_bytes"] > 0 for s in st)  # (unaligned: records do cross)
+    assert _union_digest(engs) == want
+    _close(engs)
+
+
 def test_g4_half_eight_partitions():
     """configs[3] (SNOMED×8) at half size on one GPU: ×8 of G3 at 50 % on 8 row partitions aligned
     with the copies (LOCAL transport: the RCCL protocol in process, one thread per rank).  Size-
