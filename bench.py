@@ -195,6 +195,10 @@ def parse():
                          "X -> {B} (el_copy_result)")
     ap.add_argument("--no-throughput2", action="store_true",
                     help="skip the separately reported two-in-flight throughput loop")
+    ap.add_argument("--increment", type=float, default=0.0,
+                    help="N = 1: also time an incremental classification — a random FRAC of every axiom family "
+                         "arrives as an increment (el_add_axioms) after the rest is classified; reported as "
+                         "`increment` beside the headline (0 = off)")
     ap.add_argument("--verbose", action="store_true")
     return ap.parse_args()
 
@@ -239,6 +243,45 @@ def bind_gpu_numa(dev: int):
         return {"bound": True, "pci": bus, "node": node, "cpus": len(use), "threads": threads}
     except (OSError, ValueError, AttributeError) as e:
         return {"bound": False, "reason": str(e)[:80]}
+
+
+def d2h_probe(mb: int = 64, reps: int = 4):
+    """This process's device -> page-locked host copy rate right now (GB/s): 4 × 64 MB on a
+    stream of its own, timed on the host, through the HIP runtime directly (ctypes; every buffer
+    and the stream freed after — a torch tensor here would leave torch's streams and caches
+    behind, and streams beyond the process's hardware queues share them with the engine's).  The
+    streamed result needs the rate: G3's 0.64 GB cross PCIe during ≈18.5 ms of supersteps, and the
+    rate measured on the GPU boxes is bimodal — 56 GB/s, or 30 GB/s in some processes and periods
+    (scripts/micro/d2h_streams.hip: the same binary in consecutive processes on one box, buffer
+    near or far) — so a slow period leaves a copy-back tail.  Reported in the line so a
+    tail can be read against it."""
+    import ctypes
+    try:
+        hip = ctypes.CDLL("libamdhip64.so.7")
+        n = mb << 20
+        d, h, s = ctypes.c_void_p(), ctypes.c_void_p(), ctypes.c_void_p()
+        if hip.hipMalloc(ctypes.byref(d), ctypes.c_size_t(n)) != 0:
+            return None
+        ok = hip.hipHostMalloc(ctypes.byref(h), ctypes.c_size_t(n), 0) == 0
+        ok = ok and hip.hipStreamCreateWithFlags(ctypes.byref(s), 1) == 0
+        gbs = None
+        if ok:
+            cp = lambda: hip.hipMemcpyAsync(h, d, ctypes.c_size_t(n), 2, s)  # hipMemcpyDeviceToHost
+            cp()
+            hip.hipStreamSynchronize(s)
+            t0 = time.perf_counter()
+            for _ in range(reps):
+                cp()
+            hip.hipStreamSynchronize(s)
+            gbs = round(reps * n / (time.perf_counter() - t0) / 1e9, 1)
+        if s.value:
+            hip.hipStreamDestroy(s)
+        if h.value:
+            hip.hipHostFree(h)
+        hip.hipFree(d)
+        return gbs
+    except OSError:
+        return None
 
 
 def main():
@@ -323,6 +366,8 @@ def main():
                 "init_ms": 1e3 * sum(t[0] for t in sp) / len(sp), "saturate_ms": 1e3 * sum(t[1] for t in sp) / len(sp),
                 "copyback_ms": 1e3 * sum(t[2] for t in sp) / len(sp), "inflight": len(engines)}
 
+    probe = os.environ.get("EL_D2H_PROBE", "end")  # end | both | 0
+    d2h = ({"before": d2h_probe()} if probe == "both" else {}) if has_cuda and rank == 0 and probe != "0" else None
     legs = {}
     if run_copies:
         # whole ontology (N = 1) / this rank's own copy (N > 1): no data-path collective
@@ -349,6 +394,45 @@ def main():
                             "the other's classification"}
         for e in engines:
             e.close()
+
+    def increment_leg():
+        """the base classified (untimed), then el_add_axioms(increment) +
+        el_saturate timed — the delta the reference's currInc-scored first iteration processes
+        (Type1_1AxiomProcessor.java:138-141); K repetitions, each from a freshly classified base."""
+        base, inc = ir.split_increment(ax, args.increment, seed=11)
+        e = engine.Engine(device=dev)
+        rows = []
+        for k in range(args.warmup + args.steps):
+            e.load(base)
+            e.init()
+            e.saturate()
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            e.add_axioms(inc)
+            t1 = time.perf_counter()
+            st = e.saturate()
+            t2 = time.perf_counter()
+            if k >= args.warmup:
+                rows.append((t1 - t0, t2 - t1, st, e.increment_info()))
+        e.close()
+        add_ms = 1e3 * sum(r[0] for r in rows) / len(rows)
+        sat_ms = 1e3 * sum(r[1] for r in rows) / len(rows)
+        avg = lambda k: sum(r[3][k] for r in rows) / len(rows)
+        st, info = rows[-1][2], rows[-1][3]
+        # the classification part of an increment: the device state carried over (the told
+        # closure of the new index, CSRs, sets, re-trigger lists) + the saturation; the host index
+        # build and its upload are AxiomLoader's part, reported apart as for el_load
+        cls_ms = avg("migrate_ms") + sat_ms
+        return {"frac": args.increment, "axioms": inc.counts(), "add_axioms_ms": round(add_ms, 4),
+                "index_ms": round(avg("index_ms"), 4), "upload_ms": round(avg("upload_ms"), 4),
+                "migrate_ms": round(avg("migrate_ms"), 4), "saturate_ms": round(sat_ms, 4),
+                "classification_ms": round(cls_ms, 4), "ms": round(add_ms + sat_ms, 4),
+                "supersteps": st["supersteps"],
+                "retrigger": [info["retrigger_facts"], info["retrigger_links"]],
+                "facts_after": st["s_facts"], "links_after": st["links"], "derived_after": st["derived"],
+                "schedule": "el_add_axioms (indexes rebuilt, state carried over, re-trigger lists of the facts and "
+                            "links the new axioms reach) + el_saturate (first superstep over those lists, then "
+                            "semi-naive); no result copy-back"}
 
     def exchange_leg(strong=False):
         """weak: the ×N ontology, rank i owning copy i's rows; strong: the workload itself, the
@@ -457,6 +541,8 @@ def main():
                 return name
         return None
 
+    if args.increment > 0 and world == 1:
+        legs["increment"] = increment_leg()
     xlegs = ([("exchange", False)] if run_exchange else []) + ([("strong", True)] if run_strong else [])
     if xlegs:
         done = threading.Event()
@@ -587,10 +673,18 @@ def main():
         if world > 1 or "exchange" in legs or "strong" in legs:
             for n in ("copies", "exchange", "strong"):
                 extra[n] = leg_summary(legs[n]) if n in legs else None
+        if "increment" in legs:
+            inc = dict(legs["increment"])
+            inc["vs_full_classification"] = round(inc["classification_ms"] / head["ms_per_step"], 4)
+            inc["with_index_vs_full"] = round(inc["ms"] / head["ms_per_step"], 4)
+            extra["increment"] = inc
         extra["roofline"] = roofline
         extra["cpu_baseline"] = cpu
         extra["numa"] = numa
         extra["hip_runtime"] = HIP_RUNTIME
+        if d2h is not None:
+            d2h["after"] = d2h_probe()
+        extra["d2h_gbs"] = d2h
         extra["lib"] = os.path.relpath(engine.load_library()._name, ROOT)
         line = build_line(head, head_name, extra)
         if kernels:  # the record roofline is computed from (HIP events, the profiled classification)

@@ -104,7 +104,10 @@ struct Out {
 };
 
 // Launch geometry shared by every level launch (the per-wave row reservations persist across them).
-constexpr uint32_t GRID = 1024;
+#ifndef EL_CLOSURE_GRID
+#define EL_CLOSURE_GRID 1024
+#endif
+constexpr uint32_t GRID = EL_CLOSURE_GRID;  // 4 blocks per CU (k_level: 121 VGPRs, 4 waves per SIMD)
 constexpr uint32_t BLOCK = 256;
 constexpr uint32_t SLOTS = GRID * (BLOCK / 64);
 constexpr uint32_t RSV_WORDS = 6 * SLOTS;

@@ -2354,7 +2354,9 @@ __global__ void k_reloc_claim(Reloc a) {
     b = __shfl(b, 0);
     const uint32_t k = wave_append(reinterpret_cast<uint32_t*>(a.rc + 1), won);
     if (won) {
-      a.nstart[row] = (uint32_t)(a.base + b + inc - sz);  // (the host checks the tail fits 32 bits first)
+      // (truncated to 32 bits here: the host reads the claims' total before any move and throws
+      // when the tail passes 2^32, so k_reloc_move never runs on a wrapped start)
+      a.nstart[row] = (uint32_t)(a.base + b + inc - sz);
       a.rlist[k] = row;
     }
   }
@@ -2406,6 +2408,57 @@ __global__ void k_reloc_commit(Reloc a) {
 }
 
 // rows[i] -> map[rows[i]] (pair ids after an increment re-numbered the pair universe)
+// The re-trigger lists of an increment (el_ctx::migrate_state): facts i < s_old whose A or X is
+// marked, every fact from s_old on (the new concepts' init facts), the links whose pid is marked.
+// A re-triggered fact re-expands its told closure unless it came out of one (flag 1: the fact
+// that emitted it is re-triggered too, its A being below the same changed row); an init fact's
+// closure may have grown, so flag 2 becomes 0.  Order is irrelevant to the fixpoint.
+__global__ void k_retrigger(const uint32_t* __restrict__ sx, const uint32_t* __restrict__ sa,
+                            const uint8_t* __restrict__ sf, uint32_t s_old, uint32_t s_n,
+                            const uint32_t* __restrict__ lx, const uint32_t* __restrict__ lp, uint32_t l_n,
+                            const uint8_t* __restrict__ dA, const uint8_t* __restrict__ dX,
+                            const uint8_t* __restrict__ dP, uint32_t* rx, uint32_t* ra, uint8_t* rf, uint32_t* rlx,
+                            uint32_t* rlp, unsigned long long* cnt) {
+  const uint32_t stride = gridDim.x * blockDim.x, n = max(s_n, l_n);
+  for (uint32_t base = blockIdx.x * blockDim.x; base < n; base += stride) {  // (uniform trip count)
+    const uint32_t i = base + threadIdx.x;
+    uint32_t x = 0, a = 0, f = 0, y = 0, p = 0;
+    bool ks = false, kl = false;
+    if (i < s_n) {
+      x = sx[i];
+      a = sa[i];
+      f = sf[i];
+      ks = i >= s_old || dA[a] || dX[x];
+    }
+    if (i < l_n) {
+      y = lx[i];
+      p = lp[i];
+      kl = dP[p];
+    }
+    const unsigned long long ms = __ballot(ks), ml = __ballot(kl);
+    unsigned long long bs = 0, bl = 0;
+    const int lead = __ffsll((long long)__ballot(true)) - 1;
+    if ((int)lane_id() == lead) {
+      if (ms) bs = atomicAdd(cnt, (unsigned long long)__popcll(ms));
+      if (ml) bl = atomicAdd(cnt + 1, (unsigned long long)__popcll(ml));
+    }
+    bs = __shfl(bs, lead);
+    bl = __shfl(bl, lead);
+    const unsigned long long below = (1ull << lane_id()) - 1ull;
+    if (ks) {
+      const uint64_t o = bs + __popcll(ms & below);
+      rx[o] = x;
+      ra[o] = a;
+      rf[o] = f == 1 ? 1 : 0;
+    }
+    if (kl) {
+      const uint64_t o = bl + __popcll(ml & below);
+      rlx[o] = y;
+      rlp[o] = p;
+    }
+  }
+}
+
 __global__ void k_remap(uint32_t* __restrict__ v, uint64_t n, const uint32_t* __restrict__ map) {
   const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
   for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) v[i] = map[v[i]];
@@ -2905,6 +2958,17 @@ struct el_ctx {
   }
   uint64_t wm_s[EL_NUM_RULE_TYPES] = {}, wm_l[EL_NUM_RULE_TYPES] = {}, wm_a[EL_NUM_RULE_TYPES] = {},
            wm_p[EL_NUM_RULE_TYPES] = {}, wm_x = 0;
+  // Incremental classification (el_add_axioms): the logged facts and links an increment's axioms
+  // reach, compacted (their index rows changed: the first superstep after the increment takes its
+  // triggers from here instead of the logs — migrate_state, retrigger_step)
+  uint32_t *rt_x = nullptr, *rt_a = nullptr, *rt_lx = nullptr, *rt_lp = nullptr;
+  uint8_t* rt_f = nullptr;
+  uint64_t rt_ns = 0, rt_nl = 0;
+  bool inc_pending = false;
+  double inc_ms[3] = {0, 0, 0};  // the last el_add_axioms: host index build, upload, state migration
+  bool trig_override = false;  // superstep(): k_expand reads the rt_* triggers
+  void retrigger_step();
+  void retrigger_all();  // (el_step after an increment: every logged fact once, as round 4)
   el_stats last{};
   std::vector<uint64_t> tr_s, tr_l, tr_a;
   // host-side per-kernel accounting (merge kernels, launches, times)
@@ -3202,7 +3266,8 @@ struct el_ctx {
   void launch_gap_scan(const uint32_t* len, uint32_t R, uint32_t* start_out);
   std::string install_index(el::HostIndex&& h);
   void column_window();
-  void migrate_state(uint32_t N0, const std::vector<uint32_t>& pmap);
+  void migrate_state(uint32_t N0, const std::vector<uint32_t>& pmap, const std::vector<uint8_t>& dA,
+                     const std::vector<uint8_t>& dX, const std::vector<uint8_t>& dP);
   el::AxiomStore store;  // the loaded axioms (increments append to them)
   // ELK range fillers (el_index.h elk_ranges): concepts [n_user, N) are internal; the result
   // rows cover the caller's concepts [lo, uhi()) only
@@ -3504,6 +3569,10 @@ void el_ctx::free_state() {
   dfree(plog_b);
   dfree(cp_p);
   dfree(cp_b);
+  for (uint32_t** p : {&rt_x, &rt_a, &rt_lx, &rt_lp}) dfree(*p);
+  dfree(rt_f);
+  rt_ns = rt_nl = 0;
+  inc_pending = false;
   rs.release();
   rl.release();
   if (dstream) (void)hipStreamSynchronize(dstream);
@@ -3983,6 +4052,14 @@ bool el_ctx::superstep(uint32_t mask, uint64_t sb, uint64_t se, uint64_t lb, uin
     // ---- generation (reads only the state of step t-1; candidate counters are zero here)
     refresh_acts();
     DState st = dstate();
+    DState sx = st;  // k_expand's view: the triggers from the re-trigger lists after an increment
+    if (trig_override) {
+      sx.slog_x = rt_x;
+      sx.slog_a = rt_a;
+      sx.slog_f = rt_f;
+      sx.llog_x = rt_lx;
+      sx.llog_p = rt_lp;
+    }
     ExpandArgs ea{};
     if (se > sb) wave_triggers(se - sb, tune_expand, ea.gs, ea.ts);
     if (le > lb) wave_triggers(le - lb, tune_expand, ea.gl, ea.tl);
@@ -4016,12 +4093,12 @@ bool el_ctx::superstep(uint32_t mask, uint64_t sb, uint64_t se, uint64_t lb, uin
           e1.ga = r == 2 ? ea.ga : 0u;
           e1.gp = r == 3 ? ea.gp : 0u;
           if (r == 0 && by_rule) e1.mask = (ea.mask & groups[k]) | (ea.mask & keep);
-          hipLaunchKernelGGL(k_expand, dim3(g[r]), dim3(BLOCK), 0, stream, ix, st, e1);
+          hipLaunchKernelGGL(k_expand, dim3(g[r]), dim3(BLOCK), 0, stream, ix, sx, e1);
         }
       }
     } else {
       launch(EL_K_EXPAND_S, [&] {
-        hipLaunchKernelGGL(k_expand, dim3(ea.gs + ea.gl + ea.ga + ea.gp), dim3(BLOCK), 0, stream, ix, st, ea);
+        hipLaunchKernelGGL(k_expand, dim3(ea.gs + ea.gl + ea.ga + ea.gp), dim3(BLOCK), 0, stream, ix, sx, ea);
       });
     }
     launch(EL_K_JOBS, [&] {
@@ -4971,9 +5048,20 @@ void el_ctx::join_base() {
 }
 
 // Carry a saturated state over to indexes rebuilt for old ∪ increment (el_add_axioms).
-void el_ctx::migrate_state(uint32_t N0, const std::vector<uint32_t>& pmap) {
+void el_ctx::migrate_state(uint32_t N0, const std::vector<uint32_t>& pmap, const std::vector<uint8_t>& dA,
+                           const std::vector<uint8_t>& dX, const std::vector<uint8_t>& dP) {
   const uint64_t N = hx.N, P = hx.P, W0 = W, W1 = ix.W;  // (column_window of the new index)
   sync();
+  // (EL_TRACE_INC: per-phase wall times on stderr)
+  static const bool trace = getenv("EL_TRACE_INC") != nullptr;
+  auto lap_t = std::chrono::steady_clock::now();
+  auto lap = [&](const char* what) {
+    if (!trace) return;
+    sync();
+    const auto t = std::chrono::steady_clock::now();
+    fprintf(stderr, "migrate %-10s %8.3f ms\n", what, std::chrono::duration<double, std::milli>(t - lap_t).count());
+    lap_t = t;
+  };
   if (N != N0) {  // wider bit rows, more rows: pitched copy of the old matrix
     uint32_t* nb = dalloc<uint32_t>(N * W1);
     HIPCHK(hipMemsetAsync(nb, 0, N * W1 * sizeof(uint32_t), stream));
@@ -4996,6 +5084,7 @@ void el_ctx::migrate_state(uint32_t N0, const std::vector<uint32_t>& pmap) {
     hipLaunchKernelGGL(k_summ_build, dim3(2048), dim3(BLOCK), 0, stream, bits, W, (uint64_t)(hi - lo) * W, summ, SB);
     HIPCHK(hipGetLastError());
   }
+  lap("matrix");
   rs.release();  // result rows: more rows, remapped pair ids — rebuilt on demand
   rl.release();
   dfree(act_ptr);  // the activation index covers the grown concept space
@@ -5014,12 +5103,14 @@ void el_ctx::migrate_state(uint32_t N0, const std::vector<uint32_t>& pmap) {
     sync();
     dfree(dmap);
   }
+  lap("remap");
   join_base();
   l_base = p_base = 0;  // every link goes into the set: the base links of the old index are plain links now
   ix.base = 0;
   fresh = false;
   rehash_links(lhash_cap);
   rehash_props(phash_cap);
+  lap("rehash");
   // predecessor / successor / propagation rows for the new pair and concept spaces
   PR.release();
   SC.release();
@@ -5036,12 +5127,14 @@ void el_ctx::migrate_state(uint32_t N0, const std::vector<uint32_t>& pmap) {
     PP.alloc((uint32_t)P, cp_cap + remote_bound());
     gap_build_from_log(PP, plog_p, plog_b, p_count);
   }
+  lap("csrs");
   // the told closure of the new index (every concept's: old closures may have grown), with the
   // counts of the new concepts' init facts
   free_closure();
   alloc_closure();
   closure_rows(N0, (uint32_t)N);
   set_closure_ix();
+  lap("closure");
   // the first superstep re-emits the told closure of every fact it re-triggers (the row
   // array's fill bounds the closures' total)
   const uint64_t ct_need = next_pow2(2 * (uint64_t)clt.t_tail + 1024);
@@ -5052,8 +5145,7 @@ void el_ctx::migrate_state(uint32_t N0, const std::vector<uint32_t>& pmap) {
     ct_x = dalloc<uint32_t>(ct_cap);
     ct_a = dalloc<uint32_t>(ct_cap);
   }
-  // every logged fact re-expands its told closure once (the closures may have grown)
-  if (s_count) HIPCHK(hipMemsetAsync(slog_f, 0, s_count, stream));
+  const uint64_t s_old = s_count;
   // S(X) = {X, ⊤} ∪ told*(X) for the new concepts, appended to the fact log
   if (N > N0) {
     const unsigned long long* T = clt.tot;
@@ -5079,11 +5171,83 @@ void el_ctx::migrate_state(uint32_t N0, const std::vector<uint32_t>& pmap) {
     host_ev[EL_K_INIT][EL_EV_RMW] += n;
     host_ev[EL_K_INIT][EL_EV_EMIT] += n;
   }
-  // every log re-triggers once against the new axioms, then the saturation is semi-naive again
-  for (int r = 0; r < EL_NUM_RULE_TYPES; ++r) wm_s[r] = wm_l[r] = wm_a[r] = wm_p[r] = 0;
+  lap("init");
+  // The delta (the reference's first iteration after an increment reads
+  // only the keys scored at currInc, Type1_1AxiomProcessor.java:138-141, AxiomLoader.java:119-131):
+  // the state was closed under the old axioms, so a rule instance that can conclude something new
+  // involves a new axiom, i.e. an index row that changed.  The first superstep therefore
+  // re-triggers only the logged facts (X, A) whose A has a changed row — a source of a new told /
+  // existential axiom or anything below it (told*, exr*, exl* are closed downward), an operand of a
+  // new conjunction — or whose X became a new link target (a new pair (r, X): X's CR4 half-1 pair
+  // range grew), the logged links whose role has new role axioms (or is below one), and the new
+  // concepts' init facts; from then on the saturation is semi-naive as usual (retrigger_step).
+  {
+    uint8_t* da = dupload(dA);
+    uint8_t* dx = dupload(dX);
+    uint8_t* dp = dupload(dP);
+    auto fit = [&](uint64_t n, uint32_t*& a, uint32_t*& b) {
+      dfree(a);
+      dfree(b);
+      a = dalloc<uint32_t>(std::max<uint64_t>(n, 1));
+      b = dalloc<uint32_t>(std::max<uint64_t>(n, 1));
+    };
+    fit(s_count, rt_x, rt_a);
+    dfree(rt_f);
+    rt_f = dalloc<uint8_t>(std::max<uint64_t>(s_count, 1));
+    fit(l_count, rt_lx, rt_lp);
+    unsigned long long* cnt = dalloc<unsigned long long>(2);
+    HIPCHK(hipMemsetAsync(cnt, 0, 2 * sizeof(unsigned long long), stream));
+    hipLaunchKernelGGL(k_retrigger, dim3(grid_for(std::max<uint64_t>(s_count, l_count))), dim3(BLOCK), 0, stream,
+                       slog_x, slog_a, slog_f, (uint32_t)s_old, (uint32_t)s_count, llog_x, llog_p, (uint32_t)l_count, da,
+                       dx, dp, rt_x, rt_a, rt_f, rt_lx, rt_lp, cnt);
+    HIPCHK(hipGetLastError());
+    unsigned long long h[2] = {0, 0};
+    HIPCHK(hipMemcpyAsync(h, cnt, sizeof h, hipMemcpyDeviceToHost, stream));
+    sync();
+    rt_ns = h[0];
+    rt_nl = h[1];
+    dfree(cnt);
+    dfree(da);
+    dfree(dx);
+    dfree(dp);
+    host_ev[EL_K_REHASH][EL_EV_TRIG] += s_count + l_count;  // (the selection's reads of the logs)
+  }
+  for (int r = 0; r < EL_NUM_RULE_TYPES; ++r) wm_s[r] = s_count, wm_l[r] = l_count, wm_a[r] = a_count, wm_p[r] = p_count;
   wm_x = 0;
+  inc_pending = true;
+  lap("retrigger");
   sync();
   stats_stale = true;
+}
+
+// The first superstep after an increment (migrate_state): k_expand takes its triggers from the
+// compacted re-trigger lists; the commit appends to the logs as always, so the next superstep
+// continues from the logs' watermarks.
+void el_ctx::retrigger_step() {
+  if (!inc_pending) return;
+  inc_pending = false;
+  if (!rt_ns && !rt_nl) return;
+  tr_s.push_back(rt_ns);
+  tr_l.push_back(rt_nl);
+  tr_a.push_back(0);
+  trig_override = true;
+  try {
+    superstep(M_ALL, 0, rt_ns, 0, rt_nl, a_count, a_count, p_count, p_count);
+  } catch (...) {
+    trig_override = false;
+    throw;
+  }
+  trig_override = false;
+  stream_mark();
+}
+
+// el_step after an increment: the per-rule schedule re-triggers every logged fact and link once
+// (round 4's increment: the closures may have grown, so every fact re-expands its told closure)
+void el_ctx::retrigger_all() {
+  if (!inc_pending) return;
+  inc_pending = false;
+  if (s_count) HIPCHK(hipMemsetAsync(slog_f, 0, s_count, stream));
+  for (int r = 0; r < EL_NUM_RULE_TYPES; ++r) wm_s[r] = wm_l[r] = wm_a[r] = wm_p[r] = 0;
 }
 
 // The rows of the gapped CSRs that overflowed in this step move, each alone, to gap_cap(len)
@@ -5395,11 +5559,16 @@ int el_add_axioms(el_ctx* c, const el_axioms* inc) {
     return fail(c, EL_EINVAL, "increments with range axioms need EL_FLAG_COMPAT_DISTEL_RANGE "
                               "(ELK range fillers are numbered after the concepts)");
   return guarded(c, [&] {
+    using clk = std::chrono::steady_clock;
+    const auto t0 = clk::now();
+    auto ms_since = [](clk::time_point a) { return std::chrono::duration<double, std::milli>(clk::now() - a).count(); };
     el::AxiomStore store = c->store;
     std::string e = store.append(*inc);
     el::HostIndex hx;
     if (e.empty()) e = el::build_index(store.view(), hx, c->flags);
     if (!e.empty()) return fail(c, EL_EINVAL, e);
+    c->inc_ms[0] = ms_since(t0);
+    c->inc_ms[1] = c->inc_ms[2] = 0;
     c->sync();
     if (!c->inited) {  // nothing saturated yet: a plain reload
       c->free_state();
@@ -5421,14 +5590,72 @@ int el_add_axioms(el_ctx* c, const el_axioms* inc) {
       pmap[p] = q;
     }
     const uint32_t N0 = c->hx.N;
+    const auto t1 = clk::now();
     c->free_index();
     c->n_user = store.N;
     c->store = std::move(store);
     e = c->install_index(std::move(hx));
     if (!e.empty()) return fail(c, EL_EINVAL, e);
-    c->migrate_state(N0, pmap);
+    c->sync();
+    c->inc_ms[1] = ms_since(t1);
+    const auto t2 = clk::now();
+    // What the increment's axioms reach (migrate_state re-triggers only that):
+    //  dA  concepts whose index rows changed: the sources of new told / existential axioms and
+    //      everything below them (told*, exr*, exl* are closed downward over told subs), the
+    //      operands of new conjunctions
+    //  dX  concepts that became new link targets (a new pair (r, X): X's pair range grew)
+    //  dP  pairs whose role has new role axioms (r ⊑ s, chains, domain, range) or is below one
+    const el::HostIndex& h = c->hx;
+    std::vector<uint8_t> dA(std::max<uint32_t>(h.N, 1), 0), dX(std::max<uint32_t>(h.N, 1), 0),
+        dP(std::max<uint32_t>(h.P, 1), 0), dR(h.R + 1, 0);
+    std::vector<uint32_t> stk;
+    auto markA = [&](uint32_t a) {
+      if (a < h.N && !dA[a]) dA[a] = 1, stk.push_back(a);
+    };
+    for (uint32_t i = 0; i < inc->n_sub; ++i) markA(inc->sub_a[i]);
+    for (uint32_t i = 0; i < inc->n_ex_rhs; ++i) markA(inc->exr_a[i]);
+    for (uint32_t i = 0; i < inc->n_ex_lhs; ++i) markA(inc->exl_a[i]);
+    while (!stk.empty()) {  // downward over told subs
+      const uint32_t a = stk.back();
+      stk.pop_back();
+      for (uint32_t j = h.toldT.ptr[a]; j < h.toldT.ptr[a + 1]; ++j) markA(h.toldT.a[j]);
+    }
+    for (uint32_t i = 0; i < inc->n_conj; ++i)
+      for (uint32_t k = inc->conj_ptr[i]; k < inc->conj_ptr[i + 1]; ++k)
+        if (inc->conj_ops[k] < h.N) dA[inc->conj_ops[k]] = 1;
+    std::vector<std::vector<uint32_t>> rsub(h.R);  // role -> told sub-roles (of old ∪ increment)
+    for (size_t i = 0; i < c->store.sr_r.size(); ++i)
+      if (c->store.sr_s[i] < h.R) rsub[c->store.sr_s[i]].push_back(c->store.sr_r[i]);
+    auto markR = [&](uint32_t r) {
+      if (r < h.R && !dR[r]) dR[r] = 1, stk.push_back(r);
+    };
+    for (uint32_t i = 0; i < inc->n_subrole; ++i) markR(inc->sr_r[i]);
+    for (uint32_t i = 0; i < inc->n_chain; ++i) markR(inc->ch_r[i]), markR(inc->ch_s[i]);
+    for (uint32_t i = 0; i < inc->n_domain; ++i) markR(inc->dom_r[i]);
+    for (uint32_t i = 0; i < inc->n_range; ++i) markR(inc->rng_r[i]);
+    while (!stk.empty()) {
+      const uint32_t r = stk.back();
+      stk.pop_back();
+      for (uint32_t q : rsub[r]) markR(q);
+    }
+    std::vector<uint8_t> had(std::max<uint32_t>(h.P, 1), 0);
+    for (uint32_t q : pmap) had[q] = 1;
+    for (uint32_t q = 0; q < h.P; ++q) {
+      dP[q] = dR[h.pair_role[q]];
+      if (!had[q]) dX[h.pair_y[q]] = 1;
+    }
+    c->migrate_state(N0, pmap, dA, dX, dP);
+    c->inc_ms[2] = ms_since(t2);
     return EL_OK;
   });
+}
+
+int el_increment_info(el_ctx* c, double* ms, uint64_t* retrigger) {
+  if (!c || !ms || !retrigger) return EL_EINVAL;
+  for (int i = 0; i < 3; ++i) ms[i] = c->inc_ms[i];
+  retrigger[0] = c->rt_ns;
+  retrigger[1] = c->rt_nl;
+  return EL_OK;
 }
 
 int el_init(el_ctx* c) {
@@ -5451,6 +5678,7 @@ int el_step(el_ctx* c, el_rule rule, int* changed) {
   if (c->part()) return fail(c, EL_ESTATE, "el_step needs a whole-ontology context (use el_saturate)");
   return guarded(c, [&] {
     const int r = (int)rule;
+    c->retrigger_all();  // (after an increment: every logged fact once, per rule)
     c->fresh = false;  // per-rule stepping derives every link (DistEL's granularity)
     const uint64_t se = c->s_count, le = c->l_count, ae = c->a_count, pe = c->p_count;
     bool ch = c->superstep(kRuleMask[r], c->wm_s[r], se, c->wm_l[r], le, c->wm_a[r], ae, c->wm_p[r], pe);
@@ -5487,6 +5715,7 @@ int el_saturate(el_ctx* c, el_stats* stats) {
     c->tr_s.clear();
     c->tr_l.clear();
     c->tr_a.clear();
+    if (!c->part()) c->retrigger_step();  // (the first superstep after an increment)
     // A partitioned context at its global fixpoint (an el_saturate that returned since the last
     // el_init: a re-stream into fitted buffers after EL_ERANGE, which one rank may do alone) runs
     // no collective superstep: its peers have left the exchange.

@@ -115,7 +115,7 @@ EXPORTED_SYMBOLS = [
     "el_get_stats", "el_kernel_stats", "el_superstep_trace", "el_get_subsumers", "el_copy_facts",
     "el_copy_links", "el_export_result", "el_last_error", "el_destroy", "el_group_create", "el_group_destroy",
     "el_rccl_unique_id", "el_add_axioms", "el_result_info", "el_copy_result", "el_result_wait", "el_pair_table", "el_host_alloc",
-    "el_host_free", "el_fresh_fillers", "el_stream_result", "el_pid_table",
+    "el_host_free", "el_fresh_fillers", "el_stream_result", "el_pid_table", "el_increment_info",
 ]
 
 _lib: Optional[C.CDLL] = None
@@ -139,6 +139,7 @@ def load_library(path: Optional[str] = None) -> C.CDLL:
     lib.el_load.argtypes = [P, C.POINTER(_ElAxioms)]
     lib.el_init.argtypes = [P]
     lib.el_add_axioms.argtypes = [P, C.POINTER(_ElAxioms)]
+    lib.el_increment_info.argtypes = [P, C.POINTER(C.c_double), C.POINTER(C.c_uint64)]
     lib.el_step.argtypes = [P, C.c_int, C.POINTER(C.c_int)]
     lib.el_saturate.argtypes = [P, C.POINTER(_ElStats)]
     lib.el_get_stats.argtypes = [P, C.POINTER(_ElStats)]
@@ -482,6 +483,15 @@ class Engine:
         self._check(self._lib.el_add_axioms(self._ctx, C.byref(view.struct)), "el_add_axioms")
         self.ax = merge_axioms(self.ax, inc) if self.ax is not None else inc
         self._last = None
+
+    def increment_info(self) -> Dict:
+        """The last add_axioms: host index build / upload / state migration ms, and the logged
+        facts and links the next saturate() re-triggers first (el_increment_info)."""
+        ms = (C.c_double * 3)()
+        rt = (C.c_uint64 * 2)()
+        self._check(self._lib.el_increment_info(self._ctx, ms, rt), "el_increment_info")
+        return {"index_ms": ms[0], "upload_ms": ms[1], "migrate_ms": ms[2], "retrigger_facts": int(rt[0]),
+                "retrigger_links": int(rt[1])}
 
     def step(self, rule: int) -> bool:
         ch = C.c_int(0)

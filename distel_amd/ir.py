@@ -434,6 +434,23 @@ def balanced_rows(ax: Axioms, parts: int) -> List[Tuple[int, int]]:
     return [(cuts[q], cuts[q + 1]) for q in range(parts)]
 
 
+def split_increment(ax: Axioms, frac: float, seed: int = 0) -> Tuple[Axioms, Axioms]:
+    """(base, increment) of one ontology: a random ``frac`` of every axiom family goes to the
+    increment (AxiomLoader's isIncrementalData load, AxiomLoader.java:119-131), the rest to the
+    base; both keep the whole concept and role id spaces."""
+    rng = np.random.default_rng(seed)
+    fam = {k: getattr(ax, k) for k in ("sub", "ex_rhs", "ex_lhs", "subrole", "chain", "domain", "range")}
+    conj = [(ax.conj_ops[ax.conj_ptr[i]:ax.conj_ptr[i + 1]].tolist(), int(ax.conj_b[i])) for i in range(ax.n_conj)]
+    pick = {k: rng.random(len(a)) < frac for k, a in fam.items()}
+    cpick = rng.random(len(conj)) < frac
+    out = []
+    for side in (False, True):
+        out.append(Axioms.build(ax.n_concepts, ax.n_roles, kind=ax.kind,
+                                conj=[c for c, q in zip(conj, cpick) if q == side],
+                                **{k: a[pick[k] == side] for k, a in fam.items()}))
+    return out[0], out[1]
+
+
 def copy_slice(ax: Axioms, copies: int, index: int) -> Tuple[int, int]:
     """Concept-id range [lo, hi) owned by copy ``index`` of ``replicate(ax, copies)``."""
     m = ax.n_concepts - 2

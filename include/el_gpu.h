@@ -279,6 +279,13 @@ int el_init(el_ctx* ctx);
  * concept_kind = new concepts are classes).  A saturated state is kept and the next
  * el_saturate / el_step continues from it.  Whole-ontology contexts only. */
 int el_add_axioms(el_ctx* ctx, const el_axioms* inc);
+
+/* The last el_add_axioms, for measurement: ms[0] the host index build of old ∪ increment
+   (AxiomLoader's part), ms[1] its upload, ms[2] the device state carried over (told closure of
+   the new index, CSRs, sets, re-trigger lists: classification work); retrigger[0] / [1] the logged
+   facts / links the increment's axioms reach, which the next el_saturate's first superstep
+   re-triggers (Type1_1AxiomProcessor.java:138-141 reads only the keys scored at currInc). */
+int el_increment_info(el_ctx* ctx, double ms[3], uint64_t retrigger[2]);
 int el_step(el_ctx* ctx, el_rule rule, int* changed);
 int el_saturate(el_ctx* ctx, el_stats* stats);
 int el_get_stats(el_ctx* ctx, el_stats* stats);

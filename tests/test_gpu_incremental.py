@@ -1,7 +1,8 @@
 """GPU: incremental classification.  An ontology split into a base
 and increments, classified base-first with el_add_axioms in between, must reach exactly the
 closure the CPU oracle computes from scratch on the union (size-independent property: the
-least fixpoint does not depend on the order axioms arrive in).  The random ontologies carry
+least fixpoint does not depend on the order axioms arrive in), while the first superstep after
+an increment re-triggers only what the new axioms reach (test_increment_is_a_delta).  The random ontologies carry
 range axioms, so these runs read ranges DistEL's way (EL_FLAG_COMPAT_DISTEL_RANGE): increments
 are refused with ELK range fillers (test_increment_rejects_elk_ranges)."""
 import numpy as np
@@ -107,4 +108,32 @@ def test_increment_rejects_elk_ranges():
     with pytest.raises(engine.ElError) as e:
         eng.add_axioms(inc)
     assert e.value.code == engine.EL_EINVAL
+    eng.close()
+
+
+@pytest.mark.parametrize("name,scale", [("g3", 0.05), ("g5", 0.03), ("g3x", 0.02)])
+def test_increment_is_a_delta(name, scale, oracle_lib):
+    """A 1 % increment re-triggers only the logged facts and links its axioms reach (their index
+    rows changed: AxiomLoader's currInc-scored keys, Type1_1AxiomProcessor.java:138-141), not
+    every logged fact; the closure still equals the from-scratch closure of the union."""
+    from distel_amd import ir
+    ax = generators.workload(name, scale)
+    base, inc = ir.split_increment(ax, 0.01, seed=3)
+    eng = engine.Engine(device=0, compat_range=True)
+    eng.load(base)
+    eng.init()
+    before = eng.saturate()
+    eng.add_axioms(inc)
+    st = eng.saturate()
+    tr_s, tr_l, _ = eng.trace()
+    o = oracle_lib.saturate(ax, 0, compat_range=True)
+    gx, ga = eng.facts()
+    ox, oa = o.facts()
+    assert np.array_equal(gx, ox) and np.array_equal(ga, oa), "S(X) differs from the from-scratch closure"
+    for g, c in zip(eng.links(), o.links()):
+        assert np.array_equal(g, c), "R(r) differs from the from-scratch closure"
+    assert st["derived"] == o.stats()["derived"]
+    # the first superstep's triggers: a fraction of the logs
+    assert 0 < tr_s[0] < before["s_facts"] // 2, (int(tr_s[0]), before["s_facts"])
+    assert tr_l[0] < max(before["links"] // 2, 1)
     eng.close()
