@@ -366,8 +366,8 @@ def main():
                 "init_ms": 1e3 * sum(t[0] for t in sp) / len(sp), "saturate_ms": 1e3 * sum(t[1] for t in sp) / len(sp),
                 "copyback_ms": 1e3 * sum(t[2] for t in sp) / len(sp), "inflight": len(engines)}
 
-    probe = os.environ.get("EL_D2H_PROBE", "end")  # end | both | 0
-    d2h = ({"before": d2h_probe()} if probe == "both" else {}) if has_cuda and rank == 0 and probe != "0" else None
+    # (diagnostic, EL_D2H_PROBE=1: this process's D2H rate before any engine exists)
+    d2h = {"before": d2h_probe()} if has_cuda and rank == 0 and os.environ.get("EL_D2H_PROBE") == "1" else None
     legs = {}
     if run_copies:
         # whole ontology (N = 1) / this rank's own copy (N > 1): no data-path collective
@@ -683,8 +683,7 @@ def main():
         extra["numa"] = numa
         extra["hip_runtime"] = HIP_RUNTIME
         if d2h is not None:
-            d2h["after"] = d2h_probe()
-        extra["d2h_gbs"] = d2h
+            extra["d2h_gbs"] = d2h
         extra["lib"] = os.path.relpath(engine.load_library()._name, ROOT)
         line = build_line(head, head_name, extra)
         if kernels:  # the record roofline is computed from (HIP events, the profiled classification)

@@ -4052,14 +4052,6 @@ bool el_ctx::superstep(uint32_t mask, uint64_t sb, uint64_t se, uint64_t lb, uin
     // ---- generation (reads only the state of step t-1; candidate counters are zero here)
     refresh_acts();
     DState st = dstate();
-    DState sx = st;  // k_expand's view: the triggers from the re-trigger lists after an increment
-    if (trig_override) {
-      sx.slog_x = rt_x;
-      sx.slog_a = rt_a;
-      sx.slog_f = rt_f;
-      sx.llog_x = rt_lx;
-      sx.llog_p = rt_lp;
-    }
     ExpandArgs ea{};
     if (se > sb) wave_triggers(se - sb, tune_expand, ea.gs, ea.ts);
     if (le > lb) wave_triggers(le - lb, tune_expand, ea.gl, ea.tl);
@@ -4077,6 +4069,16 @@ bool el_ctx::superstep(uint32_t mask, uint64_t sb, uint64_t se, uint64_t lb, uin
       const uint64_t waves = (uint64_t)(ea.gs + ea.gl + ea.ga + ea.gp + tune_jobs) * (BLOCK / 64);
       for (uint32_t c = 4096; c >= 1024 && !st.cs_chunk; c >>= 1)
         if (4 * waves * c <= cs_cap) st.cs_chunk = c;
+    }
+    // k_expand's view of the state (taken here: st is final for this launch): after an increment,
+    // the triggers come from the re-trigger lists
+    DState sx = st;
+    if (trig_override) {
+      sx.slog_x = rt_x;
+      sx.slog_a = rt_a;
+      sx.slog_f = rt_f;
+      sx.llog_x = rt_lx;
+      sx.llog_p = rt_lp;
     }
     if (split_expand) {  // the roles are independent: run them one launch each (rocprof sees each)
       const uint32_t g[4] = {ea.gs, ea.gl, ea.ga, ea.gp};
