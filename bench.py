@@ -100,6 +100,7 @@ WORKLOAD_DESC = {
     "g3": "G3 SNOMED-shaped synthetic (300k classes, 60 roles, 0.3N definitions, 2 chains + 3 transitive) "
           "— BASELINE configs[2]",
     "g3x": "G3X = G3 + 1% sibling disjointness (⊥), domains on 8 roles, ranges on 3",
+    "g3e": "G3E = G3 + 1% named equivalences near the roots (told cycles, Normalizer.java:277-279)",
     "g5": "G5 role-heavy synthetic (100k classes, 200 roles, depth-20 chains, hub fillers) — BASELINE configs[4]",
 }
 

@@ -2413,49 +2413,55 @@ __global__ void k_reloc_commit(Reloc a) {
 // A re-triggered fact re-expands its told closure unless it came out of one (flag 1: the fact
 // that emitted it is re-triggered too, its A being below the same changed row); an init fact's
 // closure may have grown, so flag 2 becomes 0.  Order is irrelevant to the fixpoint.
-__global__ void k_retrigger(const uint32_t* __restrict__ sx, const uint32_t* __restrict__ sa,
-                            const uint8_t* __restrict__ sf, uint32_t s_old, uint32_t s_n,
-                            const uint32_t* __restrict__ lx, const uint32_t* __restrict__ lp, uint32_t l_n,
-                            const uint8_t* __restrict__ dA, const uint8_t* __restrict__ dX,
-                            const uint8_t* __restrict__ dP, uint32_t* rx, uint32_t* ra, uint8_t* rf, uint32_t* rlx,
-                            uint32_t* rlp, unsigned long long* cnt) {
-  const uint32_t stride = gridDim.x * blockDim.x, n = max(s_n, l_n);
-  for (uint32_t base = blockIdx.x * blockDim.x; base < n; base += stride) {  // (uniform trip count)
-    const uint32_t i = base + threadIdx.x;
-    uint32_t x = 0, a = 0, f = 0, y = 0, p = 0;
-    bool ks = false, kl = false;
-    if (i < s_n) {
-      x = sx[i];
-      a = sa[i];
-      f = sf[i];
-      ks = i >= s_old || dA[a] || dX[x];
-    }
-    if (i < l_n) {
-      y = lx[i];
-      p = lp[i];
-      kl = dP[p];
-    }
+constexpr uint32_t RT_TILE = 8192;  // entries per block of k_retrigger (one counter atomic per tile)
+__global__ void __launch_bounds__(256) k_retrigger(const uint32_t* __restrict__ sx, const uint32_t* __restrict__ sa,
+                                                   const uint8_t* __restrict__ sf, uint32_t s_old, uint32_t s_n,
+                                                   const uint32_t* __restrict__ lx, const uint32_t* __restrict__ lp,
+                                                   uint32_t l_n, const uint8_t* __restrict__ dA,
+                                                   const uint8_t* __restrict__ dX, const uint8_t* __restrict__ dP,
+                                                   uint32_t* rx, uint32_t* ra, uint8_t* rf, uint32_t* rlx, uint32_t* rlp,
+                                                   unsigned long long* cnt) {
+  // two passes over the block's tile: count the kept entries (per wave, then a block prefix and
+  // one atomic per tile and list), then write them at their places
+  __shared__ uint32_t wcnt[2][4];
+  __shared__ unsigned long long gbase[2];
+  const uint32_t t0 = blockIdx.x * RT_TILE, wid = threadIdx.x >> 6;
+  auto keep_s = [&](uint32_t i) { return i < s_n && (i >= s_old || dA[sa[i]] || dX[sx[i]]); };
+  auto keep_l = [&](uint32_t i) { return i < l_n && dP[lp[i]]; };
+  uint32_t cs = 0, cl = 0;
+  for (uint32_t k = 0; k < RT_TILE; k += 256) {
+    const uint32_t i = t0 + k + threadIdx.x;
+    cs += (uint32_t)__popcll(__ballot(keep_s(i)));
+    cl += (uint32_t)__popcll(__ballot(keep_l(i)));
+  }
+  if (lane_id() == 0) wcnt[0][wid] = cs, wcnt[1][wid] = cl;
+  __syncthreads();
+  if (threadIdx.x < 2) {
+    const uint32_t* w = wcnt[threadIdx.x];
+    const unsigned long long tot = (unsigned long long)w[0] + w[1] + w[2] + w[3];
+    gbase[threadIdx.x] = tot ? atomicAdd(cnt + threadIdx.x, tot) : 0ull;
+  }
+  __syncthreads();
+  unsigned long long os = gbase[0], ol = gbase[1];
+  for (uint32_t w = 0; w < wid; ++w) os += wcnt[0][w], ol += wcnt[1][w];
+  const unsigned long long below = (1ull << lane_id()) - 1ull;
+  for (uint32_t k = 0; k < RT_TILE; k += 256) {  // (block-uniform trip count; each wave in order)
+    const uint32_t i = t0 + k + threadIdx.x;
+    const bool ks = keep_s(i), kl = keep_l(i);
     const unsigned long long ms = __ballot(ks), ml = __ballot(kl);
-    unsigned long long bs = 0, bl = 0;
-    const int lead = __ffsll((long long)__ballot(true)) - 1;
-    if ((int)lane_id() == lead) {
-      if (ms) bs = atomicAdd(cnt, (unsigned long long)__popcll(ms));
-      if (ml) bl = atomicAdd(cnt + 1, (unsigned long long)__popcll(ml));
-    }
-    bs = __shfl(bs, lead);
-    bl = __shfl(bl, lead);
-    const unsigned long long below = (1ull << lane_id()) - 1ull;
     if (ks) {
-      const uint64_t o = bs + __popcll(ms & below);
-      rx[o] = x;
-      ra[o] = a;
-      rf[o] = f == 1 ? 1 : 0;
+      const uint64_t o = os + __popcll(ms & below);
+      rx[o] = sx[i];
+      ra[o] = sa[i];
+      rf[o] = sf[i] == 1 ? 1 : 0;
     }
     if (kl) {
-      const uint64_t o = bl + __popcll(ml & below);
-      rlx[o] = y;
-      rlp[o] = p;
+      const uint64_t o = ol + __popcll(ml & below);
+      rlx[o] = lx[i];
+      rlp[o] = lp[i];
     }
+    os += __popcll(ms);
+    ol += __popcll(ml);
   }
 }
 
@@ -2963,7 +2969,7 @@ struct el_ctx {
   // triggers from here instead of the logs — migrate_state, retrigger_step)
   uint32_t *rt_x = nullptr, *rt_a = nullptr, *rt_lx = nullptr, *rt_lp = nullptr;
   uint8_t* rt_f = nullptr;
-  uint64_t rt_ns = 0, rt_nl = 0;
+  uint64_t rt_ns = 0, rt_nl = 0, rt_scap = 0, rt_lcap = 0;
   bool inc_pending = false;
   double inc_ms[3] = {0, 0, 0};  // the last el_add_axioms: host index build, upload, state migration
   bool trig_override = false;  // superstep(): k_expand reads the rt_* triggers
@@ -3571,7 +3577,7 @@ void el_ctx::free_state() {
   dfree(cp_b);
   for (uint32_t** p : {&rt_x, &rt_a, &rt_lx, &rt_lp}) dfree(*p);
   dfree(rt_f);
-  rt_ns = rt_nl = 0;
+  rt_ns = rt_nl = rt_scap = rt_lcap = 0;
   inc_pending = false;
   rs.release();
   rl.release();
@@ -5078,7 +5084,7 @@ void el_ctx::migrate_state(uint32_t N0, const std::vector<uint32_t>& pmap, const
     has_act = ha;
     W = W1;
   }
-  if (summ) {  // the summary of the (re-laid-out) matrix
+  if (summ && N != N0) {  // the summary of the re-laid-out matrix (unchanged rows keep theirs)
     dfree(summ);
     SB = summ_stride(W);
     summ = dalloc<uint8_t>((uint64_t)(hi - lo) * SB);
@@ -5187,19 +5193,28 @@ void el_ctx::migrate_state(uint32_t N0, const std::vector<uint32_t>& pmap, const
     uint8_t* da = dupload(dA);
     uint8_t* dx = dupload(dX);
     uint8_t* dp = dupload(dP);
-    auto fit = [&](uint64_t n, uint32_t*& a, uint32_t*& b) {
-      dfree(a);
-      dfree(b);
-      a = dalloc<uint32_t>(std::max<uint64_t>(n, 1));
-      b = dalloc<uint32_t>(std::max<uint64_t>(n, 1));
-    };
-    fit(s_count, rt_x, rt_a);
-    dfree(rt_f);
-    rt_f = dalloc<uint8_t>(std::max<uint64_t>(s_count, 1));
-    fit(l_count, rt_lx, rt_lp);
+    // (the lists keep their capacity across increments: a re-allocation of ~1 GB per increment
+    // cost milliseconds)
+    if (s_count > rt_scap) {
+      dfree(rt_x);
+      dfree(rt_a);
+      dfree(rt_f);
+      rt_scap = next_pow2(s_count);
+      rt_x = dalloc<uint32_t>(rt_scap);
+      rt_a = dalloc<uint32_t>(rt_scap);
+      rt_f = dalloc<uint8_t>(rt_scap);
+    }
+    if (std::max<uint64_t>(l_count, 1) > rt_lcap) {
+      dfree(rt_lx);
+      dfree(rt_lp);
+      rt_lcap = next_pow2(std::max<uint64_t>(l_count, 1));
+      rt_lx = dalloc<uint32_t>(rt_lcap);
+      rt_lp = dalloc<uint32_t>(rt_lcap);
+    }
     unsigned long long* cnt = dalloc<unsigned long long>(2);
     HIPCHK(hipMemsetAsync(cnt, 0, 2 * sizeof(unsigned long long), stream));
-    hipLaunchKernelGGL(k_retrigger, dim3(grid_for(std::max<uint64_t>(s_count, l_count))), dim3(BLOCK), 0, stream,
+    const uint64_t rn = std::max<uint64_t>(s_count, l_count);
+    hipLaunchKernelGGL(k_retrigger, dim3((uint32_t)std::max<uint64_t>((rn + RT_TILE - 1) / RT_TILE, 1)), dim3(256), 0, stream,
                        slog_x, slog_a, slog_f, (uint32_t)s_old, (uint32_t)s_count, llog_x, llog_p, (uint32_t)l_count, da,
                        dx, dp, rt_x, rt_a, rt_f, rt_lx, rt_lp, cnt);
     HIPCHK(hipGetLastError());

@@ -222,6 +222,24 @@ def g3_bottom_domain_range(seed: int = 0x5C7, n: int = 300_000) -> Axioms:
                   growth=1.4, domains=domains, ranges=ranges, disjoint_frac=0.01, disjoint_mid=30)
 
 
+def g3_equivalences(seed: int = 0x5C7, n: int = 300_000, frac: float = 0.01) -> Axioms:
+    """G3E: G3 plus frac·N named equivalences A ≡ B between neighbouring classes near the roots
+    (the first ids: the top levels of the taxonomy).  DistEL's Normalizer turns every EquivalentClasses(A B)
+    into two SubClassOf axioms (Normalizer.java:277-279), so each one is a told cycle A ⊑ B ⊑ A,
+    and everything below it is closed as a strongly connected component of the told graph."""
+    ax = g3_snomed(seed, n)
+    rng = np.random.default_rng(seed ^ 0xE9)
+    top = max(4, n // 15)
+    k = max(1, int(frac * n))
+    a = rng.choice(np.arange(2, 2 + top, dtype=np.int64), size=min(k, top - 1), replace=False)
+    b = a + 1  # a neighbour on the same level: small cycles, not one giant component
+    keep = (b < ax.n_concepts) & (ax.kind[a] == KIND_CLASS) & (ax.kind[np.minimum(b, ax.n_concepts - 1)] == KIND_CLASS)
+    eq = np.stack([a[keep], b[keep]], axis=1)
+    sub = np.concatenate([ax.sub, eq, eq[:, ::-1]]).astype(np.uint32)
+    import dataclasses
+    return dataclasses.replace(ax, sub=np.ascontiguousarray(sub))
+
+
 def g4_snomed_x(copies: int = 8, seed: int = 0x5C7, n: int = 300_000) -> Axioms:
     """G4: ``copies`` disjoint copies of G3 (OntologyMultiplier semantics)."""
     return replicate(g3_snomed(seed, n), copies)
@@ -242,6 +260,7 @@ WORKLOADS = {
     "g2": g2_nci,
     "g3": g3_snomed,
     "g3x": g3_bottom_domain_range,
+    "g3e": g3_equivalences,
     "g5": g5_role_heavy,
 }
 
@@ -251,7 +270,7 @@ def workload(name: str, scale: float = 1.0) -> Axioms:
     if name == "g4":
         return g4_snomed_x(n=int(300_000 * scale))
     fn = WORKLOADS[name]
-    default_n = {"g1": 20_000, "g2": 70_000, "g3": 300_000, "g3x": 300_000, "g5": 100_000}[name]
+    default_n = {"g1": 20_000, "g2": 70_000, "g3": 300_000, "g3x": 300_000, "g3e": 300_000, "g5": 100_000}[name]
     return fn(n=max(64, int(default_n * scale)))
 
 

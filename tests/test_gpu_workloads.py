@@ -129,3 +129,16 @@ def test_g5_full(oracle_lib):
     _, fan = np.unique(r.astype(np.int64) * ax.n_concepts + y, return_counts=True)
     assert fan.max() >= 10_000
     eng.close()
+
+
+def test_g3e_told_cycles(oracle_lib):
+    """G3E: G3 + 1 % named equivalences near the roots — told cycles (EquivalentClasses becomes
+    two SubClassOf axioms, Normalizer.java:277-279) above most of the taxonomy, so the told
+    closure's strongly connected components and everything below them take the cycle path;
+    bit-exact with the oracle (closure, links, per-superstep deltas, event counters)."""
+    ax = generators.workload("g3e", 0.05)
+    eng, st = engine.classify(ax, device=0)
+    o = oracle_lib.saturate(ax, 0)
+    _same(eng, o)
+    assert st["derived"] == o.stats()["derived"]
+    eng.close()
