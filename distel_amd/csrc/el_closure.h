@@ -51,6 +51,12 @@ struct Axioms {
   // window, which holds every concept its rows can reach and is closed under told supers); the
   // others keep empty rows and cost nothing
   uint32_t w_lo = 2, w_hi = 0xffffffffu;
+  // told cycles (el_index.h, HostIndex::scc_rep): the Kahn levels run over the condensed told
+  // graph (par / chi / xr / xl above are then the condensed rows); null when acyclic
+  const uint32_t* rep = nullptr;                        // concept -> its component's representative
+  const uint32_t *tx_ptr = nullptr, *tx = nullptr;      // representative -> the other members
+  const uint32_t* fol = nullptr;                        // the followers (non-representative members)
+  uint32_t nfol = 0;
 };
 
 // per-node statistics (Out::nd + k * N)
@@ -125,6 +131,8 @@ void start(hipStream_t s, const Axioms& ax, const Out& o);
 void level(hipStream_t s, const Axioms& ax, const Out& o, uint32_t L);
 // after the levels: T_STUCK, and every stuck concept marked dirty for the relaxation
 void check(hipStream_t s, const Axioms& ax, const Out& o);
+// after the levels: the rows of the told cycles' followers from their representatives' rows
+void follow(hipStream_t s, const Axioms& ax, const Out& o);
 // one relaxation round over the dirty concepts (told cycles), its grown rows committed;
 // Ctr::dirty = some row grew
 void relax(hipStream_t s, const Axioms& ax, const Out& o);

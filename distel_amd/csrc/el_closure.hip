@@ -325,7 +325,11 @@ __device__ void gather(const Axioms& ax, const Out& o, uint32_t A, uint32_t pb, 
                        typename RowT<T>::K* buf) {
   using K = typename RowT<T>::K;
   uint32_t off = 0;
-  if (T == R_EXR) {
+  if (T == R_TOLD && ax.tx_ptr) {  // a told cycle's representative: the other members
+    const uint32_t b0 = ax.tx_ptr[A], n0 = ax.tx_ptr[A + 1] - b0;
+    for (uint32_t i = lane(); i < n0; i += 64) M::st(buf + i, (K)ax.tx[b0 + i]);
+    off = n0;
+  } else if (T == R_EXR) {
     const uint32_t b0 = ax.xr_ptr[A], n0 = ax.xr_ptr[A + 1] - b0;
     for (uint32_t i = lane(); i < n0; i += 64) M::st(buf + i, (K)ax.xr[b0 + i]);
     off = n0;
@@ -663,14 +667,17 @@ template <uint32_t T, bool RELAX>
 __device__ bool task(const Axioms& ax, const Out& o, uint32_t A, uint32_t* lbuf, Rsv& rs, const Pre* pr = nullptr) {
   using K = typename RowT<T>::K;
   const uint32_t pb = pr ? pr->pb : ax.par_ptr[A], pe = pr ? pr->pe : ax.par_ptr[A + 1];
-  if (!RELAX && pe - pb <= 1 && task_merge1<T>(ax, o, A, *pr, lbuf, rs)) return true;
-  if (!RELAX && pe - pb == 2 && task_merge2<T>(ax, o, A, *pr, lbuf, rs)) return true;
+  // a told cycle's representative: its told row also holds the component's other members (the
+  // extras), gathered and sorted with the rest
+  const uint32_t nx = T == R_TOLD && ax.tx_ptr ? ax.tx_ptr[A + 1] - ax.tx_ptr[A] : 0u;
+  if (!RELAX && !nx && pe - pb <= 1 && task_merge1<T>(ax, o, A, *pr, lbuf, rs)) return true;
+  if (!RELAX && !nx && pe - pb == 2 && task_merge2<T>(ax, o, A, *pr, lbuf, rs)) return true;
   unsigned long long raw = 0;
   for (uint32_t q = pb + lane(); q < pe; q += 64) {
     const uint32_t p = ax.par[q];
     raw += meta_word(o.meta, p, 1, RowT<T>::comp) - meta_word(o.meta, p, 0, RowT<T>::comp) + (T == R_TOLD ? 1u : 0u);
   }
-  raw = wsum(raw);
+  raw = wsum(raw) + nx;  // (the extras once, not per lane)
   if (T == R_EXR) raw += ax.xr_ptr[A + 1] - ax.xr_ptr[A];
   if (T == R_EXL) raw += ax.xl_ptr[A + 1] - ax.xl_ptr[A];
   if (raw > 0x7fffffffull) {
@@ -741,22 +748,31 @@ __device__ __forceinline__ void for_tasks(uint32_t N, Sel&& sel, Run&& run) {
 
 // a concept outside the built set (Axioms::w_lo/w_hi): never ready, never stuck
 constexpr uint32_t SKIP = NONE - 1u;
+// a told cycle's follower: its rows come from its representative's (k_follow), never ready, never stuck
+constexpr uint32_t FOLLOW = NONE - 2u;
 __device__ __forceinline__ bool built(const Axioms& ax, uint32_t A) { return A < 2u || (A >= ax.w_lo && A < ax.w_hi); }
 
 __global__ void __launch_bounds__(BLOCK) k_start(Axioms ax, Out o) {
   const uint32_t stride = gridDim.x * blockDim.x;
-  bool root = false;
+  bool root = false, root1 = false;
   for (uint32_t A = blockIdx.x * blockDim.x + threadIdx.x; A < ax.N; A += stride) {
     const uint32_t d = ax.par_ptr[A + 1] - ax.par_ptr[A];
     const bool in = built(ax, A);
-    o.indeg[A] = d;
-    o.level[A] = !in ? SKIP : d ? NONE : 0u;
-    root |= in && d == 0;
+    // told cycles: a follower's rows come from its representative's (k_follow); a representative
+    // without outside supers still gathers its component's members into its told row, so it is a
+    // level-1 task (level 0 copies own axiom lists only)
+    const bool fol = ax.rep && ax.rep[A] != A;
+    const bool xt = ax.tx_ptr && ax.tx_ptr[A + 1] > ax.tx_ptr[A];
+    o.indeg[A] = fol ? 0u : d;
+    o.level[A] = !in ? SKIP : fol ? FOLLOW : d ? NONE : xt ? 1u : 0u;
+    root |= in && !fol && d == 0 && !xt;
+    root1 |= in && !fol && d == 0 && xt;
     o.meta[2 * A] = make_uint4(0u, ax.cidx_ptr[A], 0u, 0u);
     o.meta[2 * A + 1] = make_uint4(0u, ax.cidx_ptr[A + 1], 0u, 0u);
   }
   for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < RSV_WORDS; i += stride) o.rsv[i] = 0;
   if (root) o.lvl_flag[0] = 1;  // (zeroed by the host before this launch)
+  if (root1) o.lvl_flag[1] = 1;
 }
 
 #ifdef EL_LEVEL_WAVES  // (A/B builds: a VGPR budget for more waves per SIMD; CAPW sets the LDS one)
@@ -904,6 +920,54 @@ __global__ void __launch_bounds__(BLOCK) k_check(Axioms ax, Out o) {
     unsigned long long s = 0;
     for (uint32_t w = 0; w < WAVES; ++w) s += part[w];
     if (s) atomicAdd(&o.ctr->tot[T_STUCK], s);
+  }
+}
+
+// The followers of the told cycles (el_index.h): member m of a component with representative r
+// has told*(m) = told*(r) ∪ {r} \ {m} (the representative's row holds every other member) and
+// the same exr* / exl* rows as r, which it shares (meta points at them).  One wave per follower:
+// m's place in r's sorted row and r's insertion point by binary searches, then a coalesced copy.
+__global__ void __launch_bounds__(BLOCK) k_follow(Axioms ax, Out o) {
+  const uint32_t nw = gridDim.x * WAVES;
+  for (uint32_t i = slot_id(); i < ax.nfol; i += nw) {  // (wave-uniform)
+    const uint32_t m = ax.fol[i], r = ax.rep[m];
+    if (!built(ax, m)) continue;
+    const uint4 rb = o.meta[2 * r], re = o.meta[2 * r + 1];
+    const uint32_t b = rb.x, n = re.x - rb.x;
+    auto lower = [&](uint32_t v) {
+      uint32_t lo = 0, hi = n;
+      while (lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (o.t_val[b + mid] < v)
+          lo = mid + 1;
+        else
+          hi = mid;
+      }
+      return lo;
+    };
+    const uint32_t im = lower(m), ir = lower(r);  // (r < m: the representative is the smallest member)
+    uint32_t base = 0;
+    if (lane() == 0) base = atomicAdd(&o.ctr->t_tail, n);
+    base = __shfl(base, 0);
+    if ((uint64_t)base + n > o.t_cap) {
+      if (lane() == 0) atomicOr(&o.ctr->ovf, 1u);  // (the build is redone larger)
+      continue;
+    }
+    for (uint32_t j = lane(); j < n; j += 64) {
+      const uint32_t v = o.t_val[b + j];
+      if (j != im) o.t_val[base + j - (j > im ? 1u : 0u) + (v > r ? 1u : 0u)] = v;
+    }
+    if (lane() == 0) {
+      o.t_val[base + ir] = r;
+      uint32_t* mb = reinterpret_cast<uint32_t*>(o.meta + 2 * m);
+      uint32_t* me = reinterpret_cast<uint32_t*>(o.meta + 2 * m + 1);
+      mb[0] = base;
+      me[0] = base + n;
+      mb[2] = rb.z;
+      me[2] = re.z;
+      mb[3] = rb.w;
+      me[3] = re.w;
+    }
   }
 }
 
@@ -1329,6 +1393,12 @@ void level(hipStream_t s, const Axioms& ax, const Out& o, uint32_t L) {
 
 void check(hipStream_t s, const Axioms& ax, const Out& o) {
   hipLaunchKernelGGL(k_check, dim3(grid_for(ax.N)), dim3(BLOCK), 0, s, ax, o);
+  CCHK(hipGetLastError());
+}
+
+void follow(hipStream_t s, const Axioms& ax, const Out& o) {
+  if (!ax.nfol) return;
+  hipLaunchKernelGGL(k_follow, dim3(std::min<uint32_t>((ax.nfol + WAVES - 1) / WAVES, 2048)), dim3(BLOCK), 0, s, ax, o);
   CCHK(hipGetLastError());
 }
 

@@ -2409,7 +2409,7 @@ __global__ void k_reloc_commit(Reloc a) {
 
 // rows[i] -> map[rows[i]] (pair ids after an increment re-numbered the pair universe)
 // The re-trigger lists of an increment (el_ctx::migrate_state): facts i < s_old whose A or X is
-// marked, every fact from s_old on (the new concepts' init facts), the links whose pid is marked.
+// marked, the links whose pid is marked.
 // A re-triggered fact re-expands its told closure unless it came out of one (flag 1: the fact
 // that emitted it is re-triggered too, its A being below the same changed row); an init fact's
 // closure may have grown, so flag 2 becomes 0.  Order is irrelevant to the fixpoint.
@@ -2426,7 +2426,9 @@ __global__ void __launch_bounds__(256) k_retrigger(const uint32_t* __restrict__ 
   __shared__ uint32_t wcnt[2][4];
   __shared__ unsigned long long gbase[2];
   const uint32_t t0 = blockIdx.x * RT_TILE, wid = threadIdx.x >> 6;
-  auto keep_s = [&](uint32_t i) { return i < s_n && (i >= s_old || dA[sa[i]] || dX[sx[i]]); };
+  // (facts from s_old on — the new concepts' init facts — lie above the watermarks: the
+  // supersteps after the re-trigger step expand them)
+  auto keep_s = [&](uint32_t i) { return i < s_old && (dA[sa[i]] || dX[sx[i]]); };
   auto keep_l = [&](uint32_t i) { return i < l_n && dP[lp[i]]; };
   uint32_t cs = 0, cl = 0;
   for (uint32_t k = 0; k < RT_TILE; k += 256) {
@@ -2924,7 +2926,8 @@ struct el_ctx {
   void install_base();
 
   // ---- the told closure and what it derives (el_closure.h), rebuilt by every el_init
-  elcl::Axioms cax{};  // the told axiom rows on the device (index buffers)
+  elcl::Axioms cax{};   // the told axiom rows on the device (index buffers)
+  elcl::Axioms caxk{};  // what the Kahn levels walk: cax, or its told-cycle condensation (el_index.h)
   elcl::Out cl{};      // rows told*, exr*, exl*, meta, per-concept statistics, working storage
   struct ClHost {      // pinned readback of a build: counters, the next level's flag, meta of ⊤
     elcl::Ctr ctr;
@@ -3377,6 +3380,23 @@ std::string el_ctx::install_index(el::HostIndex&& hnew) {
     a.fp_ptr = d.fp_ptr;
     a.pair_role = d.pair_role;
     a.kind = d.kind;
+    caxk = a;
+    if (!h.scc_rep.empty()) {  // told cycles: the levels run over the condensed told graph
+      caxk.par_ptr = up32(h.told_c.ptr);
+      caxk.par = up32(h.told_c.a);
+      caxk.chi_ptr = up32(h.toldT_c.ptr);
+      caxk.chi = up32(h.toldT_c.a);
+      caxk.xr_ptr = up32(h.exr_c.ptr);
+      caxk.xr = up32(h.exr_c.a);
+      caxk.xl_ptr = up32(h.exl_c.ptr);
+      caxk.xl_r = up32(h.exl_c.a);
+      caxk.xl_b = up32(h.exl_c.b);
+      caxk.rep = up32(h.scc_rep);
+      caxk.tx_ptr = up32(h.told_x.ptr);
+      caxk.tx = up32(h.told_x.a);
+      caxk.fol = up32(h.followers);
+      caxk.nfol = (uint32_t)h.followers.size();
+    }
     key_bits = 1;
     while (key_bits < 32 && (1ull << key_bits) < h.P) ++key_bits;
   }
@@ -4593,7 +4613,8 @@ void el_ctx::closure_grow() {
 // rows' counts, and one readback (counters, the flag of level L, the rows of ⊤).
 void el_ctx::closure_tail(uint32_t a, uint32_t b, uint32_t L) {
   HIPCHK(hipMemsetAsync(&cl.ctr->tot[elcl::T_STUCK], 0, sizeof(unsigned long long), stream));
-  elcl::check(stream, cax, cl);
+  if (caxk.nfol) launch(EL_K_CLOSURE, [&] { elcl::follow(stream, caxk, cl); });  // (told cycles' followers)
+  elcl::check(stream, caxk, cl);
   elcl::stats(stream, cax, cl, 0, hx.N, use_props);  // (every row: the SC layout spans them)
   HIPCHK(hipMemsetAsync(cl.ctr->tot, 0, elcl::T_STUCK * sizeof(unsigned long long), stream));
   HIPCHK(hipMemsetAsync(cl.ctr->ev, 0, sizeof(cl.ctr->ev), stream));
@@ -4616,16 +4637,16 @@ void el_ctx::closure_rows(uint32_t a, uint32_t b) {
   const uint32_t N = hx.N;
   // a partitioned context builds the rows of its column window only (×N of G3 on N ranks: each
   // builds its own copy's closure, not the N copies')
-  cax.w_lo = part() ? ix.c_lo : 2u;
-  cax.w_hi = part() ? ix.c_hi : 0xffffffffu;
+  cax.w_lo = caxk.w_lo = part() ? ix.c_lo : 2u;
+  cax.w_hi = caxk.w_hi = part() ? ix.c_hi : 0xffffffffu;
   for (int attempt = 0;; ++attempt) {
     if (attempt > 32) throw ElError{EL_EHIP, "told closure: the build did not fit its buffers"};
-    launch(EL_K_CLOSURE, [&] { elcl::start(stream, cax, cl); });
+    launch(EL_K_CLOSURE, [&] { elcl::start(stream, caxk, cl); });
     uint32_t L = 0;
     bool redo = false;
     for (;;) {
       const uint32_t end = (uint32_t)std::min<uint64_t>((uint64_t)N + 1, (uint64_t)L + level_hint);
-      for (; L < end; ++L) launch(EL_K_CLOSURE, [&] { elcl::level(stream, cax, cl, L); });
+      for (; L < end; ++L) launch(EL_K_CLOSURE, [&] { elcl::level(stream, caxk, cl, L); });
       closure_tail(a, b, L);
       if (clh->ctr.ovf) {
         redo = true;
@@ -4639,7 +4660,7 @@ void el_ctx::closure_rows(uint32_t a, uint32_t b) {
     }
     if (!redo && clh->ctr.tot[elcl::T_STUCK]) {  // told cycles: relaxation rounds until no row grows
       for (uint64_t round = 0;; ++round) {
-        launch(EL_K_CLOSURE, [&] { elcl::relax(stream, cax, cl); });
+        launch(EL_K_CLOSURE, [&] { elcl::relax(stream, caxk, cl); });
         HIPCHK(hipMemcpyAsync(&clh->ctr, cl.ctr, sizeof(elcl::Ctr), hipMemcpyDeviceToHost, stream));
         sync();
         if (clh->ctr.ovf) {
@@ -5229,7 +5250,10 @@ void el_ctx::migrate_state(uint32_t N0, const std::vector<uint32_t>& pmap, const
     dfree(dp);
     host_ev[EL_K_REHASH][EL_EV_TRIG] += s_count + l_count;  // (the selection's reads of the logs)
   }
-  for (int r = 0; r < EL_NUM_RULE_TYPES; ++r) wm_s[r] = s_count, wm_l[r] = l_count, wm_a[r] = a_count, wm_p[r] = p_count;
+  // The watermarks stay: what lies above them (a state that was not saturated — e.g. el_init
+  // then el_add_axioms — and the new concepts' init facts) is expanded by the next supersteps
+  // with the new index as usual; what lies below was closed under the old axioms, and the
+  // re-trigger lists cover the part of it the new axioms reach.
   wm_x = 0;
   inc_pending = true;
   lap("retrigger");

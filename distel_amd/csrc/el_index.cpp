@@ -165,6 +165,77 @@ void distel_chain_set(const el_axioms& ax, std::vector<uint32_t>& r, std::vector
       for (uint32_t tt : st.second) r.push_back(rr), s.push_back(ss), t.push_back(tt);
 }
 
+// Strongly connected components of the told graph (iterative Tarjan over A -> told supers) and
+// the condensed rows of HostIndex::scc_rep (see el_index.h).  Leaves everything empty when every
+// component is a single concept.
+void told_sccs(HostIndex& o) {
+  const uint32_t N = o.N;
+  const uint32_t NONE = 0xffffffffu;
+  std::vector<uint32_t> idx(N, NONE), low(N, 0), comp(N, NONE), st, cs;
+  std::vector<uint8_t> on(N, 0);
+  std::vector<std::pair<uint32_t, uint32_t>> frames;  // (node, next edge)
+  uint32_t counter = 0;
+  bool cyclic = false;
+  for (uint32_t s0 = 0; s0 < N; ++s0) {
+    if (idx[s0] != NONE) continue;
+    frames.push_back({s0, o.told.ptr[s0]});
+    idx[s0] = low[s0] = counter++;
+    st.push_back(s0);
+    on[s0] = 1;
+    while (!frames.empty()) {
+      auto& f = frames.back();
+      const uint32_t v = f.first;
+      if (f.second < o.told.ptr[v + 1]) {
+        const uint32_t w = o.told.a[f.second++];
+        if (idx[w] == NONE) {
+          idx[w] = low[w] = counter++;
+          st.push_back(w);
+          on[w] = 1;
+          frames.push_back({w, o.told.ptr[w]});
+        } else if (on[w]) {
+          low[v] = std::min(low[v], idx[w]);
+        }
+        continue;
+      }
+      if (low[v] == idx[v]) {  // v roots a component: pop it, representative = smallest member
+        cs.clear();
+        uint32_t w;
+        do {
+          w = st.back();
+          st.pop_back();
+          on[w] = 0;
+          cs.push_back(w);
+        } while (w != v);
+        const uint32_t rep = *std::min_element(cs.begin(), cs.end());
+        for (uint32_t m : cs) comp[m] = rep;
+        cyclic |= cs.size() > 1;
+      }
+      frames.pop_back();
+      if (!frames.empty()) low[frames.back().first] = std::min(low[frames.back().first], low[v]);
+    }
+  }
+  if (!cyclic) return;
+  o.scc_rep = comp;
+  std::vector<std::array<uint32_t, 3>> tc, xc, lc, ex;
+  for (uint32_t a = 0; a < N; ++a) {
+    const uint32_t r = comp[a];
+    if (r != a) {
+      o.followers.push_back(a);
+      ex.push_back({r, a, 0});  // the representative's told row holds the other members
+    }
+    for (uint32_t j = o.told.ptr[a]; j < o.told.ptr[a + 1]; ++j)
+      if (comp[o.told.a[j]] != r) tc.push_back({r, comp[o.told.a[j]], 0});  // supers outside C
+    for (uint32_t j = o.exr.ptr[a]; j < o.exr.ptr[a + 1]; ++j) xc.push_back({r, o.exr.a[j], 0});
+    for (uint32_t j = o.exl.ptr[a]; j < o.exl.ptr[a + 1]; ++j) lc.push_back({r, o.exl.a[j], o.exl.b[j]});
+  }
+  o.told_c = make_csr(N, tc, false);
+  for (auto& e : tc) std::swap(e[0], e[1]);
+  o.toldT_c = make_csr(N, tc, false);
+  o.exr_c = make_csr(N, xc, false);
+  o.exl_c = make_csr(N, lc, true);
+  o.told_x = make_csr(N, ex, false);
+}
+
 std::string build_index(const el_axioms& ax_in, HostIndex& o, uint32_t flags) {
   el_axioms ax = ax_in;
   std::vector<uint32_t> xr, xs, xt;
@@ -362,6 +433,7 @@ std::string build_index(const el_axioms& ax_in, HostIndex& o, uint32_t flags) {
       o.sc_w[p] = w;
     }
   }
+  told_sccs(o);
 #undef CHECK
   return "";
 }

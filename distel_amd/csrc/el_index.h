@@ -46,6 +46,19 @@ struct HostIndex {
   // plus the same for its CR5 lifts (the successor-row capacity one base link asks for)
   std::vector<uint8_t> sc_self;
   std::vector<uint32_t> sc_w;
+  // Told cycles (A ⊑ B ⊑ A, e.g. a named equivalence: Normalizer.java:277-279 turns
+  // EquivalentClasses(A B) into two SubClassOf axioms): the strongly connected components of the
+  // told graph, condensed for the device closure's Kahn levels.  Every member of a component C has
+  // the same told*(A) ∪ {A} = C ∪ the supers' closures and the same exr* / exl* rows, so the
+  // closure builds them once, for C's representative (its smallest member), over C's outside
+  // supers and all members' own axioms; the other members (followers) copy the told row (with
+  // the representative in and themselves out) and share the other two.  Empty when acyclic.
+  // (A property of the told axioms, like the transpose and the role closure: the closure over it
+  // is still built on the device in every el_init.)
+  std::vector<uint32_t> scc_rep;      // concept -> its component's representative (itself if none)
+  std::vector<uint32_t> followers;    // members that are not representatives, ascending
+  Csr told_c, toldT_c, exr_c, exl_c;  // the condensed told rows / transpose / own-axiom rows
+  Csr told_x;                         // representative -> the other members (its told row's extras)
 };
 
 // Owned copy of the typed axioms (el_load copies its input; el_add_axioms appends an

@@ -253,15 +253,23 @@ def test_g4_half_eight_partitions():
     """configs[3] (SNOMED×8) at half size on one GPU: ×8 of G3 at 50 % on 8 row partitions aligned
     with the copies (LOCAL transport: the RCCL protocol in process, one thread per rank).  Size-
     independent checks: derived = 8 × derived(G3 @ 50 %); every copy's closure, shifted back to copy
-    0's ids, hashes to the whole-ontology closure of G3 @ 50 % (order-independent set digest); and
+    0's ids, hashes to the whole-ontology closure of G3 @ 50 % (order-independent set digest), which
+    hashes to the oracle's pinned closure of G3 @ 50 % (closure_digests.txt); and
     the aligned copies exchange only header words (the commit routes nothing: no other rank's
     window holds a copy's concepts)."""
+    import hashlib
     from distel_amd.result import set_digest
     base = generators.workload("g3", scale=0.5)
     eng, st0 = engine.classify(base, device=0)
     fx, fa = eng.facts()
     lx, lr, ly = eng.links()
     eng.close()
+    # the whole-ontology closure the copies are held to is itself the oracle's (G3 @ 50 % pinned
+    # in closure_digests.txt by tests/golden/make_digests.py --append g3 0.5)
+    h = hashlib.sha256()
+    for a in (fx, fa, lx, lr, ly):
+        h.update(np.ascontiguousarray(a, dtype=np.uint32).tobytes())
+    assert h.hexdigest() == _pinned_closure("g3", 0.5, base)
     k = fx >= 2
     want = set_digest(fx[k], fa[k], *(v[lx >= 2] for v in (lx, lr, ly)))
     del fx, fa, lx, lr, ly
