@@ -1217,19 +1217,24 @@ __global__ void __launch_bounds__(BLOCK) k_totals(Axioms ax, Out o, uint32_t lo,
 
 // Rows [a, b), one lane per row, slots [pos[x - a], pos[x - a + 1]) + base of the log: the
 // wave walks the concatenation of its lanes' slot ranges 64 at a time (coalesced stores).
-template <class F>
-__device__ __forceinline__ void rows_by_slot(uint32_t a, uint32_t b, const uint32_t* pos, F&& f) {
+// row(x) -> uint3 loads what a row's entries need once, by the row's lane (round 4 re-read it per
+// entry: a chain of dependent loads in every round); f(valid, x, j, slot, the owner's row value).
+template <class Row, class F>
+__device__ __forceinline__ void rows_by_slot(uint32_t a, uint32_t b, const uint32_t* pos, Row&& row, F&& f) {
   const uint32_t nw = gridDim.x * WAVES, w = blockIdx.x * WAVES + (threadIdx.x >> 6);
   for (uint32_t r0 = a + w * 64; r0 < b; r0 += nw * 64) {  // (wave-uniform)
     const uint32_t x = r0 + lane();
     uint32_t s = 0, len = 0;
+    uint3 rv = make_uint3(0u, 0u, 0u);
     if (x < b) {
       s = pos[x - a];
       len = pos[x - a + 1] - s;
+      if (len) rv = row(x);
     }
     wave_concat(len, [&](bool v, uint32_t own, uint32_t j, uint32_t) {
       const uint32_t xo = r0 + own, so = __shfl(s, (int)own);
-      f(v, xo, j, so + j);
+      const uint3 ro = make_uint3(__shfl(rv.x, (int)own), __shfl(rv.y, (int)own), __shfl(rv.z, (int)own));
+      f(v, xo, j, so + j, ro);
     });
   }
 }
@@ -1242,46 +1247,56 @@ __global__ void __launch_bounds__(BLOCK) k_init_facts(Axioms ax, Out o, uint32_t
                                                       uint32_t base, uint32_t* slog_x, uint32_t* slog_a,
                                                       uint8_t* slog_f, uint32_t* bits, uint64_t W, uint32_t c_lo,
                                                       uint32_t c_hi, uint8_t* summ, uint32_t SB) {
-  rows_by_slot(a, b, pos, [&](bool v, uint32_t x, uint32_t j, uint32_t slot) {
-    if (!v) return;
-    const bool two = two_of(ax, x);
-    const uint32_t t0 = o.meta[2 * x].x, t1 = o.meta[2 * x + 1].x;
-    uint32_t val;
-    uint8_t f = 1;
-    if (j == 0) {
-      val = x;
-      f = 2;
-    } else if (two && j == 1) {
-      val = TOP;
-      f = 0;
-    } else {
-      uint32_t c = j - 1 - (two ? 1u : 0u);
-      if (two) {  // ⊤ sorts first or right after ⊥ in told*(X): skip it there
-        const uint32_t ptop = (t0 < t1 && o.t_val[t0] == TOP) ? 0u : (t0 + 1 < t1 && o.t_val[t0 + 1] == TOP) ? 1u : NONE;
-        if (c >= ptop) ++c;
-      }
-      val = o.t_val[t0 + c];
-    }
-    slog_x[base + slot] = x;
-    slog_a[base + slot] = val;
-    slog_f[base + slot] = f;
-    const uint32_t col = val < 2u ? val : (val >= c_lo && val < c_hi ? val - c_lo + 2u : NONE);
-    if (col != NONE) {
-      __hip_atomic_fetch_or(bits + (uint64_t)x * W + (col >> 5), 1u << (col & 31u), __ATOMIC_RELAXED,
-                            __HIP_MEMORY_SCOPE_AGENT);
-      if (summ) summ[(uint64_t)x * SB + (col >> elrows::SUMM_SHIFT)] = 1;
-    }
-  });
+  rows_by_slot(
+      a, b, pos,
+      [&](uint32_t x) {  // told*(X)'s start, where ⊤ sits in it (NONE: X has no ⊤ fact), ⊤ is a fact
+        const bool two = two_of(ax, x);
+        const uint32_t t0 = o.meta[2 * x].x, t1 = o.meta[2 * x + 1].x;
+        // ⊤ sorts first or right after ⊥ in told*(X): its entry is skipped there
+        const uint32_t ptop = !two ? NONE
+                              : (t0 < t1 && o.t_val[t0] == TOP)          ? 0u
+                              : (t0 + 1 < t1 && o.t_val[t0 + 1] == TOP) ? 1u
+                                                                         : NONE;
+        return make_uint3(t0, ptop, two ? 1u : 0u);
+      },
+      [&](bool v, uint32_t x, uint32_t j, uint32_t slot, uint3 r) {
+        if (!v) return;
+        const bool two = r.z;
+        uint32_t val;
+        uint8_t f = 1;
+        if (j == 0) {
+          val = x;
+          f = 2;
+        } else if (two && j == 1) {
+          val = TOP;
+          f = 0;
+        } else {
+          uint32_t c = j - 1 - (two ? 1u : 0u);
+          if (c >= r.y) ++c;  // (r.y = NONE when there is no ⊤ entry to skip)
+          val = o.t_val[r.x + c];
+        }
+        slog_x[base + slot] = x;
+        slog_a[base + slot] = val;
+        slog_f[base + slot] = f;
+        const uint32_t col = val < 2u ? val : (val >= c_lo && val < c_hi ? val - c_lo + 2u : NONE);
+        if (col != NONE) {
+          __hip_atomic_fetch_or(bits + (uint64_t)x * W + (col >> 5), 1u << (col & 31u), __ATOMIC_RELAXED,
+                                __HIP_MEMORY_SCOPE_AGENT);
+          if (summ) summ[(uint64_t)x * SB + (col >> elrows::SUMM_SHIFT)] = 1;
+        }
+      });
 }
 
 // the base links {(X, p) : p ∈ exr*(X)} in X order
 __global__ void __launch_bounds__(BLOCK) k_base_links(Axioms ax, Out o, uint32_t a, uint32_t b, const uint32_t* pos,
                                                       uint32_t* llog_x, uint32_t* llog_p) {
-  rows_by_slot(a, b, pos, [&](bool v, uint32_t x, uint32_t j, uint32_t slot) {
-    if (!v) return;
-    llog_x[slot] = x;
-    llog_p[slot] = o.e_val[o.meta[2 * x].z + j];
-  });
+  rows_by_slot(
+      a, b, pos, [&](uint32_t x) { return make_uint3(o.meta[2 * x].z, 0u, 0u); },
+      [&](bool v, uint32_t x, uint32_t j, uint32_t slot, uint3 r) {
+        if (!v) return;
+        llog_x[slot] = x;
+        llog_p[slot] = o.e_val[r.x + j];
+      });
 }
 
 // the base propagations {((r, Y), B) : (r, B) ∈ exl*(Y), (r, Y) a pair}: pid-major (pids sort by

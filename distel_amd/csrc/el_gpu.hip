@@ -34,6 +34,7 @@
 #include <hipcub/hipcub.hpp>
 
 #include <dlfcn.h>
+#include <sys/mman.h>
 #include <rccl/rccl.h>  // types only: librccl is opened on first use (EL_XCHG_RCCL)
 
 #include <algorithm>
@@ -49,6 +50,7 @@
 #include <cstring>
 #include <stdexcept>
 #include <string>
+#include <unordered_map>
 #include <vector>
 
 #include "el_closure.h"
@@ -2410,9 +2412,13 @@ __global__ void k_reloc_commit(Reloc a) {
 // rows[i] -> map[rows[i]] (pair ids after an increment re-numbered the pair universe)
 // The re-trigger lists of an increment (el_ctx::migrate_state): facts i < s_old whose A or X is
 // marked, the links whose pid is marked.
-// A re-triggered fact re-expands its told closure unless it came out of one (flag 1: the fact
-// that emitted it is re-triggered too, its A being below the same changed row); an init fact's
-// closure may have grown, so flag 2 becomes 0.  Order is irrelevant to the fixpoint.
+// dA[A] bit 0: re-trigger the facts (X, A) over all of A's rows (flag 2: the closed rows exr*,
+// exl*); bit 1: the told closure too (flag 0: A is the source of a new told axiom).  The facts
+// re-triggered because their X is a new link target (dX) keep flag 1 — their parent fact, of the
+// same X, is re-triggered too — and walk no told closure (flag 2): A's told* did not change unless
+// A lies below a source A', and then (X, A') is in S(X) and re-walks its own.  (The migrated
+// context has no base links, so flag 2 means "closed rows, no told walk" to k_expand.)  Order is
+// irrelevant to the fixpoint.
 constexpr uint32_t RT_TILE = 8192;  // entries per block of k_retrigger (one counter atomic per tile)
 __global__ void __launch_bounds__(256) k_retrigger(const uint32_t* __restrict__ sx, const uint32_t* __restrict__ sa,
                                                    const uint8_t* __restrict__ sf, uint32_t s_old, uint32_t s_n,
@@ -2455,7 +2461,8 @@ __global__ void __launch_bounds__(256) k_retrigger(const uint32_t* __restrict__ 
       const uint64_t o = os + __popcll(ms & below);
       rx[o] = sx[i];
       ra[o] = sa[i];
-      rf[o] = sf[i] == 1 ? 1 : 0;
+      const uint8_t d = dA[sa[i]];
+      rf[o] = d & 2u ? 0 : d ? 2 : sf[i] == 1 ? 1 : 2;
     }
     if (kl) {
       const uint64_t o = ol + __popcll(ml & below);
@@ -2561,6 +2568,19 @@ uint64_t next_pow2(uint64_t v) {
   return p;
 }
 
+// a log's new capacity for n entries: 1/8 slack in 4 M-entry steps.  The logs must hold every
+// candidate of a step that could be new (count + the candidate queues), which the queues' own
+// headroom already overstates; round 4 grew them to the next power of two of 1.5× that (G3's fact
+// log: 2^30 entries = 9.7 GB for 104 M facts).
+static uint64_t log_cap(uint64_t n) {
+  const uint64_t step = 1ull << 22;
+  return (n + n / 8 + step - 1) / step * step;
+}
+// The fact and link logs, which the streamed result reads, keep power-of-two growth with
+// half again as slack: with the tight slack G3's fact log regrew mid-saturation (a device
+// and copy-stream sync, then a copy), and the result's copy-back tail grew by 7-8 ms.
+static uint64_t stream_log_cap(uint64_t n) { return next_pow2(n + n / 2); }
+
 // Triggers per wave and grid of an expand role with n triggers: a small step's triggers
 // spread over up to maxb·4 waves, T = ceil(n / waves) each (64, a lane per trigger, once n
 // fills them).  Each wave walks its triggers' index rows 64 entries a round with a dependent
@@ -2604,6 +2624,24 @@ struct GapCsr {
     val_cap = total0;
     used = total0;
     val = dalloc<uint32_t>(val_cap);
+    live = true;
+    set_ovq(ovq_entries);
+  }
+  // An increment's re-build (el_ctx::migrate_state) for n rows: the row arrays follow n, the
+  // slot array is kept (gap_build_from_log grows it if the logs need more) — freeing and
+  // re-allocating gigabytes of slots cost more than the build itself.
+  void reshape(uint32_t n, uint64_t ovq_entries) {
+    if (!live || n != rows) {
+      for (uint32_t** p : {&start, &end, &len, &start0, &nstart}) dfree(*p);
+      rows = n;
+      start = dalloc<uint32_t>(n + 1);
+      end = dalloc<uint32_t>(n);
+      len = dalloc<uint32_t>(n);
+      start0 = dalloc<uint32_t>(n + 1);
+      nstart = dalloc<uint32_t>(n);
+    }
+    laid = false;
+    total0 = used = (uint64_t)gap_cap(0) * n;
     live = true;
     set_ovq(ovq_entries);
   }
@@ -2977,6 +3015,7 @@ struct el_ctx {
   double inc_ms[3] = {0, 0, 0};  // the last el_add_axioms: host index build, upload, state migration
   bool trig_override = false;  // superstep(): k_expand reads the rt_* triggers
   void retrigger_step();
+  void mem_report() const;  // (EL_TRACE_MEM: device bytes per structure on stderr)
   void retrigger_all();  // (el_step after an increment: every logged fact once, as round 4)
   el_stats last{};
   std::vector<uint64_t> tr_s, tr_l, tr_a;
@@ -4058,7 +4097,7 @@ bool el_ctx::superstep(uint32_t mask, uint64_t sb, uint64_t se, uint64_t lb, uin
     }
     auto grow_log = [&](uint64_t used, uint64_t add, uint64_t& cap, uint32_t*& a, uint32_t*& b) {
       if (used + add <= cap) return;
-      uint64_t c = next_pow2(used + add + (used + add) / 2);
+      uint64_t c = &cap == &slog_cap || &cap == &llog_cap ? stream_log_cap(used + add) : log_cap(used + add);
       dgrow(a, used, c);
       dgrow(b, used, c);
       cap = c;
@@ -4258,7 +4297,7 @@ void el_ctx::grow_part(uint64_t new_xcap) {
   const uint64_t rb = remote_bound(), xb = (uint64_t)part_count * xcap;
   auto grow_log = [&](uint64_t used, uint64_t need, uint64_t& cap, uint32_t*& a, uint32_t*& b) {
     if (need <= cap) return;
-    const uint64_t c = next_pow2(need + need / 2);
+    const uint64_t c = log_cap(need);
     dgrow(a, used, c);
     dgrow(b, used, c);
     cap = c;
@@ -4347,7 +4386,7 @@ uint64_t el_ctx::superstep_part(uint32_t mask, uint64_t sb, uint64_t se, uint64_
       if (strm) HIPCHK(hipStreamSynchronize(dstream));
       auto grow_log = [&](uint64_t used, uint64_t add, uint64_t& cap, uint32_t*& a, uint32_t*& b) {
         if (used + add <= cap) return;
-        uint64_t c = next_pow2(used + add + (used + add) / 2);
+        uint64_t c = &cap == &slog_cap || &cap == &llog_cap ? stream_log_cap(used + add) : log_cap(used + add);
         dgrow(a, used, c);
         dgrow(b, used, c);
         cap = c;
@@ -4727,7 +4766,7 @@ void el_ctx::closure_state() {
   if (part()) {  // (the queues and the chain-link log are empty at el_init)
     fit_xqueues(cl_cap + nc, cp_cap + nbp, ca_cap);
     if (const uint64_t w = nc + cl_cap + (uint64_t)part_count * xcap; w > xlog_cap) {
-      xlog_cap = next_pow2(w);
+      xlog_cap = log_cap(w);
       realloc2(xlog_cap, xlog_x, xlog_p);
     }
   }
@@ -4737,9 +4776,9 @@ void el_ctx::closure_state() {
     dfree(slog_f);
     slog_f = dalloc<uint8_t>(slog_cap);
   }
-  if (nb + cl_cap > llog_cap) realloc2(llog_cap = next_pow2(nb + cl_cap + (nb + cl_cap) / 2), llog_x, llog_p);
+  if (nb + cl_cap > llog_cap) realloc2(llog_cap = stream_log_cap(nb + cl_cap), llog_x, llog_p);
   if (2 * (nb + cl_cap) > lhash_cap) rehash_links(next_pow2(2 * (nb + cl_cap)));
-  if (nbp + cp_cap > plog_cap) realloc2(plog_cap = next_pow2(nbp + cp_cap + (nbp + cp_cap) / 2), plog_p, plog_b);
+  if (nbp + cp_cap > plog_cap) realloc2(plog_cap = log_cap(nbp + cp_cap), plog_p, plog_b);
   if (2 * (nbp + cp_cap) > phash_cap) rehash_props(next_pow2(2 * (nbp + cp_cap)));
   // initial gapped layouts: row capacities gap_cap(c) for the first supersteps' entries c
   auto fit_gap = [&](GapCsr& g, uint64_t entries) {
@@ -5141,26 +5180,30 @@ void el_ctx::migrate_state(uint32_t N0, const std::vector<uint32_t>& pmap, const
   rehash_props(phash_cap);
   lap("rehash");
   // predecessor / successor / propagation rows for the new pair and concept spaces
-  PR.release();
-  SC.release();
-  PP.release();
   if (P && need_pred) {
-    PR.alloc((uint32_t)P, cl_cap);
+    PR.reshape((uint32_t)P, cl_cap);
     gap_build_from_log(PR, llog_p, llog_x, l_count);
+  } else {
+    PR.release();
   }
   if (need_succ) {
-    SC.alloc((uint32_t)N, cl_cap);
+    SC.reshape((uint32_t)N, cl_cap);
     gap_build_from_log(SC, llog_x, llog_p, l_count, ix.role_chs);
+  } else {
+    SC.release();
   }
   if (use_props) {
-    PP.alloc((uint32_t)P, cp_cap + remote_bound());
+    PP.reshape((uint32_t)P, cp_cap + remote_bound());
     gap_build_from_log(PP, plog_p, plog_b, p_count);
+  } else {
+    PP.release();
   }
   lap("csrs");
   // the told closure of the new index (every concept's: old closures may have grown), with the
   // counts of the new concepts' init facts
   free_closure();
   alloc_closure();
+  lap("cl-alloc");
   closure_rows(N0, (uint32_t)N);
   set_closure_ix();
   lap("closure");
@@ -5205,11 +5248,11 @@ void el_ctx::migrate_state(uint32_t N0, const std::vector<uint32_t>& pmap, const
   // only the keys scored at currInc, Type1_1AxiomProcessor.java:138-141, AxiomLoader.java:119-131):
   // the state was closed under the old axioms, so a rule instance that can conclude something new
   // involves a new axiom, i.e. an index row that changed.  The first superstep therefore
-  // re-triggers only the logged facts (X, A) whose A has a changed row — a source of a new told /
-  // existential axiom or anything below it (told*, exr*, exl* are closed downward), an operand of a
-  // new conjunction — or whose X became a new link target (a new pair (r, X): X's CR4 half-1 pair
-  // range grew), the logged links whose role has new role axioms (or is below one), and the new
-  // concepts' init facts; from then on the saturation is semi-naive as usual (retrigger_step).
+  // re-triggers only the logged facts (X, A) whose A is a source of a new told / existential axiom
+  // or an operand of a new conjunction (dA above), or whose X became a new link target (a new pair
+  // (r, X): X's CR4 half-1 pair range grew), the logged links whose role has new role axioms (or is
+  // below one), and the new concepts' init facts; from then on the saturation is semi-naive as
+  // usual (retrigger_step).
   {
     uint8_t* da = dupload(dA);
     uint8_t* dx = dupload(dX);
@@ -5259,6 +5302,47 @@ void el_ctx::migrate_state(uint32_t N0, const std::vector<uint32_t>& pmap, const
   lap("retrigger");
   sync();
   stats_stale = true;
+}
+
+// Device bytes per structure (EL_TRACE_MEM, after el_saturate): what a context holds, for the
+// multi-GPU memory budget.  "other" = the device's used bytes minus the listed ones
+// (index buffers, scan / sort scratch, stream buffers, other contexts).
+void el_ctx::mem_report() const {
+  const double G = 1e9;
+  const uint64_t N = hx.N, rows = hi - lo;
+  auto gap = [](const GapCsr& g) { return g.live ? (double)g.val_cap * 4 + (double)g.rows * 24 + 12.0 * g.ovq_cap : 0.0; };
+  struct {
+    const char* what;
+    double b;
+  } t[] = {
+      {"bit rows", (double)rows * W * 4},
+      {"block summary", summ ? (double)rows * SB : 0.0},
+      {"fact log", (double)slog_cap * 9},
+      {"told candidates", (double)ct_cap * 8},
+      {"S candidates", (double)cs_cap * 8},
+      {"link log", (double)llog_cap * 8},
+      {"link set", (double)lhash_cap * 8},
+      {"link candidates", (double)cl_cap * 8},
+      {"propagations (log, set, candidates)", (double)plog_cap * 8 + (double)phash_cap * 8 + (double)cp_cap * 8},
+      {"activations (log, set, candidates)", (double)alog_cap * 8 + (double)ahash_cap * 8 + (double)ca_cap * 8 + N},
+      {"jobs", (double)job_cap * 16},
+      {"predecessor rows", gap(PR)},
+      {"successor rows", gap(SC)},
+      {"propagation rows", gap(PP)},
+      {"closure rows", (double)cl.t_cap * 4 + (double)cl.e_cap * 4 + (double)cl.l_cap * 8 + 64.0 * N +
+                           4.0 * elcl::ND_NUM * (N + 1) + 4.0 * cl.scratch_cap + 16.0 * N},
+      {"chain-link log + exchange", (double)xlog_cap * 8 + (double)(xs_cap + xp_cap + xa_cap) * 8 +
+                                        (double)(XH + 2 * xcap) * 4 * (1 + part_count)},
+      {"re-trigger lists", (double)rt_scap * 9 + (double)rt_lcap * 8},
+  };
+  double sum = 0;
+  for (auto& e : t) sum += e.b;
+  size_t fr = 0, tot = 0;
+  (void)hipMemGetInfo(&fr, &tot);
+  fprintf(stderr, "mem rank %u rows [%u, %u) W %u: listed %.2f GB, device used %.2f GB\n", part_rank, lo, hi, (uint32_t)W,
+          sum / G, (double)(tot - fr) / G);
+  for (auto& e : t)
+    if (e.b > 1e8) fprintf(stderr, "mem   %-38s %7.2f GB\n", e.what, e.b / G);
 }
 
 // The first superstep after an increment (migrate_state): k_expand takes its triggers from the
@@ -5641,29 +5725,26 @@ int el_add_axioms(el_ctx* c, const el_axioms* inc) {
     c->inc_ms[1] = ms_since(t1);
     const auto t2 = clk::now();
     // What the increment's axioms reach (migrate_state re-triggers only that):
-    //  dA  concepts whose index rows changed: the sources of new told / existential axioms and
-    //      everything below them (told*, exr*, exl* are closed downward over told subs), the
-    //      operands of new conjunctions
+    //  dA  the sources of new told / existential axioms and the operands of new conjunctions.
+    //      told*, exr* and exl* are closed downward over told subs, so every concept below a
+    //      source A has a changed row too — but each fact (X, C) with C below A has (X, A) in
+    //      S(X) (the state is closed under CR1), and re-triggering (X, A) over the new rows
+    //      concludes what (X, C) could: the sources alone suffice (bit 1: a new told super,
+    //      the re-triggered fact re-walks its told closure)
     //  dX  concepts that became new link targets (a new pair (r, X): X's pair range grew)
     //  dP  pairs whose role has new role axioms (r ⊑ s, chains, domain, range) or is below one
     const el::HostIndex& h = c->hx;
     std::vector<uint8_t> dA(std::max<uint32_t>(h.N, 1), 0), dX(std::max<uint32_t>(h.N, 1), 0),
         dP(std::max<uint32_t>(h.P, 1), 0), dR(h.R + 1, 0);
     std::vector<uint32_t> stk;
-    auto markA = [&](uint32_t a) {
-      if (a < h.N && !dA[a]) dA[a] = 1, stk.push_back(a);
+    auto markA = [&](uint32_t a, uint8_t m) {
+      if (a < h.N) dA[a] |= m;
     };
-    for (uint32_t i = 0; i < inc->n_sub; ++i) markA(inc->sub_a[i]);
-    for (uint32_t i = 0; i < inc->n_ex_rhs; ++i) markA(inc->exr_a[i]);
-    for (uint32_t i = 0; i < inc->n_ex_lhs; ++i) markA(inc->exl_a[i]);
-    while (!stk.empty()) {  // downward over told subs
-      const uint32_t a = stk.back();
-      stk.pop_back();
-      for (uint32_t j = h.toldT.ptr[a]; j < h.toldT.ptr[a + 1]; ++j) markA(h.toldT.a[j]);
-    }
+    for (uint32_t i = 0; i < inc->n_sub; ++i) markA(inc->sub_a[i], 3);
+    for (uint32_t i = 0; i < inc->n_ex_rhs; ++i) markA(inc->exr_a[i], 1);
+    for (uint32_t i = 0; i < inc->n_ex_lhs; ++i) markA(inc->exl_a[i], 1);
     for (uint32_t i = 0; i < inc->n_conj; ++i)
-      for (uint32_t k = inc->conj_ptr[i]; k < inc->conj_ptr[i + 1]; ++k)
-        if (inc->conj_ops[k] < h.N) dA[inc->conj_ops[k]] = 1;
+      for (uint32_t k = inc->conj_ptr[i]; k < inc->conj_ptr[i + 1]; ++k) markA(inc->conj_ops[k], 1);
     std::vector<std::vector<uint32_t>> rsub(h.R);  // role -> told sub-roles (of old ∪ increment)
     for (size_t i = 0; i < c->store.sr_r.size(); ++i)
       if (c->store.sr_s[i] < h.R) rsub[c->store.sr_s[i]].push_back(c->store.sr_r[i]);
@@ -5811,6 +5892,8 @@ int el_saturate(el_ctx* c, el_stats* stats) {
     c->sync();
     double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     c->fill_stats(stats, ms);
+    static const bool trace_mem = getenv("EL_TRACE_MEM") != nullptr;
+    if (trace_mem) c->mem_report();
     return EL_OK;
   });
 }
@@ -6173,14 +6256,53 @@ int el_fresh_fillers(el_ctx* c, uint32_t* filler, uint32_t* role, size_t cap, si
   return EL_OK;
 }
 
+// Page-locked result buffers.  From 2 MB on: anonymous memory on 2-MB boundaries with
+// MADV_HUGEPAGE, touched by the calling thread (its NUMA node), then registered mapped and
+// portable — the SDMA engines' D2H copies into it ran at 56-57 GB/s in every buffer measured,
+// hipHostMalloc's 4-KB pages at 50-57 and 46-55 with huge pages refused
+// (scripts/micro/d2h_pages.hip, profiles/r05_d2h_pages.txt).  Smaller ones: hipHostMalloc.
+namespace {
+constexpr size_t HUGE_PAGE = 2ull << 20;
+std::mutex host_mu;
+std::unordered_map<void*, std::pair<void*, size_t>> host_maps;  // registered pointer -> mapping
+}  // namespace
+
 void* el_host_alloc(size_t bytes) {
   void* p = nullptr;
+  if (bytes >= HUGE_PAGE) {
+    const size_t len = (bytes + HUGE_PAGE - 1) / HUGE_PAGE * HUGE_PAGE + HUGE_PAGE;
+    void* m = mmap(nullptr, len, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
+    if (m != MAP_FAILED) {
+      p = (void*)(((uintptr_t)m + HUGE_PAGE - 1) & ~(uintptr_t)(HUGE_PAGE - 1));
+      const size_t n = len - ((char*)p - (char*)m);
+      (void)madvise(p, n, MADV_HUGEPAGE);
+      memset(p, 0, n);
+      if (hipHostRegister(p, n, hipHostRegisterMapped | hipHostRegisterPortable) == hipSuccess) {
+        std::lock_guard<std::mutex> g(host_mu);
+        host_maps[p] = {m, len};
+        return p;
+      }
+      munmap(m, len);
+    }
+  }
   if (hipHostMalloc(&p, bytes ? bytes : 1, hipHostMallocPortable) != hipSuccess) return nullptr;
   return p;
 }
 
 void el_host_free(void* p) {
-  if (p) (void)hipHostFree(p);
+  if (!p) return;
+  std::pair<void*, size_t> m{nullptr, 0};
+  {
+    std::lock_guard<std::mutex> g(host_mu);
+    auto it = host_maps.find(p);
+    if (it != host_maps.end()) m = it->second, host_maps.erase(it);
+  }
+  if (m.first) {
+    (void)hipHostUnregister(p);
+    munmap(m.first, m.second);
+  } else {
+    (void)hipHostFree(p);
+  }
 }
 
 int el_export_result(el_ctx* c, int layout, el_sink sink, void* user) {
