@@ -916,18 +916,41 @@ __device__ __forceinline__ void expand_s(const DIndex& ix, const DState& st, Blo
                          uint32_t begin, uint32_t end, uint32_t mask, uint32_t a_end, uint32_t tpw) {
   Ev ev;
   const uint32_t w0 = bid * (blockDim.x >> 6) + (threadIdx.x >> 6), nw = nb * (blockDim.x >> 6);
-  for (uint32_t base = begin + w0 * tpw; base < end; base += nw * tpw) {  // (wave-uniform)
-    const uint32_t i = base + lane_id();
-    const bool act = lane_id() < tpw && i < end;
-    uint32_t X = 0, A = 0, f = 1;
-    uint4 m0 = make_uint4(0, 0, 0, 0), m1 = m0;
-    if (act) {
-      X = st.slog_x[i];
-      A = st.slog_a[i];
-      f = st.slog_f[i];
-      ev.v[EL_EV_TRIG]++;
-      m0 = ix.meta[2 * A];  // the four rows of A at once: begins, ends
-      m1 = ix.meta[2 * A + 1];
+  const uint32_t step = nw * tpw;
+  // A software pipeline over the wave's trigger batches: while a batch walks its rows, the
+  // batch after it has its fact and its meta rows in flight and the one after that its fact,
+  // so the two dependent loads (log -> meta) at the head of a batch are off the wave's chain.
+  const uint4 z4 = make_uint4(0, 0, 0, 0);
+  auto live = [&](uint64_t b) { return lane_id() < tpw && b + lane_id() < end; };
+  uint32_t X1 = 0, A1 = 0, f1 = 1, X2 = 0, A2 = 0, f2 = 1;
+  uint4 n0 = z4, n1 = z4;
+  {
+    const uint64_t b0 = begin + (uint64_t)w0 * tpw;
+    if (live(b0)) {
+      const uint32_t i = (uint32_t)b0 + lane_id();
+      X1 = st.slog_x[i], A1 = st.slog_a[i], f1 = st.slog_f[i];
+      n0 = ix.meta[2 * A1];  // the four rows of A at once: begins, ends
+      n1 = ix.meta[2 * A1 + 1];
+    }
+    if (live(b0 + step)) {
+      const uint32_t i = (uint32_t)(b0 + step) + lane_id();
+      X2 = st.slog_x[i], A2 = st.slog_a[i], f2 = st.slog_f[i];
+    }
+  }
+  for (uint32_t base = begin + w0 * tpw; base < end; base += step) {  // (wave-uniform)
+    const bool act = live(base);
+    const uint32_t X = act ? X1 : 0u, A = act ? A1 : 0u, f = act ? f1 : 1u;
+    const uint4 m0 = act ? n0 : z4, m1 = act ? n1 : z4;
+    if (act) ev.v[EL_EV_TRIG]++;
+    X1 = X2, A1 = A2, f1 = f2;
+    n0 = n1 = z4;
+    if (live((uint64_t)base + step)) {
+      n0 = ix.meta[2 * A1];
+      n1 = ix.meta[2 * A1 + 1];
+    }
+    if (live((uint64_t)base + 2ull * step)) {
+      const uint32_t i = base + 2 * step + lane_id();
+      X2 = st.slog_x[i], A2 = st.slog_a[i], f2 = st.slog_f[i];
     }
     // A ∈ S(X), A ⊑* B  =>  B ∈ S(X), over the told closure at once; a fact that came out
     // of a closure is not re-expanded (its closure is a subset of the one that produced it)
@@ -2426,7 +2449,7 @@ __global__ void __launch_bounds__(256) k_retrigger(const uint32_t* __restrict__ 
                                                    uint32_t l_n, const uint8_t* __restrict__ dA,
                                                    const uint8_t* __restrict__ dX, const uint8_t* __restrict__ dP,
                                                    uint32_t* rx, uint32_t* ra, uint8_t* rf, uint32_t* rlx, uint32_t* rlp,
-                                                   unsigned long long* cnt) {
+                                                   const uint4* __restrict__ meta, unsigned long long* cnt) {
   // two passes over the block's tile: count the kept entries (per wave, then a block prefix and
   // one atomic per tile and list), then write them at their places
   __shared__ uint32_t wcnt[2][4];
@@ -2453,16 +2476,19 @@ __global__ void __launch_bounds__(256) k_retrigger(const uint32_t* __restrict__ 
   unsigned long long os = gbase[0], ol = gbase[1];
   for (uint32_t w = 0; w < wid; ++w) os += wcnt[0][w], ol += wcnt[1][w];
   const unsigned long long below = (1ull << lane_id()) - 1ull;
+  unsigned long long told = 0;  // told candidates the kept facts can emit (the rows they re-walk)
   for (uint32_t k = 0; k < RT_TILE; k += 256) {  // (block-uniform trip count; each wave in order)
     const uint32_t i = t0 + k + threadIdx.x;
     const bool ks = keep_s(i), kl = keep_l(i);
     const unsigned long long ms = __ballot(ks), ml = __ballot(kl);
     if (ks) {
       const uint64_t o = os + __popcll(ms & below);
+      const uint32_t a = sa[i];
+      const uint8_t d = dA[a];
       rx[o] = sx[i];
-      ra[o] = sa[i];
-      const uint8_t d = dA[sa[i]];
+      ra[o] = a;
       rf[o] = d & 2u ? 0 : d ? 2 : sf[i] == 1 ? 1 : 2;
+      if (d & 2u) told += meta[2 * a + 1].x - meta[2 * a].x;
     }
     if (kl) {
       const uint64_t o = ol + __popcll(ml & below);
@@ -2472,6 +2498,8 @@ __global__ void __launch_bounds__(256) k_retrigger(const uint32_t* __restrict__ 
     os += __popcll(ms);
     ol += __popcll(ml);
   }
+  for (int k = 32; k >= 1; k >>= 1) told += __shfl_xor(told, k);
+  if (lane_id() == 0 && told) atomicAdd(cnt + 2, told);
 }
 
 __global__ void k_remap(uint32_t* __restrict__ v, uint64_t n, const uint32_t* __restrict__ map) {
@@ -2577,8 +2605,9 @@ static uint64_t log_cap(uint64_t n) {
   return (n + n / 8 + step - 1) / step * step;
 }
 // The fact and link logs, which the streamed result reads, keep power-of-two growth with
-// half again as slack: with the tight slack G3's fact log regrew mid-saturation (a device
-// and copy-stream sync, then a copy), and the result's copy-back tail grew by 7-8 ms.
+// half again as slack: with log_cap's slack (G3's fact log 4.3 GB instead of 9.7 GB) the
+// result's copy-back tail grew by 7-8 ms in every A/B run, the supersteps unchanged (the
+// cause was not found: after the first classification neither sizing regrows the log).
 static uint64_t stream_log_cap(uint64_t n) { return next_pow2(n + n / 2); }
 
 // Triggers per wave and grid of an expand role with n triggers: a small step's triggers
@@ -2990,6 +3019,8 @@ struct el_ctx {
   uint64_t nb = 0, nbp = 0, nc = 0;  // base links, base propagations, chain-second base links
   void alloc_closure();
   void free_closure();
+  uint64_t cl_alloc_n = 0, cl_alloc_p = 0;
+  std::chrono::steady_clock::time_point inc_t0;  // (EL_TRACE_INC: el_saturate's start)  // the concept / pair counts the closure buffers were allocated for
   void set_closure_ix();
   void closure_grow();
   void closure_tail(uint32_t a, uint32_t b, uint32_t L);
@@ -3311,6 +3342,7 @@ struct el_ctx {
   unsigned long long reloc_seq = 0;
   void gap_build_from_log(GapCsr& g, const uint32_t* rows, const uint32_t* vals, uint64_t n,
                           const uint8_t* keep = nullptr);
+  void gap_build_sorted(GapCsr& g, const uint32_t* rows, const uint32_t* vals, uint64_t n, uint32_t bits);
   void launch_gap_scan(const uint32_t* len, uint32_t R, uint32_t* start_out);
   std::string install_index(el::HostIndex&& h);
   void column_window();
@@ -4094,6 +4126,11 @@ bool el_ctx::superstep(uint32_t mask, uint64_t sb, uint64_t se, uint64_t lb, uin
     if (grow) {
       sync();
       if (strm) HIPCHK(hipStreamSynchronize(dstream));  // (a streamed result may still read the logs)
+      static const bool trace = getenv("EL_TRACE_GROW") != nullptr;
+      if (trace)
+        fprintf(stderr, "grow: s %d l %d lhash %d a %d ahash %d p %d phash %d\n", s_count + cs_cap + ct_cap > slog_cap,
+                l_count + cl_cap > llog_cap, 2 * (l_count - l_base + cl_cap) > lhash_cap, a_count + ca_cap > alog_cap,
+                2 * (a_count + ca_cap) > ahash_cap, p_count + cp_cap > plog_cap, 2 * (p_count - p_base + cp_cap) > phash_cap);
     }
     auto grow_log = [&](uint64_t used, uint64_t add, uint64_t& cap, uint32_t*& a, uint32_t*& b) {
       if (used + add <= cap) return;
@@ -4115,6 +4152,10 @@ bool el_ctx::superstep(uint32_t mask, uint64_t sb, uint64_t se, uint64_t lb, uin
     if (2 * (p_count - p_base + cp_cap) > phash_cap) rehash_props(next_pow2(2 * (p_count - p_base + cp_cap)));
 
     // ---- generation (reads only the state of step t-1; candidate counters are zero here)
+    static const bool trace_inc = getenv("EL_TRACE_INC") != nullptr;
+    if (trace_inc && trig_override)
+      fprintf(stderr, "re-trigger step: capacities checked at %.3f ms\n",
+              std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - inc_t0).count());
     refresh_acts();
     DState st = dstate();
     ExpandArgs ea{};
@@ -4537,6 +4578,50 @@ void el_ctx::gap_build_from_log(GapCsr& g, const uint32_t* rows, const uint32_t*
   }
 }
 
+// The same layout and contents by a radix sort of the entries by row instead of a counter atomic
+// per entry: the predecessor rows of G3's 33 M links by pid took 5.9 ms to count and 5.2 ms to
+// fill with atomics (a hub pid's entries serialise on its counter), the sort and the grouped
+// fill well under one.  bits: bits of a row index.
+void el_ctx::gap_build_sorted(GapCsr& g, const uint32_t* rows, const uint32_t* vals, uint64_t n, uint32_t bits) {
+  const uint32_t R = g.rows;
+  if (n > 0xffffffffull) throw ElError{EL_ENOMEM, "gapped CSR beyond 2^32 entries"};
+  if (n > sk_cap) {
+    sk_cap = n + n / 8;
+    dfree(sk);
+    dfree(sv);
+    sk = dalloc<uint32_t>(sk_cap);
+    sv = dalloc<uint32_t>(sk_cap);
+  }
+  const size_t need = elcl::sort_temp_bytes((uint32_t)std::max<uint64_t>(n, 1));
+  if (need > csort_bytes) {
+    dfree(csort_tmp);
+    csort_bytes = need;
+    csort_tmp = dalloc<uint8_t>(need);
+  }
+  // first / last of each row's run: the relocation scratch (nstart) and the row ends (rewritten
+  // by k_gap_ends below)
+  HIPCHK(hipMemsetAsync(g.nstart, 0, (uint64_t)R * sizeof(uint32_t), stream));
+  HIPCHK(hipMemsetAsync(g.end, 0, (uint64_t)R * sizeof(uint32_t), stream));
+  if (n) {
+    elcl::sort_pairs(stream, csort_tmp, csort_bytes, rows, sk, vals, sv, (uint32_t)n, bits);
+    elcl::runs(stream, sk, (uint32_t)n, g.nstart, g.end);
+  }
+  elcl::caps(stream, g.nstart, g.end, R, nullptr, nullptr, nullptr, g.len);
+  launch_gap_scan(g.len, R, g.start);
+  hipLaunchKernelGGL(k_gap_ends, dim3(grid_for(R)), dim3(BLOCK), 0, stream, g.start, g.end, R);
+  HIPCHK(hipGetLastError());
+  const uint64_t total = (uint64_t)GAP_MUL * n + (uint64_t)gap_cap(0) * R;
+  if (total > 0xffffffffull) throw ElError{EL_ENOMEM, "gapped CSR beyond 2^32 slots"};
+  if (total > g.val_cap) {
+    sync();
+    dfree(g.val);
+    g.val_cap = total + total / 2;
+    g.val = dalloc<uint32_t>(g.val_cap);
+  }
+  g.used = total;
+  if (n) elcl::group_fill(stream, sk, sv, (uint32_t)n, g.nstart, g.start, g.val);
+}
+
 // ---- the told closure on the device (el_closure.h), rebuilt inside every el_init: nothing
 // derived from the axioms survives from one classification to the next except buffer sizes
 
@@ -4575,6 +4660,8 @@ void el_ctx::alloc_closure() {
     *p = dalloc<uint32_t>(P);
     HIPCHK(hipMemset(*p, 0, P * sizeof(uint32_t)));
   }
+  cl_alloc_n = N;
+  cl_alloc_p = P;
   level_hint = 32;
   set_closure_ix();
 }
@@ -5176,13 +5263,15 @@ void el_ctx::migrate_state(uint32_t N0, const std::vector<uint32_t>& pmap, const
   l_base = p_base = 0;  // every link goes into the set: the base links of the old index are plain links now
   ix.base = 0;
   fresh = false;
-  rehash_links(lhash_cap);
-  rehash_props(phash_cap);
+  // (sized as the next superstep's capacity check will ask, now that the base links and
+  // propagations are in the sets: a second rehash there cost milliseconds)
+  rehash_links(std::max<uint64_t>(lhash_cap, next_pow2(2 * (l_count + cl_cap))));
+  rehash_props(std::max<uint64_t>(phash_cap, next_pow2(2 * (p_count + cp_cap))));
   lap("rehash");
   // predecessor / successor / propagation rows for the new pair and concept spaces
   if (P && need_pred) {
     PR.reshape((uint32_t)P, cl_cap);
-    gap_build_from_log(PR, llog_p, llog_x, l_count);
+    gap_build_sorted(PR, llog_p, llog_x, l_count, key_bits);
   } else {
     PR.release();
   }
@@ -5201,22 +5290,24 @@ void el_ctx::migrate_state(uint32_t N0, const std::vector<uint32_t>& pmap, const
   lap("csrs");
   // the told closure of the new index (every concept's: old closures may have grown), with the
   // counts of the new concepts' init facts
-  free_closure();
-  alloc_closure();
+  if (cl_alloc_n == N) {  // same concept space: only the pair-keyed buffers follow P (closure_state zeroes them)
+    const uint64_t P1 = std::max<uint64_t>(P, 1);
+    if (P1 > cl_alloc_p) {
+      for (uint32_t** p : {&pr_first, &pr_last, &bpp_s, &bpp_e, &cap_pr, &cap_pp}) {
+        dfree(*p);
+        *p = dalloc<uint32_t>(P1);
+      }
+      cl_alloc_p = P1;
+    }
+    set_closure_ix();
+  } else {
+    free_closure();
+    alloc_closure();
+  }
   lap("cl-alloc");
   closure_rows(N0, (uint32_t)N);
   set_closure_ix();
   lap("closure");
-  // the first superstep re-emits the told closure of every fact it re-triggers (the row
-  // array's fill bounds the closures' total)
-  const uint64_t ct_need = next_pow2(2 * (uint64_t)clt.t_tail + 1024);
-  if (ct_need > ct_cap) {
-    dfree(ct_x);
-    dfree(ct_a);
-    ct_cap = ct_need;
-    ct_x = dalloc<uint32_t>(ct_cap);
-    ct_a = dalloc<uint32_t>(ct_cap);
-  }
   const uint64_t s_old = s_count;
   // S(X) = {X, ⊤} ∪ told*(X) for the new concepts, appended to the fact log
   if (N > N0) {
@@ -5275,18 +5366,28 @@ void el_ctx::migrate_state(uint32_t N0, const std::vector<uint32_t>& pmap, const
       rt_lx = dalloc<uint32_t>(rt_lcap);
       rt_lp = dalloc<uint32_t>(rt_lcap);
     }
-    unsigned long long* cnt = dalloc<unsigned long long>(2);
-    HIPCHK(hipMemsetAsync(cnt, 0, 2 * sizeof(unsigned long long), stream));
+    unsigned long long* cnt = dalloc<unsigned long long>(3);
+    HIPCHK(hipMemsetAsync(cnt, 0, 3 * sizeof(unsigned long long), stream));
     const uint64_t rn = std::max<uint64_t>(s_count, l_count);
     hipLaunchKernelGGL(k_retrigger, dim3((uint32_t)std::max<uint64_t>((rn + RT_TILE - 1) / RT_TILE, 1)), dim3(256), 0, stream,
                        slog_x, slog_a, slog_f, (uint32_t)s_old, (uint32_t)s_count, llog_x, llog_p, (uint32_t)l_count, da,
-                       dx, dp, rt_x, rt_a, rt_f, rt_lx, rt_lp, cnt);
+                       dx, dp, rt_x, rt_a, rt_f, rt_lx, rt_lp, cl.meta, cnt);
     HIPCHK(hipGetLastError());
-    unsigned long long h[2] = {0, 0};
+    unsigned long long h[3] = {0, 0, 0};
     HIPCHK(hipMemcpyAsync(h, cnt, sizeof h, hipMemcpyDeviceToHost, stream));
     sync();
     rt_ns = h[0];
     rt_nl = h[1];
+    // the re-trigger step's told candidates: the rows its told sources re-walk (a longer bound
+    // grew the fact log in that step — a copy of every logged fact)
+    const uint64_t ct_need = next_pow2(h[2] + 1024);
+    if (ct_need > ct_cap) {
+      dfree(ct_x);
+      dfree(ct_a);
+      ct_cap = ct_need;
+      ct_x = dalloc<uint32_t>(ct_cap);
+      ct_a = dalloc<uint32_t>(ct_cap);
+    }
     dfree(cnt);
     dfree(da);
     dfree(dx);
@@ -5837,7 +5938,10 @@ int el_saturate(el_ctx* c, el_stats* stats) {
     c->tr_s.clear();
     c->tr_l.clear();
     c->tr_a.clear();
+    const bool inc = c->inc_pending;
+    c->inc_t0 = t0;
     if (!c->part()) c->retrigger_step();  // (the first superstep after an increment)
+    const auto t_rt = std::chrono::steady_clock::now();
     // A partitioned context at its global fixpoint (an el_saturate that returned since the last
     // el_init: a re-stream into fitted buffers after EL_ERANGE, which one rank may do alone) runs
     // no collective superstep: its peers have left the exchange.
@@ -5891,6 +5995,10 @@ int el_saturate(el_ctx* c, el_stats* stats) {
     c->stream_end(rel);
     c->sync();
     double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    static const bool trace_inc = getenv("EL_TRACE_INC") != nullptr;
+    if (trace_inc && inc)
+      fprintf(stderr, "increment saturate: re-trigger step %.3f ms (host clock), all %.3f ms\n",
+              std::chrono::duration<double, std::milli>(t_rt - t0).count(), ms);
     c->fill_stats(stats, ms);
     static const bool trace_mem = getenv("EL_TRACE_MEM") != nullptr;
     if (trace_mem) c->mem_report();
