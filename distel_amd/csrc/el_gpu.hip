@@ -4630,11 +4630,14 @@ void el_ctx::alloc_closure() {
   auto cap32 = [](uint64_t v) { return (uint32_t)std::min<uint64_t>(v, 0x7fffffffull); };
   cl.meta = dalloc<uint4>(2 * N);
   cl.meta2 = dalloc<uint4>(2 * N);
-  // first guesses (G3: 24 M / 25 M / 36 M entries); an overflowing build grows and runs again
-  const uint64_t waste = std::min<uint64_t>(N, elcl::SLOTS) * elcl::CHUNK;  // partly used chunks
-  cl.t_cap = cap32(64 * N + waste + (1u << 16));
-  cl.e_cap = cap32(64 * N + waste + (1u << 16));
-  cl.l_cap = cap32(96 * N + waste + (1u << 16));
+  // first guesses (G3: 24 M / 25 M / 36 M entries) for the concepts the build covers — a
+  // partition's column window (×8 of G3: one copy's, not 8 copies' worth: 4 GB less per rank);
+  // an overflowing build grows and runs again
+  const uint64_t Nc = part() && ix.c_hi > ix.c_lo ? std::min<uint64_t>(N, (uint64_t)ix.c_hi - ix.c_lo) : N;
+  const uint64_t waste = std::min<uint64_t>(Nc, elcl::SLOTS) * elcl::CHUNK;  // partly used chunks
+  cl.t_cap = cap32(64 * Nc + waste + (1u << 16));
+  cl.e_cap = cap32(64 * Nc + waste + (1u << 16));
+  cl.l_cap = cap32(96 * Nc + waste + (1u << 16));
   cl.t_val = dalloc<uint32_t>(cl.t_cap);
   cl.e_val = dalloc<uint32_t>(cl.e_cap);
   cl.l_r = dalloc<uint32_t>(cl.l_cap);
