@@ -4249,7 +4249,14 @@ bool el_ctx::superstep(uint32_t mask, uint64_t sb, uint64_t se, uint64_t lb, uin
     }
     // the new links / propagations are already in their (gapped) CSR rows; S rows are
     // built lazily, for export only
+    auto inc_lap = [&](const char* what) {
+      if (trace_inc && trig_override)
+        fprintf(stderr, "re-trigger step: %s at %.3f ms\n", what,
+                std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - inc_t0).count());
+    };
+    inc_lap("launched");
     wait_commit(ca.pub.seq);
+    inc_lap("committed");
     if (trace_cands)  // diagnostic (EL_TRACE_CANDS): candidates vs. new facts per step
     {
       unsigned long long ln[3] = {0, 0, 0};
@@ -4269,6 +4276,7 @@ bool el_ctx::superstep(uint32_t mask, uint64_t sb, uint64_t se, uint64_t lb, uin
     a_count = hc.a_log;
     p_count = hc.p_log;
     gap_relocate_all();  // rows that outgrew their slack move to new slots before anyone reads them
+    inc_lap("relocated");
     // ---- keep the buffers ahead of demand; complete the step if one overflowed
     bool overflow = false;
     // Each trigger of the next step fans out to a few S conclusions (G3 step 1: 25 M new links
@@ -4316,6 +4324,7 @@ bool el_ctx::superstep(uint32_t mask, uint64_t sb, uint64_t se, uint64_t lb, uin
       dfree(jobs);
       jobs = dalloc<uint4>(job_cap);
     }
+    inc_lap("capacities kept");
     if (!overflow) break;
     if (trace_cands) fprintf(stderr, "step re-run after a queue overflow (attempt %d)\n", attempt + 1);
   }

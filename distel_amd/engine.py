@@ -436,10 +436,26 @@ class Engine:
         if rc != EL_OK:
             raise ElError(rc, f"el_create(device={device}) failed: no usable HIP device or bad partition")
         self.partition = partition
-        self.ax: Optional[Axioms] = None
+        self.ax = None  # the loaded ontology (old ∪ increments; see the property)
         self._last: Optional[Stats] = None   # the last saturation's stats
         self._streamed = None  # (Stream, release) of the last streamed result until result_wait
         self._stream: Optional[Stream] = None  # a streamed result armed for the next saturate()
+
+    @property
+    def ax(self) -> Optional[Axioms]:
+        """The loaded axioms, increments included.  add_axioms() leaves the merge to the first
+        reader: it is host bookkeeping (G3: ≈140 ms of array concatenation) that sat between the
+        increment and the next saturate(), the GPU idle meanwhile."""
+        if self._inc:
+            for inc in self._inc:
+                self._ax = merge_axioms(self._ax, inc) if self._ax is not None else inc
+            self._inc = []
+        return self._ax
+
+    @ax.setter
+    def ax(self, v: Optional[Axioms]) -> None:
+        self._ax = v
+        self._inc: List[Axioms] = []
 
     def _check(self, rc: int, what: str) -> None:
         cause = None
@@ -481,7 +497,7 @@ class Engine:
         possibly extended); a saturated state is kept and the next saturate() continues."""
         view = AxiomsView(inc)
         self._check(self._lib.el_add_axioms(self._ctx, C.byref(view.struct)), "el_add_axioms")
-        self.ax = merge_axioms(self.ax, inc) if self.ax is not None else inc
+        self._inc.append(inc)
         self._last = None
 
     def increment_info(self) -> Dict:
