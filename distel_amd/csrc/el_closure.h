@@ -34,6 +34,7 @@ namespace elcl {
 // The raw axiom CSRs the closure is derived from (el_load uploads them; read-only).
 struct Axioms {
   uint32_t N = 0, P = 0;
+  const uint32_t* cperm = nullptr;  // concept -> bit-matrix column (whole ontology; null: window order)
   const uint32_t *par_ptr = nullptr, *par = nullptr;    // A -> told supers B (A ⊑ B), sorted, B != A
   const uint32_t *chi_ptr = nullptr, *chi = nullptr;    // B -> told subs A (the transpose)
   const uint32_t *xr_ptr = nullptr, *xr = nullptr;      // A -> pids of A ⊑ ∃r.Y, sorted unique

@@ -1278,7 +1278,8 @@ __global__ void __launch_bounds__(BLOCK) k_init_facts(Axioms ax, Out o, uint32_t
         slog_x[base + slot] = x;
         slog_a[base + slot] = val;
         slog_f[base + slot] = f;
-        const uint32_t col = val < 2u ? val : (val >= c_lo && val < c_hi ? val - c_lo + 2u : NONE);
+        const uint32_t col =
+            val < 2u ? val : (val >= c_lo && val < c_hi ? (ax.cperm ? ax.cperm[val] : val - c_lo + 2u) : NONE);
         if (col != NONE) {
           __hip_atomic_fetch_or(bits + (uint64_t)x * W + (col >> 5), 1u << (col & 31u), __ATOMIC_RELAXED,
                                 __HIP_MEMORY_SCOPE_AGENT);

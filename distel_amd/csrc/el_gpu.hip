@@ -141,8 +141,11 @@ struct DIndex {
   // row partition (el_config.exchange != NONE): this context owns rows [lo, hi)
   uint32_t lo, hi;
   // bit-row columns: ⊥, ⊤, then the concepts [c_lo, c_hi) — every concept an owned row can
-  // hold (el_ctx::column_window; the whole ontology: 2, N, i.e. column = concept id)
+  // hold (el_ctx::column_window; the whole ontology: 2, N) — in window order (column = concept -
+  // c_lo + 2) or, for a whole ontology, in cperm's order (el_index.h column_order: the expected
+  // frequent CR4 conclusions first, so a row's new facts share lines)
   uint32_t c_lo, c_hi;
+  const uint32_t* cperm;
   uint32_t part;               // 1 = partitioned protocol (oracle/partition_model.py)
   uint32_t base;               // 1 = the base links {(X, p) : p ∈ exr(X)} and base propagations
                                // are in their logs and rows but not in their sets (install_base)
@@ -407,7 +410,9 @@ __device__ __forceinline__ void gap_append(const DGap& g, uint32_t row, uint32_t
 
 // bit-row column of concept a, NONE when no owned row can hold a (outside the window)
 __device__ __forceinline__ uint32_t col_of(const DIndex& ix, uint32_t a) {
-  return a < 2u ? a : (a >= ix.c_lo && a < ix.c_hi ? a - ix.c_lo + 2u : NONE);
+  if (a < 2u) return a;
+  if (a < ix.c_lo || a >= ix.c_hi) return NONE;
+  return ix.cperm ? ix.cperm[a] : a - ix.c_lo + 2u;
 }
 
 __device__ __forceinline__ bool test_bit(const DIndex& ix, const uint32_t* bits, uint32_t x, uint32_t b) {
@@ -1556,7 +1561,9 @@ __device__ void commit_s_sorted(const DIndex& ix, const DState& st, CommitLds& s
       hb[k] = NONE;
       if (hx[k] != NONE) {
         const uint32_t c = col_of(ix, ha[k]);
-        const uint32_t h = sbits ? ((hx[k] * 769u + (c >> 9)) * 2654435761u) >> (32 - sbits) : 0u;
+        // (the line's hash, then the word inside the 64-B line: one word's candidates adjacent)
+        const uint32_t h = sbits > 4u ? (((hx[k] * 769u + (c >> 9)) * 2654435761u) >> (36 - sbits)) << 4 | ((c >> 5) & 15u)
+                           : sbits ? ((hx[k] * 769u + (c >> 9)) * 2654435761u) >> (32 - sbits) : 0u;
         hb[k] = ((run - 1) << sbits) | h;
         hr[k] = atomicAdd(&sm.c.bin[hb[k]], 1u);
       }
@@ -1578,27 +1585,55 @@ __device__ void commit_s_sorted(const DIndex& ix, const DState& st, CommitLds& s
     for (uint32_t k = 0; k < PER; ++k)
       if (hb[k] != NONE) sm.c.srt[sm.c.bin[hb[k]] + hr[k]] = ((unsigned long long)hx[k] << 32) | ha[k];
     __syncthreads();
-    // 4. the atomics, 64 consecutive sorted candidates per wave-instruction
+    // 4. the atomics, 64 consecutive sorted candidates per wave-instruction.  The lanes holding
+    // the same (row, word) — adjacent in the sorted chunk — OR their bits together first (a
+    // segmented scan over the wave) and the segment's last lane issues one atomic for them: with
+    // the column order (DIndex::cperm) a row's frequent subsumers share a few words, whose
+    // atomics would otherwise serialise on one address.  A lane's bit is new if neither the word
+    // nor an earlier lane of its segment had it.
     bool nw[PER];
     unsigned long long key[PER];
 #pragma unroll
     for (uint32_t k = 0; k < PER; ++k) {
       const uint32_t i = k * BLOCK + tid;
-      nw[k] = false;
+      const bool v = i < total;
+      uint32_t x = 0, c = NONE;
       key[k] = 0;
-      if (i < total) {
+      if (v) {
         key[k] = sm.c.srt[i];
-        const uint32_t x = (uint32_t)(key[k] >> 32), a = (uint32_t)key[k];
+        x = (uint32_t)(key[k] >> 32);
+        c = col_of(ix, (uint32_t)key[k]);  // (every candidate of an owned row lies inside the window)
         ev.v[EL_EV_TRIG]++;
         ev.v[EL_EV_RMW]++;
-        const uint32_t c = col_of(ix, a);  // (every candidate of an owned row lies inside the window)
-        const uint32_t m = 1u << (c & 31u);
-        const uint32_t old = c != NONE ? atomicOr(st.bits + (uint64_t)x * ix.W + (c >> 5), m) : m;
-        nw[k] = (old & m) == 0;
-        if (nw[k] && st.summ) st.summ[(uint64_t)x * st.SB + (c >> elrows::SUMM_SHIFT)] = 1;  // (idempotent: plain store)
-        if (nw[k]) ev.v[EL_EV_EMIT]++;
       }
-      if (st.lines) count_lines(st.lines, i < total, (uint32_t)(key[k] >> 32), col_of(ix, (uint32_t)key[k]));
+      const bool on = v && c != NONE;
+      const uint32_t m = on ? 1u << (c & 31u) : 0u;
+      // word id (row, word); lanes without one never match a neighbour
+      const uint32_t wx = on ? x : NONE, ww = on ? c >> 5 : NONE - lane;
+      const uint32_t px = __shfl_up(wx, 1), pw = __shfl_up(ww, 1);
+      const uint32_t head = lane == 0 || px != wx || pw != ww;
+      uint32_t incl = m, f = head;
+#pragma unroll
+      for (uint32_t d = 1; d < 64; d <<= 1) {
+        const uint32_t o = __shfl_up(incl, d), of = __shfl_up(f, d);
+        if (lane >= d) {
+          if (!f) incl |= o;
+          f |= of;
+        }
+      }
+      const uint32_t before = __shfl_up(incl, 1);
+      const uint32_t excl = head ? 0u : before;
+      const uint32_t next = __shfl_down(head, 1);  // (every lane takes part: not under a short-circuit)
+      const uint32_t tail = lane == 63u || next;
+      uint32_t old = 0;
+      if (tail && incl) old = atomicOr(st.bits + (uint64_t)wx * ix.W + ww, incl);
+      const unsigned long long tails = __ballot(tail != 0);
+      const uint32_t last = lane + (uint32_t)__ffsll((long long)(tails >> lane)) - 1u;
+      const uint32_t seen = __shfl(old, (int)last) | excl;
+      nw[k] = on && (seen & m) == 0;
+      if (nw[k] && st.summ) st.summ[(uint64_t)x * st.SB + (c >> elrows::SUMM_SHIFT)] = 1;  // (idempotent: plain store)
+      if (nw[k]) ev.v[EL_EV_EMIT]++;
+      if (st.lines) count_lines(st.lines, v, x, c);
     }
     // 5. the new facts, in sorted order: per round k, the waves' counts in LDS (one barrier)
 #pragma unroll
@@ -3020,6 +3055,10 @@ struct el_ctx {
   void alloc_closure();
   void free_closure();
   uint64_t cl_alloc_n = 0, cl_alloc_p = 0;
+  // the bit matrix's columns are not in concept order (DIndex::cperm): a row read off the matrix
+  // would not come out ascending, so S rows come from the log sorts only, and the reset clears the
+  // matrix itself (no copy-back clears it as it reads)
+  bool colperm() const { return ix.cperm != nullptr; }
   std::chrono::steady_clock::time_point inc_t0;  // (EL_TRACE_INC: el_saturate's start)  // the concept / pair counts the closure buffers were allocated for
   void set_closure_ix();
   void closure_grow();
@@ -3522,6 +3561,11 @@ std::string el_ctx::install_index(el::HostIndex&& hnew) {
   d.lo = lo;
   d.hi = hi;
   column_window();
+  // the column order of a whole ontology (el_index.h column_order; EL_COLUMN_ORDER=0: id order,
+  // a diagnostic).  A partition keeps its window order: its columns are the window's.
+  static const bool col_order = !getenv("EL_COLUMN_ORDER") || getenv("EL_COLUMN_ORDER")[0] != '0';
+  d.cperm = !part() && col_order && h.cperm.size() == h.N && ix.c_lo == 2u ? up32(h.cperm) : nullptr;
+  cax.cperm = caxk.cperm = d.cperm;
   d.part = part() ? 1u : 0u;
   d.xwin = nullptr;  // (the windows of the other ranks: exchange_windows, at the first el_saturate)
   d.nranks = part() ? part_count : 1u;
@@ -4003,7 +4047,7 @@ void el_ctx::build_rows(bool facts, hipStream_t s, uint64_t* ptr, uint32_t* dst,
   if (half != 2) {
     if (facts)
       elrows::build_prep(s, sc, slog_x, slog_a, s_count, lo, R, nullptr, ptr, dst,
-                         elrows::Clear{dstate().bits, W, lo, ix.c_lo, ix.c_hi}, clear);
+                         colperm() ? elrows::Clear{} : elrows::Clear{dstate().bits, W, lo, ix.c_lo, ix.c_hi}, clear);
     else
       elrows::build_prep(s, sc, llog_x, llog_p, l_count, lo, R, pid_rank, ptr, dst, elrows::Clear{}, false);
   }
@@ -5828,6 +5872,12 @@ int el_add_axioms(el_ctx* c, const el_axioms* inc) {
       pmap[p] = q;
     }
     const uint32_t N0 = c->hx.N;
+    // the carried-over matrix keeps its columns: the old order, the new concepts after it
+    if (c->hx.cperm.size() == N0) {
+      hx.cperm.resize(hx.N);
+      std::copy(c->hx.cperm.begin(), c->hx.cperm.end(), hx.cperm.begin());
+      for (uint32_t a = N0; a < hx.N; ++a) hx.cperm[a] = a;
+    }
     const auto t1 = clk::now();
     c->free_index();
     c->n_user = store.N;
@@ -6185,7 +6235,7 @@ int el_copy_result(el_ctx* c, el_result* res) {
     const bool async = (res->flags & EL_RESULT_ASYNC) != 0;
     if (async && !release) return fail(c, EL_EINVAL, "EL_RESULT_ASYNC needs EL_RESULT_RELEASE");
     // the S-row sorts clear the bit matrix only when they write every row (no ELK range fillers)
-    const bool fuse_clear = release && c->uhi() == c->hi;
+    const bool fuse_clear = release && c->uhi() == c->hi && !c->colperm();
     struct Part {
       bool facts;
       uint64_t* ptr_out;
@@ -6216,7 +6266,7 @@ int el_copy_result(el_ctx* c, el_result* res) {
       // (measured: G3, matrix / rows = 46, read-out 0.6 ms faster; G5, 61, 0.17 ms slower)
       // With the block summary the read-out loads only marked blocks, so the matrix-to-rows ratio
       // no longer decides (the dense read-out keeps it).
-      p.readout = p.direct && p.facts && !c->readout_off && p.val_out && p.n >= c->readout_min &&
+      p.readout = p.direct && p.facts && !c->readout_off && !c->colperm() && p.val_out && p.n >= c->readout_min &&
                   (c->summ || (uint64_t)(c->uhi() - c->lo) * c->W * 4 <= 48 * 4 * p.n);
       if (p.readout) {
         if (!r.ptr) r.ptr = dalloc<uint64_t>(R1);

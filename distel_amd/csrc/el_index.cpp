@@ -21,6 +21,8 @@ namespace el {
 
 namespace {
 
+constexpr uint32_t NONE32 = 0xffffffffu;
+
 // Build a CSR from (key, a[, b]) triples: rows sorted by (a, b), duplicates removed.
 Csr make_csr(uint32_t rows, std::vector<std::array<uint32_t, 3>>& t, bool two) {
   std::sort(t.begin(), t.end());
@@ -236,6 +238,49 @@ void told_sccs(HostIndex& o) {
   o.told_x = make_csr(N, ex, false);
 }
 
+// The bit-matrix column order of a whole-ontology context (see el_index.h).  A subsumer B that
+// a CR4 axiom ∃r.A ⊑ B concludes reaches every concept with an r-link to a concept holding A: its
+// expected row count is about (concepts below A) × (r-links per concept), the first factor from
+// the told DAG alone (desc(A) = 1 + Σ over told subs c of desc(c), shared descendants counted once
+// per path, told cycles left at their partial count), the second from the A ⊑ ∃r.C axioms of r.
+// The HOT highest-scoring concepts take the columns after ⊥ and ⊤, everyone else keeps id order.
+// G3 (scripts/column_order.py, distinct 128-B lines the commits touch, from the oracle's fact
+// log): superstep 0 23.1 M -> 5.0 M lines, all supersteps 36.1 M -> 13.4 M, the init facts'
+// 4.5 M unchanged.
+void column_order(const el_axioms& ax, HostIndex& o) {
+  constexpr uint32_t HOT = 16384;
+  const uint32_t N = o.N;
+  std::vector<double> desc(N, 1.0);
+  std::vector<uint32_t> pending(N), stk;
+  for (uint32_t b = 0; b < N; ++b) pending[b] = o.toldT.ptr[b + 1] - o.toldT.ptr[b];
+  for (uint32_t a = 0; a < N; ++a)
+    if (!pending[a]) stk.push_back(a);
+  while (!stk.empty()) {
+    const uint32_t a = stk.back();
+    stk.pop_back();
+    for (uint32_t k = o.told.ptr[a]; k < o.told.ptr[a + 1]; ++k) {
+      const uint32_t b = o.told.a[k];
+      desc[b] += desc[a];
+      if (--pending[b] == 0) stk.push_back(b);
+    }
+  }
+  std::vector<double> links(o.R, 0.0), score(N, 0.0);
+  for (uint32_t i = 0; i < ax.n_ex_rhs; ++i) links[ax.exr_r[i]] += 1.0;
+  for (uint32_t i = 0; i < ax.n_ex_lhs; ++i) score[ax.exl_b[i]] += desc[ax.exl_a[i]] * links[ax.exl_r[i]];
+  std::vector<uint32_t> hot;
+  for (uint32_t a = 2; a < N; ++a)
+    if (score[a] > 0.0) hot.push_back(a);
+  std::stable_sort(hot.begin(), hot.end(), [&](uint32_t x, uint32_t y) { return score[x] > score[y]; });
+  if (hot.size() > HOT) hot.resize(HOT);
+  o.cperm.assign(N, NONE32);
+  o.cperm[0] = 0;
+  if (N > 1) o.cperm[1] = 1;
+  uint32_t c = 2;
+  for (uint32_t a : hot) o.cperm[a] = c++;
+  for (uint32_t a = 2; a < N; ++a)
+    if (o.cperm[a] == NONE32) o.cperm[a] = c++;
+}
+
 std::string build_index(const el_axioms& ax_in, HostIndex& o, uint32_t flags) {
   el_axioms ax = ax_in;
   std::vector<uint32_t> xr, xs, xt;
@@ -434,6 +479,7 @@ std::string build_index(const el_axioms& ax_in, HostIndex& o, uint32_t flags) {
     }
   }
   told_sccs(o);
+  column_order(ax, o);
 #undef CHECK
   return "";
 }

@@ -59,6 +59,10 @@ struct HostIndex {
   std::vector<uint32_t> followers;    // members that are not representatives, ascending
   Csr told_c, toldT_c, exr_c, exl_c;  // the condensed told rows / transpose / own-axiom rows
   Csr told_x;                         // representative -> the other members (its told row's extras)
+  // concept -> bit-matrix column of a whole-ontology context (column_order): ⊥ and ⊤ at 0 and 1,
+  // the concepts expected to be the most frequent CR4 conclusions next, then the rest in id order.
+  // (A layout of the axioms' statistics, like the transposes: no concept closure is used.)
+  std::vector<uint32_t> cperm;
 };
 
 // Owned copy of the typed axioms (el_load copies its input; el_add_axioms appends an
@@ -79,6 +83,7 @@ struct AxiomStore {
 // message (the reference throws on unknown concepts, AxiomLoader.java:1343-1354).
 // flags: el_config.flags (EL_FLAG_COMPAT_DISTEL_CHAIN indexes the DistEL chain set).
 std::string build_index(const el_axioms& ax, HostIndex& out, uint32_t flags = 0);
+void column_order(const el_axioms& ax, HostIndex& o);
 
 // H1, the default: ranges read the ELK way, as the normalizer eliminates
 // them (Normalizer.java:122-137, 455-497).  Every CR3 axiom A ⊑ ∃r.B whose role has ranges
