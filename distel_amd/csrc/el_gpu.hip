@@ -3561,10 +3561,14 @@ std::string el_ctx::install_index(el::HostIndex&& hnew) {
   d.lo = lo;
   d.hi = hi;
   column_window();
-  // the column order of a whole ontology (el_index.h column_order; EL_COLUMN_ORDER=0: id order,
-  // a diagnostic).  A partition keeps its window order: its columns are the window's.
+  // the column order (el_index.h column_order; EL_COLUMN_ORDER=0: id order, a diagnostic): a
+  // whole ontology's, or a partition's over its own column window
   static const bool col_order = !getenv("EL_COLUMN_ORDER") || getenv("EL_COLUMN_ORDER")[0] != '0';
-  d.cperm = !part() && col_order && h.cperm.size() == h.N && ix.c_lo == 2u ? up32(h.cperm) : nullptr;
+  d.cperm = nullptr;
+  if (col_order && !part() && h.cperm.size() == h.N && ix.c_lo == 2u)
+    d.cperm = up32(h.cperm);
+  else if (col_order && part() && h.cscore.size() == h.N && ix.c_hi > ix.c_lo)
+    d.cperm = up32(el::column_perm(h, ix.c_lo, ix.c_hi));
   cax.cperm = caxk.cperm = d.cperm;
   d.part = part() ? 1u : 0u;
   d.xwin = nullptr;  // (the windows of the other ranks: exchange_windows, at the first el_saturate)

@@ -243,12 +243,12 @@ void told_sccs(HostIndex& o) {
 // expected row count is about (concepts below A) × (r-links per concept), the first factor from
 // the told DAG alone (desc(A) = 1 + Σ over told subs c of desc(c), shared descendants counted once
 // per path, told cycles left at their partial count), the second from the A ⊑ ∃r.C axioms of r.
-// The HOT highest-scoring concepts take the columns after ⊥ and ⊤, everyone else keeps id order.
+// column_perm: the HOT highest-scoring concepts of a column window take the columns after ⊥ and
+// ⊤, everyone else in it keeps id order (a whole ontology: the window is every concept).
 // G3 (scripts/column_order.py, distinct 128-B lines the commits touch, from the oracle's fact
 // log): superstep 0 23.1 M -> 5.0 M lines, all supersteps 36.1 M -> 13.4 M, the init facts'
 // 4.5 M unchanged.
 void column_order(const el_axioms& ax, HostIndex& o) {
-  constexpr uint32_t HOT = 16384;
   const uint32_t N = o.N;
   std::vector<double> desc(N, 1.0);
   std::vector<uint32_t> pending(N), stk;
@@ -264,21 +264,28 @@ void column_order(const el_axioms& ax, HostIndex& o) {
       if (--pending[b] == 0) stk.push_back(b);
     }
   }
-  std::vector<double> links(o.R, 0.0), score(N, 0.0);
+  std::vector<double> links(o.R, 0.0);
+  o.cscore.assign(N, 0.0);
   for (uint32_t i = 0; i < ax.n_ex_rhs; ++i) links[ax.exr_r[i]] += 1.0;
-  for (uint32_t i = 0; i < ax.n_ex_lhs; ++i) score[ax.exl_b[i]] += desc[ax.exl_a[i]] * links[ax.exl_r[i]];
-  std::vector<uint32_t> hot;
-  for (uint32_t a = 2; a < N; ++a)
-    if (score[a] > 0.0) hot.push_back(a);
-  std::stable_sort(hot.begin(), hot.end(), [&](uint32_t x, uint32_t y) { return score[x] > score[y]; });
+  for (uint32_t i = 0; i < ax.n_ex_lhs; ++i) o.cscore[ax.exl_b[i]] += desc[ax.exl_a[i]] * links[ax.exl_r[i]];
+  o.cperm = column_perm(o, 2, N);
+}
+
+std::vector<uint32_t> column_perm(const HostIndex& o, uint32_t lo, uint32_t hi) {
+  constexpr uint32_t HOT = 16384;
+  const uint32_t N = o.N;
+  std::vector<uint32_t> hot, perm(N, NONE32);
+  for (uint32_t a = std::max(lo, 2u); a < std::min(hi, N); ++a)
+    if (o.cscore[a] > 0.0) hot.push_back(a);
+  std::stable_sort(hot.begin(), hot.end(), [&](uint32_t x, uint32_t y) { return o.cscore[x] > o.cscore[y]; });
   if (hot.size() > HOT) hot.resize(HOT);
-  o.cperm.assign(N, NONE32);
-  o.cperm[0] = 0;
-  if (N > 1) o.cperm[1] = 1;
+  perm[0] = 0;
+  if (N > 1) perm[1] = 1;
   uint32_t c = 2;
-  for (uint32_t a : hot) o.cperm[a] = c++;
-  for (uint32_t a = 2; a < N; ++a)
-    if (o.cperm[a] == NONE32) o.cperm[a] = c++;
+  for (uint32_t a : hot) perm[a] = c++;
+  for (uint32_t a = std::max(lo, 2u); a < std::min(hi, N); ++a)
+    if (perm[a] == NONE32) perm[a] = c++;
+  return perm;
 }
 
 std::string build_index(const el_axioms& ax_in, HostIndex& o, uint32_t flags) {

@@ -63,6 +63,7 @@ struct HostIndex {
   // the concepts expected to be the most frequent CR4 conclusions next, then the rest in id order.
   // (A layout of the axioms' statistics, like the transposes: no concept closure is used.)
   std::vector<uint32_t> cperm;
+  std::vector<double> cscore;  // the order's score per concept (a partition orders its window by it)
 };
 
 // Owned copy of the typed axioms (el_load copies its input; el_add_axioms appends an
@@ -84,6 +85,9 @@ struct AxiomStore {
 // flags: el_config.flags (EL_FLAG_COMPAT_DISTEL_CHAIN indexes the DistEL chain set).
 std::string build_index(const el_axioms& ax, HostIndex& out, uint32_t flags = 0);
 void column_order(const el_axioms& ax, HostIndex& o);
+// concept -> column for the window [lo, hi): ⊥, ⊤, the window's HOT highest scores, the rest of
+// the window in id order (entries outside the window: NONE)
+std::vector<uint32_t> column_perm(const HostIndex& o, uint32_t lo, uint32_t hi);
 
 // H1, the default: ranges read the ELK way, as the normalizer eliminates
 // them (Normalizer.java:122-137, 455-497).  Every CR3 axiom A ⊑ ∃r.B whose role has ranges
