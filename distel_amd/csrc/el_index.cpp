@@ -246,7 +246,7 @@ void told_sccs(HostIndex& o) {
 // column_perm: the HOT highest-scoring concepts of a column window take the columns after ⊥ and
 // ⊤, everyone else in it keeps id order (a whole ontology: the window is every concept).
 // G3 (scripts/column_order.py, distinct 128-B lines the commits touch, from the oracle's fact
-// log): superstep 0 23.1 M -> 5.0 M lines, all supersteps 36.1 M -> 13.4 M, the init facts'
+// log, 16 k hot): superstep 0 23.1 M -> 5.0 M lines, all supersteps 36.1 M -> 13.4 M, the init facts'
 // 4.5 M unchanged.
 void column_order(const el_axioms& ax, HostIndex& o) {
   const uint32_t N = o.N;
@@ -272,7 +272,7 @@ void column_order(const el_axioms& ax, HostIndex& o) {
 }
 
 std::vector<uint32_t> column_perm(const HostIndex& o, uint32_t lo, uint32_t hi) {
-  constexpr uint32_t HOT = 16384;
+  constexpr uint32_t HOT = 65536;
   const uint32_t N = o.N;
   std::vector<uint32_t> hot, perm(N, NONE32);
   for (uint32_t a = std::max(lo, 2u); a < std::min(hi, N); ++a)
