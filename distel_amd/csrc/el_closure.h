@@ -87,7 +87,8 @@ struct Ctr {
   uint32_t ovf;                     // a row or the scratch did not fit: the build is redone larger
   unsigned long long s_tail;        // big-row scratch: next free 64-bit word
   uint32_t dirty;                   // relaxation: some row changed in this round
-  uint32_t pad[3];
+  uint32_t bad;                     // k_follow met a representative's row without its follower
+  uint32_t pad[2];
   unsigned long long tot[T_NUM];
   unsigned long long ev[E_NUM];
 };
@@ -133,7 +134,9 @@ void level(hipStream_t s, const Axioms& ax, const Out& o, uint32_t L);
 // after the levels: T_STUCK, and every stuck concept marked dirty for the relaxation
 void check(hipStream_t s, const Axioms& ax, const Out& o);
 // after the levels: the rows of the told cycles' followers from their representatives' rows
-void follow(hipStream_t s, const Axioms& ax, const Out& o);
+// followers of told cycles whose representative's row is final (level < L: built by the levels
+// launched so far; all: every representative, after the relaxation rounds)
+void follow(hipStream_t s, const Axioms& ax, const Out& o, uint32_t L, bool all);
 // one relaxation round over the dirty concepts (told cycles), its grown rows committed;
 // Ctr::dirty = some row grew
 void relax(hipStream_t s, const Axioms& ax, const Out& o);

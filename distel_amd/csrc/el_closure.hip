@@ -750,6 +750,7 @@ __device__ __forceinline__ void for_tasks(uint32_t N, Sel&& sel, Run&& run) {
 constexpr uint32_t SKIP = NONE - 1u;
 // a told cycle's follower: its rows come from its representative's (k_follow), never ready, never stuck
 constexpr uint32_t FOLLOW = NONE - 2u;
+constexpr uint32_t FOLLOWED = NONE - 3u;  // (k_follow wrote its rows)
 __device__ __forceinline__ bool built(const Axioms& ax, uint32_t A) { return A < 2u || (A >= ax.w_lo && A < ax.w_hi); }
 
 __global__ void __launch_bounds__(BLOCK) k_start(Axioms ax, Out o) {
@@ -927,13 +928,28 @@ __global__ void __launch_bounds__(BLOCK) k_check(Axioms ax, Out o) {
 // has told*(m) = told*(r) ∪ {r} \ {m} (the representative's row holds every other member) and
 // the same exr* / exl* rows as r, which it shares (meta points at them).  One wave per follower:
 // m's place in r's sorted row and r's insertion point by binary searches, then a coalesced copy.
-__global__ void __launch_bounds__(BLOCK) k_follow(Axioms ax, Out o) {
+// Runs after every batch of levels (closure_tail): a follower is copied once, when its
+// representative's row is final — the representative was a task of a level already launched
+// (level < L), or `all` after the relaxation rounds — and is then marked FOLLOWED.  (Round 5 ran
+// every follower at every tail: one whose representative sat in a later batch read an empty row
+// (n = 0), reserved 0 slots and still stored the representative at t_val[base] — the first slot
+// of another wave's row, or one past t_cap: the kat_cycle illegal access and a wrong closure.)
+// A representative's row must hold the follower (its component's other members): anything else
+// is a broken condensation and fails the build (ctr->bad) instead of writing.
+__global__ void __launch_bounds__(BLOCK) k_follow(Axioms ax, Out o, uint32_t L, uint32_t all) {
   const uint32_t nw = gridDim.x * WAVES;
   for (uint32_t i = slot_id(); i < ax.nfol; i += nw) {  // (wave-uniform)
-    const uint32_t m = ax.fol[i], r = ax.rep[m];
-    if (!built(ax, m)) continue;
+    const uint32_t m = ax.fol[i];
+    if (m >= ax.N || !built(ax, m) || o.level[m] != FOLLOW) continue;
+    const uint32_t r = ax.rep[m];
+    const uint32_t lr = r < ax.N ? o.level[r] : NONE;
+    if (!all && !(lr < L)) continue;  // (the representative's row is not built yet)
     const uint4 rb = o.meta[2 * r], re = o.meta[2 * r + 1];
     const uint32_t b = rb.x, n = re.x - rb.x;
+    if (r >= m || n == 0 || re.x < rb.x) {
+      if (lane() == 0) atomicOr(&o.ctr->bad, 1u);
+      continue;
+    }
     auto lower = [&](uint32_t v) {
       uint32_t lo = 0, hi = n;
       while (lo < hi) {
@@ -946,6 +962,10 @@ __global__ void __launch_bounds__(BLOCK) k_follow(Axioms ax, Out o) {
       return lo;
     };
     const uint32_t im = lower(m), ir = lower(r);  // (r < m: the representative is the smallest member)
+    if (im >= n || o.t_val[b + im] != m || ir > im) {  // (wave-uniform: every lane read the same row)
+      if (lane() == 0) atomicOr(&o.ctr->bad, 1u);
+      continue;
+    }
     uint32_t base = 0;
     if (lane() == 0) base = atomicAdd(&o.ctr->t_tail, n);
     base = __shfl(base, 0);
@@ -967,6 +987,7 @@ __global__ void __launch_bounds__(BLOCK) k_follow(Axioms ax, Out o) {
       me[2] = re.z;
       mb[3] = rb.w;
       me[3] = re.w;
+      o.level[m] = FOLLOWED;
     }
   }
 }
@@ -1412,9 +1433,10 @@ void check(hipStream_t s, const Axioms& ax, const Out& o) {
   CCHK(hipGetLastError());
 }
 
-void follow(hipStream_t s, const Axioms& ax, const Out& o) {
+void follow(hipStream_t s, const Axioms& ax, const Out& o, uint32_t L, bool all) {
   if (!ax.nfol) return;
-  hipLaunchKernelGGL(k_follow, dim3(std::min<uint32_t>((ax.nfol + WAVES - 1) / WAVES, 2048)), dim3(BLOCK), 0, s, ax, o);
+  hipLaunchKernelGGL(k_follow, dim3(std::min<uint32_t>((ax.nfol + WAVES - 1) / WAVES, 2048)), dim3(BLOCK), 0, s, ax, o, L,
+                     all ? 1u : 0u);
   CCHK(hipGetLastError());
 }
 

@@ -3062,7 +3062,7 @@ struct el_ctx {
   std::chrono::steady_clock::time_point inc_t0;  // (EL_TRACE_INC: el_saturate's start)  // the concept / pair counts the closure buffers were allocated for
   void set_closure_ix();
   void closure_grow();
-  void closure_tail(uint32_t a, uint32_t b, uint32_t L);
+  void closure_tail(uint32_t a, uint32_t b, uint32_t L, bool all);
   void closure_rows(uint32_t a, uint32_t b);
   void closure_state();
   // The logs are indexed by uint32 counters on the device (DCounters): a step whose logs could
@@ -3082,6 +3082,9 @@ struct el_ctx {
   uint8_t* rt_f = nullptr;
   uint64_t rt_ns = 0, rt_nl = 0, rt_scap = 0, rt_lcap = 0;
   bool inc_pending = false;
+  // the masks (dA, dX by concept, dP by pair id) of the increments carried over since the last
+  // saturation: a second el_add_axioms before el_saturate re-triggers what either reaches
+  std::vector<uint8_t> pend_dA, pend_dX, pend_dP;
   double inc_ms[3] = {0, 0, 0};  // the last el_add_axioms: host index build, upload, state migration
   bool trig_override = false;  // superstep(): k_expand reads the rt_* triggers
   void retrigger_step();
@@ -3718,6 +3721,9 @@ void el_ctx::free_state() {
   dfree(rt_f);
   rt_ns = rt_nl = rt_scap = rt_lcap = 0;
   inc_pending = false;
+  pend_dA.clear();
+  pend_dX.clear();
+  pend_dP.clear();
   rs.release();
   rl.release();
   if (dstream) (void)hipStreamSynchronize(dstream);
@@ -3936,6 +3942,13 @@ void el_ctx::reset_state() {
     reset_device(stream);
   }
   bits_logged = true;  // from here on every set bit is in the fact log (the init facts and k_commit append)
+  // an increment carried over into the state this reset discards re-triggers nothing: the next
+  // el_saturate starts from the fresh init facts (round-5 advisor: a stale re-trigger step ran here)
+  inc_pending = false;
+  rt_ns = rt_nl = 0;
+  pend_dA.clear();
+  pend_dX.clear();
+  pend_dP.clear();
   uc_s_n = uc_l_n = ~0ull;
   s_count = l_count = a_count = p_count = s_init = x_count = 0;
   part_fixpoint = false;
@@ -4797,9 +4810,10 @@ void el_ctx::closure_grow() {
 
 // After the Kahn levels launched so far: stuck concepts, totals over [a, b), the scans of the
 // rows' counts, and one readback (counters, the flag of level L, the rows of ⊤).
-void el_ctx::closure_tail(uint32_t a, uint32_t b, uint32_t L) {
+void el_ctx::closure_tail(uint32_t a, uint32_t b, uint32_t L, bool all) {
   HIPCHK(hipMemsetAsync(&cl.ctr->tot[elcl::T_STUCK], 0, sizeof(unsigned long long), stream));
-  if (caxk.nfol) launch(EL_K_CLOSURE, [&] { elcl::follow(stream, caxk, cl); });  // (told cycles' followers)
+  // (told cycles' followers whose representative is final; each once per build)
+  if (caxk.nfol) launch(EL_K_CLOSURE, [&] { elcl::follow(stream, caxk, cl, L, all); });
   elcl::check(stream, caxk, cl);
   elcl::stats(stream, cax, cl, 0, hx.N, use_props);  // (every row: the SC layout spans them)
   HIPCHK(hipMemsetAsync(cl.ctr->tot, 0, elcl::T_STUCK * sizeof(unsigned long long), stream));
@@ -4833,7 +4847,8 @@ void el_ctx::closure_rows(uint32_t a, uint32_t b) {
     for (;;) {
       const uint32_t end = (uint32_t)std::min<uint64_t>((uint64_t)N + 1, (uint64_t)L + level_hint);
       for (; L < end; ++L) launch(EL_K_CLOSURE, [&] { elcl::level(stream, caxk, cl, L); });
-      closure_tail(a, b, L);
+      closure_tail(a, b, L, false);
+      if (clh->ctr.bad) throw ElError{EL_EHIP, "told closure: a told cycle's representative row lacks its follower"};
       if (clh->ctr.ovf) {
         redo = true;
         break;
@@ -4856,7 +4871,11 @@ void el_ctx::closure_rows(uint32_t a, uint32_t b) {
         if (!clh->ctr.dirty) break;
         if (round > (uint64_t)N + 1) throw ElError{EL_EHIP, "told closure: relaxation did not converge"};
       }
-      if (!redo) closure_tail(a, b, L);
+      if (!redo) {
+        closure_tail(a, b, L, true);
+        if (clh->ctr.bad) throw ElError{EL_EHIP, "told closure: a told cycle's representative row lacks its follower"};
+        redo = clh->ctr.ovf != 0;
+      }
     }
     if (!redo) break;
     closure_grow();
@@ -5512,6 +5531,9 @@ void el_ctx::mem_report() const {
 void el_ctx::retrigger_step() {
   if (!inc_pending) return;
   inc_pending = false;
+  pend_dA.clear();
+  pend_dX.clear();
+  pend_dP.clear();
   if (!rt_ns && !rt_nl) return;
   tr_s.push_back(rt_ns);
   tr_l.push_back(rt_nl);
@@ -5532,6 +5554,9 @@ void el_ctx::retrigger_step() {
 void el_ctx::retrigger_all() {
   if (!inc_pending) return;
   inc_pending = false;
+  pend_dA.clear();
+  pend_dX.clear();
+  pend_dP.clear();
   if (s_count) HIPCHK(hipMemsetAsync(slog_f, 0, s_count, stream));
   for (int r = 0; r < EL_NUM_RULE_TYPES; ++r) wm_s[r] = wm_l[r] = wm_a[r] = wm_p[r] = 0;
 }
@@ -5933,7 +5958,18 @@ int el_add_axioms(el_ctx* c, const el_axioms* inc) {
       dP[q] = dR[h.pair_role[q]];
       if (!had[q]) dX[h.pair_y[q]] = 1;
     }
+    // an earlier increment not saturated yet (round-5 advisor): its re-trigger lists are rebuilt
+    // from the logs below, so its masks join this one's (concept ids are stable, its pair ids move
+    // by pmap) — otherwise what only its axioms reach would sit below the watermarks unexpanded
+    if (c->inc_pending) {
+      for (size_t a = 0; a < c->pend_dA.size() && a < dA.size(); ++a) dA[a] |= c->pend_dA[a];
+      for (size_t a = 0; a < c->pend_dX.size() && a < dX.size(); ++a) dX[a] |= c->pend_dX[a];
+      for (size_t p = 0; p < c->pend_dP.size() && p < pmap.size(); ++p) dP[pmap[p]] |= c->pend_dP[p];
+    }
     c->migrate_state(N0, pmap, dA, dX, dP);
+    c->pend_dA = std::move(dA);
+    c->pend_dX = std::move(dX);
+    c->pend_dP = std::move(dP);
     c->inc_ms[2] = ms_since(t2);
     return EL_OK;
   });

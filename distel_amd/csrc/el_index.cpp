@@ -167,10 +167,47 @@ void distel_chain_set(const el_axioms& ax, std::vector<uint32_t>& r, std::vector
       for (uint32_t tt : st.second) r.push_back(rr), s.push_back(ss), t.push_back(tt);
 }
 
+// The invariants k_follow and the condensed Kahn levels index by (round-5 fault: a follower
+// copied before its representative's row existed).  Every id in range; a representative is the
+// smallest member and its own representative; a follower has no condensed rows of its own and is
+// in its representative's told_x row; condensed told edges join representatives or plain
+// concepts only, never a follower, and never a component to itself.
+std::string check_condensation(const HostIndex& o) {
+  const uint32_t N = o.N;
+  char msg[160];
+  auto bad = [&](const char* what, uint32_t a) {
+    snprintf(msg, sizeof msg, "told-cycle condensation: %s (concept %u)", what, a);
+    return std::string(msg);
+  };
+  if (o.scc_rep.size() != N) return bad("representative table size", N);
+  for (const Csr* c : {&o.told_c, &o.toldT_c, &o.exr_c, &o.exl_c, &o.told_x})
+    if (c->ptr.size() != (size_t)N + 1 || c->ptr[N] != c->a.size()) return bad("condensed row table size", N);
+  for (uint32_t a = 0; a < N; ++a) {
+    const uint32_t r = o.scc_rep[a];
+    if (r >= N || r > a || o.scc_rep[r] != r) return bad("representative out of range or not the smallest member", a);
+    const bool fol = r != a;
+    if (fol && (o.told_c.ptr[a + 1] != o.told_c.ptr[a] || o.exr_c.ptr[a + 1] != o.exr_c.ptr[a] ||
+                o.exl_c.ptr[a + 1] != o.exl_c.ptr[a] || o.told_x.ptr[a + 1] != o.told_x.ptr[a]))
+      return bad("a follower has condensed rows", a);
+    if (fol && !std::binary_search(o.told_x.a.begin() + o.told_x.ptr[r], o.told_x.a.begin() + o.told_x.ptr[r + 1], a))
+      return bad("a follower is missing from its representative's members", a);
+    for (uint32_t j = o.told_c.ptr[a]; j < o.told_c.ptr[a + 1]; ++j) {
+      const uint32_t s = o.told_c.a[j];
+      if (s >= N || o.scc_rep[s] != s || s == a) return bad("a condensed told edge leaves the representatives", a);
+    }
+    for (uint32_t j = o.toldT_c.ptr[a]; j < o.toldT_c.ptr[a + 1]; ++j)
+      if (o.toldT_c.a[j] >= N || o.scc_rep[o.toldT_c.a[j]] != o.toldT_c.a[j]) return bad("a condensed sub edge", a);
+  }
+  for (size_t i = 0; i < o.followers.size(); ++i)
+    if (o.followers[i] >= N || o.scc_rep[o.followers[i]] == o.followers[i] || (i && o.followers[i] <= o.followers[i - 1]))
+      return bad("follower list", i < o.followers.size() ? o.followers[i] : 0);
+  return "";
+}
+
 // Strongly connected components of the told graph (iterative Tarjan over A -> told supers) and
 // the condensed rows of HostIndex::scc_rep (see el_index.h).  Leaves everything empty when every
 // component is a single concept.
-void told_sccs(HostIndex& o) {
+std::string told_sccs(HostIndex& o) {
   const uint32_t N = o.N;
   const uint32_t NONE = 0xffffffffu;
   std::vector<uint32_t> idx(N, NONE), low(N, 0), comp(N, NONE), st, cs;
@@ -216,7 +253,7 @@ void told_sccs(HostIndex& o) {
       if (!frames.empty()) low[frames.back().first] = std::min(low[frames.back().first], low[v]);
     }
   }
-  if (!cyclic) return;
+  if (!cyclic) return "";
   o.scc_rep = comp;
   std::vector<std::array<uint32_t, 3>> tc, xc, lc, ex;
   for (uint32_t a = 0; a < N; ++a) {
@@ -236,6 +273,7 @@ void told_sccs(HostIndex& o) {
   o.exr_c = make_csr(N, xc, false);
   o.exl_c = make_csr(N, lc, true);
   o.told_x = make_csr(N, ex, false);
+  return check_condensation(o);
 }
 
 // The bit-matrix column order of a whole-ontology context (see el_index.h).  A subsumer B that
@@ -485,7 +523,7 @@ std::string build_index(const el_axioms& ax_in, HostIndex& o, uint32_t flags) {
       o.sc_w[p] = w;
     }
   }
-  told_sccs(o);
+  if (std::string e = told_sccs(o); !e.empty()) return e;
   column_order(ax, o);
 #undef CHECK
   return "";

@@ -137,3 +137,72 @@ def test_increment_is_a_delta(name, scale, oracle_lib):
     assert 0 < tr_s[0] < before["s_facts"] // 2, (int(tr_s[0]), before["s_facts"])
     assert tr_l[0] < max(before["links"] // 2, 1)
     eng.close()
+
+
+@pytest.mark.parametrize("seed", range(12))
+def test_two_increments_one_saturate(seed, oracle_lib):
+    """Two el_add_axioms before one el_saturate (round-5 advisor, high): the second increment's
+    carry-over must keep what the first one's axioms reach — the re-trigger masks of both are
+    merged — or the facts only the first increment reaches stay below the watermarks."""
+    ax = generators.random_small(100 + seed, n=20 + seed * 3, n_roles=1 + seed % 4)
+    pieces = _split(ax, 3, 100 + seed, grow=bool(seed % 2))
+    eng = engine.Engine(device=0, compat_range=True)
+    eng.load(pieces[0])
+    eng.init()
+    eng.saturate()
+    eng.add_axioms(pieces[1])
+    eng.add_axioms(pieces[2])
+    st = eng.saturate()
+    o = oracle_lib.saturate(ax, 0, compat_range=True)
+    assert np.array_equal(np.stack(eng.facts()), np.stack(o.facts())), "S(X) differs from the union's closure"
+    for g, c in zip(eng.links(), o.links()):
+        assert np.array_equal(g, c), "R(r) differs from the union's closure"
+    assert st["derived"] == o.stats()["derived"]
+    eng.close()
+
+
+def test_two_increments_one_saturate_g3(oracle_lib):
+    from distel_amd import ir
+    ax = generators.workload("g3", 0.03)
+    base, inc = ir.split_increment(ax, 0.02, seed=11)
+    inc1, inc2 = _split(inc, 2, 11, grow=False)
+    eng = engine.Engine(device=0, compat_range=True)
+    eng.load(base)
+    eng.init()
+    eng.saturate()
+    eng.add_axioms(inc1)
+    eng.add_axioms(inc2)
+    st = eng.saturate()
+    o = oracle_lib.saturate(ax, 0, compat_range=True)
+    assert np.array_equal(np.stack(eng.facts()), np.stack(o.facts()))
+    for g, c in zip(eng.links(), o.links()):
+        assert np.array_equal(g, c)
+    assert st["derived"] == o.stats()["derived"]
+    eng.close()
+
+
+def test_increment_then_init_is_a_fresh_run(oracle_lib):
+    """el_add_axioms, then el_init, then el_saturate (round-5 advisor, medium): the re-init drops
+    the carried-over re-trigger lists, so the run equals a fresh load of old ∪ inc — closure,
+    per-superstep deltas and per-kernel event counters alike."""
+    from distel_amd import ir
+    ax = generators.workload("g1", 0.05)
+    base, inc = ir.split_increment(ax, 0.02, seed=4)
+    eng = engine.Engine(device=0, compat_range=True)
+    eng.load(base)
+    eng.init()
+    eng.saturate()
+    eng.add_axioms(inc)
+    eng.init()
+    st = eng.saturate()
+    ref = engine.Engine(device=0, compat_range=True)
+    ref.load(eng.ax)
+    ref.init()
+    st_ref = ref.saturate()
+    assert np.array_equal(np.stack(eng.facts()), np.stack(ref.facts()))
+    assert [np.asarray(t).tolist() for t in eng.trace()] == [np.asarray(t).tolist() for t in ref.trace()]
+    assert st["derived"] == st_ref["derived"] == oracle_lib.saturate(ax, 0, compat_range=True).stats()["derived"]
+    for ke, kr in zip(eng.kernel_stats(), ref.kernel_stats()):  # (el_init zeroes the counters)
+        assert ke["events"] == kr["events"], ke["kernel"]
+    ref.close()
+    eng.close()

@@ -249,36 +249,33 @@ def test_strong_full_size(name, parts):
     _close(engs)
 
 
-def test_g4_half_eight_partitions():
-    """configs[3] (SNOMED×8) at half size on one GPU: ×8 of G3 at 50 % on 8 row partitions aligned
-    with the copies (LOCAL transport: the RCCL protocol in process, one thread per rank).  Size-
-    independent checks: derived = 8 × derived(G3 @ 50 %); every copy's closure, shifted back to copy
-    0's ids, hashes to the whole-ontology closure of G3 @ 50 % (order-independent set digest), which
-    hashes to the oracle's pinned closure of G3 @ 50 % (closure_digests.txt); and
-    the aligned copies exchange only header words (the commit routes nothing: no other rank's
-    window holds a copy's concepts)."""
+def _copies_partitioned(scale: float, copies: int):
+    """×copies of G3 @ scale on `copies` row partitions aligned with the copies (LOCAL transport:
+    the RCCL protocol in process, one thread per rank).  Size-independent checks: derived =
+    copies × derived(G3 @ scale); every copy's closure, shifted back to copy 0's ids, hashes to the
+    whole-ontology closure of G3 @ scale (order-independent set digest), which hashes to the
+    oracle's pinned closure (closure_digests.txt); the aligned copies exchange only header words
+    (no other rank's window holds a copy's concepts); lock-step supersteps."""
     import hashlib
     from distel_amd.result import set_digest
-    base = generators.workload("g3", scale=0.5)
+    base = generators.workload("g3", scale=scale)
     eng, st0 = engine.classify(base, device=0)
     fx, fa = eng.facts()
     lx, lr, ly = eng.links()
     eng.close()
-    # the whole-ontology closure the copies are held to is itself the oracle's (G3 @ 50 % pinned
-    # in closure_digests.txt by tests/golden/make_digests.py --append g3 0.5)
     h = hashlib.sha256()
     for a in (fx, fa, lx, lr, ly):
         h.update(np.ascontiguousarray(a, dtype=np.uint32).tobytes())
-    assert h.hexdigest() == _pinned_closure("g3", 0.5, base)
+    assert h.hexdigest() == _pinned_closure("g3", scale, base)
     k = fx >= 2
     want = set_digest(fx[k], fa[k], *(v[lx >= 2] for v in (lx, lr, ly)))
-    del fx, fa, lx, lr, ly
-    copies = 8
+    del fx, fa, lx, lr, ly, k
     ax = ir.replicate(base, copies)
     bounds = [ir.copy_slice(base, copies, i) for i in range(copies)]
     bounds[0] = (0, bounds[0][1])
     engs, st = engine.classify_partitioned(ax, copies, rows=bounds)
     assert sum(s["derived"] for s in st) == copies * st0["derived"]
+    assert all(s["derived"] == st0["derived"] for s in st)
     assert len({s["supersteps"] for s in st}) == 1
     m, R = base.n_concepts - 2, base.n_roles
     for i, e in enumerate(engs):
@@ -288,6 +285,23 @@ def test_g4_half_eight_partitions():
         k, kl = x >= 2, lx >= 2
         assert set_digest(cshift(x[k]), cshift(a[k]), cshift(lx[kl]), lr[kl].astype(np.int64) - i * R,
                           cshift(ly[kl])) == want, f"copy {i}"
+        del x, a, lx, lr, ly, k, kl
         # per superstep: two header rounds (XH words per rank); nothing else
         assert st[i]["exchange_bytes"] <= st[i]["supersteps"] * 2 * copies * 2 * 16 * 4, st[i]["exchange_bytes"]
     _close(engs)
+    return st0, st
+
+
+def test_g4_half_eight_partitions():
+    """configs[3] (SNOMED×8) at half size on one GPU: ×8 of G3 at 50 % on 8 aligned partitions."""
+    _copies_partitioned(0.5, 8)
+
+
+def test_g4_full_four_partitions():
+    """configs[3] at FULL per-copy size (round-5 verdict #1): ×4 of the whole G3 (OntologyMultiplier
+    semantics, OntologyMultiplier.java:44-83) on 4 aligned partitions in one process — the largest
+    ×k of full G3 one MI355X holds (≈47 GB per partition; ×8 needs 8 GPUs).  Every copy's closure
+    equals the pinned full-G3 closure (closure_digests.txt) and derived = 4 × 136,499,458."""
+    st0, st = _copies_partitioned(1.0, 4)
+    assert st0["derived"] == 136_499_458
+    assert sum(s["derived"] for s in st) == 4 * 136_499_458
