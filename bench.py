@@ -435,6 +435,43 @@ def main():
                             "links the new axioms reach) + el_saturate (first superstep over those lists, then "
                             "semi-naive); no result copy-back"}
 
+    def profile_once(peng, workload, pmc):
+        """One classification of an engine already loaded, in the timed schedule (streamed copy-back
+        armed), with HIP events around every launch on its engine stream: the dominant kernel
+        (largest Σ time; phases sharing a launch add their algorithmic bytes) as `roofline`, and
+        the whole table.  A partitioned engine runs it on every rank together (collectives)."""
+        peng.init()
+        if args.copyback == "stream":
+            peng.stream_result(engine.Stream())  # (not released: the event counters are read after)
+        pst = peng.saturate()
+        if args.copyback == "stream":
+            peng.result_wait()
+        ks = peng.kernel_stats()
+        launches = {}
+        for k in ks:
+            g = launches.setdefault(k["group"], {"kernel": k["group"].split(":")[0], "launches": 0, "ms": 0.0,
+                                                 "bytes": 0})
+            g["bytes"] += k["bytes"]
+            if k["kernel"] == k["group"]:
+                g["launches"], g["ms"] = k["launches"], k["ms"]
+        prof = [g for g in launches.values() if g["launches"] and g["ms"] > 0]
+        dom = max(prof, key=lambda g: g["ms"])
+        per_launch_bytes = dom["bytes"] / dom["launches"]
+        avg_ms = dom["ms"] / dom["launches"]
+        achieved = per_launch_bytes / (avg_ms * 1e-3) / 1e9
+        roof = {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 6),
+                "traffic": pmc_traffic(workload, dom["kernel"]) if pmc else None,
+                "kernel": dom["kernel"], "bytes_per_launch": int(per_launch_bytes),
+                "avg_launch_us": round(avg_ms * 1e3, 3), "launches": dom["launches"],
+                "profiled_ms": round(pst["ms"], 3),
+                "source": "HIP events around every launch on the engine stream of one profiled classification "
+                          "in the timed schedule; the whole table is this line's `kernels` "
+                          "(launches, ms, algorithmic bytes per kernel)"}
+        table = {g["kernel"]: {"launches": g["launches"], "ms": round(g["ms"], 4), "bytes": g["bytes"]}
+                 for g in launches.values() if g["launches"]}
+        return roof, table
+
     def exchange_leg(strong=False):
         """weak: the ×N ontology, rank i owning copy i's rows; strong: the workload itself, the
         rows balanced by told edges (ir.balanced_rows) — one ontology's concept space sharded
@@ -467,6 +504,24 @@ def main():
         leg = timed([xeng], args.steps, args.warmup)
         leg["load_s"] = load_s
         leg["rows"] = rows
+        if not args.no_profile:
+            # per-rank roofline (round-5 verdict #1): one more classification of the partitioned
+            # context with HIP events on, every rank together; the line carries the slowest rank's
+            # dominant kernel (PMC traffic is measured on the N = 1 schedule only: null here)
+            xeng.set_profile(True)
+            roof, table = profile_once(xeng, args.workload, pmc=False)
+            xeng.set_profile(False)
+            allr = D.gather_objects(rk, (roof, table))
+            slow = max(range(len(allr)), key=lambda i: allr[i][0]["profiled_ms"])
+            roof = dict(allr[slow][0])
+            roof["rank"] = slow
+            roof["per_rank"] = [{"rank": i, "kernel": r[0]["kernel"], "frac": r[0]["frac"],
+                                 "avg_launch_us": r[0]["avg_launch_us"], "profiled_ms": r[0]["profiled_ms"]}
+                                for i, r in enumerate(allr)]
+            roof["source"] = ("HIP events around every launch on each rank's engine stream, one profiled "
+                              "classification of the partitioned context in the timed schedule (all ranks "
+                              "together); the slowest rank's dominant kernel; `kernels` is that rank's table")
+            leg["profile"] = {"roofline": roof, "kernels": allr[slow][1]}
         xeng.close()
         return leg
 
@@ -576,43 +631,16 @@ def main():
 
     roofline = None
     kernels = None
-    if rank == 0 and not args.no_profile:
+    head_prof = head.get("profile")
+    if head_prof is not None:  # N > 1: the partitioned leg profiled on every rank, the slowest rank's
+        roofline, kernels = head_prof["roofline"], head_prof["kernels"]
+    elif rank == 0 and not args.no_profile:
         # profiled classification in the timed step's schedule (the streamed copy-back beside the
         # supersteps): HIP events bracket every launch on the engine stream
         peng = engine.Engine(device=dev, profile=True)
         peng.load(ax)
-        peng.init()
-        if args.copyback == "stream":
-            peng.stream_result(engine.Stream())  # (not released: the event counters are read after)
-        pst = peng.saturate()
-        if args.copyback == "stream":
-            peng.result_wait()
-        ks = peng.kernel_stats()
+        roofline, kernels = profile_once(peng, args.workload, pmc=True)
         peng.close()
-        # one row per launch: phases that share a launch (el_kernel_stat.group) add their bytes
-        launches = {}
-        for k in ks:
-            g = launches.setdefault(k["group"], {"kernel": k["group"].split(":")[0], "launches": 0, "ms": 0.0,
-                                                 "bytes": 0})
-            g["bytes"] += k["bytes"]
-            if k["kernel"] == k["group"]:
-                g["launches"], g["ms"] = k["launches"], k["ms"]
-        prof = [g for g in launches.values() if g["launches"] and g["ms"] > 0]
-        dom = max(prof, key=lambda g: g["ms"])
-        per_launch_bytes = dom["bytes"] / dom["launches"]
-        avg_ms = dom["ms"] / dom["launches"]
-        achieved = per_launch_bytes / (avg_ms * 1e-3) / 1e9
-        roofline = {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                    "frac": round(achieved / HBM_PEAK_GBS, 6),
-                    "traffic": pmc_traffic(args.workload, dom["kernel"]),
-                    "kernel": dom["kernel"], "bytes_per_launch": int(per_launch_bytes),
-                    "avg_launch_us": round(avg_ms * 1e3, 3), "launches": dom["launches"],
-                    "profiled_ms": round(pst["ms"], 3),
-                    "source": "HIP events around every launch on the engine stream of one profiled classification "
-                              "in the timed schedule; the whole table is this line's `kernels` "
-                              "(launches, ms, algorithmic bytes per kernel)"}
-        kernels = {g["kernel"]: {"launches": g["launches"], "ms": round(g["ms"], 4), "bytes": g["bytes"]}
-                   for g in launches.values() if g["launches"]}
 
     cpu = None
     if rank == 0 and not args.no_cpu:

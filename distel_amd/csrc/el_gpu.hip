@@ -6143,6 +6143,15 @@ int el_kernel_stats(el_ctx* c, el_kernel_stat* out, int n) {
   });
 }
 
+int el_set_profile(el_ctx* c, int on) {
+  if (!c) return EL_EINVAL;
+  return guarded(c, [&] {
+    c->sync();  // (events of launches already bracketed are read into kms first)
+    c->profile = on ? 1 : 0;
+    return EL_OK;
+  });
+}
+
 int el_superstep_trace(el_ctx* c, uint64_t* ds, uint64_t* dl, uint64_t* da, size_t cap, size_t* n) {
   if (!c || !n) return EL_EINVAL;
   *n = c->tr_s.size();

@@ -95,6 +95,15 @@ def run_weak(rk: Ranks, classify: Callable[[], dict], steps: int, warmup: int,
     return t_max, derived, st
 
 
+def gather_objects(rk: Ranks, obj) -> list:
+    """Every rank's ``obj`` (picklable), in rank order, on every rank."""
+    if rk.dist is None:
+        return [obj]
+    out = [None] * rk.world
+    rk.dist.all_gather_object(out, obj)
+    return out
+
+
 def shutdown(rk: Ranks) -> None:
     if rk.dist is not None and rk.dist.is_initialized():
         rk.dist.destroy_process_group()

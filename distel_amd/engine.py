@@ -112,7 +112,7 @@ _ALLGATHER = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t
 
 EXPORTED_SYMBOLS = [
     "el_abi_version", "el_device_count", "el_create", "el_load", "el_init", "el_step", "el_saturate",
-    "el_get_stats", "el_kernel_stats", "el_superstep_trace", "el_get_subsumers", "el_copy_facts",
+    "el_get_stats", "el_kernel_stats", "el_set_profile", "el_superstep_trace", "el_get_subsumers", "el_copy_facts",
     "el_copy_links", "el_export_result", "el_last_error", "el_destroy", "el_group_create", "el_group_destroy",
     "el_rccl_unique_id", "el_add_axioms", "el_result_info", "el_copy_result", "el_result_wait", "el_pair_table", "el_host_alloc",
     "el_host_free", "el_fresh_fillers", "el_stream_result", "el_pid_table", "el_increment_info",
@@ -144,6 +144,7 @@ def load_library(path: Optional[str] = None) -> C.CDLL:
     lib.el_saturate.argtypes = [P, C.POINTER(_ElStats)]
     lib.el_get_stats.argtypes = [P, C.POINTER(_ElStats)]
     lib.el_kernel_stats.argtypes = [P, C.POINTER(_ElKernelStat), C.c_int]
+    lib.el_set_profile.argtypes = [P, C.c_int]
     lib.el_superstep_trace.argtypes = [P, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64), C.POINTER(C.c_uint64),
                                        C.c_size_t, C.POINTER(C.c_size_t)]
     lib.el_get_subsumers.argtypes = [P, C.c_uint32, _u32p, C.c_size_t, C.POINTER(C.c_size_t)]
@@ -529,6 +530,10 @@ class Engine:
         s = _ElStats()
         self._check(self._lib.el_get_stats(self._ctx, C.byref(s)), "el_get_stats")
         return Stats.from_c(s)
+
+    def set_profile(self, on: bool) -> None:
+        """Per-kernel HIP-event timing from the next launch on (el_set_profile)."""
+        self._check(self._lib.el_set_profile(self._ctx, 1 if on else 0), "el_set_profile")
 
     def kernel_stats(self) -> List[Dict]:
         arr = (_ElKernelStat * NUM_KERNELS)()

@@ -290,6 +290,10 @@ int el_step(el_ctx* ctx, el_rule rule, int* changed);
 int el_saturate(el_ctx* ctx, el_stats* stats);
 int el_get_stats(el_ctx* ctx, el_stats* stats);
 int el_kernel_stats(el_ctx* ctx, el_kernel_stat* out, int n);
+/* Per-kernel HIP-event timing on or off between calls (config.profile at el_create sets the
+   start): a partitioned context whose ranks time their steps unprofiled can profile one more
+   classification, all ranks together, without a new communicator. */
+int el_set_profile(el_ctx* ctx, int on);
 /* per-superstep delta sizes of the last el_saturate (|ΔS|, |Δlink|, |Δact|) */
 int el_superstep_trace(el_ctx* ctx, uint64_t* ds, uint64_t* dl, uint64_t* da, size_t cap, size_t* n);
 
