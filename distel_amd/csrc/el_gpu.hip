@@ -118,9 +118,11 @@ struct DIndex {
   // exl*(A) at [begin, end) of meta below
   const uint32_t* told_b;
   const uint32_t *cidx_ptr, *cidx_c;
-  // per cidx entry j of A: a binary conjunction {A, p} ⊑ B as p | (p sorts before A) << 31 and B
-  // (cidx_p = NONE: another arity, walked through conj_ptr / conj_ops)
-  const uint32_t *cidx_p, *cidx_b;
+  // per cidx entry j of A: a binary conjunction {A, p} ⊑ B as {p | (p sorts before A) << 31, B,
+  // column of p, column of B} (x = NONE: another arity, walked through conj_ptr / conj_ops).  The
+  // columns (col_of at el_load: window and column order applied) let both bit words load at once
+  // instead of the chain entry -> cperm[p] -> word -> cperm[B] -> word (round 6)
+  const uint4* cidx_q;
   const uint32_t *conj_ptr, *conj_ops, *conj_b;
   const uint32_t* exr_pid;
   const uint32_t *exl_r, *exl_b;
@@ -982,24 +984,29 @@ __device__ __forceinline__ void expand_s(const DIndex& ix, const DState& st, Blo
     if (act && (mask & M_R2)) {  // A1..An ∈ S(X), ⊓Ai ⊑ B  =>  B ∈ S(X)
       ev.v[EL_EV_ROW]++;
       for (uint32_t j = m0.y; j < m1.y; ++j) {
-        const uint32_t pp = ix.cidx_p[j];
+        const uint4 cq = ix.cidx_q[j];
         ev.v[EL_EV_ENT]++;
         ev.v[EL_EV_ROW]++;
-        if (pp != NONE) {
-          // binary A ⊓ p ⊑ B from the entry itself: two independent loads instead of the chain
-          // conj id -> operand row -> operands.  Events as the operand walk counts them (the
-          // sorted operands: A's entry is read before p's, or after it only if p ∈ S(X))
-          const uint32_t p = pp & 0x7fffffffu, B = ix.cidx_b[j];
-          const bool p_first = pp >> 31;
+        if (cq.x != NONE) {
+          // binary A ⊓ p ⊑ B from the entry itself: one 16-B load instead of the chain conj id ->
+          // operand row -> operands, and the two bit words (p's and B's) loaded together from
+          // the entry's columns.  Events as the operand walk counts them (the sorted operands:
+          // A's entry is read before p's, or after it only if p ∈ S(X)); B's word is a
+          // speculative load, counted only when the walk would test it
+          const uint32_t B = cq.y;
+          const bool p_first = cq.x >> 31;
+          const uint32_t* row = st.bits + (uint64_t)X * ix.W;
+          const uint32_t wp = cq.z != NONE ? row[cq.z >> 5] : 0u;
+          const uint32_t wb = cq.w != NONE ? row[cq.w >> 5] : 0u;
           ev.v[EL_EV_ENT]++;
           ev.v[EL_EV_TEST]++;
-          const bool ok = test_bit(ix, st.bits, X, p);
+          const bool ok = cq.z != NONE && ((wp >> (cq.z & 31u)) & 1u);
           if (ok || !p_first) ev.v[EL_EV_ENT]++;
           bool nw = false;
           if (ok) {
             ev.v[EL_EV_ENT]++;
             ev.v[EL_EV_TEST]++;
-            nw = !test_bit(ix, st.bits, X, B);
+            nw = !(cq.w != NONE && ((wb >> (cq.w & 31u)) & 1u));
           }
           emit_s(st, q, nw, X, B, ev);
           continue;
@@ -3422,20 +3429,6 @@ std::string el_ctx::install_index(el::HostIndex&& hnew) {
   d.kind = up8(h.kind);
   d.cidx_ptr = up32(h.cidx.ptr);
   d.cidx_c = up32(h.cidx.a);
-  {
-    std::vector<uint32_t> cp(h.cidx.a.size(), NONE), cb(h.cidx.a.size(), 0);
-    for (uint32_t a = 0; a < h.N; ++a)
-      for (uint32_t j = h.cidx.ptr[a]; j < h.cidx.ptr[a + 1]; ++j) {
-        const uint32_t c = h.cidx.a[j], o0 = h.conj.ptr[c];
-        cb[j] = h.conj_b[c];
-        if (h.conj.ptr[c + 1] - o0 != 2 || h.N > 0x7fffffffu) continue;
-        const uint32_t u = h.conj.a[o0], v = h.conj.a[o0 + 1];  // (sorted, distinct)
-        if (u != a && v != a) continue;
-        cp[j] = a == u ? v : u | 0x80000000u;
-      }
-    d.cidx_p = up32(cp);
-    d.cidx_b = up32(cb);
-  }
   d.conj_ptr = up32(h.conj.ptr);
   d.conj_ops = up32(h.conj.a);
   d.conj_b = up32(h.conj_b);
@@ -3568,11 +3561,34 @@ std::string el_ctx::install_index(el::HostIndex&& hnew) {
   // whole ontology's, or a partition's over its own column window
   static const bool col_order = !getenv("EL_COLUMN_ORDER") || getenv("EL_COLUMN_ORDER")[0] != '0';
   d.cperm = nullptr;
+  std::vector<uint32_t> perm;
   if (col_order && !part() && h.cperm.size() == h.N && ix.c_lo == 2u)
-    d.cperm = up32(h.cperm);
+    perm = h.cperm;
   else if (col_order && part() && h.cscore.size() == h.N && ix.c_hi > ix.c_lo)
-    d.cperm = up32(el::column_perm(h, ix.c_lo, ix.c_hi));
+    perm = el::column_perm(h, ix.c_lo, ix.c_hi);
+  if (!perm.empty()) d.cperm = up32(perm);
   cax.cperm = caxk.cperm = d.cperm;
+  {  // binary conjunctions per cidx entry, with the bit columns of p and B (DIndex::cidx_q)
+    auto col = [&](uint32_t a) -> uint32_t {  // (col_of on the host)
+      if (a < 2u) return a;
+      if (a < ix.c_lo || a >= ix.c_hi) return NONE;
+      return d.cperm ? perm[a] : a - ix.c_lo + 2u;
+    };
+    std::vector<uint4> cq(std::max<size_t>(h.cidx.a.size(), 1), make_uint4(NONE, 0u, NONE, NONE));
+    for (uint32_t a = 0; a < h.N; ++a)
+      for (uint32_t j = h.cidx.ptr[a]; j < h.cidx.ptr[a + 1]; ++j) {
+        const uint32_t c = h.cidx.a[j], o0 = h.conj.ptr[c];
+        cq[j].y = h.conj_b[c];
+        if (h.conj.ptr[c + 1] - o0 != 2 || h.N > 0x7fffffffu) continue;
+        const uint32_t u = h.conj.a[o0], v = h.conj.a[o0 + 1];  // (sorted, distinct)
+        if (u != a && v != a) continue;
+        const uint32_t p = a == u ? v : u;
+        cq[j] = make_uint4(a == u ? v : u | 0x80000000u, h.conj_b[c], col(p), col(h.conj_b[c]));
+      }
+    uint4* pq = dupload(cq);
+    index_bufs.push_back(pq);
+    d.cidx_q = pq;
+  }
   d.part = part() ? 1u : 0u;
   d.xwin = nullptr;  // (the windows of the other ranks: exchange_windows, at the first el_saturate)
   d.nranks = part() ? part_count : 1u;
