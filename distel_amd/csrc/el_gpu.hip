@@ -902,6 +902,109 @@ __device__ __forceinline__ void wave_rows4(uint32_t b, uint32_t e, First&& first
   }
 }
 
+// wave_rows NR rounds at a time: f(valid[NR], own[NR], j[NR]) gets NR rounds of entries (every
+// lane, every call) and runs their chains in lockstep, NR dependent loads in flight per step.
+#ifndef EL_XR
+#define EL_XR 2  // (4: 106 VGPRs, 4 waves per SIMD, slower; 2: 87 VGPRs, 5 waves — G3 A/B, round 6)
+#endif
+constexpr uint32_t XR = EL_XR;
+template <uint32_t NR, class F>
+__device__ __forceinline__ void wave_rows_x(uint32_t b, uint32_t e, F&& f) {
+  const uint32_t lane = lane_id(), len = e - b;
+  uint32_t inc = len;
+#pragma unroll
+  for (uint32_t o = 1; o < 64; o <<= 1) {
+    const uint32_t v = __shfl_up(inc, o);
+    if (lane >= o) inc += v;
+  }
+  const uint32_t total = __shfl(inc, 63), excl = inc - len;
+  for (uint32_t base = 0; base < total; base += NR * 64) {  // (wave-uniform)
+    uint32_t own[NR], j[NR];
+    bool valid[NR];
+#pragma unroll
+    for (uint32_t r = 0; r < NR; ++r) {
+      const uint32_t k = base + r * 64 + lane;
+      uint32_t ow = 0;
+#pragma unroll
+      for (uint32_t step = 32; step > 0; step >>= 1)
+        if (__shfl(inc, (int)(ow + step - 1)) <= k) ow += step;
+      valid[r] = k < total;
+      own[r] = valid[r] ? ow : 0u;
+      j[r] = __shfl(b, (int)own[r]) + (k - __shfl(excl, (int)own[r]));
+    }
+    f(valid, own, j);
+  }
+}
+
+// NR binary searches of sorted a[lo, hi) for v in lockstep (one probe of each per step: NR
+// loads in flight); the probe sequence of each is base_has's, so are its events (one entry per probe)
+template <uint32_t NR>
+__device__ __forceinline__ void bsearch_x(const uint32_t* a, uint32_t (&lo)[NR], uint32_t (&hi)[NR],
+                                          const uint32_t (&v)[NR], bool (&found)[NR], Ev& ev) {
+  bool any = false;
+#pragma unroll
+  for (uint32_t r = 0; r < NR; ++r) any |= lo[r] < hi[r];
+  while (any) {
+    uint32_t mid[NR], x[NR];
+#pragma unroll
+    for (uint32_t r = 0; r < NR; ++r) {
+      mid[r] = (lo[r] + hi[r]) >> 1;
+      x[r] = lo[r] < hi[r] ? a[mid[r]] : 0u;
+    }
+    any = false;
+#pragma unroll
+    for (uint32_t r = 0; r < NR; ++r) {
+      if (lo[r] < hi[r]) {
+        ev.v[EL_EV_ENT]++;
+        if (x[r] == v[r]) {
+          found[r] = true;
+          lo[r] = hi[r];
+        } else if (x[r] < v[r]) {
+          lo[r] = mid[r] + 1;
+        } else {
+          hi[r] = mid[r];
+        }
+      }
+      any |= lo[r] < hi[r];
+    }
+  }
+}
+
+// NR open-addressing probes in lockstep (hash_contains each)
+template <uint32_t NR>
+__device__ __forceinline__ void hash_contains_x(const unsigned long long* t, unsigned long long mask,
+                                                const unsigned long long (&key)[NR], const bool (&ask)[NR],
+                                                bool (&found)[NR]) {
+  unsigned long long h[NR];
+  bool pend[NR], any = false;
+#pragma unroll
+  for (uint32_t r = 0; r < NR; ++r) {
+    pend[r] = ask[r];
+    found[r] = false;
+    h[r] = mix64(key[r]) & mask;
+    any |= pend[r];
+  }
+  while (any) {
+    unsigned long long k[NR];
+#pragma unroll
+    for (uint32_t r = 0; r < NR; ++r) k[r] = pend[r] ? t[h[r]] : EMPTY_KEY;
+    any = false;
+#pragma unroll
+    for (uint32_t r = 0; r < NR; ++r) {
+      if (!pend[r]) continue;
+      if (k[r] == key[r]) {
+        found[r] = true;
+        pend[r] = false;
+      } else if (k[r] == EMPTY_KEY) {
+        pend[r] = false;
+      } else {
+        h[r] = (h[r] + 1) & mask;
+        any = true;
+      }
+    }
+  }
+}
+
 // the bit word holding (x, b)'s bit, and the bit (NONE-column: no word, bit 32 = never set)
 __device__ __forceinline__ uint32_t bit_word(const DIndex& ix, const uint32_t* bits, uint32_t x, uint32_t b) {
   const uint32_t c = col_of(ix, b);
@@ -1041,16 +1144,46 @@ __device__ __forceinline__ void expand_s(const DIndex& ix, const DState& st, Blo
       // (an init fact's own links are the base links, already in place)
       const bool on = star && (mask & M_R3) && !(ix.base && f == 2);
       if (on) ev.v[EL_EV_ROW]++;
-      wave_rows(on ? m0.z : 0u, on ? m1.z : 0u, [&](bool v, uint32_t own, uint32_t j) {
-        const uint32_t Xo = __shfl(X, (int)own);
-        uint32_t pid = 0;
-        bool nw = false;
-        if (v) {
-          pid = ix.exr_pid[j];
-          ev.v[EL_EV_ENT]++;
-          nw = !link_known(ix, st, Xo, pid, mask & M_LEMPTY, ev);
+      // X's own exr* row (the base links {(X, p) : p ∈ exr*(X)}), read once per trigger
+      uint32_t xb = 0, xe = 0;
+      if (on && ix.base) {
+        xb = ix.meta[2 * X].z;
+        xe = ix.meta[2 * X + 1].z;
+      }
+      const bool lempty = mask & M_LEMPTY;
+      // XR rounds of entries at a time, their chains (entry -> base-link search -> set probe) in
+      // lockstep: XR dependent loads in flight per lane instead of one (round 6)
+      wave_rows_x<XR>(on ? m0.z : 0u, on ? m1.z : 0u, [&](const bool (&v)[XR], const uint32_t (&own)[XR],
+                                                          const uint32_t (&j)[XR]) {
+        uint32_t Xo[XR], pid[XR], lo[XR], hi[XR];
+        bool known[XR], ask[XR], found[XR];
+        unsigned long long key[XR];
+#pragma unroll
+        for (uint32_t k = 0; k < XR; ++k) {
+          Xo[k] = __shfl(X, (int)own[k]);
+          lo[k] = __shfl(xb, (int)own[k]);
+          hi[k] = __shfl(xe, (int)own[k]);
         }
-        emit_l(st, q, nw, Xo, pid, ev);
+#pragma unroll
+        for (uint32_t k = 0; k < XR; ++k) {
+          pid[k] = v[k] ? ix.exr_pid[j[k]] : 0u;
+          known[k] = false;
+          if (v[k]) ev.v[EL_EV_ENT]++;
+          if (v[k] && ix.base)
+            ev.v[EL_EV_ROW]++;  // (base_has: the row lookup)
+          else
+            lo[k] = hi[k];
+        }
+        bsearch_x<XR>(ix.exr_pid, lo, hi, pid, known, ev);
+#pragma unroll
+        for (uint32_t k = 0; k < XR; ++k) {
+          ask[k] = v[k] && !known[k] && !lempty;
+          if (ask[k]) ev.v[EL_EV_HASH]++;
+          key[k] = link_key(pid[k], Xo[k]);
+        }
+        hash_contains_x<XR>(st.lhash, st.lmask, key, ask, found);
+#pragma unroll
+        for (uint32_t k = 0; k < XR; ++k) emit_l(st, q, v[k] && !known[k] && !found[k], Xo[k], pid[k], ev);
       });
     }
     {  // A ∈ S(Y=X) new, ∃r.A ⊑ B  =>  propagation ((r, Y), B)
@@ -1072,28 +1205,88 @@ __device__ __forceinline__ void expand_s(const DIndex& ix, const DState& st, Blo
           on = false;
         }
       }
-      wave_rows(on ? m0.w : 0u, on ? m1.w : 0u, [&](bool v, uint32_t own, uint32_t j) {
-        const uint32_t Yo = __shfl(X, (int)own);
-        const uint32_t pb0 = __shfl(fpb, (int)own), pe0 = __shfl(fpe, (int)own);
-        uint32_t pid = NONE, B = 0, pb = 0, pl = 0;
-        bool fresh = false;
-        if (v) {
-          const uint32_t r = ix.exl_r[j];
-          B = ix.exl_b[j];
-          ev.v[EL_EV_ENT] += 2;
-          pid = pair_scan(ix, r, pb0, pe0, ev);
-          if (pid != NONE) {
-            fresh = !prop_known(ix, st, pid, B, mask & M_PEMPTY, ev);
-            if (fresh && (mask & M_R4D)) {  // fused mode: B reaches today's predecessors now
+      // Y's first PR_REG pair roles in registers, loaded once per trigger (round 6): an entry's
+      // pair lookup is then a comparison against its owner's roles (shuffled) instead of a loop
+      // of dependent pair_role loads per entry; longer ranges keep the loop.  Events as the
+      // loop counts them: one pair-row lookup, and the roles read up to the first >= r.
+      constexpr uint32_t PR_REG = 4;
+      uint32_t prr[PR_REG];
+#pragma unroll
+      for (uint32_t k = 0; k < PR_REG; ++k) prr[k] = on && fpb + k < fpe ? ix.pair_role[fpb + k] : NONE;
+      const bool pempty = mask & M_PEMPTY;
+      // XR rounds in lockstep, as CR3 above: entry -> pair -> base-propagation search -> set
+      // probe -> predecessor row (fused fan-out)
+      wave_rows_x<XR>(on ? m0.w : 0u, on ? m1.w : 0u, [&](const bool (&v)[XR], const uint32_t (&own)[XR],
+                                                          const uint32_t (&j)[XR]) {
+        uint32_t pid[XR], B[XR], rr[XR], lo[XR], hi[XR], pb[XR], pl[XR];
+        bool known[XR], ask[XR], found[XR];
+        unsigned long long key[XR];
+#pragma unroll
+        for (uint32_t k = 0; k < XR; ++k) {
+          rr[k] = v[k] ? ix.exl_r[j[k]] : 0u;
+          B[k] = v[k] ? ix.exl_b[j[k]] : 0u;
+          if (v[k]) ev.v[EL_EV_ENT] += 2;
+        }
+#pragma unroll
+        for (uint32_t k = 0; k < XR; ++k) {
+          const uint32_t pb0 = __shfl(fpb, (int)own[k]), pe0 = __shfl(fpe, (int)own[k]);
+          uint32_t ro[PR_REG];
+#pragma unroll
+          for (uint32_t i = 0; i < PR_REG; ++i) ro[i] = __shfl(prr[i], (int)own[k]);
+          pid[k] = NONE;
+          if (v[k]) {
+            const uint32_t K = pe0 - pb0, r = rr[k];
+            if (K <= PR_REG) {
+              uint32_t idx = 0;
+#pragma unroll
+              for (uint32_t i = 0; i < PR_REG; ++i) idx += (i < K && ro[i] < r) ? 1u : 0u;
               ev.v[EL_EV_ROW]++;
-              const uint2 row = gap_row(st.pr, pid);
-              pb = row.x;
-              pl = row.y;
+              ev.v[EL_EV_ENT] += idx < K ? idx + 1 : K;
+              bool hit = false;
+#pragma unroll
+              for (uint32_t i = 0; i < PR_REG; ++i) hit |= i == idx && i < K && ro[i] == r;
+              pid[k] = hit ? pb0 + idx : NONE;
+            } else {
+              pid[k] = pair_scan(ix, r, pb0, pe0, ev);
             }
           }
         }
-        emit_p(st, fresh, pid, B, ev);
-        emit_job(st, q, pl > 0, (mask & M_LEMPTY) ? JOB_PRED_U : JOB_PRED_S, pb, pl, 0, B, ev);
+        // prop_known: a base propagation (binary search of bpp(pid), B ascending), else the set
+#pragma unroll
+        for (uint32_t k = 0; k < XR; ++k) {
+          known[k] = false;
+          lo[k] = hi[k] = 0;
+          if (pid[k] != NONE && ix.base) {
+            ev.v[EL_EV_ROW]++;
+            lo[k] = ix.bpp_s[pid[k]];
+            hi[k] = ix.bpp_e[pid[k]];
+          }
+        }
+        bsearch_x<XR>(st.plog_b, lo, hi, B, known, ev);
+#pragma unroll
+        for (uint32_t k = 0; k < XR; ++k) {
+          ask[k] = pid[k] != NONE && !known[k] && !pempty;
+          if (ask[k]) ev.v[EL_EV_HASH]++;
+          key[k] = link_key(pid[k], B[k]);
+        }
+        hash_contains_x<XR>(st.phash, st.pmask, key, ask, found);
+#pragma unroll
+        for (uint32_t k = 0; k < XR; ++k) {
+          const bool fresh = pid[k] != NONE && !known[k] && !found[k];
+          pb[k] = pl[k] = 0;
+          if (fresh && (mask & M_R4D)) {  // fused mode: B reaches today's predecessors now
+            ev.v[EL_EV_ROW]++;
+            const uint2 row = gap_row(st.pr, pid[k]);
+            pb[k] = row.x;
+            pl[k] = row.y;
+          }
+          found[k] = fresh;
+        }
+#pragma unroll
+        for (uint32_t k = 0; k < XR; ++k) {
+          emit_p(st, found[k], pid[k], B[k], ev);
+          emit_job(st, q, pl[k] > 0, (mask & M_LEMPTY) ? JOB_PRED_U : JOB_PRED_S, pb[k], pl[k], 0, B[k], ev);
+        }
       });
     }
     if (act && (mask & M_RBOT) && ix.has_bot && A == EL_BOTTOM) {  // ⊥ ∈ S(Y=X) new, (X', Y) ∈ R(*)  =>  ⊥ ∈ S(X')
@@ -1304,6 +1497,8 @@ __global__ void k_jobs(DIndex ix, DState st, uint32_t mask) {
       ev.v[EL_EV_JOB]++;
     }
     const uint32_t type = jb.y >> 28;
+    // the column of a JOB_PRED_S's B, once per job (every entry tests the same column)
+    const uint32_t jcol = (lane < tpw && j < njobs && type == JOB_PRED_S) ? col_of(ix, jb.w) : NONE;
     // (four rounds of entries at a time: the list entry, then the bit word a JOB_PRED_S tests)
     wave_rows4(
         jb.x, jb.x + len,
@@ -1312,11 +1507,12 @@ __global__ void k_jobs(DIndex ix, DState st, uint32_t mask) {
           return v ? ((t == JOB_R6A) ? st.sc.val[k] : st.pr.val[k]) : 0u;
         },
         [&](bool v, uint32_t own, uint32_t val) {
-          const uint32_t t = __shfl(type, (int)own), b = __shfl(jb.w, (int)own);
-          return (v && t == JOB_PRED_S) ? bit_word(ix, st.bits, val, b) : 0u;
+          const uint32_t c = __shfl(jcol, (int)own);
+          return (v && c != NONE) ? st.bits[(uint64_t)val * ix.W + (c >> 5)] : 0u;
         },
         [&](bool v, uint32_t own, uint32_t val, uint32_t word) {
       const uint32_t t = __shfl(type, (int)own), a = __shfl(jb.z, (int)own), b = __shfl(jb.w, (int)own);
+      const uint32_t jc = __shfl(jcol, (int)own);
       const uint4 e = make_uint4(val, t, a, b);
       if (t == JOB_PRED_S || t == JOB_PRED_U) {  // preds(pid) × {B}
         uint32_t xp = 0;
@@ -1327,7 +1523,7 @@ __global__ void k_jobs(DIndex ix, DState st, uint32_t mask) {
           nw = true;
           if (t == JOB_PRED_S) {
             ev.v[EL_EV_TEST]++;
-            nw = !bit_in(ix, word, b);
+            nw = !(jc != NONE && ((word >> (jc & 31u)) & 1u));
           }
         }
         emit_s(st, q, nw, xp, b, ev);
@@ -1846,7 +2042,11 @@ __device__ __forceinline__ void expand_x(const DIndex& ix, const DState& st, Blo
   q_flush(q, st);
   ev_flush(st.ev, EL_K_EXPAND_L, ev);
 }
+#ifdef EL_EXPAND_WAVES  // (A/B builds: a VGPR budget for more waves per SIMD)
+__global__ void __attribute__((amdgpu_waves_per_eu(EL_EXPAND_WAVES, 8))) k_expand(DIndex ix, DState st, ExpandArgs a) {
+#else
 __global__ void k_expand(DIndex ix, DState st, ExpandArgs a) {
+#endif
   __shared__ BlockQ q;
   q_init(q);
   uint32_t b = blockIdx.x;
