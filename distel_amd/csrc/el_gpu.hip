@@ -108,6 +108,16 @@ struct ElError {
                     std::string(#expr) + ": " + hipGetErrorString(e_)};               \
   } while (0)
 
+// (EL_TRACE_INIT: host wall time since el_init's entry at each phase's end, on stderr; no syncs
+// are added, so it shows where el_init's host side spends its time)
+thread_local std::chrono::steady_clock::time_point init_t0;
+void init_lap(const char* what) {
+  static const bool trace = getenv("EL_TRACE_INIT") != nullptr;
+  if (trace)
+    fprintf(stderr, "init %-16s %8.3f ms\n", what,
+            std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - init_t0).count());
+}
+
 // ---------------------------------------------------------------- device views
 
 struct DIndex {
@@ -580,8 +590,9 @@ struct WaveQ {
   uint32_t sx[WQ], sa[WQ];  // S candidates
   uint32_t tx[WQ], ta[WQ];  // CR1 told-closure candidates
   uint32_t lx[WQ], lp[WQ];  // link candidates
+  uint32_t px[WQ], pb[WQ];  // CR4 propagation candidates (pid, B)
   uint4 jb[WQJ];            // fan-out jobs
-  uint32_t ns, nt, nl, nj;
+  uint32_t ns, nt, nl, nj, np;
   uint32_t rs_base, rs_left, rs_next;  // S queue: this wave's reserved slots, next reservation size
 };
 struct BlockQ {
@@ -592,7 +603,7 @@ __device__ __forceinline__ WaveQ& wave_q(BlockQ& q) { return q.w[threadIdx.x >> 
 
 __device__ __forceinline__ void q_init(BlockQ& q) {
   WaveQ& w = wave_q(q);
-  if (lane_id() == 0) w.ns = w.nt = w.nl = w.nj = w.rs_left = w.rs_next = 0;
+  if (lane_id() == 0) w.ns = w.nt = w.nl = w.nj = w.np = w.rs_left = w.rs_next = 0;
   for (uint32_t i = lane_id(); i < DEDUP_SLOTS; i += 64) w.seen[i] = ~0ull;
   __syncthreads();
 }
@@ -766,16 +777,13 @@ __device__ __forceinline__ void emit_a(const DState& st, bool pred, uint32_t y, 
   }
 }
 
-// CR4 propagations: a few per S-fact at most, plain wave-aggregated global append
-__device__ __forceinline__ void emit_p(const DState& st, bool pred, uint32_t pid, uint32_t b, Ev& ev) {
-  uint32_t slot = wave_append(&st.ctr->cand_p, pred);
-  if (pred) {
-    ev.v[EL_EV_EMIT]++;
-    if (slot < st.cp_cap) {
-      st.cp_p[slot] = pid;
-      st.cp_b[slot] = b;
-    }
-  }
+// CR4 propagations, staged in the wave's queue like the links (round 6: a wave-aggregated global
+// append per wave-instruction put every emitting round of the CR4 half-1 walk on one counter —
+// same-address atomics serialise at ~12 ns)
+__device__ __forceinline__ void emit_p(const DState& st, BlockQ& q, bool pred, uint32_t pid, uint32_t b, Ev& ev) {
+  WaveQ& w = wave_q(q);
+  if (pred) ev.v[EL_EV_EMIT]++;
+  wq_push(w.px, w.pb, w.np, pred, pid, b, &st.ctr->cand_p, st.cp_p, st.cp_b, st.cp_cap);
 }
 
 // Publish what this wave still has staged (every lane of the block calls it at the end
@@ -793,8 +801,9 @@ __device__ void q_flush(BlockQ& q, const DState& st) {
   }
   wq_publish(w.tx, w.ta, w.nt, &st.ctr->cand_t, st.ct_x, st.ct_a, st.ct_cap);
   wq_publish(w.lx, w.lp, w.nl, &st.ctr->cand_l, st.cl_x, st.cl_p, st.cl_cap);
+  wq_publish(w.px, w.pb, w.np, &st.ctr->cand_p, st.cp_p, st.cp_b, st.cp_cap);
   wq_publish<uint4>(w.jb, nullptr, w.nj, &st.ctr->jobs, st.jobs, nullptr, st.job_cap);
-  if (lane_id() == 0) w.ns = w.nt = w.nl = w.nj = 0;
+  if (lane_id() == 0) w.ns = w.nt = w.nl = w.nj = w.np = 0;
 }
 
 // The wave queues publish themselves when full: nothing to do between loop rounds.
@@ -1284,7 +1293,7 @@ __device__ __forceinline__ void expand_s(const DIndex& ix, const DState& st, Blo
         }
 #pragma unroll
         for (uint32_t k = 0; k < XR; ++k) {
-          emit_p(st, found[k], pid[k], B[k], ev);
+          emit_p(st, q, found[k], pid[k], B[k], ev);
           emit_job(st, q, pl[k] > 0, (mask & M_LEMPTY) ? JOB_PRED_U : JOB_PRED_S, pb[k], pl[k], 0, B[k], ev);
         }
       });
@@ -1296,7 +1305,7 @@ __device__ __forceinline__ void expand_s(const DIndex& ix, const DState& st, Blo
         if (ix.part) {  // partitioned: ⊥ rides the propagation set ((r, Y), ⊥) to every rank
           ev.v[EL_EV_HASH]++;
           const bool fresh = !hash_contains(st.phash, st.pmask, link_key(p, EL_BOTTOM));
-          emit_p(st, fresh, p, EL_BOTTOM, ev);
+          emit_p(st, q, fresh, p, EL_BOTTOM, ev);
           if (!fresh || !(mask & M_R4D)) continue;
           // fused: this rank's own predecessors now (the other ranks' after the import)
         }
@@ -5063,7 +5072,9 @@ void el_ctx::closure_rows(uint32_t a, uint32_t b) {
     for (;;) {
       const uint32_t end = (uint32_t)std::min<uint64_t>((uint64_t)N + 1, (uint64_t)L + level_hint);
       for (; L < end; ++L) launch(EL_K_CLOSURE, [&] { elcl::level(stream, caxk, cl, L); });
+      init_lap("levels enqueued");
       closure_tail(a, b, L, false);
+      init_lap("closure tail read");
       if (clh->ctr.bad) throw ElError{EL_EHIP, "told closure: a told cycle's representative row lacks its follower"};
       if (clh->ctr.ovf) {
         redo = true;
@@ -5190,6 +5201,7 @@ void el_ctx::closure_state() {
     }
   }
   set_closure_ix();
+  init_lap("state sized");
   // ---- the init facts: a random-access kernel (a bit per fact) beside the base links and the
   // layouts below (streaming work), on rstream unless profiled; they touch disjoint buffers and the
   // engine stream joins at the end of closure_state
@@ -6203,9 +6215,16 @@ int el_init(el_ctx* c) {
   if (!c) return EL_EINVAL;
   if (!c->loaded) return fail(c, EL_ESTATE, "el_init before el_load");
   return guarded(c, [&] {
+    // (EL_TRACE_INIT: host wall time at each phase's end, no syncs added: where el_init's host
+    // side spends its time)
+    init_t0 = std::chrono::steady_clock::now();
+    auto lap = init_lap;
     c->reset_state();
+    lap("reset");
     c->closure_rows(c->lo, c->hi);  // told*, exr*, exl* of every concept (el_closure.h)
+    lap("closure rows");
     c->closure_state();             // the init facts; base links / propagations, row layouts
+    lap("state enqueued");
     c->fresh = true;
     c->inited = true;
     c->stats_stale = true;
