@@ -58,6 +58,14 @@ struct Axioms {
   const uint32_t *tx_ptr = nullptr, *tx = nullptr;      // representative -> the other members
   const uint32_t* fol = nullptr;                        // the followers (non-representative members)
   uint32_t nfol = 0;
+  // Static Kahn levels (round 6): a concept's level is a property of the told axioms (and of the
+  // built window), computed once at el_load (el_ctx::static_levels): level(A) = 0 without told
+  // supers, 1 for a cycle's representative without outside supers, else 1 + the largest level
+  // of its supers; SKIP / FOLLOW / NONE (never ready) as k_start marks them.  With them the
+  // level launches read their concepts off a list (no scan of 3N tasks per level, no pending-count
+  // atomics) and get grids sized to the level.  Null: the dynamic levels.
+  const uint32_t* slevel = nullptr;                     // concept -> static level
+  const uint32_t* lvl_ids = nullptr;                    // the concepts of levels >= 1, by level
 };
 
 // per-node statistics (Out::nd + k * N)
@@ -118,6 +126,8 @@ struct Out {
 constexpr uint32_t GRID = EL_CLOSURE_GRID;  // 4 blocks per CU (k_level: 121 VGPRs, 4 waves per SIMD)
 constexpr uint32_t BLOCK = 256;
 constexpr uint32_t SLOTS = GRID * (BLOCK / 64);
+// level marks (Out::level, Axioms::slevel)
+constexpr uint32_t LVL_NONE = 0xffffffffu, LVL_SKIP = LVL_NONE - 1u, LVL_FOLLOW = LVL_NONE - 2u;
 constexpr uint32_t RSV_WORDS = 6 * SLOTS;
 // per-wave row reservation (entries): a row array holds its rows plus at most one partly used
 // chunk per wave slot
@@ -131,6 +141,8 @@ void start(hipStream_t s, const Axioms& ax, const Out& o);
 // one level (reads its concepts off level[]; sets the next level's flag): the three row types
 // of each of its concepts are independent tasks spread over all waves
 void level(hipStream_t s, const Axioms& ax, const Out& o, uint32_t L);
+// one static level L >= 1: its n concepts at ax.lvl_ids[first, first + n)
+void level_list(hipStream_t s, const Axioms& ax, const Out& o, uint32_t L, uint32_t first, uint32_t n);
 // after the levels: T_STUCK, and every stuck concept marked dirty for the relaxation
 void check(hipStream_t s, const Axioms& ax, const Out& o);
 // after the levels: the rows of the told cycles' followers from their representatives' rows

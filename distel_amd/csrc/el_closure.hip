@@ -748,8 +748,10 @@ __device__ __forceinline__ void for_tasks(uint32_t N, Sel&& sel, Run&& run) {
 
 // a concept outside the built set (Axioms::w_lo/w_hi): never ready, never stuck
 constexpr uint32_t SKIP = NONE - 1u;
+static_assert(SKIP == LVL_SKIP, "level marks");
 // a told cycle's follower: its rows come from its representative's (k_follow), never ready, never stuck
 constexpr uint32_t FOLLOW = NONE - 2u;
+static_assert(FOLLOW == LVL_FOLLOW, "level marks");
 constexpr uint32_t FOLLOWED = NONE - 3u;  // (k_follow wrote its rows)
 __device__ __forceinline__ bool built(const Axioms& ax, uint32_t A) { return A < 2u || (A >= ax.w_lo && A < ax.w_hi); }
 
@@ -764,8 +766,8 @@ __global__ void __launch_bounds__(BLOCK) k_start(Axioms ax, Out o) {
     // level-1 task (level 0 copies own axiom lists only)
     const bool fol = ax.rep && ax.rep[A] != A;
     const bool xt = ax.tx_ptr && ax.tx_ptr[A + 1] > ax.tx_ptr[A];
-    o.indeg[A] = fol ? 0u : d;
-    o.level[A] = !in ? SKIP : fol ? FOLLOW : d ? NONE : xt ? 1u : 0u;
+    o.indeg[A] = fol || ax.slevel ? 0u : d;
+    o.level[A] = ax.slevel ? ax.slevel[A] : !in ? SKIP : fol ? FOLLOW : d ? NONE : xt ? 1u : 0u;
     root |= in && !fol && d == 0 && !xt;
     root1 |= in && !fol && d == 0 && xt;
     o.meta[2 * A] = make_uint4(0u, ax.cidx_ptr[A], 0u, 0u);
@@ -832,6 +834,39 @@ __global__ void __launch_bounds__(BLOCK) k_level(Axioms ax, Out o, uint32_t L) {
   if (threadIdx.x == 0 && sany) o.lvl_flag[L + 1] = 1;
 }
 
+// One static level L (Axioms::slevel): the 3n tasks of its n concepts ids[0, n) spread over the
+// launch's waves as in k_level, read off the list instead of a scan of every concept's level; no
+// pending counts (every super is in an earlier level, done by an earlier launch).
+__global__ void __launch_bounds__(BLOCK) k_level_list(Axioms ax, Out o, uint32_t L, const uint32_t* __restrict__ ids,
+                                                      uint32_t n) {
+  __shared__ unsigned long long lds[WAVES * (CAPW / 2)];
+  uint32_t* lbuf = reinterpret_cast<uint32_t*>(lds + (threadIdx.x >> 6) * (CAPW / 2));
+  Rsv rs = rsv_load(o);
+  const uint32_t nw = gridDim.x * WAVES, w = slot_id();
+  const uint64_t ntask = 3ull * n;
+  for (uint64_t base = 0; base * nw + w < ntask; base += 64) {  // (wave-uniform)
+    const uint64_t t0 = (base + lane()) * nw + w;
+    const bool in = t0 < ntask;
+    const uint32_t A0 = in ? ids[t0 / 3] : 0u, T0 = (uint32_t)(t0 % 3);
+    const Pre mine = in ? pre_load(ax, o, A0, T0) : Pre{};
+    unsigned long long m = __ballot(in);
+    while (m) {
+      const int i = __ffsll((long long)m) - 1;
+      m &= m - 1;
+      const uint32_t A = __shfl(A0, i), T = __shfl(T0, i);
+      const Pre pr = pre_of(mine, i);
+      if (T == R_EXR)
+        task<R_EXR, false>(ax, o, A, lbuf, rs, &pr);
+      else if (T == R_EXL)
+        task<R_EXL, false>(ax, o, A, lbuf, rs, &pr);
+      else
+        task<R_TOLD, false>(ax, o, A, lbuf, rs, &pr);
+    }
+  }
+  rsv_store(o, rs);
+  (void)L;
+}
+
 // Level 0 — the concepts without told supers: told* is empty and exr* / exl* are the concept's
 // own axiom lists (sorted, unique), so a lane per concept copies them (the wave reserves its
 // lanes' rows with one atomic per row type), and the subs whose last super it was are counted
@@ -887,15 +922,16 @@ __global__ void __launch_bounds__(BLOCK) k_level0(Axioms ax, Out o) {
       reinterpret_cast<uint32_t*>(o.meta + 2 * A)[RowT<R_EXL>::comp] = l0;
       reinterpret_cast<uint32_t*>(o.meta + 2 * A + 1)[RowT<R_EXL>::comp] = l0 + nl;
     }
-    wave_concat(nc, [&](bool v, uint32_t own, uint32_t j, uint32_t) {
-      const uint32_t cbo = __shfl(cb, (int)own);
-      if (!v) return;
-      const uint32_t c = ax.chi[cbo + j];
-      if (atomicSub(o.indeg + c, 1u) == 1u && o.level[c] != SKIP) {  // (as in k_level)
-        o.level[c] = 1u;
-        any = true;
-      }
-    });
+    if (!ax.slevel)  // (static levels: the next levels are known already)
+      wave_concat(nc, [&](bool v, uint32_t own, uint32_t j, uint32_t) {
+        const uint32_t cbo = __shfl(cb, (int)own);
+        if (!v) return;
+        const uint32_t c = ax.chi[cbo + j];
+        if (atomicSub(o.indeg + c, 1u) == 1u && o.level[c] != SKIP) {  // (as in k_level)
+          o.level[c] = 1u;
+          any = true;
+        }
+      });
   }
   if (any) sany = 1;
   __syncthreads();
@@ -943,6 +979,10 @@ __global__ void __launch_bounds__(BLOCK) k_follow(Axioms ax, Out o, uint32_t L, 
     if (m >= ax.N || !built(ax, m) || o.level[m] != FOLLOW) continue;
     const uint32_t r = ax.rep[m];
     const uint32_t lr = r < ax.N ? o.level[r] : NONE;
+    // a representative outside the built window (a partition's window is a contiguous id range,
+    // so it may hold a follower no owned row reaches while its representative lies below the
+    // range): the follower's rows are never read — left empty
+    if (lr == SKIP) continue;
     if (!all && !(lr < L)) continue;  // (the representative's row is not built yet)
     const uint4 rb = o.meta[2 * r], re = o.meta[2 * r + 1];
     const uint32_t b = rb.x, n = re.x - rb.x;
@@ -1425,6 +1465,14 @@ void level(hipStream_t s, const Axioms& ax, const Out& o, uint32_t L) {
     hipLaunchKernelGGL(k_level0, dim3(grid_for(ax.N)), dim3(BLOCK), 0, s, ax, o);
   else
     hipLaunchKernelGGL(k_level, dim3(GRID), dim3(BLOCK), 0, s, ax, o, L);
+  CCHK(hipGetLastError());
+}
+
+void level_list(hipStream_t s, const Axioms& ax, const Out& o, uint32_t L, uint32_t first, uint32_t n) {
+  if (!n) return;
+  // (a small level gets a small grid: its ramp is the launch's cost, not its few tasks)
+  const uint32_t g = std::min<uint32_t>(GRID, std::max<uint32_t>(1, (3 * n + WAVES - 1) / WAVES));
+  hipLaunchKernelGGL(k_level_list, dim3(g), dim3(BLOCK), 0, s, ax, o, L, ax.lvl_ids + first, n);
   CCHK(hipGetLastError());
 }
 

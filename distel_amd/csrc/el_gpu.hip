@@ -3280,6 +3280,10 @@ struct el_ctx {
   void closure_grow();
   void closure_tail(uint32_t a, uint32_t b, uint32_t L, bool all);
   void closure_rows(uint32_t a, uint32_t b);
+  // static Kahn levels of the built window (elcl::Axioms::slevel): concepts of level L >= 1 at
+  // lvl_ids[lvl_ptr[L], lvl_ptr[L + 1]); empty: the dynamic levels
+  std::vector<uint32_t> lvl_ptr;
+  void static_levels();
   void closure_state();
   // The logs are indexed by uint32 counters on the device (DCounters): a step whose logs could
   // pass 2^32 entries (count + every candidate new) fails with EL_ENOMEM instead of wrapping.
@@ -3802,7 +3806,67 @@ std::string el_ctx::install_index(el::HostIndex&& hnew) {
   d.xwin = nullptr;  // (the windows of the other ranks: exchange_windows, at the first el_saturate)
   d.nranks = part() ? part_count : 1u;
   d.me = part_rank;
+  static_levels();
   return "";
+}
+
+// The Kahn levels of the told closure are a property of the told axioms and of the built window:
+// computed here once per index (O(N + told edges) on the host), uploaded as each concept's level
+// and the concepts of every level >= 1 in level order (elcl::Axioms::slevel / lvl_ids).  The same
+// marks as k_start: ⊥ / ⊤ and the window built, a told cycle's follower FOLLOW, level 0 without
+// condensed supers (1 for a representative with members), else 1 + the largest super level; a
+// concept never reached (a super outside the window) stays NONE and goes to the relaxation.
+void el_ctx::static_levels() {
+  lvl_ptr.clear();
+  caxk.slevel = caxk.lvl_ids = nullptr;
+  static const bool dynamic = getenv("EL_DYNAMIC_LEVELS") && getenv("EL_DYNAMIC_LEVELS")[0] == '1';
+  if (dynamic) return;
+  const el::HostIndex& h = hx;
+  const uint32_t N = h.N;
+  const bool scc = !h.scc_rep.empty();
+  const el::Csr& par = scc ? h.told_c : h.told;
+  const el::Csr& chi = scc ? h.toldT_c : h.toldT;
+  const uint32_t w_lo = part() ? ix.c_lo : 2u, w_hi = part() ? ix.c_hi : 0xffffffffu;
+  std::vector<uint32_t> lev(N), pend(N, 0), stk;
+  for (uint32_t A = 0; A < N; ++A) {
+    const bool in = A < 2u || (A >= w_lo && A < w_hi);
+    const bool fol = scc && h.scc_rep[A] != A;
+    const uint32_t d = par.ptr[A + 1] - par.ptr[A];
+    const bool xt = scc && h.told_x.ptr[A + 1] > h.told_x.ptr[A];
+    lev[A] = !in ? elcl::LVL_SKIP : fol ? elcl::LVL_FOLLOW : d ? elcl::LVL_NONE : xt ? 1u : 0u;
+    pend[A] = (in && !fol) ? d : 0u;
+    if (lev[A] == 0u || lev[A] == 1u) stk.push_back(A);
+  }
+  std::vector<uint32_t> cand(N, 0);
+  uint32_t depth = 0;
+  while (!stk.empty()) {  // (any order: a concept is pushed once, when its last super is done)
+    const uint32_t A = stk.back();
+    stk.pop_back();
+    depth = std::max(depth, lev[A]);
+    for (uint32_t j = chi.ptr[A]; j < chi.ptr[A + 1]; ++j) {
+      const uint32_t c = chi.a[j];
+      if (lev[c] != elcl::LVL_NONE) continue;  // (skipped, followers)
+      cand[c] = std::max(cand[c], lev[A] + 1);
+      if (--pend[c] == 0) {
+        lev[c] = cand[c];
+        stk.push_back(c);
+      }
+    }
+  }
+  lvl_ptr.assign(depth + 2, 0);
+  for (uint32_t A = 0; A < N; ++A)
+    if (lev[A] >= 1u && lev[A] <= depth) lvl_ptr[lev[A] + 1]++;
+  for (uint32_t L = 0; L <= depth; ++L) lvl_ptr[L + 1] += lvl_ptr[L];
+  std::vector<uint32_t> ids(std::max<uint32_t>(lvl_ptr[depth + 1], 1)), at(lvl_ptr.begin(), lvl_ptr.end() - 1);
+  for (uint32_t A = 0; A < N; ++A)
+    if (lev[A] >= 1u && lev[A] <= depth) ids[at[lev[A]]++] = A;
+  auto up = [&](const std::vector<uint32_t>& v) {
+    uint32_t* p = dupload(v);
+    index_bufs.push_back(p);
+    return (const uint32_t*)p;
+  };
+  caxk.slevel = up(lev);
+  caxk.lvl_ids = up(ids);
 }
 
 // Every rank's column window, all-gathered once per el_load (the first el_saturate: collective).
@@ -5069,7 +5133,18 @@ void el_ctx::closure_rows(uint32_t a, uint32_t b) {
     launch(EL_K_CLOSURE, [&] { elcl::start(stream, caxk, cl); });
     uint32_t L = 0;
     bool redo = false;
-    for (;;) {
+    if (caxk.slevel) {  // static levels: exactly the levels there are, each a list of its concepts
+      launch(EL_K_CLOSURE, [&] { elcl::level(stream, caxk, cl, 0); });
+      const uint32_t depth = (uint32_t)lvl_ptr.size() - 2;
+      for (L = 1; L <= depth; ++L)
+        launch(EL_K_CLOSURE, [&] { elcl::level_list(stream, caxk, cl, L, lvl_ptr[L], lvl_ptr[L + 1] - lvl_ptr[L]); });
+      init_lap("levels enqueued");
+      closure_tail(a, b, L, false);
+      init_lap("closure tail read");
+      if (clh->ctr.bad) throw ElError{EL_EHIP, "told closure: a told cycle's representative row lacks its follower"};
+      redo = clh->ctr.ovf != 0;
+    }
+    for (; !caxk.slevel;) {
       const uint32_t end = (uint32_t)std::min<uint64_t>((uint64_t)N + 1, (uint64_t)L + level_hint);
       for (; L < end; ++L) launch(EL_K_CLOSURE, [&] { elcl::level(stream, caxk, cl, L); });
       init_lap("levels enqueued");
