@@ -4542,15 +4542,18 @@ bool el_ctx::superstep(uint32_t mask, uint64_t sb, uint64_t se, uint64_t lb, uin
       const bool by_rule = getenv("EL_SPLIT_EXPAND")[0] == '2';
       const uint32_t keep = M_LEMPTY | M_PEMPTY;
       const uint32_t groups[5] = {M_R1, M_R2, M_R3, M_R4Y | M_R4D, ~(M_R1 | M_R2 | M_R3 | M_R4Y | M_R4D)};
+      // (and the link role per rule group: CR4 half-2, CR5, CR6, the rest)
+      const uint32_t lgroups[4] = {M_R4L | M_R4D, M_R5, M_R6, ~(M_R4L | M_R5 | M_R6)};
       for (int r = 0; r < 4; ++r) {
         if (!g[r]) continue;
-        for (int k = 0; k < (r == 0 && by_rule ? 5 : 1); ++k) {
+        for (int k = 0; k < (by_rule && r < 2 ? 5 - r : 1); ++k) {
           ExpandArgs e1 = ea;
           e1.gs = r == 0 ? ea.gs : 0u;
           e1.gl = r == 1 ? ea.gl : 0u;
           e1.ga = r == 2 ? ea.ga : 0u;
           e1.gp = r == 3 ? ea.gp : 0u;
           if (r == 0 && by_rule) e1.mask = (ea.mask & groups[k]) | (ea.mask & keep);
+          if (r == 1 && by_rule) e1.mask = (ea.mask & lgroups[k]) | (ea.mask & keep);
           hipLaunchKernelGGL(k_expand, dim3(g[r]), dim3(BLOCK), 0, stream, ix, sx, e1);
         }
       }

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """k_expand time per rule group and superstep from a rocprofv3 trace of a run with
 EL_SPLIT_EXPAND=2 (the S role launched once per rule group CR1, CR2, CR3, CR4, rest; then the
-link, activation and propagation roles).  Usage: scripts/split_rules_steps.py DB [classification]"""
+link role per rule group CR4 half-2, CR5, CR6, rest; then the activation and propagation roles).  Usage: scripts/split_rules_steps.py DB [classification]"""
 import glob
 import sqlite3
 import sys
@@ -16,7 +16,7 @@ rows = list(c.execute(f"select k.display_name, d.start, d.end from {kd} d join {
                       "order by d.start"))
 starts = [i for i, r in enumerate(rows) if "k_start" in r[0]] + [len(rows)]
 seg = rows[starts[which]:starts[which + 1]]
-cols = ["S:CR1", "S:CR2", "S:CR3", "S:CR4", "S:rest", "L", "jobs", "commit"]
+cols = ["S:CR1", "S:CR2", "S:CR3", "S:CR4", "S:rest", "L:CR4", "L:CR5", "L:CR6", "L:rest", "jobs", "commit"]
 print("step " + " ".join(f"{x:>8s}" for x in cols))
 run, jobs, com, k = [], 0.0, 0.0, 0
 tot = [0.0] * len(cols)
@@ -25,10 +25,12 @@ for name, s, e in seg + [("k_expand", 0, 0)]:
     if "k_expand" in name:
         if com > 0 or jobs > 0:  # a new superstep starts
             v = [0.0] * len(cols)
-            lab = ["S:CR1", "S:CR2", "S:CR3", "S:CR4", "S:rest", "L", "L", "L"] if len(run) >= 5 else ["L", "L", "L"]
+            S = ["S:CR1", "S:CR2", "S:CR3", "S:CR4", "S:rest"]
+            L = ["L:CR4", "L:CR5", "L:CR6", "L:rest"]
+            lab = S + L if len(run) >= 9 else S if len(run) == 5 else L
             for i, x in enumerate(run):
                 v[cols.index(lab[min(i, len(lab) - 1)])] += x
-            v[6], v[7] = jobs, com
+            v[-2], v[-1] = jobs, com
             tot = [a + b for a, b in zip(tot, v)]
             print(f"{k:4d} " + " ".join(f"{x:8.1f}" for x in v))
             k += 1
