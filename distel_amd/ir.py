@@ -415,17 +415,52 @@ def elk_ranges(ax: Axioms) -> Tuple[Axioms, List[int], List[int]]:
     return out, fb, fr
 
 
+def told_depth(ax: Axioms) -> np.ndarray:
+    """Kahn level of every concept over its told supers (0 without any; 1 + the largest of its
+    supers' otherwise) — the device closure's level structure, from the axioms alone.  Concepts
+    in or below a told cycle get one more than the deepest level reached."""
+    n = ax.n_concepts
+    depth = np.zeros(n, dtype=np.int64)
+    if not len(ax.sub):
+        return depth
+    sub = ax.sub.astype(np.int64)
+    sub = sub[sub[:, 0] != sub[:, 1]]
+    nsup = np.bincount(sub[:, 0], minlength=n)
+    order = np.argsort(sub[:, 1], kind="stable")
+    cptr = np.zeros(n + 1, dtype=np.int64)
+    np.add.at(cptr, sub[:, 1] + 1, 1)
+    cptr = np.cumsum(cptr)
+    chi = sub[order, 0]
+    pend = nsup.copy()
+    frontier = np.nonzero(pend == 0)[0]
+    level = 0
+    done = np.zeros(n, dtype=bool)
+    while len(frontier):  # level by level: a concept is ready when its last super is done
+        done[frontier] = True
+        depth[frontier] = level
+        kids = np.concatenate([chi[cptr[a]:cptr[a + 1]] for a in frontier]) if len(frontier) < 4096 else \
+            chi[np.concatenate([np.arange(cptr[a], cptr[a + 1]) for a in frontier])]
+        np.subtract.at(pend, kids, 1)
+        kids = np.unique(kids)
+        frontier = kids[(pend[kids] == 0) & ~done[kids]]
+        level += 1
+    depth[~done] = level
+    return depth
+
+
 def balanced_rows(ax: Axioms, parts: int) -> List[Tuple[int, int]]:
     """Contiguous row ranges [lo, hi) of ONE ontology for ``parts`` ranks (strong scaling:
     the concept space sharded, as DistEL shards its keys over Redis nodes,
-    ``AxiomLoader.java:665-667``), balanced by told edges: concept X weighs 1 + its told supers
-    + its CR3 axioms + the CR4 axioms it fills.  ⊥ and ⊤ stay on rank 0; the last rank's range
-    ends at n_concepts (the engine gives it the ELK range fillers too)."""
+    ``AxiomLoader.java:665-667``), balanced by the expected facts per row: concept X weighs
+    1 + depth(X)², its told depth (told_depth).  A row's subsumers are its told ancestors and the
+    CR4 conclusions its inherited existentials reach, both of which grow with the depth; on G3
+    (the oracle's per-row fact counts, profiles/r06_strong_balance.txt) 1 + depth² splits the facts
+    1.03 / 1.05 (max / min over 2 / 4 ranks) where told edges (round 5) split them 1.50 / 2.58.
+    ⊥ and ⊤ stay on rank 0; the last rank's range ends at n_concepts (the engine gives it the ELK
+    range fillers too)."""
     n = ax.n_concepts
-    w = np.ones(n, dtype=np.int64)
-    for col, arr in ((0, ax.sub), (0, ax.ex_rhs), (1, ax.ex_lhs)):
-        if len(arr):
-            w += np.bincount(arr[:, col].astype(np.int64), minlength=n)[:n]
+    d = told_depth(ax).astype(np.float64)
+    w = 1.0 + d * d
     cum = np.cumsum(w)
     cuts = [0] + [int(np.searchsorted(cum, cum[-1] * q / parts, side="right")) for q in range(1, parts)] + [n]
     cuts = [max(c, 2) if 0 < q < parts else c for q, c in enumerate(cuts)]
