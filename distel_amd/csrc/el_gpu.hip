@@ -1612,7 +1612,10 @@ __device__ __forceinline__ void expand_a(const DIndex& ix, const DState& st, Blo
 }
 
 // S candidates per chunk of the sorted S commit (commit_s_sorted)
-constexpr uint32_t CC_BITS = 11, CC = 1u << CC_BITS;
+#ifndef EL_CC_BITS
+#define EL_CC_BITS 11  // (12: 48 KB of LDS per block, G3 21.9 ms; 10: 19.8-20.1 ms; 11: 19.8 — round 6)
+#endif
+constexpr uint32_t CC_BITS = EL_CC_BITS, CC = 1u << CC_BITS;
 static_assert(CC % BLOCK == 0, "chunk per thread");
 constexpr uint32_t CSORT_MIN = 1u << 18;  // smaller commits: plain order (the sort's barriers cost more)
 

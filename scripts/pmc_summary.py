@@ -16,7 +16,8 @@ file ties the numbers to the build that produced them (bench.py uses them only f
 
 # read pattern per kernel: random gathers (FETCH_SIZE = bytes of the line requests) or
 # coalesced streaming (FETCH_SIZE = half the bytes); calibration: r03_pmc_calibration.json
-RANDOM_READ = {"k_expand", "k_jobs", "k_commit", "k_commit_told", "k_rehash", "k_level", "k_relax", "k_reloc_move",
+RANDOM_READ = {"k_expand", "k_jobs", "k_commit", "k_commit_told", "k_rehash", "k_level", "k_level_list", "k_relax",
+               "k_reloc_move",
                "k_reloc_claim", "k_ximport", "k_clear_logged", "k_init_facts", "k_stats", "k_succ_fill", "k_group_fill"}
 import csv
 import glob
@@ -63,6 +64,19 @@ def main():
                      "/ dispatches with f = 1 for random-gather kernels and 2 for streaming ones, as calibrated in "
                      "profiles/pmc/r03_pmc_calibration.json (scripts/micro/pmc_cal.hip)",
            "kernels": {}}
+    # the HIP runtime the passes ran on (the bench line each pass printed): the system runtime's
+    # copies go to an SDMA engine, torch's bundled runtime blits them on the CUs
+    # (__amd_rocclr_copyBuffer dispatches in the table come from the bench's own small D2D / D2H
+    # copies: counter readbacks, the profiled classification's run-buffer DMAs, not the timed step)
+    for log in sorted(glob.glob(os.path.join(tag, "p*.log"))):
+        for line in open(log, errors="replace"):
+            if line.startswith("{") and '"hip_runtime"' in line:
+                try:
+                    res["hip_runtime"] = json.loads(line).get("hip_runtime")
+                except ValueError:
+                    pass
+        if "hip_runtime" in res:
+            break
     # informational passes (p3: L2 hit/miss, p4: SQ wave/issue cycles), when present
     extra = {c: load(os.path.join(tag, d), c) for d, c in
              (("p3", "TCC_HIT_sum"), ("p3", "TCC_MISS_sum"), ("p4", "SQ_WAVE_CYCLES"),
