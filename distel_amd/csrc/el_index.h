@@ -64,6 +64,7 @@ struct HostIndex {
   // (A layout of the axioms' statistics, like the transposes: no concept closure is used.)
   std::vector<uint32_t> cperm;
   std::vector<double> cscore;  // the order's score per concept (a partition orders its window by it)
+  std::vector<double> cdesc;   // told-DAG descendants per concept (paths counted): the init facts' weight
 };
 
 // Owned copy of the typed axioms (el_load copies its input; el_add_axioms appends an

@@ -144,7 +144,8 @@ def load_library(path: Optional[str] = None) -> C.CDLL:
     lib.el_saturate.argtypes = [P, C.POINTER(_ElStats)]
     lib.el_get_stats.argtypes = [P, C.POINTER(_ElStats)]
     lib.el_kernel_stats.argtypes = [P, C.POINTER(_ElKernelStat), C.c_int]
-    lib.el_set_profile.argtypes = [P, C.c_int]
+    if hasattr(lib, "el_set_profile"):  # (ABI 7 builds before round 6 lack it: A/B variants)
+        lib.el_set_profile.argtypes = [P, C.c_int]
     lib.el_superstep_trace.argtypes = [P, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64), C.POINTER(C.c_uint64),
                                        C.c_size_t, C.POINTER(C.c_size_t)]
     lib.el_get_subsumers.argtypes = [P, C.c_uint32, _u32p, C.c_size_t, C.POINTER(C.c_size_t)]
