@@ -190,10 +190,13 @@ def parse():
                     help="classifications in flight in the timed loop: 1 = one at a time (the default: "
                          "ms_per_step is one classification's wall-clock); 2 = two engines alternate, one's "
                          "result copy-back (EL_RESULT_ASYNC) rides over PCIe under the other's classification")
-    ap.add_argument("--copyback", default="stream", choices=["stream", "rows"],
-                    help="stream: the result node's facts and links cross PCIe as the supersteps commit them "
-                         "(el_stream_result; commit order, row-run encoded); rows: after the fixpoint, as sorted CSR rows "
-                         "X -> {B} (el_copy_result)")
+    ap.add_argument("--copyback", default="auto", choices=["auto", "packed", "stream", "rows"],
+                    help="packed / stream: the result node's facts and links cross PCIe as the supersteps commit "
+                         "them (el_stream_result; commit order, row-run encoded; packed = EL_STREAM_PACKED, each "
+                         "fact's value a 16-bit column code, escapes for values outside the coded columns); auto: "
+                         "stream or packed, whichever classified faster in two untimed probes of each before the "
+                         "warmup (max over ranks); rows: after the fixpoint, as sorted CSR rows X -> {B} "
+                         "(el_copy_result)")
     ap.add_argument("--no-throughput2", action="store_true",
                     help="skip the separately reported two-in-flight throughput loop")
     ap.add_argument("--increment", type=float, default=0.0,
@@ -314,8 +317,11 @@ def main():
         the row counts) while this thread starts the other's classification (ctypes drops the
         GIL inside the library, and the two threads never share an engine); drain() waits for
         the last copy-backs inside the timed region."""
-        stream = args.copyback == "stream"
-        results = [engine.Stream() if stream else engine.Result() for _ in engines]  # page-locked, reused
+        stream = args.copyback != "rows"
+        modes = ["stream", "packed"] if args.copyback == "auto" else [args.copyback]
+        results = [{m: engine.Stream(packed=m == "packed") for m in modes} if stream else engine.Result()
+                   for _ in engines]  # page-locked, reused
+        cur = [modes[0]]  # page-locked, reused
         split = []  # (init, saturate, copy-back) seconds per step; the last `steps` are the timed ones
         turn = [0]
         pool = ThreadPoolExecutor(max_workers=1) if len(engines) == 2 else None
@@ -324,7 +330,7 @@ def main():
         def classify():
             i = turn[0] % len(engines)
             turn[0] += 1
-            e, res = engines[i], results[i]
+            e, res = engines[i], (results[i][cur[0]] if stream else results[i])
             if copying[i] is not None:
                 copying[i].result()  # (the enqueue finished long ago; errors surface here)
                 copying[i] = None
@@ -352,20 +358,35 @@ def main():
                     copying[i] = None
                 e.result_wait()
 
+        probe = None
+        if len(modes) > 1:  # auto: two untimed classifications with each encoding, the faster kept
+            probe = {m: [] for m in modes}
+            for _ in range(2):
+                for m in modes:
+                    cur[0] = m
+                    t0 = time.perf_counter()
+                    classify()
+                    drain()
+                    probe[m].append(time.perf_counter() - t0)
+            probe = {m: 1e3 * D.allreduce(rk, min(v), "max") for m, v in probe.items()}
+            cur[0] = min(modes, key=lambda m: probe[m])
+        split.clear()
         t_max, derived_all, st = D.run_weak(rk, classify, steps, warmup, drain=drain)
         if pool is not None:
             pool.shutdown()
+        results = [r[cur[0]] if stream else r for r in results]
         for r in results:
             assert (r.n_facts, r.n_links) == (st["s_facts"], st["links"]) or (len(ax.range) and not stream) or \
                 engines[0].partition is not None, "copy-back lost facts"
         res = results[(turn[0] - 1) % len(engines)]
-        copy_bytes = (4 * (res.n_facts + res.n_links) + 8 * (res.n_s_runs + res.n_l_runs) if stream else
+        copy_bytes = (res.bytes() if stream else
                       8 * 2 * (res.row_hi - res.row_lo + 1) + 4 * (res.n_facts + res.n_links))
         sp = split[-steps:]
         return {"t_max": t_max, "derived": derived_all, "st": st, "ms_per_step": 1e3 * t_max / steps,
                 "value": derived_all * steps / t_max, "copy_bytes": int(copy_bytes),
                 "init_ms": 1e3 * sum(t[0] for t in sp) / len(sp), "saturate_ms": 1e3 * sum(t[1] for t in sp) / len(sp),
-                "copyback_ms": 1e3 * sum(t[2] for t in sp) / len(sp), "inflight": len(engines)}
+                "copyback_ms": 1e3 * sum(t[2] for t in sp) / len(sp), "inflight": len(engines),
+                "encoding": cur[0] if stream else "rows", "probe_ms": probe}
 
     # (diagnostic, EL_D2H_PROBE=1: this process's D2H rate before any engine exists)
     d2h = {"before": d2h_probe()} if has_cuda and rank == 0 and os.environ.get("EL_D2H_PROBE") == "1" else None
@@ -435,16 +456,16 @@ def main():
                             "links the new axioms reach) + el_saturate (first superstep over those lists, then "
                             "semi-naive); no result copy-back"}
 
-    def profile_once(peng, workload, pmc):
+    def profile_once(peng, workload, pmc, encoding):
         """One classification of an engine already loaded, in the timed schedule (streamed copy-back
         armed), with HIP events around every launch on its engine stream: the dominant kernel
         (largest Σ time; phases sharing a launch add their algorithmic bytes) as `roofline`, and
         the whole table.  A partitioned engine runs it on every rank together (collectives)."""
         peng.init()
-        if args.copyback == "stream":
-            peng.stream_result(engine.Stream())  # (not released: the event counters are read after)
+        if encoding != "rows":
+            peng.stream_result(engine.Stream(packed=encoding == "packed"))  # (not released: counters read after)
         pst = peng.saturate()
-        if args.copyback == "stream":
+        if encoding != "rows":
             peng.result_wait()
         ks = peng.kernel_stats()
         launches = {}
@@ -509,7 +530,7 @@ def main():
             # context with HIP events on, every rank together; the line carries the slowest rank's
             # dominant kernel (PMC traffic is measured on the N = 1 schedule only: null here)
             xeng.set_profile(True)
-            roof, table = profile_once(xeng, args.workload, pmc=False)
+            roof, table = profile_once(xeng, args.workload, pmc=False, encoding=leg["encoding"])
             xeng.set_profile(False)
             allr = D.gather_objects(rk, (roof, table))
             slow = max(range(len(allr)), key=lambda i: allr[i][0]["profiled_ms"])
@@ -571,10 +592,14 @@ def main():
             "latency_ms": round(head["ms_per_step"], 4) if head["inflight"] == 1 else None,
             "copyback": ("streamed: the result node's facts and links in commit order, row-run encoded "
                          "(B / pair id per entry + (X, end) per run), crossing PCIe as the supersteps commit "
-                         "them (el_stream_result)"
-                         if args.copyback == "stream" else
+                         "them (el_stream_result)" + ("; packed: B as a 16-bit column code, escapes for B outside "
+                                                      "the coded columns (EL_STREAM_PACKED)"
+                                                      if head["encoding"] == "packed" else "")
+                         if args.copyback != "rows" else
                          "rows: S(X) and links as sorted CSR rows after the fixpoint (el_copy_result)"),
             "copyback_bytes": head["copy_bytes"],
+            "copyback_encoding": head["encoding"],
+            "copyback_probe_ms": ({m: round(v, 3) for m, v in head["probe_ms"].items()} if head["probe_ms"] else None),
             "copyback_gbs": (round(head["copy_bytes"] / (head["copyback_ms"] * 1e-3) / 1e9, 2)
                              if head["copyback_ms"] > 0 and args.copyback == "rows" else None),
             "throughput_inflight2": copies.get("throughput2") if copies else None,
@@ -639,7 +664,7 @@ def main():
         # supersteps): HIP events bracket every launch on the engine stream
         peng = engine.Engine(device=dev, profile=True)
         peng.load(ax)
-        roofline, kernels = profile_once(peng, args.workload, pmc=True)
+        roofline, kernels = profile_once(peng, args.workload, pmc=True, encoding=head["encoding"])
         peng.close()
 
     cpu = None

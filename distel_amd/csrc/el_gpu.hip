@@ -55,6 +55,8 @@
 
 #include "el_closure.h"
 #include "el_stream.h"
+
+#include <type_traits>
 #include "el_gpu.h"
 #include "el_index.h"
 #include "el_rows.h"
@@ -3558,12 +3560,25 @@ struct el_ctx {
   hipEvent_t ev_run = nullptr;                         // after the last encoding enqueued
   bool run_pending = false;
   void runs_out(bool wait);
-  uint32_t *rcnt = nullptr, *roff = nullptr;  // per-tile run counts / their scan
+  uint32_t *rcnt = nullptr, *roff = nullptr;  // per-tile run counts / their scan (packed: escapes from rtiles_cap)
   uint64_t rtiles_cap = 0;
   void* rscan_tmp = nullptr;
   size_t rscan_bytes = 0;
   unsigned long long* rbase = nullptr;    // runs written so far: S, links (device)
   void stream_runs(const uint32_t* keys, uint64_t a, uint64_t b, uint2* out, uint64_t cap, int which);
+  void stream_tiles(uint64_t nt);  // (the per-tile scratch of the encodings: rcnt, roff)
+  // EL_STREAM_PACKED: the facts' values as 16-bit codes (their bit column) + escapes, encoded on
+  // nstream beside the runs into device buffers, DMA'd with the runs (runs_out)
+  bool packed = false;
+  uint16_t* scode = nullptr;           // codes at log positions (device), scode_cap = the caller's s_cap
+  uint64_t scode_cap = 0;
+  uint32_t* sesc = nullptr;            // escape values (device)
+  uint64_t sesc_cap = 0;
+  uint16_t* s_code_dev = nullptr;      // device addresses of the caller's code / escape buffers
+  uint32_t* s_esc_dev = nullptr;
+  uint64_t code_enc = 0, code_sent = 0, esc_sent = 0;  // codes encoded (behind ev_run) / DMA'd; escapes DMA'd
+  unsigned long long *ebase = nullptr, *etot_h = nullptr, *etot_d = nullptr;  // escapes written (device / mapped)
+  std::vector<uint32_t> code_table;    // code -> concept (el_stream_codes), per index
   void stream_out();    // stream_mark + stream_flush
   void stream_mark();
   // force: flush whatever is marked; else only a segment of stream_min entries or more (a late
@@ -3784,6 +3799,13 @@ std::string el_ctx::install_index(el::HostIndex&& hnew) {
     perm = el::column_perm(h, ix.c_lo, ix.c_hi);
   if (!perm.empty()) d.cperm = up32(perm);
   cax.cperm = caxk.cperm = d.cperm;
+  {  // code -> concept of a packed stream: the concept of bit column c < 0xFFFF (elst::code_of)
+    code_table.assign(elst::CODE_ESC, NONE);
+    for (uint32_t a = 0; a < h.N; ++a) {
+      const uint32_t c = a < 2u ? a : (a < ix.c_lo || a >= ix.c_hi) ? NONE : perm.empty() ? a - ix.c_lo + 2u : perm[a];
+      if (c < elst::CODE_ESC) code_table[c] = a;
+    }
+  }
   {  // binary conjunctions per cidx entry, with the bit columns of p and B (DIndex::cidx_q)
     auto col = [&](uint32_t a) -> uint32_t {  // (col_of on the host)
       if (a < 2u) return a;
@@ -5479,9 +5501,9 @@ void el_ctx::stream_flush(bool force) {
     else
       HIPCHK(hipMemcpyAsync(dst + a, src + a, (b - a) * sizeof(uint32_t), hipMemcpyDeviceToHost, dstream));
   };
-  dma(strm->s_b, s_b_dev, slog_a, strm_s, s1, strm->s_cap);
+  if (!packed) dma(strm->s_b, s_b_dev, slog_a, strm_s, s1, strm->s_cap);
   dma(strm->l_p, l_p_dev, llog_p, strm_l, l1, strm->l_cap);
-  if ((strm->s_b && s1 > strm->s_cap) || (strm->l_p && l1 > strm->l_cap)) strm_ovf = true;
+  if (((strm->s_b || packed) && s1 > strm->s_cap) || (strm->l_p && l1 > strm->l_cap)) strm_ovf = true;
   runs_out(false);  // (the runs of the earlier segments whose encoding is done)
   if (s_run_dev) stream_runs(slog_x, strm_s, s1, srun, strm->s_run_cap, 0);
   if (l_run_dev) stream_runs(llog_x, strm_l, l1, lrun, strm->l_run_cap, 1);
@@ -5525,13 +5547,49 @@ void el_ctx::runs_out(bool wait) {
                             hipMemcpyDeviceToDeviceNoCU, dstream));
     run_sent[w] = n;
   }
+  if (packed) {  // the codes of the segments encoded, and the escapes written so far
+    auto to_host = [&](void* host, void* host_dev, const void* src, uint64_t bytes) {
+      if (dma_hostptr || !host_dev)
+        HIPCHK(hipMemcpyAsync(host, src, bytes, hipMemcpyDeviceToHost, dstream));
+      else
+        HIPCHK(hipMemcpyAsync(host_dev, src, bytes, hipMemcpyDeviceToDeviceNoCU, dstream));
+    };
+    const uint64_t ce = std::min<uint64_t>(code_enc, strm->s_cap);
+    if (ce > code_sent)
+      to_host(strm->s_code + code_sent, s_code_dev ? s_code_dev + code_sent : nullptr, scode + code_sent,
+              (ce - code_sent) * sizeof(uint16_t));
+    code_sent = std::max(code_sent, ce);
+    const uint64_t ee = std::min<uint64_t>(etot_h[0], strm->s_esc_cap);
+    if (ee > esc_sent)
+      to_host(strm->s_esc + esc_sent, s_esc_dev ? s_esc_dev + esc_sent : nullptr, sesc + esc_sent,
+              (ee - esc_sent) * sizeof(uint32_t));
+    esc_sent = std::max(esc_sent, ee);
+  }
 }
 
 // The runs of x over keys[a, b) (a log segment) into the caller's run buffer, numbered on from
 // the runs of the earlier segments (rbase[which]); on nstream, which waited for the commit.
+// Packed, the fact log's pass (which = 0) also writes the segment's codes and escapes.
 void el_ctx::stream_runs(const uint32_t* keys, uint64_t a, uint64_t b, uint2* out, uint64_t cap, int which) {
   if (b <= a) return;
   const uint64_t nt = elst::tiles(b - a);
+  stream_tiles(nt);
+  elst::Codes pk;
+  const bool pack = packed && which == 0;
+  if (pack) {
+    pk.vals = slog_a, pk.cperm = ix.cperm, pk.c_lo = ix.c_lo, pk.c_hi = ix.c_hi;
+    pk.cnt = rcnt + rtiles_cap, pk.off = roff + rtiles_cap;
+    pk.codes = scode, pk.code_cap = scode_cap, pk.esc = sesc, pk.esc_cap = sesc_cap;
+    pk.base = ebase, pk.total = etot_d;
+  }
+  elst::count(nstream, keys, a, b, rcnt, pack ? &pk : nullptr);
+  elcl::scan(nstream, rscan_tmp, rscan_bytes, rcnt, roff, (uint32_t)nt);
+  if (pack) elcl::scan(nstream, rscan_tmp, rscan_bytes, rcnt + rtiles_cap, roff + rtiles_cap, (uint32_t)nt);
+  elst::emit(nstream, keys, a, b, roff, rcnt, out, cap, rbase + which, rtot_d + which, pack ? &pk : nullptr);
+  if (pack) code_enc = b;
+}
+
+void el_ctx::stream_tiles(uint64_t nt) {
   if (nt > rtiles_cap) {
     HIPCHK(hipStreamSynchronize(nstream));  // (the scratch of the last segment is free)
     dfree(rcnt);
@@ -5539,14 +5597,11 @@ void el_ctx::stream_runs(const uint32_t* keys, uint64_t a, uint64_t b, uint2* ou
     dfree(rscan_tmp);
     rtiles_cap = std::max<uint64_t>(2 * nt, 4096);
     if (rtiles_cap > 0x7fffffffull) throw ElError{EL_ENOMEM, "streamed result: log segment too long"};
-    rcnt = dalloc<uint32_t>(rtiles_cap);
-    roff = dalloc<uint32_t>(rtiles_cap);
+    rcnt = dalloc<uint32_t>(2 * rtiles_cap);
+    roff = dalloc<uint32_t>(2 * rtiles_cap);
     rscan_bytes = elcl::scan_temp_bytes((uint32_t)rtiles_cap);
     rscan_tmp = dalloc<uint8_t>(rscan_bytes);
   }
-  elst::count(nstream, keys, a, b, rcnt);
-  elcl::scan(nstream, rscan_tmp, rscan_bytes, rcnt, roff, (uint32_t)nt);
-  elst::emit(nstream, keys, a, b, roff, rcnt, out, cap, rbase + which, rtot_d + which);
 }
 
 // The fixpoint: the last segments, the counts, and (release) the next classification's reset on
@@ -5563,6 +5618,8 @@ void el_ctx::stream_end(bool release) {
   strm->n_s_runs = s_run_dev ? rtot_h[0] : 0;
   strm->n_l_runs = l_run_dev ? rtot_h[1] : 0;
   if (strm->n_s_runs > strm->s_run_cap || strm->n_l_runs > strm->l_run_cap) strm_ovf = true;
+  strm->n_s_esc = packed ? etot_h[0] : 0;
+  if (packed && strm->n_s_esc > strm->s_esc_cap) strm_ovf = true;
   strm = nullptr;
   HIPCHK(hipEventRecord(ev_copied[0], cstream));
   HIPCHK(hipEventRecord(ev_copied[1], stream));
@@ -6721,7 +6778,7 @@ int el_result_wait(el_ctx* c) {
 int el_stream_result(el_ctx* c, el_stream* s) {
   if (!c || !s) return EL_EINVAL;
   if (!c->inited) return fail(c, EL_ESTATE, "el_stream_result before el_init");
-  if (s->flags & ~EL_RESULT_RELEASE) return fail(c, EL_EINVAL, "unknown el_stream flags");
+  if (s->flags & ~(EL_RESULT_RELEASE | EL_STREAM_PACKED)) return fail(c, EL_EINVAL, "unknown el_stream flags");
   return guarded(c, [&] {
     // the run buffers are written by the device: page-locked and mapped (el_host_alloc)
     c->s_run_dev = reinterpret_cast<uint2*>(mapped_for_device(s->s_run));
@@ -6730,6 +6787,31 @@ int el_stream_result(el_ctx* c, el_stream* s) {
     c->l_p_dev = mapped_for_device(s->l_p);
     if ((s->s_run && !c->s_run_dev) || (s->l_run && !c->l_run_dev))
       return fail(c, EL_EINVAL, "el_stream run buffers must be page-locked host memory (el_host_alloc)");
+    c->packed = (s->flags & EL_STREAM_PACKED) != 0;
+    if (c->packed) {
+      c->s_code_dev = reinterpret_cast<uint16_t*>(mapped_for_device(s->s_code));
+      c->s_esc_dev = mapped_for_device(s->s_esc);
+      if (!s->s_code || !s->s_esc || !s->s_run)
+        return fail(c, EL_EINVAL, "EL_STREAM_PACKED needs s_code, s_esc and s_run buffers");
+      if (!c->ebase) {
+        c->ebase = dalloc<unsigned long long>(1);
+        HIPCHK(hipHostMalloc((void**)&c->etot_h, sizeof(unsigned long long), hipHostMallocMapped));
+        HIPCHK(hipHostGetDevicePointer((void**)&c->etot_d, c->etot_h, 0));
+      }
+      auto fitv = [&](auto*& d, uint64_t& cap, uint64_t want) {
+        if (want <= cap) return;
+        HIPCHK(hipStreamSynchronize(c->nstream));
+        HIPCHK(hipStreamSynchronize(c->dstream));
+        dfree(d);
+        d = dalloc<std::remove_reference_t<decltype(*d)>>(want);
+        cap = want;
+      };
+      fitv(c->scode, c->scode_cap, s->s_cap);
+      fitv(c->sesc, c->sesc_cap, s->s_esc_cap);
+      HIPCHK(hipMemsetAsync(c->ebase, 0, sizeof(unsigned long long), c->nstream));
+      c->etot_h[0] = 0;
+      c->code_enc = c->code_sent = c->esc_sent = 0;
+    }
     if (!c->rbase) {
       c->rbase = dalloc<unsigned long long>(2);
       HIPCHK(hipHostMalloc((void**)&c->rtot_h, 2 * sizeof(unsigned long long), hipHostMallocMapped));
@@ -6757,8 +6839,18 @@ int el_stream_result(el_ctx* c, el_stream* s) {
     c->strm_s = c->strm_l = 0;
     c->mark_pending = c->strm_marked = false;
     s->n_facts = s->n_links = s->n_s_runs = s->n_l_runs = 0;
+    if (c->packed) s->n_s_esc = 0;
     return EL_OK;
   });
+}
+
+int el_stream_codes(el_ctx* c, uint32_t* concept, size_t cap, size_t* n) {
+  if (!c || !n) return EL_EINVAL;
+  if (!c->loaded) return fail(c, EL_ESTATE, "no ontology loaded");
+  *n = c->code_table.size();
+  if (cap < *n) return EL_ERANGE;
+  if (concept) std::copy(c->code_table.begin(), c->code_table.end(), concept);
+  return EL_OK;
 }
 
 int el_pid_table(el_ctx* c, uint32_t* role, uint32_t* filler, size_t cap, size_t* n) {
@@ -6921,6 +7013,10 @@ void el_destroy(el_ctx* c) {
   dfree(c->rscan_tmp);
   dfree(c->rbase);
   dfree(c->srun);
+  dfree(c->scode);
+  dfree(c->sesc);
+  dfree(c->ebase);
+  if (c->etot_h) (void)hipHostFree(c->etot_h);
   dfree(c->lrun);
   if (c->rtot_h) (void)hipHostFree(c->rtot_h);
   if (c->ev_run) (void)hipEventDestroy(c->ev_run);

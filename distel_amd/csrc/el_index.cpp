@@ -289,20 +289,30 @@ std::string told_sccs(HostIndex& o) {
 // 4.5 M unchanged.
 void column_order(const el_axioms& ax, HostIndex& o) {
   const uint32_t N = o.N;
-  std::vector<double> desc(N, 1.0);
+  // Over the condensed told graph when it has cycles: a component counts its members once and
+  // every member gets the component's count (each member subsumes all the component's
+  // descendants).  On the raw graph a cycle never drains, leaving it and everything above it —
+  // G3E's equivalences sit near the roots, so the most frequent subsumers — at partial counts.
+  const bool cyc = !o.followers.empty();
+  const Csr& up = cyc ? o.told_c : o.told;
+  const Csr& down = cyc ? o.toldT_c : o.toldT;
+  std::vector<double> desc(N, 0.0);
+  for (uint32_t a = 0; a < N; ++a) desc[cyc ? o.scc_rep[a] : a] += 1.0;
   std::vector<uint32_t> pending(N), stk;
-  for (uint32_t b = 0; b < N; ++b) pending[b] = o.toldT.ptr[b + 1] - o.toldT.ptr[b];
+  for (uint32_t b = 0; b < N; ++b) pending[b] = down.ptr[b + 1] - down.ptr[b];
   for (uint32_t a = 0; a < N; ++a)
-    if (!pending[a]) stk.push_back(a);
+    if (!pending[a] && (!cyc || o.scc_rep[a] == a)) stk.push_back(a);
   while (!stk.empty()) {
     const uint32_t a = stk.back();
     stk.pop_back();
-    for (uint32_t k = o.told.ptr[a]; k < o.told.ptr[a + 1]; ++k) {
-      const uint32_t b = o.told.a[k];
+    for (uint32_t k = up.ptr[a]; k < up.ptr[a + 1]; ++k) {
+      const uint32_t b = up.a[k];
       desc[b] += desc[a];
       if (--pending[b] == 0) stk.push_back(b);
     }
   }
+  if (cyc)
+    for (uint32_t a = 0; a < N; ++a) desc[a] = desc[o.scc_rep[a]];
   std::vector<double> links(o.R, 0.0);
   o.cscore.assign(N, 0.0);
   for (uint32_t i = 0; i < ax.n_ex_rhs; ++i) links[ax.exr_r[i]] += 1.0;

@@ -40,7 +40,7 @@ def test_exports_every_symbol(lib):
 
 def test_abi_version(lib):
     from distel_amd import engine
-    assert lib.el_abi_version() == engine.ABI_VERSION == 7
+    assert lib.el_abi_version() == engine.ABI_VERSION == 8
 
 
 def test_config_struct_layout():

@@ -374,13 +374,14 @@ def _assert_stream_matches(eng, strm, o, n_user):
         assert np.array_equal(g, c)
 
 
+@pytest.mark.parametrize("packed", [False, True], ids=["values", "packed"])
 @pytest.mark.parametrize("path", kat.kat_files()[:12], ids=lambda p: os.path.basename(p))
-def test_stream_result_kat(path, oracle_lib):
+def test_stream_result_kat(path, packed, oracle_lib):
     ax, _ = kat.load_kat(path)
     eng = engine.Engine(device=0)
     eng.load(ax)
     eng.init()
-    strm = eng.stream_result(engine.Stream())
+    strm = eng.stream_result(engine.Stream(packed=packed))
     st = eng.saturate()
     eng.result_wait()
     # every logged fact / link streamed once (the ELK range fillers' rows included)
@@ -389,10 +390,11 @@ def test_stream_result_kat(path, oracle_lib):
     eng.close()
 
 
-def test_stream_result_fuzz_release(oracle_lib):
+@pytest.mark.parametrize("packed", [False, True], ids=["values", "packed"])
+def test_stream_result_fuzz_release(packed, oracle_lib):
     """Random ontologies (told cycles included), streamed with release, one engine reused."""
     eng = engine.Engine(device=0)
-    strm = engine.Stream()
+    strm = engine.Stream(packed=packed)
     for seed in range(60):
         ax = generators.random_small(4400 + seed, n=8 + seed % 50, n_roles=1 + seed % 4)
         eng.load(ax)
@@ -451,6 +453,39 @@ def test_stream_result_small_buffers_erange():
     eng.close()
 
 
+def test_stream_packed_short_escapes_erange(oracle_lib):
+    """EL_STREAM_PACKED with an escape buffer far too short: EL_ERANGE with the state kept and
+    the escape count reported; re-armed with it, the fixpoint streams the whole log again.
+    (78,002 concepts: more than the 65,535 coded columns, so some facts escape.)"""
+    ax = generators.workload("g3", 0.2)
+    eng = engine.Engine(device=0)
+    eng.load(ax)
+    eng.init()
+    st = eng.saturate()
+    eng.init()
+    strm = engine.Stream(packed=True)
+    strm.fit(st["s_facts"], st["links"], st["s_facts"], st["links"], 16)
+    s = engine._ElStream()
+    s.flags = engine.EL_RESULT_RELEASE | engine.EL_STREAM_PACKED
+    s.s_code = strm.s_code.ctypes.data_as(engine.C.POINTER(engine.C.c_uint16))
+    s.s_cap = strm.s_code.size
+    s.s_esc, s.s_esc_cap = strm.s_esc.ctypes.data_as(engine._u32p), 4
+    s.s_run, s.s_run_cap = strm.s_run.ctypes.data_as(engine._u32p), strm.s_run.shape[0]
+    s.l_p, s.l_cap = strm.l_p.ctypes.data_as(engine._u32p), strm.l_p.size
+    s.l_run, s.l_run_cap = strm.l_run.ctypes.data_as(engine._u32p), strm.l_run.shape[0]
+    assert eng._lib.el_stream_result(eng._ctx, engine.C.byref(s)) == engine.EL_OK
+    eng._lib.el_saturate(eng._ctx, None)
+    assert s.n_s_esc > 4
+    assert eng._lib.el_result_wait(eng._ctx) == engine.EL_ERANGE
+    strm.n_facts, strm.n_links, strm.n_s_runs, strm.n_l_runs = s.n_facts, s.n_links, s.n_s_runs, s.n_l_runs
+    strm.n_s_esc = s.n_s_esc
+    eng.stream_result(strm, release=True, n_facts=s.n_facts, n_links=s.n_links)
+    eng.saturate()
+    eng.result_wait()
+    _assert_stream_matches(eng, strm, oracle_lib.saturate(ax, 0), ax.n_concepts)
+    eng.close()
+
+
 def _set_digest(name, scale):
     """Pinned order-independent closure digest (tests/golden/set_digests.txt: the oracle's closure,
     cross-checked against its SHA-256 pin by make_set_digests.py)."""
@@ -461,7 +496,8 @@ def _set_digest(name, scale):
     raise AssertionError(f"no pinned set digest for {name} {scale}")
 
 
-def test_stream_result_g3_digest_two_engines():
+@pytest.mark.parametrize("packed", [False, True], ids=["values", "packed"])
+def test_stream_result_g3_digest_two_engines(packed):
     """The bench's schedule at full G3 with the streamed copy-back: one engine serial, then two
     alternating (one's DMA tail beside the other's classification); every result hashes to the
     pinned closure digest.  The digest is order-independent (a sum of per-entry hashes,
@@ -472,7 +508,7 @@ def test_stream_result_g3_digest_two_engines():
     engs = [engine.Engine(device=0) for _ in range(2)]
     for e in engs:
         e.load(ax)
-    strms = [engine.Stream(), engine.Stream()]
+    strms = [engine.Stream(packed=packed), engine.Stream(packed=packed)]
     role, filler = engs[0].pid_table()
 
     def digest(e, s):

@@ -144,8 +144,9 @@ def test_g4_shape_eight_partitions(name, oracle_lib):
     _close(engs)
 
 
+@pytest.mark.parametrize("packed", [False, True], ids=["values", "packed"])
 @pytest.mark.parametrize("short_rank", [None, 1], ids=["fitted", "short_buffer_rank1"])
-def test_partitioned_stream_result(short_rank, oracle_lib):
+def test_partitioned_stream_result(short_rank, packed, oracle_lib):
     """Every rank of a row partition streams its own rows while the collective supersteps run
     (el_stream_result with release, as bench.py's exchange leg does); the union of the streamed
     rows is the oracle's closure.  short_buffer_rank1: rank 1's buffers are far too small, so its
@@ -159,7 +160,7 @@ def test_partitioned_stream_result(short_rank, oracle_lib):
             for q in range(parts)]
     for e in engs:
         e.load(ax)
-    strms = [engine.Stream() for _ in range(parts)]
+    strms = [engine.Stream(packed=packed) for _ in range(parts)]
     errs = []
 
     if short_rank is not None:  # (buffers sized from "the last saturation": 16 facts, 16 links)
@@ -184,7 +185,7 @@ def test_partitioned_stream_result(short_rank, oracle_lib):
     assert not any(t.is_alive() for t in ts), "a rank is stuck"
     assert not errs, errs
     if short_rank is not None:
-        assert strms[short_rank].s_b.size > 64  # (refitted by the recovery)
+        assert (strms[short_rank].s_code if packed else strms[short_rank].s_b).size > 64  # (refitted by the recovery)
     fx = np.concatenate([s.facts(ax.n_concepts)[0] for s in strms])
     fa = np.concatenate([s.facts(ax.n_concepts)[1] for s in strms])
     o = np.lexsort((fa, fx))

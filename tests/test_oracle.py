@@ -118,7 +118,7 @@ def test_closure_digests(oracle_lib):
             name, scale, inp, clo = line.split()
             want[(name, float(scale))] = (inp, clo)
     for (name, scale), (inp, clo) in want.items():
-        if name == "g3" and scale > 0.5:
+        if name in ("g3", "g3e") and scale > 0.5:
             continue  # minutes of oracle time: pinned by oracle/pin_digests.py, checked on the GPU
         ax = generators.workload(name, scale)
         assert ax.digest() == inp, name
