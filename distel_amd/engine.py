@@ -162,7 +162,8 @@ def load_library(path: Optional[str] = None) -> C.CDLL:
     lib.el_pair_table.argtypes = [P, _u32p, _u32p, C.c_size_t, C.POINTER(C.c_size_t)]
     lib.el_pid_table.argtypes = [P, _u32p, _u32p, C.c_size_t, C.POINTER(C.c_size_t)]
     lib.el_stream_result.argtypes = [P, C.POINTER(_ElStream)]
-    lib.el_stream_codes.argtypes = [P, _u32p, C.c_size_t, C.POINTER(C.c_size_t)]
+    if hasattr(lib, "el_stream_codes"):  # (an A/B variant built from an older source may lack it)
+        lib.el_stream_codes.argtypes = [P, _u32p, C.c_size_t, C.POINTER(C.c_size_t)]
     lib.el_host_alloc.argtypes = [C.c_size_t]
     lib.el_host_alloc.restype = C.c_void_p
     lib.el_host_free.argtypes = [C.c_void_p]
