@@ -2,6 +2,7 @@
 #include "el_stream.h"
 
 
+#include <cstdlib>
 #include <stdexcept>
 #include <string>
 #include <vector>
@@ -17,7 +18,16 @@ namespace {
 
 constexpr uint32_t WAVES = BLOCK / 64;
 
-uint32_t grid(uint64_t nt) { return (uint32_t)(nt < 1024 ? (nt ? nt : 1) : 1024); }
+// Workgroups of an encoding launch: one per tile up to a cap (EL_RUN_GRID, default 1024; the
+// encodings run beside the supersteps and share the CUs with them).
+uint32_t grid(uint64_t nt) {
+  static const uint64_t cap = [] {
+    const char* e = getenv("EL_RUN_GRID");
+    const unsigned long v = e ? strtoul(e, nullptr, 10) : 1024ul;
+    return (uint64_t)(v ? v : 1024ul);
+  }();
+  return (uint32_t)(nt < cap ? (nt ? nt : 1) : cap);
+}
 
 // A run starts at e when e opens its tile or its key differs from the one before.
 __device__ __forceinline__ bool run_head(const uint32_t* __restrict__ keys, uint64_t e, uint64_t t0, uint32_t key) {
