@@ -155,9 +155,6 @@ void relax(hipStream_t s, const Axioms& ax, const Out& o);
 // per-concept statistics (Out::nd) of the final rows of [a, b); props: count the base
 // propagations (ND_PROPS)
 void stats(hipStream_t s, const Axioms& ax, const Out& o, uint32_t a, uint32_t b, bool props);
-// the same for the concepts ids[0, n) (device list): a level's rows are final once its launch is
-// done, so its statistics can run beside the next level
-void stats_list(hipStream_t s, const Axioms& ax, const Out& o, const uint32_t* ids, uint32_t n, bool props);
 // totals over the own rows [lo, hi) and the closure events over all rows (adds to Ctr::tot / ev)
 void totals(hipStream_t s, const Axioms& ax, const Out& o, uint32_t lo, uint32_t hi);
 

@@ -1140,15 +1140,13 @@ __device__ __forceinline__ void wave_concat4(uint32_t len, First&& first, Second
 constexpr uint32_t STATS_CH = EL_STATS_CH;
 static_assert(STATS_CH >= 1 && STATS_CH <= 64, "k_stats chunk: 1..64 concepts (lanes)");
 
-// ids: the concepts ids[lo, hi) instead of the range [lo, hi) (a level's list, beside the next level)
-__global__ void __launch_bounds__(BLOCK) k_stats(Axioms ax, Out o, uint32_t lo, uint32_t hi, uint32_t props,
-                                                 const uint32_t* __restrict__ ids) {
+__global__ void __launch_bounds__(BLOCK) k_stats(Axioms ax, Out o, uint32_t lo, uint32_t hi, uint32_t props) {
   __shared__ uint32_t acc[WAVES][6][64];
   uint32_t(&a)[6][64] = acc[threadIdx.x >> 6];
   const uint32_t N1 = ax.N + 1, nw = gridDim.x * WAVES, w = slot_id();
   for (uint32_t x0 = lo + w * STATS_CH; x0 < hi; x0 += nw * STATS_CH) {  // (wave-uniform)
-    const bool ok = lane() < STATS_CH && x0 + lane() < hi;
-    const uint32_t x = ids ? (ok ? ids[x0 + lane()] : 0u) : x0 + lane();
+    const uint32_t x = x0 + lane();
+    const bool ok = lane() < STATS_CH && x < hi;
     uint4 b = make_uint4(0, 0, 0, 0), e = b;
     uint32_t fb = 0, fe = 0;
     if (ok) {
@@ -1500,14 +1498,7 @@ void relax(hipStream_t s, const Axioms& ax, const Out& o) {
 void stats(hipStream_t s, const Axioms& ax, const Out& o, uint32_t a, uint32_t b, bool props) {
   if (b <= a) return;
   hipLaunchKernelGGL(k_stats, dim3(grid_for((uint64_t)(b - a) * (64 / STATS_CH), 2048)), dim3(BLOCK), 0, s, ax, o, a, b,
-                     props ? 1u : 0u, (const uint32_t*)nullptr);
-  CCHK(hipGetLastError());
-}
-
-void stats_list(hipStream_t s, const Axioms& ax, const Out& o, const uint32_t* ids, uint32_t n, bool props) {
-  if (!n) return;
-  hipLaunchKernelGGL(k_stats, dim3(grid_for((uint64_t)n * (64 / STATS_CH), 2048)), dim3(BLOCK), 0, s, ax, o, 0u, n,
-                     props ? 1u : 0u, ids);
+                     props ? 1u : 0u);
   CCHK(hipGetLastError());
 }
 

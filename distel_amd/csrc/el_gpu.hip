@@ -3283,9 +3283,7 @@ struct el_ctx {
   std::chrono::steady_clock::time_point inc_t0;  // (EL_TRACE_INC: el_saturate's start)  // the concept / pair counts the closure buffers were allocated for
   void set_closure_ix();
   void closure_grow();
-  void closure_tail(uint32_t a, uint32_t b, uint32_t L, bool all, bool listed = false);
-  const uint32_t* stat_rest = nullptr;  // the concepts no level list holds (static levels)
-  uint32_t n_rest = 0;
+  void closure_tail(uint32_t a, uint32_t b, uint32_t L, bool all);
   void closure_rows(uint32_t a, uint32_t b);
   // static Kahn levels of the built window (elcl::Axioms::slevel): concepts of level L >= 1 at
   // lvl_ids[lvl_ptr[L], lvl_ptr[L + 1]); empty: the dynamic levels
@@ -3592,9 +3590,7 @@ struct el_ctx {
   bool mark_pending = false;
   void stream_end(bool release);
   hipEvent_t ev_base[2] = {nullptr, nullptr};  // base links logged (stream) / in the link set (rstream)
-  // closure rows ready (stream) / init facts written (rstream) / a level done (stream) / the
-  // levels' statistics done (cstream)
-  hipEvent_t ev_init[4] = {nullptr, nullptr, nullptr, nullptr};
+  hipEvent_t ev_init[2] = {nullptr, nullptr};  // closure rows ready (stream) / init facts written (rstream)
   bool base_filling = false;                   // the set fill runs beside the first superstep
   void join_base();
   bool pre_reset = false;         // the device part of the next reset_state is already enqueued
@@ -3848,8 +3844,6 @@ std::string el_ctx::install_index(el::HostIndex&& hnew) {
 void el_ctx::static_levels() {
   lvl_ptr.clear();
   caxk.slevel = caxk.lvl_ids = nullptr;
-  stat_rest = nullptr;
-  n_rest = 0;
   static const bool dynamic = getenv("EL_DYNAMIC_LEVELS") && getenv("EL_DYNAMIC_LEVELS")[0] == '1';
   if (dynamic) return;
   const el::HostIndex& h = hx;
@@ -3898,11 +3892,6 @@ void el_ctx::static_levels() {
   };
   caxk.slevel = up(lev);
   caxk.lvl_ids = up(ids);
-  std::vector<uint32_t> rest;  // (level 0, followers, concepts outside the window or never reached)
-  for (uint32_t A = 0; A < N; ++A)
-    if (!(lev[A] >= 1u && lev[A] <= depth)) rest.push_back(A);
-  n_rest = (uint32_t)rest.size();
-  if (n_rest) stat_rest = up(rest);
 }
 
 // Every rank's column window, all-gathered once per el_load (the first el_saturate: collective).
@@ -5138,20 +5127,12 @@ void el_ctx::closure_grow() {
 
 // After the Kahn levels launched so far: stuck concepts, totals over [a, b), the scans of the
 // rows' counts, and one readback (counters, the flag of level L, the rows of ⊤).
-// listed: the statistics of the level lists ran beside the levels on cstream (closure_rows);
-// here those of the other concepts, then the engine stream waits for both.
-void el_ctx::closure_tail(uint32_t a, uint32_t b, uint32_t L, bool all, bool listed) {
+void el_ctx::closure_tail(uint32_t a, uint32_t b, uint32_t L, bool all) {
   HIPCHK(hipMemsetAsync(&cl.ctr->tot[elcl::T_STUCK], 0, sizeof(unsigned long long), stream));
   // (told cycles' followers whose representative is final; each once per build)
   if (caxk.nfol) launch(EL_K_CLOSURE, [&] { elcl::follow(stream, caxk, cl, L, all); });
   elcl::check(stream, caxk, cl);
-  if (listed) {
-    elcl::stats_list(stream, cax, cl, stat_rest, n_rest, use_props);
-    HIPCHK(hipEventRecord(ev_init[3], cstream));
-    HIPCHK(hipStreamWaitEvent(stream, ev_init[3], 0));
-  } else {
-    elcl::stats(stream, cax, cl, 0, hx.N, use_props);  // (every row: the SC layout spans them)
-  }
+  elcl::stats(stream, cax, cl, 0, hx.N, use_props);  // (every row: the SC layout spans them)
   HIPCHK(hipMemsetAsync(cl.ctr->tot, 0, elcl::T_STUCK * sizeof(unsigned long long), stream));
   HIPCHK(hipMemsetAsync(cl.ctr->ev, 0, sizeof(cl.ctr->ev), stream));
   elcl::totals(stream, cax, cl, a, b);
@@ -5183,16 +5164,10 @@ void el_ctx::closure_rows(uint32_t a, uint32_t b) {
     if (caxk.slevel) {  // static levels: exactly the levels there are, each a list of its concepts
       launch(EL_K_CLOSURE, [&] { elcl::level(stream, caxk, cl, 0); });
       const uint32_t depth = (uint32_t)lvl_ptr.size() - 2;
-      // each level's statistics (k_stats over its list) on cstream beside the next level: a
-      // level's rows are final once its launch is done (the tail adds the other concepts')
-      for (L = 1; L <= depth; ++L) {
+      for (L = 1; L <= depth; ++L)
         launch(EL_K_CLOSURE, [&] { elcl::level_list(stream, caxk, cl, L, lvl_ptr[L], lvl_ptr[L + 1] - lvl_ptr[L]); });
-        HIPCHK(hipEventRecord(ev_init[2], stream));
-        HIPCHK(hipStreamWaitEvent(cstream, ev_init[2], 0));
-        elcl::stats_list(cstream, cax, cl, caxk.lvl_ids + lvl_ptr[L], lvl_ptr[L + 1] - lvl_ptr[L], use_props);
-      }
       init_lap("levels enqueued");
-      closure_tail(a, b, L, false, true);
+      closure_tail(a, b, L, false);
       init_lap("closure tail read");
       if (clh->ctr.bad) throw ElError{EL_EHIP, "told closure: a told cycle's representative row lacks its follower"};
       redo = clh->ctr.ovf != 0;
