@@ -5334,24 +5334,17 @@ void el_ctx::closure_state() {
   // ---- base links / propagations and the layouts they ask for
   {
     const uint32_t n32 = (uint32_t)N, p32 = (uint32_t)P;
-    {  // the pair-keyed row bounds and capacities zeroed by one k_fill (six fill launches before)
-      FillArgs f{};
-      auto add = [&](void* p) { f.seg[f.n++] = FillSeg{p, P * sizeof(uint32_t), 0u}; };
-      if (P) add(bpp_s), add(bpp_e);
-      if (P && PR.live) add(pr_first), add(pr_last), add(cap_pr);
-      if (P && PP.live) add(cap_pp);
-      if (f.n) {
-        hipLaunchKernelGGL(k_fill, dim3(std::min<uint64_t>(1024, (P * 4 + 16 * BLOCK - 1) / (16 * BLOCK))), dim3(BLOCK), 0,
-                           stream, f);
-        HIPCHK(hipGetLastError());
-      }
-    }
     if (nb) elcl::base_links(stream, cax, cl, lo, hi, cpos[1], llog_x, llog_p);
+    if (P) {
+      HIPCHK(hipMemsetAsync(bpp_s, 0, P * sizeof(uint32_t), stream));
+      HIPCHK(hipMemsetAsync(bpp_e, 0, P * sizeof(uint32_t), stream));
+    }
     if (nbp) {
       elcl::base_props(stream, cax, cl, lo, hi, cpos[2], plog_p, plog_b);
       elcl::runs(stream, plog_p, (uint32_t)nbp, bpp_s, bpp_e);
     }
     if (PR.live) {
+      for (uint32_t* p : {pr_first, pr_last, cap_pr}) HIPCHK(hipMemsetAsync(p, 0, P * sizeof(uint32_t), stream));
       if (nb) {
         elcl::sort_pairs(stream, csort_tmp, csort_bytes, llog_p, sk, llog_x, sv, (uint32_t)nb, key_bits);
         elcl::runs(stream, sk, (uint32_t)nb, pr_first, pr_last);
@@ -5374,6 +5367,7 @@ void el_ctx::closure_state() {
       SC.laid = true;
     }
     if (PP.live) {
+      HIPCHK(hipMemsetAsync(cap_pp, 0, P * sizeof(uint32_t), stream));
       elcl::caps(stream, bpp_s, bpp_e, p32, nullptr, nullptr, cap_pp, nullptr);
       launch_gap_scan(cap_pp, p32, PP.start0);
       PP.laid = true;
