@@ -42,8 +42,10 @@ Csr make_csr(uint32_t rows, std::vector<std::array<uint32_t, 3>>& t, bool two) {
   size_t n = 0;
   for (uint32_t r = 0; r < rows; ++r) {
     auto b = v.begin() + at[r], e = v.begin() + at[r + 1];
-    std::sort(b, e);
-    e = std::unique(b, e);
+    if (e - b > 1) {  // (most rows hold one entry)
+      std::sort(b, e);
+      e = std::unique(b, e);
+    }
     for (auto it = b; it != e; ++it) v[n++] = *it;  // (n <= the row's first index: in place)
     c.ptr[r + 1] = (uint32_t)n;
   }
@@ -505,8 +507,10 @@ std::string build_index(const el_axioms& ax_in, HostIndex& o, uint32_t flags) {
     size_t n = 0;
     for (uint32_t y = 0; y < N; ++y) {
       auto b = rr.begin() + at[y], e = rr.begin() + at[y + 1];
-      std::sort(b, e);
-      e = std::unique(b, e);
+      if (e - b > 1) {
+        std::sort(b, e);
+        e = std::unique(b, e);
+      }
       for (auto it = b; it != e; ++it) pairs[n++] = {y, *it};
     }
     pairs.resize(n);
